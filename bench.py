@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node SHA-256d hashes/sec (+ scrypt) on N MI355X.
+
+BASELINE.json metric: "hashes/sec (whole node) SHA-256d + scrypt at 1/2/4/8
+MI355X; p50 share latency". Reference headline: ~75 MH/s SHA-256d on a whole
+Ryzen 9 7950X (BENCHMARKS.md:46, CPU only).
+
+One rank per GPU (torchrun). One timed step =
+  R1  broadcast of the job blob from rank 0 (torch.distributed / RCCL),
+  K1  SHA-256d search of the FULL 2^32 nonce space of this rank's next header
+      variant (fixed midstate per variant; variants striped across ranks),
+  R2  all_gather of every rank's on-device hit buffer,
+  R3  all_reduce of the hash counters.
+Data: synthetic 80-byte block headers (random prev-hash / merkle root), share
+target = difficulty 1. Every hit found in the timed region is re-verified on
+the CPU after timing. Weak scaling: per-GPU work is fixed as N grows.
+
+Then scrypt(1024,1,1) is timed the same way (HBM-resident scratchpads), and
+p50 share latency is measured end-to-end (GPU hit -> SV2 SubmitSharesStandard
+-> pool validation -> SubmitSharesSuccess) against the in-process local pool.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_HPS = 75e6  # BENCHMARKS.md:46 (whole 7950X, SHA-256d)
+METRIC = "hashes/sec (whole node) SHA-256d + scrypt at 1/2/4/8 MI355X; p50 share latency"
+
+
+def synthetic_job(seed: int = 1) -> dict:
+    from otedama_amd.models.header import DIFF1_TARGET_INT, int_to_hash
+
+    h = hashlib.sha256(f"otedama-bench-{seed}".encode()).digest()
+    prev = hashlib.sha256(h).digest()
+    header = (0x20000000).to_bytes(4, "little") + prev + h + (1_700_000_000).to_bytes(4, "little") \
+        + (0x1703A30C).to_bytes(4, "little") + bytes(4)
+    return {
+        "header": header,
+        "target": int_to_hash(DIFF1_TARGET_INT),
+        "epoch": 1,
+        "job_id": "bench",
+        "version_mask": 0x1FFFE000,  # BIP320 version rolling: 2^16 variants
+        "ntime_roll": 0,
+    }
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
+    ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
+    ap.add_argument("--scrypt-gap", type=int, default=1)
+    ap.add_argument("--no-latency", action="store_true")
+    args = ap.parse_args()
+
+    from otedama_amd.ops import native
+    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch
+    from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
+
+    if not torch.cuda.is_available():
+        print("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU config",
+              file=sys.stderr)
+        return 2
+    N = native.require_native()
+    info = init_from_env()
+    comm = NodeComm(info)
+    dev = info.device
+
+    job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1
+    stripe = stripe_for(info.rank, info.world_size)
+    search = Sha256dSearch(dev, grid=args.grid or None)
+    world = info.world_size
+    gathered = torch.zeros(world, 1 + search.cap, dtype=torch.int32, device=dev)
+    counters_hashes = 0
+
+    def variant_params(step: int) -> tuple[bytes, bytes]:
+        v = stripe.start + step * stripe.stride
+        hdr, _ver, _nt, _en2 = N.variant_header(job, v)
+        return hdr, N.sha256d_prepare(hdr, job["target"])
+
+    hits_log: list[tuple[bytes, torch.Tensor]] = []
+
+    def step(i: int, record: bool) -> None:
+        nonlocal counters_hashes
+        if world > 1:  # R1: job blob fan-out (kept on device; decoded only on job change)
+            comm._run(lambda: torch.distributed.broadcast(comm._job, src=0))
+        hdr, params = variant_params(i)
+        r = search.launch(params, 0, 1 << 32)  # K1: full 2^32 nonce space
+        if world > 1:  # R2: on-device hit buffers, gathered on the comm stream
+            comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered, r.buf))
+        else:
+            gathered[0].copy_(r.buf)
+        counters_hashes += 1 << 32
+        if record:
+            hits_log.append((hdr, gathered[info.rank].clone()))
+
+    for i in range(args.warmup):
+        step(1000 + i, False)
+    torch.cuda.synchronize(dev)
+    barrier(info)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, True)
+    total = comm.allreduce_counters(args.steps << 32)[0] if world > 1 else args.steps << 32  # R3
+    torch.cuda.synchronize(dev)
+    barrier(info)
+    torch.cuda.synchronize(dev)
+    elapsed = comm.allreduce_max(time.perf_counter() - t0)
+    sha_hps = total / elapsed
+
+    # Re-verify every hit of the timed region on the CPU (full 256-bit compare).
+    found = verified = 0
+    for hdr, buf in hits_log:
+        host = buf.cpu().tolist()
+        n = min(host[0] & 0xFFFFFFFF, search.cap)
+        for nonce in host[1 : 1 + n]:
+            nonce &= 0xFFFFFFFF
+            found += 1
+            h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
+            if int.from_bytes(h, "little") <= int.from_bytes(job["target"], "little"):
+                verified += 1
+    found, verified, _, _ = comm.allreduce_counters(found, verified)
+
+    # ---------------------------------------------------------------- scrypt
+    scrypt_hps = None
+    ssteps = args.steps if args.scrypt_steps < 0 else args.scrypt_steps
+    scrypt_info = {}
+    if ssteps > 0:
+        from otedama_amd.models.algorithms import ALGORITHMS
+        from otedama_amd.models.header import int_to_hash
+
+        sc = ScryptSearch(dev, gap=args.scrypt_gap)
+        starget = int_to_hash(ALGORITHMS["scrypt"].diff1)
+        hdr, _, _, _ = N.variant_header(job, stripe.start)
+        sparams = N.scrypt_prepare(hdr, starget)
+        sc.launch(sparams, 0)
+        torch.cuda.synchronize(dev)
+        barrier(info)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(ssteps):
+            sc.launch(sparams, (i * sc.batch) & 0xFFFFFFFF)
+        torch.cuda.synchronize(dev)
+        barrier(info)
+        torch.cuda.synchronize(dev)
+        selapsed = comm.allreduce_max(time.perf_counter() - t0)
+        stotal = comm.allreduce_counters(ssteps * sc.batch)[0] if world > 1 else ssteps * sc.batch
+        scrypt_hps = stotal / selapsed
+        scrypt_info = {"lookup_gap": sc.gap, "lanes": sc.batch, "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2)}
+        del sc
+        torch.cuda.empty_cache()
+
+    # ---------------------------------------------------------- share latency
+    latency = None
+    if not args.no_latency and info.is_primary:
+        try:
+            from otedama_amd.engine.latency_probe import measure_share_latency
+
+            latency = measure_share_latency(device_index=dev.index or 0, seconds=6.0)
+        except Exception as exc:  # noqa: BLE001 - latency is auxiliary; never fail the headline
+            latency = {"error": f"{type(exc).__name__}: {exc}"}
+
+    if info.is_primary:
+        out = {
+            "metric": METRIC,
+            "value": sha_hps,
+            "unit": "hashes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": sha_hps / BASELINE_HPS,
+            "dtype": "u32",
+            "data": "synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1",
+            "config": {
+                "model": "sha256d",
+                "global_batch": (1 << 32) * world,
+                "seq_len": 80,
+                "parallelism": f"dp{world} (nonce-space: per-rank variant stripe, full 2^32 nonces per step)",
+                "algorithm": "SHA-256d nonce search, fixed midstate per variant",
+                "grid": search.grid,
+            },
+            "sha256d_hashes_per_sec": sha_hps,
+            "sha256d_per_gpu_hashes_per_sec": sha_hps / world,
+            "hits_found": found,
+            "hits_verified": verified,
+            "scrypt_hashes_per_sec": scrypt_hps,
+            "scrypt": scrypt_info,
+            "p50_share_latency_ms": (latency or {}).get("p50_ms") if isinstance(latency, dict) else None,
+            "share_latency": latency,
+        }
+        print(json.dumps(out))
+    shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,226 @@
+// pybind11 bindings: `otedama_amd._native`.
+//
+// Exposes the host SHA-256 / scrypt primitives, the per-job folding for the
+// gfx950 kernels, raw kernel launches (for torch-owned buffers / streams), and
+// the native GpuMiner / CpuMiner runtime objects.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "otedama/job.h"
+#include "otedama/runtime.h"
+#include "otedama/sha256.h"
+
+namespace py = pybind11;
+using namespace otedama;
+
+namespace otedama {
+void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
+                       uintptr_t stream);
+void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
+                      uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
+uint64_t scrypt_scratch_bytes(int grid, int gap);
+int gpu_device_count();
+std::string gpu_arch_name(int device);
+int gpu_cu_count(int device);
+}  // namespace otedama
+
+namespace {
+
+std::string need(const py::bytes& b, size_t n, const char* what) {
+  std::string s = b;
+  if (s.size() != n) throw std::invalid_argument(std::string(what) + ": expected " + std::to_string(n) + " bytes");
+  return s;
+}
+
+py::bytes to_bytes(const uint8_t* p, size_t n) { return py::bytes(reinterpret_cast<const char*>(p), n); }
+
+std::shared_ptr<JobTemplate> make_job(const py::dict& d) {
+  auto j = std::make_shared<JobTemplate>();
+  auto get = [&](const char* k) -> py::object {
+    if (d.contains(k)) return py::object(d[k]);
+    return py::none();
+  };
+  std::string hdr = need(d["header"].cast<py::bytes>(), 80, "header");
+  std::memcpy(j->header, hdr.data(), 80);
+  std::string tgt = need(d["target"].cast<py::bytes>(), 32, "target");
+  std::memcpy(j->target, tgt.data(), 32);
+  if (!get("epoch").is_none()) j->epoch = d["epoch"].cast<uint64_t>();
+  if (!get("job_id").is_none()) j->job_id = d["job_id"].cast<std::string>();
+  if (!get("channel_id").is_none()) j->channel_id = d["channel_id"].cast<uint32_t>();
+  if (!get("algo").is_none()) {
+    auto a = d["algo"].cast<std::string>();
+    if (a == "sha256d") j->algo = Algo::kSha256d;
+    else if (a == "scrypt") j->algo = Algo::kScrypt;
+    else throw std::invalid_argument("unsupported algo for the native miner: " + a);
+  }
+  if (!get("version_mask").is_none()) j->version_mask = d["version_mask"].cast<uint32_t>();
+  if (!get("ntime_roll").is_none()) j->ntime_roll = d["ntime_roll"].cast<uint32_t>();
+  if (!get("coinb1").is_none()) {
+    j->has_coinbase = true;
+    std::string c1 = d["coinb1"].cast<py::bytes>(), c2 = d["coinb2"].cast<py::bytes>();
+    std::string e1 = d["extranonce1"].cast<py::bytes>();
+    j->coinb1.assign(c1.begin(), c1.end());
+    j->coinb2.assign(c2.begin(), c2.end());
+    j->extranonce1.assign(e1.begin(), e1.end());
+    j->extranonce2_size = d["extranonce2_size"].cast<uint32_t>();
+    for (auto& br : d["merkle_branches"].cast<py::list>()) {
+      std::string b = br.cast<py::bytes>();
+      j->merkle_branches.emplace_back(b.begin(), b.end());
+    }
+  }
+  if (!get("variant_start").is_none()) j->variant_start = d["variant_start"].cast<uint64_t>();
+  if (!get("variant_stride").is_none()) j->variant_stride = d["variant_stride"].cast<uint64_t>();
+  if (j->variant_stride == 0) j->variant_stride = 1;
+  return j;
+}
+
+py::list shares_to_list(std::vector<ShareRecord>&& v) {
+  py::list out;
+  for (auto& s : v) {
+    py::dict d;
+    d["epoch"] = s.epoch;
+    d["job_id"] = s.job_id;
+    d["channel_id"] = s.channel_id;
+    d["nonce"] = s.nonce;
+    d["ntime"] = s.ntime;
+    d["version"] = s.version;
+    d["extranonce2"] = s.extranonce2;
+    d["extranonce2_size"] = s.extranonce2_size;
+    d["hash"] = to_bytes(s.hash, 32);
+    d["device_id"] = s.device_id;
+    out.append(d);
+  }
+  return out;
+}
+
+py::dict stats_to_dict(const MinerStats& s) {
+  py::dict d;
+  d["hashes"] = s.hashes;
+  d["candidates"] = s.candidates;
+  d["shares"] = s.shares;
+  d["dropped"] = s.dropped;
+  d["launches"] = s.launches;
+  d["rejected_candidates"] = s.rejected_candidates;
+  d["busy_seconds"] = s.busy_seconds;
+  d["faulted"] = s.faulted;
+  d["error"] = s.error;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "Otedama MI355X native runtime (gfx950 HIP kernels + C++ host runtime)";
+
+  m.def("cpu_has_sha_ni", &cpu_has_sha_ni);
+  m.def("sha256", [](const py::bytes& b) {
+    std::string s = b; uint8_t o[32];
+    sha256(reinterpret_cast<const uint8_t*>(s.data()), s.size(), o);
+    return to_bytes(o, 32);
+  });
+  m.def("sha256d", [](const py::bytes& b) {
+    std::string s = b; uint8_t o[32];
+    { py::gil_scoped_release r; sha256d(reinterpret_cast<const uint8_t*>(s.data()), s.size(), o); }
+    return to_bytes(o, 32);
+  });
+  m.def("hmac_sha256", [](const py::bytes& k, const py::bytes& msg) {
+    std::string ks = k, ms = msg; uint8_t o[32];
+    hmac_sha256(reinterpret_cast<const uint8_t*>(ks.data()), ks.size(),
+                reinterpret_cast<const uint8_t*>(ms.data()), ms.size(), o);
+    return to_bytes(o, 32);
+  });
+  m.def("scrypt_1024_1_1", [](const py::bytes& h) {
+    std::string s = need(h, 80, "header"); uint8_t o[32];
+    { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }
+    return to_bytes(o, 32);
+  });
+  m.def("cpu_scan_sha256d", [](const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
+    std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
+    std::vector<uint32_t> hits;
+    {
+      py::gil_scoped_release r;
+      hits = cpu_scan_sha256d(reinterpret_cast<const uint8_t*>(hs.data()), reinterpret_cast<const uint8_t*>(ts.data()),
+                              start, count);
+    }
+    return hits;
+  }, py::arg("header"), py::arg("target"), py::arg("start"), py::arg("count"));
+  m.def("merkle_root", [](const py::dict& job, uint64_t en2) {
+    auto j = make_job(job); uint8_t root[32];
+    merkle_root_from_coinbase(*j, en2, root);
+    return to_bytes(root, 32);
+  });
+  m.def("variant_header", [](const py::dict& job, uint64_t v) {
+    auto j = make_job(job);
+    uint8_t hdr[80]; uint32_t ver, nt; uint64_t en2;
+    j->variant_header(v, hdr, &ver, &nt, &en2);
+    return py::make_tuple(to_bytes(hdr, 80), ver, nt, en2);
+  });
+  m.def("variant_space", [](const py::dict& job) { return make_job(job)->variant_space(); });
+
+  // Kernel parameter blocks are returned as opaque bytes and passed back in.
+  m.def("sha256d_prepare", [](const py::bytes& h, const py::bytes& t) {
+    std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
+    Sha256dParams p;
+    sha256d_prepare(reinterpret_cast<const uint8_t*>(hs.data()), reinterpret_cast<const uint8_t*>(ts.data()), &p);
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
+  });
+  m.def("scrypt_prepare", [](const py::bytes& h, const py::bytes& t) {
+    std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
+    ScryptParams p;
+    scrypt_prepare(reinterpret_cast<const uint8_t*>(hs.data()), reinterpret_cast<const uint8_t*>(ts.data()), &p);
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
+  });
+
+  m.def("gpu_device_count", &gpu_device_count);
+  m.def("gpu_arch_name", &gpu_arch_name);
+  m.def("gpu_cu_count", &gpu_cu_count);
+  m.def("scrypt_scratch_bytes", &scrypt_scratch_bytes);
+  m.def("launch_sha256d", [](const py::bytes& params, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap,
+                             int grid, uintptr_t stream) {
+    std::string ps = need(params, sizeof(Sha256dParams), "params");
+    Sha256dParams p; std::memcpy(&p, ps.data(), sizeof p);
+    if (count == 0 || count > (1ull << 32)) throw std::invalid_argument("count must be in [1, 2^32]");
+    if (grid <= 0 || out == 0) throw std::invalid_argument("bad grid / out");
+    py_launch_sha256d(p, base, count, out, cap, grid, stream);
+  }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
+     py::arg("stream"));
+  m.def("launch_scrypt", [](const py::bytes& params, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch,
+                            int gap, uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
+    std::string ps = need(params, sizeof(ScryptParams), "params");
+    ScryptParams p; std::memcpy(&p, ps.data(), sizeof p);
+    if (gap != 1 && gap != 2 && gap != 4) throw std::invalid_argument("gap must be 1, 2 or 4");
+    if (grid <= 0 || out == 0 || xbuf == 0 || scratch == 0 || count == 0) throw std::invalid_argument("bad launch args");
+    py_launch_scrypt(p, base, count, xbuf, scratch, gap, out, cap, grid, stream);
+  }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("xbuf"), py::arg("scratch"), py::arg("gap"),
+     py::arg("out"), py::arg("cap"), py::arg("grid"), py::arg("stream"));
+
+  py::class_<MinerBase, std::shared_ptr<MinerBase>>(m, "Miner")
+      .def("start", &MinerBase::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &MinerBase::stop, py::call_guard<py::gil_scoped_release>())
+      .def("set_job", [](MinerBase& self, py::object job) {
+        if (job.is_none()) { py::gil_scoped_release r; self.set_job(nullptr); return; }
+        auto j = make_job(job.cast<py::dict>());
+        py::gil_scoped_release r;
+        self.set_job(j);
+      })
+      .def("poll", [](MinerBase& self, size_t max) {
+        std::vector<ShareRecord> v;
+        { py::gil_scoped_release r; v = self.poll(max); }
+        return shares_to_list(std::move(v));
+      }, py::arg("max") = 256)
+      .def("stats", [](MinerBase& self) { return stats_to_dict(self.stats()); })
+      .def_property_readonly("device_id", &MinerBase::device_id);
+
+  py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")
+      .def(py::init<int, std::string, uint64_t, int, size_t>(), py::arg("device"), py::arg("device_id"),
+           py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024);
+  py::class_<CpuMiner, MinerBase, std::shared_ptr<CpuMiner>>(m, "CpuMiner")
+      .def(py::init<int, std::string, size_t>(), py::arg("threads"), py::arg("device_id") = "cpu-0",
+           py::arg("queue_cap") = 1024);
+
+  m.attr("SHA256D_PARAMS_SIZE") = sizeof(Sha256dParams);
+  m.attr("SCRYPT_PARAMS_SIZE") = sizeof(ScryptParams);
+}

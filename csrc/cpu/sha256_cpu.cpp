@@ -1,0 +1,209 @@
+// Host SHA-256: portable C++ compression plus an x86 SHA-NI path.
+//
+// The SHA-NI path is the CPU baseline of BASELINE.json config 1 ("SHA-256d
+// single-thread CPU miner"), which the reference gets from Go's stdlib assembly
+// (internal/miner/sha256d.go:13-20). It is selected at run time via CPUID.
+#include "otedama/sha256.h"
+
+#include <cpuid.h>
+#include <immintrin.h>
+
+namespace otedama {
+
+const uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+const uint32_t kSha256IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                               0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+void sha256_compress_portable(uint32_t state[8], const uint8_t block[64]) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; ++i) w[i] = load_be32(block + 4 * i);
+  for (int i = 16; i < 64; ++i) {
+    uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = state[0], b = state[1], c = state[2], d = state[3];
+  uint32_t e = state[4], f = state[5], g = state[6], h = state[7];
+  for (int i = 0; i < 64; ++i) {
+    uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + kSha256K[i] + w[i];
+    uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  state[0] += a; state[1] += b; state[2] += c; state[3] += d;
+  state[4] += e; state[5] += f; state[6] += g; state[7] += h;
+}
+
+// SHA-NI compression (Intel SHA extensions). Standard message-schedule
+// pipelining with sha256msg1/msg2 and two rounds per sha256rnds2.
+__attribute__((target("sha,sse4.1")))
+static void sha256_compress_shani(uint32_t state[8], const uint8_t block[64]) {
+  const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  __m128i TMP = _mm_loadu_si128((const __m128i*)&state[0]);
+  __m128i STATE1 = _mm_loadu_si128((const __m128i*)&state[4]);
+  TMP = _mm_shuffle_epi32(TMP, 0xB1);          // CDAB
+  STATE1 = _mm_shuffle_epi32(STATE1, 0x1B);    // EFGH
+  __m128i STATE0 = _mm_alignr_epi8(TMP, STATE1, 8);  // ABEF
+  STATE1 = _mm_blend_epi16(STATE1, TMP, 0xF0);       // CDGH
+  const __m128i ABEF_SAVE = STATE0, CDGH_SAVE = STATE1;
+
+  __m128i MSG, MSG0, MSG1, MSG2, MSG3;
+  const __m128i* K = (const __m128i*)kSha256K;
+
+  MSG0 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block + 0)), MASK);
+  MSG1 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block + 16)), MASK);
+  MSG2 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block + 32)), MASK);
+  MSG3 = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block + 48)), MASK);
+
+#define QROUND(Mi, k)                                              \
+  MSG = _mm_add_epi32(Mi, _mm_loadu_si128(K + (k)));               \
+  STATE1 = _mm_sha256rnds2_epu32(STATE1, STATE0, MSG);             \
+  MSG = _mm_shuffle_epi32(MSG, 0x0E);                              \
+  STATE0 = _mm_sha256rnds2_epu32(STATE0, STATE1, MSG);
+
+  // Rounds 0..15
+  QROUND(MSG0, 0);
+  QROUND(MSG1, 1); MSG0 = _mm_sha256msg1_epu32(MSG0, MSG1);
+  QROUND(MSG2, 2); MSG1 = _mm_sha256msg1_epu32(MSG1, MSG2);
+  QROUND(MSG3, 3);
+  // Rounds 16..63: schedule W[t] for the next group while hashing this one.
+  for (int k = 4; k < 16; k += 4) {
+    TMP = _mm_alignr_epi8(MSG3, MSG2, 4); MSG0 = _mm_add_epi32(MSG0, TMP);
+    MSG0 = _mm_sha256msg2_epu32(MSG0, MSG3); MSG2 = _mm_sha256msg1_epu32(MSG2, MSG3);
+    QROUND(MSG0, k);
+    TMP = _mm_alignr_epi8(MSG0, MSG3, 4); MSG1 = _mm_add_epi32(MSG1, TMP);
+    MSG1 = _mm_sha256msg2_epu32(MSG1, MSG0); MSG3 = _mm_sha256msg1_epu32(MSG3, MSG0);
+    QROUND(MSG1, k + 1);
+    TMP = _mm_alignr_epi8(MSG1, MSG0, 4); MSG2 = _mm_add_epi32(MSG2, TMP);
+    MSG2 = _mm_sha256msg2_epu32(MSG2, MSG1); MSG0 = _mm_sha256msg1_epu32(MSG0, MSG1);
+    QROUND(MSG2, k + 2);
+    TMP = _mm_alignr_epi8(MSG2, MSG1, 4); MSG3 = _mm_add_epi32(MSG3, TMP);
+    MSG3 = _mm_sha256msg2_epu32(MSG3, MSG2); MSG1 = _mm_sha256msg1_epu32(MSG1, MSG2);
+    QROUND(MSG3, k + 3);
+  }
+#undef QROUND
+
+  STATE0 = _mm_add_epi32(STATE0, ABEF_SAVE);
+  STATE1 = _mm_add_epi32(STATE1, CDGH_SAVE);
+  TMP = _mm_shuffle_epi32(STATE0, 0x1B);            // FEBA
+  STATE1 = _mm_shuffle_epi32(STATE1, 0xB1);         // DCHG
+  STATE0 = _mm_blend_epi16(TMP, STATE1, 0xF0);      // DCBA
+  STATE1 = _mm_alignr_epi8(STATE1, TMP, 8);         // ABEF -> HGFE
+  _mm_storeu_si128((__m128i*)&state[0], STATE0);
+  _mm_storeu_si128((__m128i*)&state[4], STATE1);
+}
+
+bool cpu_has_sha_ni() {
+  static int cached = -1;
+  if (cached < 0) {
+    unsigned a, b, c, d;
+    bool ok = false;
+    if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) ok = (b >> 29) & 1;  // EBX bit 29 = SHA
+    unsigned a1, b1, c1, d1;
+    if (ok && __get_cpuid(1, &a1, &b1, &c1, &d1)) ok = (c1 >> 19) & 1;  // SSE4.1
+    cached = ok ? 1 : 0;
+  }
+  return cached == 1;
+}
+
+void sha256_compress(uint32_t state[8], const uint8_t block[64]) {
+  if (cpu_has_sha_ni()) sha256_compress_shani(state, block);
+  else sha256_compress_portable(state, block);
+}
+
+void sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
+  uint32_t st[8];
+  std::memcpy(st, kSha256IV, sizeof st);
+  size_t off = 0;
+  while (len - off >= 64) { sha256_compress(st, data + off); off += 64; }
+  uint8_t tail[128] = {0};
+  size_t rem = len - off;
+  std::memcpy(tail, data + off, rem);
+  tail[rem] = 0x80;
+  size_t tl = (rem + 9 <= 64) ? 64 : 128;
+  uint64_t bits = uint64_t(len) * 8;
+  for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = uint8_t(bits >> (8 * i));
+  sha256_compress(st, tail);
+  if (tl == 128) sha256_compress(st, tail + 64);
+  for (int i = 0; i < 8; ++i) store_be32(out + 4 * i, st[i]);
+}
+
+void sha256d(const uint8_t* data, size_t len, uint8_t out[32]) {
+  uint8_t h[32];
+  sha256(data, len, h);
+  sha256(h, 32, out);
+}
+
+void hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen, uint8_t out[32]) {
+  uint8_t k[64] = {0};
+  if (klen > 64) sha256(key, klen, k);
+  else std::memcpy(k, key, klen);
+  uint8_t ipad[64], opad[64];
+  for (int i = 0; i < 64; ++i) { ipad[i] = k[i] ^ 0x36; opad[i] = k[i] ^ 0x5c; }
+  // inner = H(ipad || msg)
+  uint32_t st[8];
+  std::memcpy(st, kSha256IV, sizeof st);
+  sha256_compress(st, ipad);
+  size_t off = 0;
+  while (mlen - off >= 64) { sha256_compress(st, msg + off); off += 64; }
+  uint8_t tail[128] = {0};
+  size_t rem = mlen - off;
+  std::memcpy(tail, msg + off, rem);
+  tail[rem] = 0x80;
+  size_t tl = (rem + 9 <= 64) ? 64 : 128;
+  uint64_t bits = uint64_t(64 + mlen) * 8;
+  for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = uint8_t(bits >> (8 * i));
+  sha256_compress(st, tail);
+  if (tl == 128) sha256_compress(st, tail + 64);
+  uint8_t inner[32];
+  for (int i = 0; i < 8; ++i) store_be32(inner + 4 * i, st[i]);
+  // outer = H(opad || inner)
+  std::memcpy(st, kSha256IV, sizeof st);
+  sha256_compress(st, opad);
+  uint8_t blk[64] = {0};
+  std::memcpy(blk, inner, 32);
+  blk[32] = 0x80;
+  blk[62] = 0x03;  // (64 + 32) * 8 = 768 = 0x300
+  blk[63] = 0x00;
+  sha256_compress(st, blk);
+  for (int i = 0; i < 8; ++i) store_be32(out + 4 * i, st[i]);
+}
+
+void pbkdf2_sha256(const uint8_t* pw, size_t pwlen, const uint8_t* salt, size_t saltlen,
+                   uint32_t iters, uint8_t* out, size_t outlen) {
+  uint8_t buf[1024];
+  uint8_t* msg = saltlen + 4 <= sizeof buf ? buf : new uint8_t[saltlen + 4];
+  std::memcpy(msg, salt, saltlen);
+  uint32_t blockno = 1;
+  size_t done = 0;
+  while (done < outlen) {
+    msg[saltlen] = uint8_t(blockno >> 24); msg[saltlen + 1] = uint8_t(blockno >> 16);
+    msg[saltlen + 2] = uint8_t(blockno >> 8); msg[saltlen + 3] = uint8_t(blockno);
+    uint8_t u[32], t[32];
+    hmac_sha256(pw, pwlen, msg, saltlen + 4, u);
+    std::memcpy(t, u, 32);
+    for (uint32_t it = 1; it < iters; ++it) {
+      hmac_sha256(pw, pwlen, u, 32, u);
+      for (int j = 0; j < 32; ++j) t[j] ^= u[j];
+    }
+    size_t n = outlen - done < 32 ? outlen - done : 32;
+    std::memcpy(out + done, t, n);
+    done += n;
+    ++blockno;
+  }
+  if (msg != buf) delete[] msg;
+}
+
+}  // namespace otedama

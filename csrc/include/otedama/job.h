@@ -1,0 +1,41 @@
+// Job parameter blocks handed from the host runtime to the gfx950 search kernels.
+//
+// Everything that does not depend on the nonce is folded on the host once per
+// job variant (midstate of block 1, rounds 0..2 of block 2, W16/W17), so the
+// per-nonce work on the GPU starts at round 3 with the nonce as W3. The
+// reference hashes the whole 80-byte header per nonce with no midstate
+// (internal/miner/sha256d.go:114-117, worker.go:250-280).
+#pragma once
+#include <cstdint>
+
+namespace otedama {
+
+// Kernel argument block for sha256d_search (passed by value -> SGPRs).
+struct Sha256dParams {
+  uint32_t mid[8];     // SHA-256 state after block 1 (header bytes 0..63)
+  uint32_t st3[8];     // a..h of block 2 after rounds 0..2
+  uint32_t w0, w1, w2; // block-2 words: merkle tail, ntime, nbits (big-endian loads)
+  uint32_t w16, w17;   // nonce-independent schedule words
+  uint32_t pre3;       // round-3 T1 without the nonce: h + S1(e) + Ch(e,f,g) + K3
+  uint32_t t2_3;       // round-3 T2: S0(a) + Maj(a,b,c)
+  uint32_t target_hi;  // most-significant 32 bits of the LE share target (bytes 28..31)
+};
+
+// Builds the kernel parameter block from an 80-byte header (nonce bytes ignored)
+// and a 32-byte little-endian target.
+void sha256d_prepare(const uint8_t header80[80], const uint8_t target32[32], Sha256dParams* out);
+
+// Scrypt (N, r=1, p=1) job parameters: the 76-byte header prefix; the nonce is
+// appended per lane as bytes 76..79.
+// The HMAC key is the whole 80-byte header (> 64 B, so K' = SHA-256(header)),
+// which contains the nonce: only SHA-256 of the first 64 header bytes (hmid) is
+// nonce-independent; the PBKDF2 layers run per lane.
+struct ScryptParams {
+  uint32_t hdr[19];    // header words 0..18 as little-endian loads (bytes 0..75)
+  uint32_t hmid[8];    // SHA-256 state after header bytes 0..63
+  uint32_t target_hi;  // most-significant 32 bits of the LE share target
+};
+
+void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], ScryptParams* out);
+
+}  // namespace otedama

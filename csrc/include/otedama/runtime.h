@@ -1,0 +1,159 @@
+// Native mining runtime: job templates with search-space rolling, the GPU and
+// CPU miners (one host thread each driving launches / SHA-NI loops), and the
+// bounded share queue the Python control plane polls.
+//
+// Parity:
+//   * miner.Worker (internal/miner/worker.go:46-298): Start/Stop/SetWork/Stats,
+//     non-blocking share send with a drop counter (worker.go:266-275), job
+//     epochs (workVer, worker.go:94-96,231-237).
+//   * Reference defects NOT reproduced: every device gets a
+//     disjoint variant stripe instead of identical Work (engine/run.go:1294), and
+//     the search space extends past 2^32 via extranonce2 / BIP320 version /
+//     ntime rolling instead of silently wrapping (worker.go:279).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace otedama {
+
+enum class Algo : int { kSha256d = 0, kScrypt = 1 };
+
+// A pool job plus the rules for deriving header variants from it.
+struct JobTemplate {
+  uint64_t epoch = 0;       // bumped by the control plane on every new job / target
+  std::string job_id;       // opaque pool job id (SV2: decimal u32, V1: hex string)
+  uint32_t channel_id = 0;
+  Algo algo = Algo::kSha256d;
+  uint8_t header[80] = {0};  // version | prevhash | merkle | ntime | nbits | nonce(ignored)
+  uint8_t target[32] = {0};  // share target, little-endian (byte 31 most significant)
+  uint32_t version_mask = 0;  // BIP320 rollable version bits (0 = no version rolling)
+  uint32_t ntime_roll = 0;    // max ntime offset (0 = no ntime rolling)
+  // Stratum V1: coinbase = coinb1 | extranonce1 | extranonce2 | coinb2; merkle
+  // root = fold(sha256d(coinbase), branches). Empty coinb1/coinb2 = fixed merkle.
+  bool has_coinbase = false;
+  std::vector<uint8_t> coinb1, coinb2, extranonce1;
+  uint32_t extranonce2_size = 0;
+  std::vector<std::vector<uint8_t>> merkle_branches;
+  // Variant stripe owned by this device: v = variant_start + k * variant_stride.
+  uint64_t variant_start = 0;
+  uint64_t variant_stride = 1;
+
+  uint64_t variant_space() const;
+  // Materialises variant v: full 80-byte header (nonce 0) and the rolled fields.
+  void variant_header(uint64_t v, uint8_t out[80], uint32_t* version, uint32_t* ntime,
+                      uint64_t* extranonce2) const;
+};
+
+struct ShareRecord {
+  uint64_t epoch;
+  std::string job_id;
+  uint32_t channel_id;
+  uint32_t nonce;
+  uint32_t ntime;
+  uint32_t version;
+  uint64_t extranonce2;
+  uint32_t extranonce2_size;
+  uint8_t hash[32];
+  std::string device_id;
+};
+
+struct MinerStats {
+  uint64_t hashes = 0;      // nonces searched (counted per launch, not per hash)
+  uint64_t candidates = 0;  // kernel hits before host re-verification
+  uint64_t shares = 0;      // verified shares queued
+  uint64_t dropped = 0;     // shares dropped because the queue was full
+  uint64_t launches = 0;
+  uint64_t rejected_candidates = 0;  // top-word ties that failed the full compare
+  double busy_seconds = 0;           // device (or thread) time spent hashing
+  bool faulted = false;              // the device thread died on a HIP error
+  std::string error;
+};
+
+// Full-target re-verification of a candidate (host SHA-256d / scrypt).
+bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32], uint8_t hash_out[32]);
+void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]);
+void merkle_root_from_coinbase(const JobTemplate& job, uint64_t extranonce2, uint8_t root_out[32]);
+
+class ShareQueue {
+ public:
+  explicit ShareQueue(size_t cap) : cap_(cap) {}
+  bool push(ShareRecord&& s);  // false (and counted) when full
+  std::vector<ShareRecord> drain(size_t max);
+  size_t size();
+  uint64_t dropped() const { return dropped_.load(); }
+ private:
+  std::mutex mu_;
+  std::deque<ShareRecord> q_;
+  size_t cap_;
+  std::atomic<uint64_t> dropped_{0};
+};
+
+class MinerBase {
+ public:
+  MinerBase(std::string device_id, size_t queue_cap) : device_id_(std::move(device_id)), queue_(queue_cap) {}
+  virtual ~MinerBase() = default;
+  virtual void start() = 0;
+  virtual void stop() = 0;
+  // nullptr job = pause (curtailment / arbitration idles the device).
+  void set_job(std::shared_ptr<const JobTemplate> job);
+  std::vector<ShareRecord> poll(size_t max) { return queue_.drain(max); }
+  MinerStats stats();
+  const std::string& device_id() const { return device_id_; }
+
+ protected:
+  std::shared_ptr<const JobTemplate> current_job(uint64_t* gen);
+  std::string device_id_;
+  ShareQueue queue_;
+  std::mutex job_mu_;
+  std::condition_variable job_cv_;
+  std::shared_ptr<const JobTemplate> job_;
+  uint64_t job_gen_ = 0;
+  std::atomic<bool> running_{false};
+  std::mutex stats_mu_;
+  MinerStats stats_;
+};
+
+// One host thread per GPU: double-buffered batches on a private HIP stream.
+class GpuMiner : public MinerBase {
+ public:
+  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap);
+  ~GpuMiner() override;
+  void start() override;
+  void stop() override;
+ private:
+  void loop();
+  int device_;
+  uint64_t batch_;
+  int grid_;
+  std::thread th_;
+};
+
+// CPU SHA-256d miner: `threads` workers claiming 64Ki-nonce chunks (SHA-NI).
+class CpuMiner : public MinerBase {
+ public:
+  CpuMiner(int threads, std::string device_id, size_t queue_cap);
+  ~CpuMiner() override;
+  void start() override;
+  void stop() override;
+ private:
+  void loop(int tid);
+  int threads_;
+  std::vector<std::thread> ths_;
+  std::atomic<uint64_t> cursor_{0};
+  std::atomic<uint64_t> cursor_gen_{~0ull};
+  std::mutex cursor_mu_;
+};
+
+// Single-thread CPU scan of [start, start+count) nonces (bench + tests).
+// Returns the nonces (header byte order) whose SHA-256d meets the target.
+std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
+                                       uint64_t count);
+
+}  // namespace otedama

@@ -1,0 +1,57 @@
+// SHA-256 host primitives shared by the CPU miner, the job precompute that feeds
+// the gfx950 search kernels, share validation and the scrypt/PBKDF2 code.
+//
+// Parity: reference hot function is internal/miner/sha256d.go:107-117 (SHA256d,
+// HashHeader). The reference re-serialises the 80-byte header and runs three
+// full compressions per nonce; here the first 64 bytes are compressed once per
+// job (midstate) and only block 2 + the digest block run per nonce.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+
+namespace otedama {
+
+extern const uint32_t kSha256K[64];
+extern const uint32_t kSha256IV[8];
+
+static inline uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+static inline uint32_t load_be32(const uint8_t* p) {
+  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+}
+static inline uint32_t load_le32(const uint8_t* p) {
+  return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+static inline void store_be32(uint8_t* p, uint32_t v) {
+  p[0] = uint8_t(v >> 24); p[1] = uint8_t(v >> 16); p[2] = uint8_t(v >> 8); p[3] = uint8_t(v);
+}
+static inline void store_le32(uint8_t* p, uint32_t v) {
+  p[0] = uint8_t(v); p[1] = uint8_t(v >> 8); p[2] = uint8_t(v >> 16); p[3] = uint8_t(v >> 24);
+}
+static inline uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// One SHA-256 compression of a 64-byte block into `state` (portable C++).
+void sha256_compress_portable(uint32_t state[8], const uint8_t block[64]);
+// Dispatches to SHA-NI when the CPU has it, else portable.
+void sha256_compress(uint32_t state[8], const uint8_t block[64]);
+bool cpu_has_sha_ni();
+
+// Full SHA-256 of an arbitrary message.
+void sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+// SHA-256(SHA-256(data)).
+void sha256d(const uint8_t* data, size_t len, uint8_t out[32]);
+
+// HMAC-SHA256 and PBKDF2-HMAC-SHA256 (used by scrypt's outer layers).
+void hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen, uint8_t out[32]);
+void pbkdf2_sha256(const uint8_t* pw, size_t pwlen, const uint8_t* salt, size_t saltlen,
+                   uint32_t iters, uint8_t* out, size_t outlen);
+
+// 256-bit little-endian compare (byte 31 most significant): a <= b.
+static inline bool le256_leq(const uint8_t a[32], const uint8_t b[32]) {
+  for (int i = 31; i >= 0; --i) {
+    if (a[i] != b[i]) return a[i] < b[i];
+  }
+  return true;
+}
+
+}  // namespace otedama

@@ -1,0 +1,259 @@
+// scrypt_search — Litecoin-parameter scrypt (N=1024, r=1, p=1) nonce search on
+// gfx950. [NO REFERENCE CODE]: v3 of the reference removed scrypt PoW
+// (CHANGELOG.md:6623); the only scrypt there is the wallet KDF
+// (internal/lightning/seedstore.go:68-72). BASELINE.json config 3.
+//
+// Design: one lane = one hash. The 128 KiB ROMix scratchpad of
+// every in-flight lane lives in HBM (hundreds of thousands of lanes = tens of GB,
+// sized against the 288 GB of HBM3E), laid out entry-major:
+//     V[(i / GAP) * nslots + slot]   (one 128-byte entry = 8 x uint4)
+// so the write phase is a fully coalesced 8 KiB store per wave per entry, and a
+// read-phase lookup is one full 128-byte line per lane. GAP > 1 is the
+// lookup-gap time/memory trade-off: only every GAP-th entry is stored and the
+// missing ones are recomputed from the previous stored entry.
+// PBKDF2-HMAC-SHA256 runs per lane (the HMAC key is the header, which holds the
+// nonce); only SHA-256 of header bytes 0..63 is hoisted to the host.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cdna_bitops.h"
+#include "otedama/job.h"
+
+namespace {
+
+using namespace otedama_dev;
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ void salsa20_8(uint32_t B[16]) {
+  uint32_t x0 = B[0], x1 = B[1], x2 = B[2], x3 = B[3], x4 = B[4], x5 = B[5], x6 = B[6], x7 = B[7];
+  uint32_t x8 = B[8], x9 = B[9], x10 = B[10], x11 = B[11], x12 = B[12], x13 = B[13], x14 = B[14], x15 = B[15];
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    x4 ^= rol(x0 + x12, 7);   x8 ^= rol(x4 + x0, 9);    x12 ^= rol(x8 + x4, 13);   x0 ^= rol(x12 + x8, 18);
+    x9 ^= rol(x5 + x1, 7);    x13 ^= rol(x9 + x5, 9);   x1 ^= rol(x13 + x9, 13);   x5 ^= rol(x1 + x13, 18);
+    x14 ^= rol(x10 + x6, 7);  x2 ^= rol(x14 + x10, 9);  x6 ^= rol(x2 + x14, 13);   x10 ^= rol(x6 + x2, 18);
+    x3 ^= rol(x15 + x11, 7);  x7 ^= rol(x3 + x15, 9);   x11 ^= rol(x7 + x3, 13);   x15 ^= rol(x11 + x7, 18);
+    x1 ^= rol(x0 + x3, 7);    x2 ^= rol(x1 + x0, 9);    x3 ^= rol(x2 + x1, 13);    x0 ^= rol(x3 + x2, 18);
+    x6 ^= rol(x5 + x4, 7);    x7 ^= rol(x6 + x5, 9);    x4 ^= rol(x7 + x6, 13);    x5 ^= rol(x4 + x7, 18);
+    x11 ^= rol(x10 + x9, 7);  x8 ^= rol(x11 + x10, 9);  x9 ^= rol(x8 + x11, 13);   x10 ^= rol(x9 + x8, 18);
+    x12 ^= rol(x15 + x14, 7); x13 ^= rol(x12 + x15, 9); x14 ^= rol(x13 + x12, 13); x15 ^= rol(x14 + x13, 18);
+  }
+  B[0] += x0; B[1] += x1; B[2] += x2; B[3] += x3; B[4] += x4; B[5] += x5; B[6] += x6; B[7] += x7;
+  B[8] += x8; B[9] += x9; B[10] += x10; B[11] += x11; B[12] += x12; B[13] += x13; B[14] += x14; B[15] += x15;
+}
+
+// BlockMix_salsa20/8 with r = 1: X = [B0 | B1] (32 words).
+__device__ __forceinline__ void blockmix(uint32_t X[32]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) X[k] ^= X[16 + k];
+  salsa20_8(X);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) X[16 + k] ^= X[k];
+  salsa20_8(X + 16);
+}
+
+__device__ __forceinline__ void store_entry(uint4* __restrict__ dst, const uint32_t X[32]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) dst[q] = make_uint4(X[4 * q], X[4 * q + 1], X[4 * q + 2], X[4 * q + 3]);
+}
+__device__ __forceinline__ void load_entry(const uint4* __restrict__ src, uint32_t T[32]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint4 v = src[q];
+    T[4 * q] = v.x; T[4 * q + 1] = v.y; T[4 * q + 2] = v.z; T[4 * q + 3] = v.w;
+  }
+}
+
+// HMAC-SHA256 pad states for key K' (8 words).
+__device__ __forceinline__ void hmac_states(const uint32_t key[8], uint32_t istate[8], uint32_t ostate[8]) {
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[i] = key[i] ^ 0x36363636u;
+#pragma unroll
+  for (int i = 8; i < 16; ++i) blk[i] = 0x36363636u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) istate[i] = kSha256IVd[i];
+  sha256_compress(istate, blk);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[i] = key[i] ^ 0x5c5c5c5cu;
+#pragma unroll
+  for (int i = 8; i < 16; ++i) blk[i] = 0x5c5c5c5cu;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ostate[i] = kSha256IVd[i];
+  sha256_compress(ostate, blk);
+}
+
+// Outer HMAC step: H(opad-state || digest) with fixed padding (768-bit message).
+__device__ __forceinline__ void hmac_outer(const uint32_t ostate[8], const uint32_t digest[8], uint32_t out[8]) {
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[i] = digest[i];
+  blk[8] = 0x80000000u;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) blk[i] = 0u;
+  blk[15] = 768u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = ostate[i];
+  sha256_compress(out, blk);
+}
+
+// Stage 1: PBKDF2 #1 for `nonce` -> X[32] (LE words of the 128-byte B).
+__device__ __forceinline__ void scrypt_pbkdf_in(const otedama::ScryptParams& p, uint32_t nonce, uint32_t X[32]) {
+  // K' = SHA-256(header80) (key longer than the block size).
+  uint32_t hdrbe[20];
+#pragma unroll
+  for (int i = 0; i < 19; ++i) hdrbe[i] = bswap(p.hdr[i]);
+  hdrbe[19] = bswap(nonce);
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = p.hmid[i];
+  {
+    uint32_t blk[16] = {hdrbe[16], hdrbe[17], hdrbe[18], hdrbe[19], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u};
+    sha256_compress(key, blk);
+  }
+  uint32_t istate[8], ostate[8];
+  hmac_states(key, istate, ostate);
+  // salt = header80, 4 blocks of 32 bytes.
+  uint32_t ist2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ist2[i] = istate[i];
+  sha256_compress(ist2, hdrbe);  // header bytes 0..63
+#pragma unroll
+  for (int blkno = 1; blkno <= 4; ++blkno) {
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = ist2[i];
+    uint32_t blk[16] = {hdrbe[16], hdrbe[17], hdrbe[18], hdrbe[19], uint32_t(blkno), 0x80000000u,
+                        0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 84u) * 8u};
+    sha256_compress(st, blk);
+    uint32_t t[8];
+    hmac_outer(ostate, st, t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) X[8 * (blkno - 1) + i] = bswap(t[i]);
+  }
+}
+
+// Stage 3: PBKDF2 #2 over X (salt = X || INT(1)); returns final state word 7.
+__device__ __forceinline__ uint32_t scrypt_pbkdf_out(const otedama::ScryptParams& p, uint32_t nonce,
+                                                     const uint32_t X[32]) {
+  uint32_t key[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) key[i] = p.hmid[i];
+  {
+    uint32_t blk[16] = {bswap(p.hdr[16]), bswap(p.hdr[17]), bswap(p.hdr[18]), bswap(nonce), 0x80000000u,
+                        0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u};
+    sha256_compress(key, blk);
+  }
+  uint32_t istate[8], ostate[8];
+  hmac_states(key, istate, ostate);
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) st[i] = istate[i];
+  uint32_t blk[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) blk[i] = bswap(X[i]);
+  sha256_compress(st, blk);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) blk[i] = bswap(X[16 + i]);
+  sha256_compress(st, blk);
+  uint32_t tail[16] = {1u, 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (64u + 132u) * 8u};
+  sha256_compress(st, tail);
+  uint32_t out[8];
+  hmac_outer(ostate, st, out);
+  return out[7];
+}
+
+// Stage 2: ROMix on X in place with the lane's GAP-strided scratchpad slot.
+template <int GAP>
+__device__ __forceinline__ void scrypt_romix(uint32_t X[32], uint4* __restrict__ V, uint64_t slot, uint64_t nslots) {
+  for (int i = 0; i < 1024; ++i) {
+    if (i % GAP == 0) store_entry(V + ((uint64_t(i / GAP) * nslots + slot) << 3), X);
+    blockmix(X);
+  }
+  for (int i = 0; i < 1024; ++i) {
+    const uint32_t j = X[16] & 1023u;
+    uint32_t T[32];
+    load_entry(V + ((uint64_t(j / GAP) * nslots + slot) << 3), T);
+    if constexpr (GAP > 1) {
+      for (uint32_t r = 0; r < (j % GAP); ++r) blockmix(T);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) X[k] ^= T[k];
+    blockmix(X);
+  }
+}
+
+}  // namespace
+
+// The three stages are separate launches so the ROMix kernel is register-lean
+// (X, T and the salsa state only): fused, the unrolled SHA-256 schedules of the
+// PBKDF2 layers pushed the kernel to 256 VGPRs (1-2 waves/SIMD). The stages
+// exchange 128 bytes per hash through `xbuf` (0.1% of the ROMix traffic).
+extern "C" __global__ __launch_bounds__(256) void otd_scrypt_pbkdf_in(const otedama::ScryptParams p, uint32_t base,
+                                                                      uint32_t count, uint4* __restrict__ xbuf) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t X[32];
+  scrypt_pbkdf_in(p, base + i, X);
+  store_entry(xbuf + (uint64_t(i) << 3), X);
+}
+
+template <int GAP>
+__global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* __restrict__ xbuf,
+                                                        uint4* __restrict__ V) {
+  const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = slot; i < count; i += nslots) {
+    uint32_t X[32];
+    load_entry(xbuf + (i << 3), X);
+    scrypt_romix<GAP>(X, V, slot, nslots);
+    store_entry(xbuf + (i << 3), X);
+  }
+}
+
+// out[0]: candidate count; out[1..cap]: nonces.
+extern "C" __global__ __launch_bounds__(256) void otd_scrypt_pbkdf_out(const otedama::ScryptParams p, uint32_t base,
+                                                                       uint32_t count, const uint4* __restrict__ xbuf,
+                                                                       uint32_t* __restrict__ out, uint32_t cap) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint32_t X[32];
+  load_entry(xbuf + (uint64_t(i) << 3), X);
+  const uint32_t h7 = scrypt_pbkdf_out(p, base + i, X);
+  if (bswap(h7) <= p.target_hi) {
+    const uint32_t s = atomicAdd(out, 1u);
+    if (s < cap) out[1 + s] = base + i;
+  }
+}
+
+template __global__ void otd_scrypt_romix<1>(uint32_t, uint4*, uint4*);
+template __global__ void otd_scrypt_romix<2>(uint32_t, uint4*, uint4*);
+template __global__ void otd_scrypt_romix<4>(uint32_t, uint4*, uint4*);
+
+namespace otedama {
+
+// Scratchpad bytes for `grid` ROMix blocks of 256 lane slots at lookup gap `gap`.
+uint64_t scrypt_scratch_bytes(int grid, int gap) {
+  return uint64_t(grid) * 256ull * (1024ull / uint64_t(gap)) * 128ull;
+}
+
+// xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
+hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
+                                int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream) {
+  uint4* X = static_cast<uint4*>(xbuf);
+  uint4* V = static_cast<uint4*>(scratch);
+  const int eg = int((count + 255) / 256);
+  hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
+  switch (gap) {
+    case 1: hipLaunchKernelGGL(otd_scrypt_romix<1>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
+    case 2: hipLaunchKernelGGL(otd_scrypt_romix<2>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
+    case 4: hipLaunchKernelGGL(otd_scrypt_romix<4>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
+    default: return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(otd_scrypt_pbkdf_out, dim3(eg), dim3(256), 0, stream, p, base, count, X, out, cap);
+  return hipGetLastError();
+}
+
+}  // namespace otedama

@@ -1,0 +1,232 @@
+// GpuMiner: one host thread per GPU driving double-buffered search batches on a
+// private HIP stream (short launches + pinned result buffers so a
+// job switch or a found share is never more than ~one batch away).
+//
+// Per batch: hipMemsetAsync(hit counter) -> search kernel -> hipMemcpyAsync of
+// the hit slots into pinned host memory -> event. While batch k runs on the GPU
+// the thread re-verifies batch k-1's candidates on the CPU (full 256-bit compare)
+// and queues shares tagged with the job epoch that produced them.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "otedama/job.h"
+#include "otedama/runtime.h"
+#include "otedama/sha256.h"
+
+namespace otedama {
+
+hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, uint32_t* out,
+                                 uint32_t cap, int grid, hipStream_t stream);
+hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
+                                int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
+uint64_t scrypt_scratch_bytes(int grid, int gap);
+
+#define OTD_HIP(call)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #call); \
+  } while (0)
+
+namespace {
+constexpr uint32_t kHitCap = 1024;
+
+struct Slot {
+  uint32_t* d_out = nullptr;
+  uint32_t* h_out = nullptr;
+  hipEvent_t start{}, done{};
+  bool busy = false;
+  std::shared_ptr<const JobTemplate> job;
+  uint64_t gen = 0;
+  uint64_t variant = 0;
+  uint64_t count = 0;
+  uint8_t header[80];
+  uint32_t version = 0, ntime = 0;
+  uint64_t en2 = 0;
+};
+}  // namespace
+
+GpuMiner::GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap)
+    : MinerBase(std::move(device_id), queue_cap), device_(device), batch_(batch_nonces), grid_(grid) {
+  if (batch_ == 0 || batch_ > (1ull << 32)) batch_ = 1ull << 30;
+  // Batches must tile the 2^32 nonce range exactly.
+  while ((1ull << 32) % batch_) --batch_;
+}
+
+GpuMiner::~GpuMiner() { stop(); }
+
+void GpuMiner::start() {
+  if (running_.exchange(true)) return;
+  th_ = std::thread([this] {
+    try {
+      loop();
+    } catch (const std::exception& ex) {
+      // A device fault removes this device's stripe; the engine sees it in
+      // stats().faulted and through the hashrate window.
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.faulted = true;
+      stats_.error = ex.what();
+    }
+  });
+}
+
+void GpuMiner::stop() {
+  if (!running_.exchange(false)) return;
+  job_cv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+void GpuMiner::loop() {
+  OTD_HIP(hipSetDevice(device_));
+  hipStream_t stream;
+  OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  Slot slots[2];
+  for (auto& s : slots) {
+    OTD_HIP(hipMalloc(&s.d_out, (1 + 2 * kHitCap) * sizeof(uint32_t)));
+    OTD_HIP(hipHostMalloc(&s.h_out, (1 + 2 * kHitCap) * sizeof(uint32_t), hipHostMallocDefault));
+    OTD_HIP(hipEventCreate(&s.start));
+    OTD_HIP(hipEventCreate(&s.done));
+  }
+  // scrypt scratch (allocated lazily on the first scrypt job)
+  void* scratch = nullptr;
+  void* xbuf = nullptr;
+  const int scrypt_gap = 2;
+  const int scrypt_grid = grid_;
+  const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u * 2u;
+
+  uint64_t cur_gen = ~0ull;
+  uint64_t k = 0;       // variant-stripe position
+  uint64_t nonce_off = 0;
+  int which = 0;
+
+  auto finish = [&](Slot& s) {
+    if (!s.busy) return;
+    OTD_HIP(hipEventSynchronize(s.done));
+    float ms = 0;
+    hipEventElapsedTime(&ms, s.start, s.done);
+    const uint32_t n = s.h_out[0] < kHitCap ? s.h_out[0] : kHitCap;
+    uint64_t good = 0, bad = 0;
+    const bool multi = false;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t nonce = multi ? s.h_out[1 + 2 * i] : s.h_out[1 + i];
+      uint8_t hdr[80];
+      std::memcpy(hdr, s.header, 80);
+      store_le32(hdr + 76, nonce);
+      ShareRecord r{};
+      if (!verify_share(s.job->algo, hdr, s.job->target, r.hash)) { ++bad; continue; }
+      r.epoch = s.job->epoch; r.job_id = s.job->job_id; r.channel_id = s.job->channel_id;
+      r.nonce = nonce; r.ntime = s.ntime; r.version = s.version; r.extranonce2 = s.en2;
+      r.extranonce2_size = s.job->extranonce2_size; r.device_id = device_id_;
+      queue_.push(std::move(r));
+      ++good;
+    }
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.hashes += s.count;
+    stats_.candidates += s.h_out[0];
+    stats_.shares += good;
+    stats_.rejected_candidates += bad;
+    stats_.busy_seconds += ms * 1e-3;
+    stats_.launches += 1;
+    s.busy = false;
+    s.job.reset();
+  };
+
+  while (running_.load()) {
+    uint64_t gen = 0;
+    auto job = current_job(&gen);
+    if (!job) {
+      finish(slots[which ^ 1]);
+      continue;
+    }
+    if (gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
+    const uint64_t v = job->variant_start + k * job->variant_stride;
+    if (v >= job->variant_space()) {  // stripe exhausted; wait for fresh work
+      finish(slots[which ^ 1]);
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      continue;
+    }
+    Slot& s = slots[which];
+    finish(s);  // slot reuse: make sure its previous batch is consumed
+    s.job = job;
+    s.gen = gen;
+    s.variant = v;
+    job->variant_header(v, s.header, &s.version, &s.ntime, &s.en2);
+    OTD_HIP(hipMemsetAsync(s.d_out, 0, sizeof(uint32_t), stream));
+    OTD_HIP(hipEventRecord(s.start, stream));
+    if (job->algo == Algo::kScrypt) {
+      if (!scratch) {
+        OTD_HIP(hipMalloc(&scratch, scrypt_scratch_bytes(scrypt_grid, scrypt_gap)));
+        OTD_HIP(hipMalloc(&xbuf, uint64_t(scrypt_batch) * 128));
+      }
+      ScryptParams p;
+      scrypt_prepare(s.header, job->target, &p);
+      const uint64_t remaining = (1ull << 32) - nonce_off;
+      s.count = remaining < scrypt_batch ? remaining : scrypt_batch;
+      OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, s.d_out,
+                                   kHitCap, scrypt_grid, stream));
+    } else {
+      Sha256dParams p;
+      sha256d_prepare(s.header, job->target, &p);
+      s.count = batch_;
+      OTD_HIP(launch_sha256d_search(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_, stream));
+    }
+    OTD_HIP(hipMemcpyAsync(s.h_out, s.d_out, (1 + kHitCap) * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    OTD_HIP(hipEventRecord(s.done, stream));
+    s.busy = true;
+    nonce_off += s.count;
+    if (nonce_off >= (1ull << 32)) { nonce_off = 0; ++k; }
+    which ^= 1;
+    finish(slots[which]);  // consume the previous batch while this one runs
+  }
+  finish(slots[0]);
+  finish(slots[1]);
+  for (auto& s : slots) {
+    hipFree(s.d_out);
+    hipHostFree(s.h_out);
+    hipEventDestroy(s.start);
+    hipEventDestroy(s.done);
+  }
+  if (scratch) hipFree(scratch);
+  if (xbuf) hipFree(xbuf);
+  hipStreamDestroy(stream);
+}
+
+// ------------------------------------------------------------- direct launches
+// Synchronous-free launch API for the Python ops layer (torch-owned buffers and
+// streams): pointers and the stream arrive as integers.
+
+void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
+                       uintptr_t stream) {
+  OTD_HIP(launch_sha256d_search(p, base, count, reinterpret_cast<uint32_t*>(out), cap, grid,
+                                reinterpret_cast<hipStream_t>(stream)));
+}
+
+void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
+                      uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
+  OTD_HIP(launch_scrypt_search(p, base, count, reinterpret_cast<void*>(xbuf), reinterpret_cast<void*>(scratch), gap,
+                               reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream)));
+}
+
+int gpu_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::string gpu_arch_name(int device) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return "";
+  return prop.gcnArchName;
+}
+
+int gpu_cu_count(int device) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+  return prop.multiProcessorCount;
+}
+
+}  // namespace otedama

@@ -1,0 +1,319 @@
+// Host side of the mining runtime: job variants, share verification, the share
+// queue, the CPU miner and the CPU scrypt reference.
+#include <immintrin.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "otedama/job.h"
+#include "otedama/runtime.h"
+#include "otedama/sha256.h"
+
+namespace otedama {
+
+// ---------------------------------------------------------------- job variants
+
+static uint32_t popcount32(uint32_t x) { return uint32_t(__builtin_popcount(x)); }
+
+// Scatter the low bits of `v` into the set bits of `mask` (software pdep).
+static uint32_t deposit_bits(uint32_t v, uint32_t mask) {
+  uint32_t out = 0;
+  for (uint32_t bit = 1; mask; bit <<= 1) {
+    uint32_t low = mask & (~mask + 1);
+    if (v & bit) out |= low;
+    mask &= mask - 1;
+  }
+  return out;
+}
+
+static uint64_t en2_space(const JobTemplate& j) {
+  if (!j.has_coinbase || j.extranonce2_size == 0) return 1;
+  if (j.extranonce2_size >= 8) return ~0ull;
+  return 1ull << (8 * j.extranonce2_size);
+}
+
+uint64_t JobTemplate::variant_space() const {
+  const uint64_t e = en2_space(*this);
+  const uint32_t vb = popcount32(version_mask);
+  const uint64_t v = vb >= 32 ? (1ull << 32) : (1ull << vb);
+  const uint64_t t = uint64_t(ntime_roll) + 1;
+  // saturating product
+  uint64_t s = e;
+  if (s > (~0ull) / v) return ~0ull;
+  s *= v;
+  if (s > (~0ull) / t) return ~0ull;
+  return s * t;
+}
+
+void merkle_root_from_coinbase(const JobTemplate& j, uint64_t en2, uint8_t root[32]) {
+  std::vector<uint8_t> cb;
+  cb.reserve(j.coinb1.size() + j.extranonce1.size() + j.extranonce2_size + j.coinb2.size());
+  cb.insert(cb.end(), j.coinb1.begin(), j.coinb1.end());
+  cb.insert(cb.end(), j.extranonce1.begin(), j.extranonce1.end());
+  for (uint32_t i = 0; i < j.extranonce2_size; ++i) cb.push_back(i < 8 ? uint8_t(en2 >> (8 * i)) : 0);
+  cb.insert(cb.end(), j.coinb2.begin(), j.coinb2.end());
+  sha256d(cb.data(), cb.size(), root);
+  uint8_t buf[64];
+  for (const auto& br : j.merkle_branches) {
+    std::memcpy(buf, root, 32);
+    std::memcpy(buf + 32, br.data(), br.size() < 32 ? br.size() : 32);
+    sha256d(buf, 64, root);
+  }
+}
+
+void JobTemplate::variant_header(uint64_t v, uint8_t out[80], uint32_t* version, uint32_t* ntime,
+                                 uint64_t* extranonce2) const {
+  std::memcpy(out, header, 80);
+  const uint64_t es = en2_space(*this);
+  uint64_t en2 = 0;
+  if (es > 1) {
+    if (es == ~0ull) { en2 = v; v = 0; }
+    else { en2 = v % es; v /= es; }
+  }
+  const uint32_t vb = popcount32(version_mask);
+  uint32_t ver = load_le32(header);
+  if (vb) {
+    const uint64_t vs = vb >= 32 ? (1ull << 32) : (1ull << vb);
+    const uint32_t bits = uint32_t(v % vs);
+    v /= vs;
+    ver = (ver & ~version_mask) | deposit_bits(bits, version_mask);
+    store_le32(out, ver);
+  }
+  uint32_t nt = load_le32(header + 68);
+  if (ntime_roll) {
+    nt += uint32_t(v % (uint64_t(ntime_roll) + 1));
+    store_le32(out + 68, nt);
+  }
+  if (has_coinbase) {
+    uint8_t root[32];
+    merkle_root_from_coinbase(*this, en2, root);
+    std::memcpy(out + 36, root, 32);
+  }
+  if (version) *version = ver;
+  if (ntime) *ntime = nt;
+  if (extranonce2) *extranonce2 = en2;
+}
+
+// ------------------------------------------------------------------- scrypt
+
+static inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+static void salsa20_8(uint32_t B[16]) {
+  uint32_t x[16];
+  std::memcpy(x, B, 64);
+  for (int i = 0; i < 8; i += 2) {
+    x[4] ^= rotl32(x[0] + x[12], 7);   x[8] ^= rotl32(x[4] + x[0], 9);
+    x[12] ^= rotl32(x[8] + x[4], 13);  x[0] ^= rotl32(x[12] + x[8], 18);
+    x[9] ^= rotl32(x[5] + x[1], 7);    x[13] ^= rotl32(x[9] + x[5], 9);
+    x[1] ^= rotl32(x[13] + x[9], 13);  x[5] ^= rotl32(x[1] + x[13], 18);
+    x[14] ^= rotl32(x[10] + x[6], 7);  x[2] ^= rotl32(x[14] + x[10], 9);
+    x[6] ^= rotl32(x[2] + x[14], 13);  x[10] ^= rotl32(x[6] + x[2], 18);
+    x[3] ^= rotl32(x[15] + x[11], 7);  x[7] ^= rotl32(x[3] + x[15], 9);
+    x[11] ^= rotl32(x[7] + x[3], 13);  x[15] ^= rotl32(x[11] + x[7], 18);
+    x[1] ^= rotl32(x[0] + x[3], 7);    x[2] ^= rotl32(x[1] + x[0], 9);
+    x[3] ^= rotl32(x[2] + x[1], 13);   x[0] ^= rotl32(x[3] + x[2], 18);
+    x[6] ^= rotl32(x[5] + x[4], 7);    x[7] ^= rotl32(x[6] + x[5], 9);
+    x[4] ^= rotl32(x[7] + x[6], 13);   x[5] ^= rotl32(x[4] + x[7], 18);
+    x[11] ^= rotl32(x[10] + x[9], 7);  x[8] ^= rotl32(x[11] + x[10], 9);
+    x[9] ^= rotl32(x[8] + x[11], 13);  x[10] ^= rotl32(x[9] + x[8], 18);
+    x[12] ^= rotl32(x[15] + x[14], 7); x[13] ^= rotl32(x[12] + x[15], 9);
+    x[14] ^= rotl32(x[13] + x[12], 13); x[15] ^= rotl32(x[14] + x[13], 18);
+  }
+  for (int i = 0; i < 16; ++i) B[i] += x[i];
+}
+
+// scrypt(N=1024, r=1, p=1) of an 80-byte header, password = salt = header.
+void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]) {
+  uint8_t b[128];
+  pbkdf2_sha256(header80, 80, header80, 80, 1, b, 128);
+  uint32_t X[32];
+  for (int i = 0; i < 32; ++i) X[i] = load_le32(b + 4 * i);
+  std::vector<uint32_t> V(32 * 1024);
+  for (int i = 0; i < 1024; ++i) {
+    std::memcpy(&V[32 * i], X, 128);
+    for (int k = 0; k < 16; ++k) X[k] ^= X[16 + k];
+    salsa20_8(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] ^= X[k];
+    salsa20_8(X + 16);
+  }
+  for (int i = 0; i < 1024; ++i) {
+    const uint32_t j = X[16] & 1023;
+    for (int k = 0; k < 32; ++k) X[k] ^= V[32 * j + k];
+    for (int k = 0; k < 16; ++k) X[k] ^= X[16 + k];
+    salsa20_8(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] ^= X[k];
+    salsa20_8(X + 16);
+  }
+  for (int i = 0; i < 32; ++i) store_le32(b + 4 * i, X[i]);
+  pbkdf2_sha256(header80, 80, b, 128, 1, out, 32);
+}
+
+bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32], uint8_t hash_out[32]) {
+  if (algo == Algo::kScrypt) scrypt_1024_1_1(header80, hash_out);
+  else sha256d(header80, 80, hash_out);
+  return le256_leq(hash_out, target);
+}
+
+// -------------------------------------------------------------- share queue
+
+bool ShareQueue::push(ShareRecord&& s) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (q_.size() >= cap_) {
+    dropped_.fetch_add(1);
+    return false;
+  }
+  q_.push_back(std::move(s));
+  return true;
+}
+
+std::vector<ShareRecord> ShareQueue::drain(size_t max) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<ShareRecord> out;
+  while (!q_.empty() && out.size() < max) {
+    out.push_back(std::move(q_.front()));
+    q_.pop_front();
+  }
+  return out;
+}
+
+size_t ShareQueue::size() {
+  std::lock_guard<std::mutex> g(mu_);
+  return q_.size();
+}
+
+// --------------------------------------------------------------- miner base
+
+void MinerBase::set_job(std::shared_ptr<const JobTemplate> job) {
+  {
+    std::lock_guard<std::mutex> g(job_mu_);
+    job_ = std::move(job);
+    ++job_gen_;
+  }
+  job_cv_.notify_all();
+}
+
+std::shared_ptr<const JobTemplate> MinerBase::current_job(uint64_t* gen) {
+  std::unique_lock<std::mutex> g(job_mu_);
+  if (!job_ && running_.load()) {
+    job_cv_.wait_for(g, std::chrono::milliseconds(10));
+  }
+  if (gen) *gen = job_gen_;
+  return job_;
+}
+
+MinerStats MinerBase::stats() {
+  std::lock_guard<std::mutex> g(stats_mu_);
+  MinerStats s = stats_;
+  s.dropped = queue_.dropped();
+  return s;
+}
+
+// ---------------------------------------------------------- CPU SHA-256d scan
+
+// Per-nonce work with a midstate: block 2 (16 B of header + padding) and the
+// 32-byte digest block. 2 compressions per nonce instead of the reference's 3.
+static inline void sha256d_from_mid(const uint32_t mid[8], uint8_t blk2[64], uint8_t dblk[64],
+                                    uint8_t out[32]) {
+  uint32_t st[8];
+  std::memcpy(st, mid, 32);
+  sha256_compress(st, blk2);
+  for (int i = 0; i < 8; ++i) store_be32(dblk + 4 * i, st[i]);
+  std::memcpy(st, kSha256IV, 32);
+  sha256_compress(st, dblk);
+  for (int i = 0; i < 8; ++i) store_be32(out + 4 * i, st[i]);
+}
+
+std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
+                                       uint64_t count) {
+  uint32_t mid[8];
+  std::memcpy(mid, kSha256IV, 32);
+  sha256_compress(mid, header80);
+  uint8_t blk2[64] = {0};
+  std::memcpy(blk2, header80 + 64, 16);
+  blk2[16] = 0x80;
+  blk2[62] = 0x02;  // 640 bits
+  blk2[63] = 0x80;
+  uint8_t dblk[64] = {0};
+  dblk[32] = 0x80;
+  dblk[62] = 0x01;  // 256 bits
+  std::vector<uint32_t> hits;
+  uint8_t h[32];
+  const uint32_t thi = load_le32(target + 28);
+  for (uint64_t i = 0; i < count; ++i) {
+    const uint32_t nonce = start + uint32_t(i);
+    store_le32(blk2 + 12, nonce);
+    sha256d_from_mid(mid, blk2, dblk, h);
+    if (load_le32(h + 28) <= thi && le256_leq(h, target)) hits.push_back(nonce);
+  }
+  return hits;
+}
+
+// ------------------------------------------------------------------ CPU miner
+
+CpuMiner::CpuMiner(int threads, std::string device_id, size_t queue_cap)
+    : MinerBase(std::move(device_id), queue_cap), threads_(threads > 0 ? threads : 1) {}
+
+CpuMiner::~CpuMiner() { stop(); }
+
+void CpuMiner::start() {
+  if (running_.exchange(true)) return;
+  for (int t = 0; t < threads_; ++t) ths_.emplace_back([this, t] { loop(t); });
+}
+
+void CpuMiner::stop() {
+  if (!running_.exchange(false)) return;
+  job_cv_.notify_all();
+  for (auto& t : ths_) if (t.joinable()) t.join();
+  ths_.clear();
+}
+
+void CpuMiner::loop(int /*tid*/) {
+  constexpr uint64_t kChunk = 1ull << 16;
+  while (running_.load()) {
+    uint64_t gen = 0;
+    auto job = current_job(&gen);
+    if (!job) continue;
+    if (job->algo != Algo::kSha256d) {  // CPU scrypt mining is not a supported config
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      continue;
+    }
+    uint64_t claim;
+    {
+      std::lock_guard<std::mutex> g(cursor_mu_);
+      if (cursor_gen_.load() != gen) { cursor_gen_.store(gen); cursor_.store(0); }
+      claim = cursor_.fetch_add(kChunk);
+    }
+    // claim indexes (variant-stripe slot k, nonce chunk)
+    const uint64_t chunks_per_variant = (1ull << 32) / kChunk;
+    const uint64_t k = claim / kChunk / chunks_per_variant;
+    const uint32_t nonce0 = uint32_t((claim / kChunk % chunks_per_variant) * kChunk);
+    const uint64_t v = job->variant_start + k * job->variant_stride;
+    if (v >= job->variant_space()) {  // stripe exhausted: wait for new work
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+      continue;
+    }
+    uint8_t hdr[80];
+    uint32_t ver, nt;
+    uint64_t en2;
+    job->variant_header(v, hdr, &ver, &nt, &en2);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto hits = cpu_scan_sha256d(hdr, job->target, nonce0, kChunk);
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    for (uint32_t n : hits) {
+      ShareRecord s{};
+      s.epoch = job->epoch; s.job_id = job->job_id; s.channel_id = job->channel_id;
+      s.nonce = n; s.ntime = nt; s.version = ver; s.extranonce2 = en2;
+      s.extranonce2_size = job->extranonce2_size; s.device_id = device_id_;
+      store_le32(hdr + 76, n);
+      sha256d(hdr, 80, s.hash);
+      queue_.push(std::move(s));
+    }
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.hashes += kChunk;
+    stats_.candidates += hits.size();
+    stats_.shares += hits.size();
+    stats_.busy_seconds += dt;
+  }
+}
+
+}  // namespace otedama

@@ -1,0 +1,124 @@
+"""In-tree build of the native extension ``otedama_amd._native``.
+
+HIP sources (gfx950 kernels + the GPU runtime) are compiled with ``hipcc
+--offload-arch=gfx950``; host C++ (SHA-NI SHA-256, scrypt reference, CPU miner,
+pybind11 bindings) with ``g++``; everything links into one shared object next
+to this file, so it travels with the repo snapshot to the GPU box.
+
+Usage: ``python -m otedama_amd._build [-v] [-j N] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "native"
+ARCH = os.environ.get("OTEDAMA_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = [
+    "kernels/sha256d_search.hip",
+    "kernels/scrypt_search.hip",
+    "kernels/x11_search.hip",
+    "runtime/gpu_miner.hip",
+]
+CXX_SOURCES = [
+    "cpu/sha256_cpu.cpp",
+    "cpu/job_prepare.cpp",
+    "cpu/x11_cpu.cpp",
+    "runtime/miner_common.cpp",
+    "bindings.cpp",
+]
+
+
+def ext_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return ROOT / "otedama_amd" / f"_native{suffix}"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build the gfx950 kernels)")
+
+
+def _headers() -> list[Path]:
+    return sorted(p for p in CSRC.rglob("*.h"))
+
+
+def _stale(obj: Path, src: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+
+
+def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
+    import pybind11
+
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    deps = _headers()
+    py_inc = sysconfig.get_paths()["include"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", f"-I{CSRC / 'kernels'}"]
+    tasks: list[list[str]] = []
+    objs: list[Path] = []
+    for rel in HIP_SOURCES:
+        src = CSRC / rel
+        if not src.exists():
+            continue
+        obj = BUILD / (rel.replace("/", "_") + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src, deps):
+            tasks.append([hipcc, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)])
+    for rel in CXX_SOURCES:
+        src = CSRC / rel
+        if not src.exists():
+            continue
+        obj = BUILD / (rel.replace("/", "_") + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src, deps):
+            tasks.append(["g++", *common, "-march=x86-64-v2", f"-I{py_inc}", f"-I{pybind11.get_include()}",
+                          "-fvisibility=hidden", "-c", str(src), "-o", str(obj)])
+    n = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        for f in [ex.submit(_compile, t, verbose) for t in tasks]:
+            f.result()
+    out = ext_path()
+    if force or tasks or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+        tmp = out.with_suffix(".tmp.so")
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread"]
+        _compile(link, verbose)
+        os.replace(tmp, out)
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    p = build(a.verbose, a.jobs, a.force)
+    print(p)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

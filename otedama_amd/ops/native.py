@@ -1,0 +1,60 @@
+"""Loader for the in-tree native extension ``otedama_amd._native``.
+
+The extension is built by ``otedama_amd._build`` (``__graft_entry__.build()``).
+On a machine with a GPU a missing extension is an error, never a silent
+fallback: every GPU op calls :func:`require_native`.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+_err: Exception | None = None
+
+
+def load(build_if_missing: bool = True):
+    """Import (building first if needed) and return the native module."""
+    global _mod, _err
+    with _lock:
+        if _mod is not None:
+            return _mod
+        try:
+            _mod = importlib.import_module("otedama_amd._native")
+            return _mod
+        except ImportError as exc:  # not built yet
+            _err = exc
+        if build_if_missing and os.environ.get("OTEDAMA_NO_AUTOBUILD") != "1":
+            try:
+                from otedama_amd import _build
+
+                _build.build()
+                _mod = importlib.import_module("otedama_amd._native")
+                return _mod
+            except Exception as exc:  # noqa: BLE001 - surfaced by require_native
+                _err = exc
+        return None
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def require_native():
+    mod = load()
+    if mod is None:
+        raise RuntimeError(f"otedama_amd._native is not available (build with `python -m otedama_amd._build`): {_err}")
+    return mod
+
+
+def gpu_count() -> int:
+    """Number of visible HIP devices (0 when the extension or driver is missing)."""
+    mod = load()
+    if mod is None:
+        return 0
+    try:
+        return int(mod.gpu_device_count())
+    except Exception:  # noqa: BLE001
+        return 0

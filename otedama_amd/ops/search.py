@@ -1,0 +1,119 @@
+"""Python-facing launchers for the gfx950 search kernels on torch-owned buffers.
+
+These are the "ops" of the framework: each call enqueues a HIP kernel on the
+current torch stream (so it composes with RCCL collectives issued through
+``torch.distributed`` on the same device) and returns immediately; results are
+read back with :meth:`SearchResult.nonces` after a synchronize.
+
+Kernels (csrc/kernels):
+  * ``otd_sha256d_search``   — SHA-256d nonce search (K1)
+  * ``otd_scrypt_*``         — scrypt N=1024,r=1,p=1 three-stage search (K5)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from otedama_amd.ops.native import require_native
+
+# Blocks of 256 lanes per CU that stay resident for the SHA-256d kernel
+# (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
+SHA256D_BLOCKS_PER_CU = 6
+SCRYPT_BLOCKS_PER_CU = 8
+
+
+def _device_index(device) -> int:
+    d = torch.device(device)
+    return 0 if d.index is None else d.index
+
+
+def default_grid(device, blocks_per_cu: int) -> int:
+    n = require_native()
+    cus = n.gpu_cu_count(_device_index(device)) or 256
+    return cus * blocks_per_cu
+
+
+@dataclass
+class SearchResult:
+    buf: torch.Tensor  # int32 [1 + cap]: count, nonces
+    cap: int
+
+    def count(self) -> int:
+        return int(self.buf[0].item()) & 0xFFFFFFFF
+
+    def nonces(self) -> list[int]:
+        host = self.buf.cpu().tolist()
+        n = min(host[0] & 0xFFFFFFFF, self.cap)
+        return [x & 0xFFFFFFFF for x in host[1 : 1 + n]]
+
+
+class Sha256dSearch:
+    """Reusable SHA-256d search launcher bound to one device."""
+
+    def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None):
+        self.native = require_native()
+        self.device = torch.device(device)
+        self.cap = cap
+        self.grid = grid or default_grid(self.device, SHA256D_BLOCKS_PER_CU)
+        self.out = torch.zeros(1 + cap, dtype=torch.int32, device=self.device)
+
+    def prepare(self, header80: bytes, target32: bytes) -> bytes:
+        return self.native.sha256d_prepare(header80, target32)
+
+    def launch(self, params: bytes, base: int = 0, count: int = 1 << 32, out: torch.Tensor | None = None,
+               stream: torch.cuda.Stream | None = None) -> SearchResult:
+        out = self.out if out is None else out
+        if out.numel() < 1 + self.cap or out.dtype != torch.int32 or out.device != self.device:
+            raise ValueError("out must be an int32 tensor of >= 1+cap elements on the search device")
+        stream = stream or torch.cuda.current_stream(self.device)
+        out[:1].zero_()
+        self.native.launch_sha256d(params, base & 0xFFFFFFFF, int(count), out.data_ptr(), self.cap, self.grid,
+                                   stream.cuda_stream)
+        return SearchResult(out, self.cap)
+
+    def search(self, header80: bytes, target32: bytes, base: int = 0, count: int = 1 << 32) -> list[int]:
+        r = self.launch(self.prepare(header80, target32), base, count)
+        torch.cuda.synchronize(self.device)
+        return r.nonces()
+
+
+class ScryptSearch:
+    """scrypt(1024,1,1) search: PBKDF2-in -> ROMix (HBM scratchpad) -> PBKDF2-out."""
+
+    def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, gap: int = 1,
+                 lanes_per_slot: int = 1):
+        self.native = require_native()
+        self.device = torch.device(device)
+        self.cap = cap
+        self.gap = gap
+        self.grid = grid or default_grid(self.device, SCRYPT_BLOCKS_PER_CU)
+        self.batch = self.grid * 256 * lanes_per_slot
+        nbytes = self.native.scrypt_scratch_bytes(self.grid, gap)
+        self.scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self.xbuf = torch.empty(self.batch * 128, dtype=torch.uint8, device=self.device)
+        self.out = torch.zeros(1 + cap, dtype=torch.int32, device=self.device)
+
+    @property
+    def scratch_bytes(self) -> int:
+        return self.scratch.numel()
+
+    def prepare(self, header80: bytes, target32: bytes) -> bytes:
+        return self.native.scrypt_prepare(header80, target32)
+
+    def launch(self, params: bytes, base: int = 0, count: int | None = None,
+               stream: torch.cuda.Stream | None = None) -> SearchResult:
+        count = self.batch if count is None else count
+        if not 0 < count <= self.batch:
+            raise ValueError(f"count must be in [1, {self.batch}]")
+        stream = stream or torch.cuda.current_stream(self.device)
+        self.out[:1].zero_()
+        self.native.launch_scrypt(params, base & 0xFFFFFFFF, int(count), self.xbuf.data_ptr(),
+                                  self.scratch.data_ptr(), self.gap, self.out.data_ptr(), self.cap, self.grid,
+                                  stream.cuda_stream)
+        return SearchResult(self.out, self.cap)
+
+    def search(self, header80: bytes, target32: bytes, base: int = 0, count: int | None = None) -> list[int]:
+        r = self.launch(self.prepare(header80, target32), base, count)
+        torch.cuda.synchronize(self.device)
+        return r.nonces()

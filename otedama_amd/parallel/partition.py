@@ -1,0 +1,38 @@
+"""Search-space partitioning across ranks and devices.
+
+The search index is hierarchical: ``variant ‖ nonce32`` where a variant is one
+(extranonce2, BIP320 version bits, ntime offset) combination with its own
+midstate. Every device owns a disjoint variant stripe
+``v = g, g + G, g + 2G, ...`` (g = global device index, G = devices in the
+node), so no per-nonce coordination ever crosses a GPU boundary.
+
+The reference instead hands every device the identical Work
+(internal/engine/run.go:1294-1296) and wraps the nonce at 2^32
+(internal/miner/worker.go:279) — both defects are fixed here.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Stripe:
+    start: int
+    stride: int
+
+    def variants(self, n: int) -> list[int]:
+        return [self.start + k * self.stride for k in range(n)]
+
+
+def stripe_for(rank: int, world_size: int, device_index: int = 0, devices_per_rank: int = 1) -> Stripe:
+    if not 0 <= rank < world_size or not 0 <= device_index < devices_per_rank:
+        raise ValueError("rank/device out of range")
+    total = world_size * devices_per_rank
+    return Stripe(rank * devices_per_rank + device_index, total)
+
+
+def apply_stripe(job: dict, stripe: Stripe) -> dict:
+    out = dict(job)
+    out["variant_start"] = stripe.start
+    out["variant_stride"] = stripe.stride
+    return out

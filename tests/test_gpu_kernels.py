@@ -1,0 +1,150 @@
+"""gfx950 kernels vs the CPU oracle (run on a real MI355X via gpurun).
+
+Numerics for an integer hash kernel are exact: the set of nonces a kernel
+reports for a target must equal the set the CPU (hashlib / C++ reference)
+computes for the same header window.
+"""
+import hashlib
+import os
+import struct
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _native():
+    from otedama_amd.ops.native import require_native
+
+    return require_native()
+
+
+def _ref_hits_sha256d(hdr, base, count, target_int):
+    out = []
+    for n in range(base, base + count):
+        h = hashlib.sha256(hashlib.sha256(hdr[:76] + struct.pack("<I", n & 0xFFFFFFFF)).digest()).digest()
+        if int.from_bytes(h, "little") <= target_int:
+            out.append(n & 0xFFFFFFFF)
+    return out
+
+
+def test_native_gpu_visible():
+    N = _native()
+    assert N.gpu_device_count() >= 1
+    assert N.gpu_arch_name(0).startswith("gfx950")
+
+
+def test_sha256d_genesis_nonce():
+    from otedama_amd.models.header import GENESIS_HEADER_HEX, int_to_hash
+    from otedama_amd.ops.search import Sha256dSearch
+
+    hdr = bytes.fromhex(GENESIS_HEADER_HEX)
+    s = Sha256dSearch("cuda:0")
+    nonce = 2083236893
+    assert s.search(hdr, int_to_hash(0xFFFF << 208), nonce - 1000, 5000) == [nonce]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sha256d_matches_cpu_easy_target(seed):
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import Sha256dSearch
+
+    rng = __import__("random").Random(seed)
+    hdr = bytes(rng.getrandbits(8) for _ in range(76)) + bytes(4)
+    target_int = (1 << 248) - 1  # ~1/256 hit rate -> ~256 hits in 65536
+    s = Sha256dSearch("cuda:0", cap=4096)
+    base = rng.getrandbits(32) & ~0xFFFF
+    got = sorted(s.search(hdr, int_to_hash(target_int), base, 1 << 16))
+    N = _native()
+    ref = sorted(N.cpu_scan_sha256d(hdr, int_to_hash(target_int), base, 1 << 16))
+    assert got == ref and len(ref) > 100
+    # spot-check against hashlib too
+    assert ref[:20] == _ref_hits_sha256d(hdr, base, ref[19] - base + 1, target_int)[:20]
+
+
+def test_sha256d_target_hi_tie_filtered_by_host():
+    """Kernel compares only the top word; a target whose top word ties must still
+    produce only hits that the full compare accepts (host re-verification)."""
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import Sha256dSearch
+
+    hdr = os.urandom(76) + bytes(4)
+    target_int = (0x00FFFFFF << 224) | 0x1  # top word 0x00ffffff, low bits tiny
+    s = Sha256dSearch("cuda:0", cap=4096)
+    cands = s.search(hdr, int_to_hash(target_int), 0, 1 << 16)
+    N = _native()
+    strict = N.cpu_scan_sha256d(hdr, int_to_hash(target_int), 0, 1 << 16)
+    assert set(strict) <= set(cands)
+
+
+def test_sha256d_wraps_nonce_space():
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import Sha256dSearch
+
+    hdr = os.urandom(76) + bytes(4)
+    t = int_to_hash((1 << 250) - 1)
+    s = Sha256dSearch("cuda:0", cap=4096)
+    got = sorted(s.search(hdr, t, 0xFFFFF000, 0x2000))
+    N = _native()
+    ref = sorted(N.cpu_scan_sha256d(hdr, t, 0xFFFFF000, 0x1000) + N.cpu_scan_sha256d(hdr, t, 0, 0x1000))
+    assert got == ref
+
+
+@pytest.mark.parametrize("gap", [1, 2, 4])
+def test_scrypt_matches_hashlib(gap):
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import ScryptSearch
+
+    hdr = os.urandom(76) + bytes(4)
+    sc = ScryptSearch("cuda:0", grid=8, gap=gap, cap=1024)
+    n = 192
+    # target: ~1/4 of hashes pass -> checks filtering as well as hashing
+    target_int = (1 << 254) - 1
+    got = sorted(sc.search(hdr, int_to_hash(target_int), 5000, n))
+    ref = []
+    for nonce in range(5000, 5000 + n):
+        h80 = hdr[:76] + struct.pack("<I", nonce)
+        d = hashlib.scrypt(h80, salt=h80, n=1024, r=1, p=1, dklen=32)
+        if int.from_bytes(d, "little") <= target_int:
+            ref.append(nonce)
+    assert got == ref and 0 < len(ref) < n
+
+
+def test_scrypt_more_lanes_than_slots():
+    """count > grid*256 exercises the grid-stride reuse of a scratchpad slot."""
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import ScryptSearch
+
+    hdr = os.urandom(76) + bytes(4)
+    sc = ScryptSearch("cuda:0", grid=1, gap=1, lanes_per_slot=2, cap=1024)
+    got = sorted(sc.search(hdr, int_to_hash((1 << 256) - 1), 0, 512))
+    assert got == list(range(512))
+
+
+def test_gpu_miner_runtime_shares():
+    from otedama_amd.models.header import int_to_hash
+
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    tgt = int_to_hash((1 << 232) - 1)  # ~1 per 2^24
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28)
+    m.set_job({"header": hdr, "target": tgt, "epoch": 3, "job_id": "j1", "version_mask": 0x1FFFE000})
+    m.start()
+    deadline = time.time() + 20
+    shares = []
+    while time.time() < deadline and len(shares) < 20:
+        shares += m.poll(256)
+        time.sleep(0.02)
+    m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["hashes"] >= 1 << 28
+    assert len(shares) >= 5, st
+    for s in shares:
+        h80 = bytearray(hdr)
+        struct.pack_into("<I", h80, 0, s["version"])
+        struct.pack_into("<I", h80, 76, s["nonce"])
+        d = hashlib.sha256(hashlib.sha256(bytes(h80)).digest()).digest()
+        assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
+        assert s["epoch"] == 3 and s["job_id"] == "j1"

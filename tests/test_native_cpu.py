@@ -1,0 +1,145 @@
+"""Native host code (C++ SHA-NI SHA-256, scrypt reference, job variants, CPU miner)
+against Python hashlib oracles. Runs without a GPU."""
+import hashlib
+import os
+import struct
+import time
+
+import pytest
+
+from otedama_amd.models.header import GENESIS_HEADER_HEX, int_to_hash, sha256d
+from otedama_amd.ops.native import require_native
+
+N = require_native()
+GEN = bytes.fromhex(GENESIS_HEADER_HEX)
+
+
+@pytest.mark.parametrize("n", [0, 1, 55, 56, 63, 64, 65, 80, 119, 120, 128, 1000])
+def test_sha256_lengths(n):
+    data = os.urandom(n)
+    assert N.sha256(data) == hashlib.sha256(data).digest()
+    assert N.sha256d(data) == sha256d(data)
+
+
+def test_hmac_matches_stdlib():
+    import hmac
+
+    for klen in (0, 5, 64, 80, 100):
+        k = os.urandom(klen)
+        m = os.urandom(77)
+        assert N.hmac_sha256(k, m) == hmac.new(k, m, hashlib.sha256).digest()
+
+
+def test_scrypt_reference_matches_hashlib():
+    for _ in range(3):
+        h = os.urandom(80)
+        assert N.scrypt_1024_1_1(h) == hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32)
+
+
+def test_cpu_scan_finds_genesis_nonce():
+    nonce = 2083236893
+    tgt = int_to_hash(0xFFFF << 208)
+    assert N.cpu_scan_sha256d(GEN, tgt, nonce - 500, 1000) == [nonce]
+
+
+def test_cpu_scan_matches_python_on_easy_target():
+    hdr = os.urandom(76) + bytes(4)
+    tgt = int_to_hash((1 << 248) - 1)  # ~1/256 of nonces
+    hits = N.cpu_scan_sha256d(hdr, tgt, 1000, 4096)
+    ref = [n for n in range(1000, 1000 + 4096)
+           if int.from_bytes(sha256d(hdr[:76] + struct.pack("<I", n)), "little") <= int.from_bytes(tgt, "little")]
+    assert hits == ref
+
+
+def test_cpu_single_thread_beats_reference():
+    # reference single-thread claim: ~2.5 MH/s (BENCHMARKS.md:25); SHA-NI + midstate
+    if not N.cpu_has_sha_ni():
+        pytest.skip("no SHA-NI on this CPU")
+    t0 = time.perf_counter()
+    N.cpu_scan_sha256d(GEN, bytes(32), 0, 500_000)
+    rate = 500_000 / (time.perf_counter() - t0)
+    assert rate > 1.0e6
+
+
+def _job(**kw):
+    j = {"header": GEN, "target": int_to_hash(0xFFFF << 208), "epoch": 1, "job_id": "1"}
+    j.update(kw)
+    return j
+
+
+def test_variant_version_rolling_bits():
+    mask = 0x1FFFE000
+    j = _job(version_mask=mask)
+    assert N.variant_space(j) == 1 << 16
+    seen = set()
+    for v in range(64):
+        hdr, ver, nt, en2 = N.variant_header(j, v)
+        assert ver & ~mask == 1 & ~mask
+        assert struct.unpack_from("<I", hdr, 0)[0] == ver
+        seen.add(ver)
+    assert len(seen) == 64
+
+
+def test_variant_ntime_rolling():
+    j = _job(ntime_roll=10)
+    assert N.variant_space(j) == 11
+    base = struct.unpack_from("<I", GEN, 68)[0]
+    for v in range(11):
+        hdr, ver, nt, en2 = N.variant_header(j, v)
+        assert nt == base + v
+        assert struct.unpack_from("<I", hdr, 68)[0] == nt
+
+
+def test_merkle_root_from_coinbase_matches_python():
+    coinb1, coinb2, en1 = os.urandom(40), os.urandom(50), bytes.fromhex("f8002c90")
+    branches = [os.urandom(32) for _ in range(3)]
+    j = _job(coinb1=coinb1, coinb2=coinb2, extranonce1=en1, extranonce2_size=4, merkle_branches=branches)
+    for en2 in (0, 1, 0xDEADBEEF):
+        cb = coinb1 + en1 + en2.to_bytes(4, "little") + coinb2
+        root = sha256d(cb)
+        for b in branches:
+            root = sha256d(root + b)
+        assert N.merkle_root(j, en2) == root
+        hdr, _, _, got_en2 = N.variant_header(j, en2)
+        assert hdr[36:68] == root and got_en2 == en2
+    assert N.variant_space(j) == 1 << 32
+
+
+def test_prepare_sizes():
+    assert len(N.sha256d_prepare(GEN, bytes(32))) == N.SHA256D_PARAMS_SIZE
+    assert len(N.scrypt_prepare(GEN, bytes(32))) == N.SCRYPT_PARAMS_SIZE
+
+
+def test_cpu_miner_runtime_emits_verified_shares():
+    m = N.CpuMiner(2, "cpu-0")
+    tgt = int_to_hash((1 << 244) - 1)
+    m.set_job(_job(target=tgt, version_mask=0x1FFFE000, epoch=7, job_id="abc"))
+    m.start()
+    deadline = time.time() + 5
+    shares = []
+    while time.time() < deadline and len(shares) < 5:
+        shares += m.poll(64)
+        time.sleep(0.05)
+    m.stop()
+    st = m.stats()
+    assert st["hashes"] > 0
+    assert shares, st
+    for s in shares:
+        hdr = bytearray(GEN)
+        struct.pack_into("<I", hdr, 0, s["version"])
+        struct.pack_into("<I", hdr, 76, s["nonce"])
+        h = sha256d(bytes(hdr))
+        assert h == s["hash"]
+        assert int.from_bytes(h, "little") <= int.from_bytes(tgt, "little")
+        assert s["epoch"] == 7 and s["job_id"] == "abc" and s["device_id"] == "cpu-0"
+
+
+def test_cpu_miner_pause_with_none_job():
+    m = N.CpuMiner(1, "cpu-0")
+    m.start()
+    m.set_job(None)
+    time.sleep(0.05)
+    h0 = m.stats()["hashes"]
+    time.sleep(0.1)
+    assert m.stats()["hashes"] == h0
+    m.stop()
