@@ -103,6 +103,10 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     out = ext_path()
     if force or tasks or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         tmp = out.with_suffix(".tmp.so")
+        # DT_NEEDED is the sonames libamdhip64.so.7 / libhsa-runtime64.so.1,
+        # which torch's bundled runtime also carries: ops.native imports torch
+        # first, so the extension binds to the runtime already in the process
+        # (two HIP/HSA runtimes in one process fail to enumerate the GPU).
         link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread"]
         _compile(link, verbose)
         os.replace(tmp, out)

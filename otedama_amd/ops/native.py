@@ -21,6 +21,15 @@ def load(build_if_missing: bool = True):
     with _lock:
         if _mod is not None:
             return _mod
+        # torch must load its bundled HIP runtime BEFORE the extension: the
+        # extension's libamdhip64.so.7 / libhsa-runtime64.so.1 needs are then
+        # satisfied by torch's copies (same sonames). Loading the extension
+        # first pulls /opt/rocm's runtime and torch then adds a second one, and
+        # two HSA runtimes in one process cannot both enumerate the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         try:
             _mod = importlib.import_module("otedama_amd._native")
             return _mod
