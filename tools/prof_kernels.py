@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""Fixed workload for rocprofv3: SHA-256d full-range launches + scrypt batches."""
+import sys
+
+import torch
+
+from otedama_amd.ops.native import require_native
+from otedama_amd.ops.search import ScryptSearch, Sha256dSearch
+
+algo = sys.argv[1] if len(sys.argv) > 1 else "both"
+N = require_native()
+hdr = bytes(range(76)) + bytes(4)
+tgt = bytes(28) + b"\xff\xff\x00\x00"
+if algo in ("both", "sha256d"):
+    s = Sha256dSearch("cuda:0")
+    p = N.sha256d_prepare(hdr, tgt)
+    for _ in range(3):
+        s.launch(p, 0, 1 << 32)
+    torch.cuda.synchronize()
+if algo in ("both", "scrypt"):
+    gap = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    sc = ScryptSearch("cuda:0", gap=gap)
+    sp = N.scrypt_prepare(hdr, tgt)
+    for i in range(4):
+        sc.launch(sp, i * sc.batch)
+    torch.cuda.synchronize()
+print("done")
