@@ -1,0 +1,561 @@
+"""Local Stratum pool: SV2 + V1 listeners, job lifecycle, share validation,
+vardiff, duplicate / stale detection, share journal, block payouts.
+
+[NO REFERENCE CODE] — the reference v3 is a client only ("Pool operator mode"
+removed, CHANGELOG.md:6623-6624). Wire formats follow the
+reference encoders (stratum/messages.go, handshake.go) so
+the reference client and this framework's client can both mine against it,
+and — unlike the reference's test fakes (engine/integration_test.go:23-209,
+run_test.go:32-166) — every share is re-hashed and validated.
+
+Validation of a submitted share:
+  1. job known and from the current block            else "stale-job"
+  2. version only differs inside the negotiated BIP320 mask   "invalid-version-bits"
+  3. ntime in [job ntime, now + 2h]                           "invalid-ntime"
+  4. (job, extranonce, ntime, nonce, version) not seen yet    "duplicate-share"
+  5. header hash (sha256d or scrypt) <= share target
+     (current difficulty, or the previous one within 10 s of a retarget)
+                                                              "low-difficulty-share"
+  6. hash <= network target (nBits) -> block found: PPLNS payouts, new block
+The reject strings land in the engine's reject taxonomy (engine/stats.go:263-277).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import struct
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+
+from otedama_amd.metrics import Registry
+from otedama_amd.models import algorithms
+from otedama_amd.models.header import hash_to_int, target_from_difficulty, target_from_nbits
+from otedama_amd.pool.journal import Journal, ShareRow
+from otedama_amd.pool.template import BlockTemplate, TemplateSource, merkle_root_from_branches
+from otedama_amd.pool.vardiff import Vardiff, VardiffConfig, VardiffState
+from otedama_amd.poolproto.stratumv1 import prevhash_to_stratum
+from otedama_amd.stratum import messages as M
+from otedama_amd.stratum.frame import read_frame_async
+
+BIP320_MASK = 0x1FFFE000
+EN1_SIZE = 4
+EN2_SIZE = 4
+MAX_NTIME_FUTURE = 7200
+RETARGET_GRACE = 10.0
+
+
+@dataclass
+class PoolOptions:
+    algorithm: str = "sha256d"
+    listen_sv2: str = "127.0.0.1:0"
+    listen_v1: str = "127.0.0.1:0"
+    payout_address: str | None = None
+    initial_difficulty: float = 1.0
+    target_share_seconds: float = 10.0
+    retarget_seconds: float = 30.0
+    min_difficulty: float = 1e-6
+    nbits: int = 0x1703A30C
+    n_txs: int = 7
+    job_interval: float = 30.0
+    block_interval: float = 600.0
+    journal_path: str = ":memory:"
+    payout_scheme: str = "pplns"
+    coinbase_message: str = "/otedama-mi355x/"
+    dialect: str = M.REFERENCE
+    allow_version_rolling: bool = True
+
+
+@dataclass
+class PoolJob:
+    job_int: int
+    block: BlockTemplate
+    version: int
+    ntime: int
+    coinb1: bytes
+    coinb2: bytes
+    branches: list[bytes]
+    clean: bool
+    created: float = field(default_factory=time.time)
+
+    @property
+    def job_id(self) -> str:
+        return f"{self.job_int:x}"
+
+
+@dataclass
+class Verdict:
+    accepted: bool
+    reason: str = ""
+    difficulty: float = 0.0
+    hash: bytes = b""
+    block: bool = False
+
+
+class _Worker:
+    def __init__(self, name: str, vd: VardiffState, version_mask: int):
+        self.name = name
+        self.vd = vd
+        self.prev_difficulty = vd.difficulty
+        self.retarget_at = 0.0
+        self.version_mask = version_mask
+        self.accepted = 0
+        self.rejected = 0
+
+
+class PoolServer:
+    def __init__(self, opts: PoolOptions | None = None, registry: Registry | None = None, log=None):
+        self.opts = opts or PoolOptions()
+        self.algo = algorithms.get(self.opts.algorithm)
+        self.log = log or (lambda level, msg: None)
+        self.templates = TemplateSource(self.opts.payout_address, nbits=self.opts.nbits, n_txs=self.opts.n_txs,
+                                        coinbase_message=self.opts.coinbase_message)
+        self.vardiff = Vardiff(VardiffConfig(target_share_seconds=self.opts.target_share_seconds,
+                                             retarget_seconds=self.opts.retarget_seconds,
+                                             min_difficulty=self.opts.min_difficulty),
+                               diff1_hashes=float(2 ** 256) / self.algo.diff1)
+        self.journal = Journal(self.opts.journal_path)
+        self.block: BlockTemplate | None = None
+        self.jobs: "OrderedDict[str, PoolJob]" = OrderedDict()
+        self._job_counter = 0
+        self._seen: set = set()
+        self._en_counter = int.from_bytes(os.urandom(2), "little") << 16
+        self._v1: set[_V1Conn] = set()
+        self._v2: set[_V2Conn] = set()
+        self._servers: list[asyncio.base_events.Server] = []
+        self._tasks: list[asyncio.Task] = []
+        self.addr_sv2 = ""
+        self.addr_v1 = ""
+        self.blocks_found = 0
+        self.accepted = 0
+        self.rejected = 0
+        self.reject_reasons: dict[str, int] = {}
+        self._init_metrics(registry)
+
+    # ------------------------------------------------------------ metrics
+    def _init_metrics(self, reg: Registry | None) -> None:
+        self.registry = reg or Registry()
+        lab = {"algo": self.algo.name}
+        r = self.registry
+        self.m_accepted = r.new_counter("otedama_pool_shares_total", "Shares validated by the local pool.",
+                                        {**lab, "status": "accepted"})
+        self.m_rejected = r.new_counter("otedama_pool_shares_total", "Shares validated by the local pool.",
+                                        {**lab, "status": "rejected"})
+        self.m_blocks = r.new_counter("otedama_pool_blocks_found_total", "Blocks found by the local pool.", lab)
+        self.m_clients = r.new_gauge("otedama_pool_connected_clients", "Connected miners.", lab)
+        self.m_hashrate = r.new_gauge("otedama_pool_hashrate_hashes_per_second",
+                                      "Pool hashrate estimated from accepted share work.", lab)
+        self.m_work = r.new_counter("otedama_pool_accepted_work_total",
+                                    "Sum of accepted share difficulties.", lab)
+        self._work_t0 = time.monotonic()
+        self._work_sum = 0.0
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self) -> None:
+        self.new_block()
+        if self.opts.listen_sv2:
+            h, p = _split(self.opts.listen_sv2)
+            srv = await asyncio.start_server(self._serve_v2, h, p)
+            self._servers.append(srv)
+            a = srv.sockets[0].getsockname()
+            self.addr_sv2 = f"{a[0]}:{a[1]}"
+        if self.opts.listen_v1:
+            h, p = _split(self.opts.listen_v1)
+            srv = await asyncio.start_server(self._serve_v1, h, p, limit=64 * 1024)
+            self._servers.append(srv)
+            a = srv.sockets[0].getsockname()
+            self.addr_v1 = f"{a[0]}:{a[1]}"
+        self._tasks.append(asyncio.ensure_future(self._refresh_loop()))
+        self.log("info", f"pool[{self.algo.name}]: listening sv2={self.addr_sv2 or '-'} v1={self.addr_v1 or '-'}")
+
+    async def stop(self) -> None:
+        for t in self._tasks:
+            t.cancel()
+        for s in self._servers:
+            s.close()
+        for c in list(self._v1) + list(self._v2):
+            c.close()
+        for s in self._servers:
+            try:
+                await asyncio.wait_for(s.wait_closed(), 2)
+            except asyncio.TimeoutError:
+                pass
+        self.journal.close()
+
+    async def _refresh_loop(self) -> None:
+        last_block = time.monotonic()
+        while True:
+            await asyncio.sleep(min(self.opts.job_interval, self.opts.block_interval))
+            if time.monotonic() - last_block >= self.opts.block_interval:
+                last_block = time.monotonic()
+                self.new_block()
+            else:
+                self.new_job(clean=False)
+            self._update_hashrate()
+
+    def _update_hashrate(self) -> None:
+        dt = time.monotonic() - self._work_t0
+        if dt > 0:
+            self.m_hashrate.set(self._work_sum * self.vardiff.diff1_hashes / dt)
+        self._work_t0, self._work_sum = time.monotonic(), 0.0
+
+    # ------------------------------------------------------------ jobs
+    def new_block(self) -> PoolJob:
+        self.block = self.templates.next_block()
+        self.jobs.clear()
+        self._seen.clear()
+        job = self._make_job(clean=True)
+        self.log("info", f"pool[{self.algo.name}]: new block height={self.block.height}")
+        return job
+
+    def new_job(self, clean: bool = False) -> PoolJob:
+        return self._make_job(clean)
+
+    def _make_job(self, clean: bool) -> PoolJob:
+        assert self.block is not None
+        self._job_counter += 1
+        coinb1, coinb2 = self.block.coinbase_parts(EN1_SIZE + EN2_SIZE)
+        job = PoolJob(self._job_counter, self.block, self.block.version, max(int(time.time()), self.block.ntime),
+                      coinb1, coinb2, self.block.branches(), clean)
+        self.jobs[job.job_id] = job
+        while len(self.jobs) > 16:
+            self.jobs.popitem(last=False)
+        for c in list(self._v1):
+            c.send_job(job)
+        for c in list(self._v2):
+            c.send_job(job)
+        return job
+
+    def next_extranonce(self, size: int) -> bytes:
+        self._en_counter += 1
+        return (self._en_counter & ((1 << (8 * size)) - 1)).to_bytes(size, "big")
+
+    def header_for(self, job: PoolJob, extranonce: bytes, version: int, ntime: int, nonce: int) -> bytes:
+        coinbase = job.coinb1 + extranonce + job.coinb2
+        from otedama_amd.models.header import sha256d
+
+        root = merkle_root_from_branches(sha256d(coinbase), job.branches)
+        return (struct.pack("<I", version & 0xFFFFFFFF) + job.block.prev_hash + root
+                + struct.pack("<III", ntime & 0xFFFFFFFF, job.block.nbits, nonce & 0xFFFFFFFF))
+
+    def merkle_root_for(self, job: PoolJob, extranonce: bytes) -> bytes:
+        from otedama_amd.models.header import sha256d
+
+        return merkle_root_from_branches(sha256d(job.coinb1 + extranonce + job.coinb2), job.branches)
+
+    # ------------------------------------------------------------ validation
+    def validate(self, worker: _Worker, job_id: str, extranonce: bytes, ntime: int, nonce: int,
+                 version: int) -> Verdict:
+        job = self.jobs.get(job_id)
+        if job is None or job.block is not self.block:
+            return self._reject(worker, job_id, "stale-job")
+        if (version ^ job.version) & ~worker.version_mask & 0xFFFFFFFF:
+            return self._reject(worker, job_id, "invalid-version-bits")
+        if ntime < job.ntime or ntime > max(time.time(), job.ntime) + MAX_NTIME_FUTURE:
+            return self._reject(worker, job_id, "invalid-ntime")
+        key = (job_id, extranonce, ntime, nonce, version)
+        if key in self._seen:
+            return self._reject(worker, job_id, "duplicate-share")
+        hdr = self.header_for(job, extranonce, version, ntime, nonce)
+        h = self.algo.hash(hdr)
+        hv = hash_to_int(h)
+        diff = worker.vd.difficulty
+        if hv > hash_to_int(target_from_difficulty(diff, self.algo.diff1)):
+            grace = time.monotonic() - worker.retarget_at < RETARGET_GRACE
+            if grace and hv <= hash_to_int(target_from_difficulty(worker.prev_difficulty, self.algo.diff1)):
+                diff = worker.prev_difficulty
+            else:
+                return self._reject(worker, job_id, "low-difficulty-share", h)
+        self._seen.add(key)
+        is_block = hv <= hash_to_int(target_from_nbits(job.block.nbits))
+        worker.accepted += 1
+        self.accepted += 1
+        self.m_accepted.inc()
+        self.m_work.add(int(diff)) if diff >= 1 else None
+        self._work_sum += diff
+        self.journal.append(ShareRow(time.time(), worker.name, self.algo.name, job_id, diff, True, "", h[::-1].hex(),
+                                     is_block))
+        if is_block:
+            self.blocks_found += 1
+            self.m_blocks.inc()
+            pay = self.journal.record_block(job.block.height, h[::-1].hex(), worker.name, job.block.coinbase_value,
+                                            self.opts.payout_scheme)
+            self.log("info", f"pool[{self.algo.name}]: BLOCK FOUND height={job.block.height} by {worker.name} "
+                             f"payouts={json.dumps(pay)}")
+            asyncio.get_event_loop().call_soon(self.new_block)
+        return Verdict(True, "", diff, h, is_block)
+
+    def _reject(self, worker: _Worker, job_id: str, reason: str, h: bytes = b"") -> Verdict:
+        worker.rejected += 1
+        self.rejected += 1
+        self.reject_reasons[reason] = self.reject_reasons.get(reason, 0) + 1
+        self.m_rejected.inc()
+        self.journal.append(ShareRow(time.time(), worker.name, self.algo.name, job_id, worker.vd.difficulty, False,
+                                     reason, h[::-1].hex() if h else ""))
+        return Verdict(False, reason, 0.0, h)
+
+    def new_worker(self, name: str, version_mask: int) -> _Worker:
+        d = self.journal.load_worker(name) or self.opts.initial_difficulty
+        return _Worker(name, self.vardiff.new_state(d), version_mask)
+
+    def after_accept(self, w: _Worker) -> float | None:
+        old = w.vd.difficulty
+        new = self.vardiff.on_share(w.vd)
+        if new is not None:
+            w.prev_difficulty, w.retarget_at = old, time.monotonic()
+            self.journal.save_worker(w.name, new)
+        return new
+
+    def stats(self) -> dict:
+        return {
+            "algorithm": self.algo.name, "height": self.block.height if self.block else 0,
+            "clients_v1": len(self._v1), "clients_v2": len(self._v2), "accepted": self.accepted,
+            "rejected": self.rejected, "reject_reasons": dict(self.reject_reasons), "blocks_found": self.blocks_found,
+            "hashrate": self.m_hashrate.value(), "sv2": self.addr_sv2, "v1": self.addr_v1,
+        }
+
+    # ------------------------------------------------------------ listeners
+    async def _serve_v1(self, reader, writer) -> None:
+        c = _V1Conn(self, reader, writer)
+        self._v1.add(c)
+        self.m_clients.set(len(self._v1) + len(self._v2))
+        try:
+            await c.run()
+        finally:
+            self._v1.discard(c)
+            self.m_clients.set(len(self._v1) + len(self._v2))
+
+    async def _serve_v2(self, reader, writer) -> None:
+        c = _V2Conn(self, reader, writer)
+        self._v2.add(c)
+        self.m_clients.set(len(self._v1) + len(self._v2))
+        try:
+            await c.run()
+        finally:
+            self._v2.discard(c)
+            self.m_clients.set(len(self._v1) + len(self._v2))
+
+
+def _split(addr: str) -> tuple[str, int]:
+    h, _, p = addr.rpartition(":")
+    return h or "0.0.0.0", int(p or 0)
+
+
+class _V1Conn:
+    """One Stratum V1 miner connection (JSON-RPC lines)."""
+
+    def __init__(self, pool: PoolServer, reader, writer):
+        self.pool, self.reader, self.writer = pool, reader, writer
+        self.en1 = pool.next_extranonce(EN1_SIZE)
+        self.subscribed = False
+        self.authorized = False
+        self.version_mask = 0
+        self.worker: _Worker | None = None
+
+    def close(self) -> None:
+        try:
+            self.writer.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _write(self, obj) -> None:
+        try:
+            self.writer.write(json.dumps(obj).encode() + b"\n")
+        except Exception:  # noqa: BLE001
+            pass
+
+    def send_job(self, job: PoolJob) -> None:
+        if not (self.subscribed and self.authorized):
+            return
+        self._write({"id": None, "method": "mining.notify", "params": [
+            job.job_id, prevhash_to_stratum(job.block.prev_hash), job.coinb1.hex(), job.coinb2.hex(),
+            [b.hex() for b in job.branches], f"{job.version:08x}", f"{job.block.nbits:08x}", f"{job.ntime:08x}",
+            job.clean]})
+
+    def _send_difficulty(self) -> None:
+        self._write({"id": None, "method": "mining.set_difficulty", "params": [self.worker.vd.difficulty]})
+
+    async def run(self) -> None:
+        try:
+            while True:
+                line = await asyncio.wait_for(self.reader.readuntil(b"\n"), 600)
+                try:
+                    msg = json.loads(line)
+                except ValueError:
+                    continue
+                if isinstance(msg, dict):
+                    await self._handle(msg)
+        except (asyncio.IncompleteReadError, asyncio.LimitOverrunError, asyncio.TimeoutError, ConnectionError,
+                OSError):
+            pass
+        finally:
+            self.close()
+
+    async def _handle(self, msg: dict) -> None:
+        mid, method, params = msg.get("id"), msg.get("method"), msg.get("params") or []
+        if method == "mining.configure":
+            res = {}
+            exts = params[0] if params and isinstance(params[0], list) else []
+            if "version-rolling" in exts and self.pool.opts.allow_version_rolling:
+                req = params[1].get("version-rolling.mask", "ffffffff") if len(params) > 1 and isinstance(
+                    params[1], dict) else "ffffffff"
+                self.version_mask = int(req, 16) & BIP320_MASK
+                res = {"version-rolling": True, "version-rolling.mask": f"{self.version_mask:08x}"}
+            self._write({"id": mid, "result": res, "error": None})
+        elif method == "mining.subscribe":
+            self.subscribed = True
+            self._write({"id": mid, "result": [[["mining.notify", self.en1.hex()]], self.en1.hex(), EN2_SIZE],
+                         "error": None})
+        elif method == "mining.authorize":
+            user = params[0] if params and isinstance(params[0], str) else ""
+            if not user:
+                self._write({"id": mid, "result": False, "error": [24, "unauthorized worker", None]})
+                return
+            self.authorized = True
+            self.worker = self.pool.new_worker(user, self.version_mask)
+            self._write({"id": mid, "result": True, "error": None})
+            self._send_difficulty()
+            if self.pool.jobs:
+                self.send_job(next(reversed(self.pool.jobs.values())))
+        elif method in ("mining.extranonce.subscribe", "extranonce.subscribe"):
+            self._write({"id": mid, "result": True, "error": None})
+        elif method == "mining.submit":
+            if not self.authorized or self.worker is None:
+                self._write({"id": mid, "result": None, "error": [24, "unauthorized worker", None]})
+                return
+            try:
+                _w, job_id, en2_hex, ntime_hex, nonce_hex = params[:5]
+                en2 = bytes.fromhex(en2_hex)
+                ntime, nonce = int(ntime_hex, 16), int(nonce_hex, 16)
+                job = self.pool.jobs.get(str(job_id))
+                base_version = job.version if job else 0
+                # BIP310: version = (job_version & ~mask) | (version_bits & mask); bits outside
+                # the mask make the version differ from the job outside the mask -> rejected.
+                vbits = int(params[5], 16) if len(params) > 5 and params[5] else None
+                if vbits is None:
+                    version = base_version
+                elif vbits & ~self.version_mask & 0xFFFFFFFF:
+                    version = base_version ^ (vbits & ~self.version_mask)
+                else:
+                    version = (base_version & ~self.version_mask) | vbits
+                if len(en2) != EN2_SIZE:
+                    raise ValueError("bad extranonce2 size")
+            except (ValueError, TypeError, IndexError):
+                self._write({"id": mid, "result": None, "error": [20, "invalid submit parameters", None]})
+                return
+            v = self.pool.validate(self.worker, str(job_id), self.en1 + en2, ntime, nonce, version)
+            if v.accepted:
+                self._write({"id": mid, "result": True, "error": None})
+                if self.pool.after_accept(self.worker) is not None:
+                    self._send_difficulty()
+            else:
+                code = {"stale-job": 21, "duplicate-share": 22, "low-difficulty-share": 23}.get(v.reason, 20)
+                self._write({"id": mid, "result": None, "error": [code, v.reason, None]})
+        elif mid is not None:
+            self._write({"id": mid, "result": None, "error": [20, f"unknown method {method}", None]})
+
+
+class _V2Conn:
+    """One Stratum V2 miner connection (standard channels)."""
+
+    def __init__(self, pool: PoolServer, reader, writer):
+        self.pool, self.reader, self.writer = pool, reader, writer
+        self.dialect = pool.opts.dialect
+        self.version_rolling = False
+        self.channels: dict[int, tuple[_Worker, bytes]] = {}  # channel id -> (worker, extranonce prefix)
+        self._next_channel = 1
+        self.setup = False
+
+    def close(self) -> None:
+        try:
+            self.writer.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _send(self, msg: M.Message) -> None:
+        try:
+            self.writer.write(M.encode_message(msg, self.dialect))
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _job_msgs(self, ch: int, job: PoolJob, prefix: bytes, future: bool) -> list[M.Message]:
+        root = self.pool.merkle_root_for(job, prefix)
+        j = M.NewMiningJob(ch, job.job_int, has_min_ntime=not future, min_ntime=0 if future else job.ntime,
+                           version=job.version, merkle_root=root)
+        if future:
+            return [j, M.SetNewPrevHash(ch, job.job_int, job.block.prev_hash, job.ntime, job.block.nbits)]
+        return [j]
+
+    def send_job(self, job: PoolJob) -> None:
+        for ch, (_w, prefix) in self.channels.items():
+            for m in self._job_msgs(ch, job, prefix, future=job.clean):
+                self._send(m)
+
+    async def run(self) -> None:
+        try:
+            while True:
+                f = await asyncio.wait_for(read_frame_async(self.reader), 600)
+                msg = M.dispatch_frame(f, self.dialect)
+                await self._handle(msg)
+                await self.writer.drain()
+        except (asyncio.IncompleteReadError, asyncio.TimeoutError, ConnectionError, OSError, M.MessageError,
+                EOFError):
+            pass
+        finally:
+            self.close()
+
+    async def _handle(self, msg: M.Message) -> None:
+        if isinstance(msg, M.SetupConnection):
+            try:
+                M.validate_setup_connection(msg)
+                if not msg.min_version <= 2 <= msg.max_version:
+                    raise M.MessageError("unsupported-protocol-version")
+            except M.MessageError as exc:
+                self._send(M.SetupConnectionError(0, str(exc)[:255]))
+                return
+            self.setup = True
+            self.version_rolling = bool(msg.flags & M.FLAG_REQUIRES_VERSION_ROLLING) and \
+                self.pool.opts.allow_version_rolling
+            self._send(M.SetupConnectionSuccess(2, M.FLAG_REQUIRES_VERSION_ROLLING if self.version_rolling else 0))
+        elif isinstance(msg, M.OpenMiningChannel):
+            if not self.setup or not msg.user:
+                self._send(M.OpenMiningChannelError(msg.req_id, "unknown-user" if self.setup else "setup-required"))
+                return
+            ch = self._next_channel
+            self._next_channel += 1
+            prefix = self.pool.next_extranonce(EN1_SIZE + EN2_SIZE)
+            w = self.pool.new_worker(msg.user, BIP320_MASK if self.version_rolling else 0)
+            if msg.nominal_hashrate > 0 and self.pool.journal.load_worker(msg.user) is None:
+                w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
+                w.prev_difficulty = w.vd.difficulty
+            self.channels[ch] = (w, prefix)
+            self._send(M.OpenMiningChannelSuccess(
+                msg.req_id, ch, target_from_difficulty(w.vd.difficulty, self.pool.algo.diff1), prefix,
+                extranonce2_size=0))
+            if self.pool.jobs:
+                for m in self._job_msgs(ch, next(reversed(self.pool.jobs.values())), prefix, future=True):
+                    self._send(m)
+        elif isinstance(msg, M.SubmitSharesStandard):
+            ent = self.channels.get(msg.channel_id)
+            if ent is None:
+                self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, "invalid-channel-id"))
+                return
+            w, prefix = ent
+            v = self.pool.validate(w, f"{msg.job_id:x}", prefix, msg.ntime, msg.nonce, msg.nversion)
+            if v.accepted:
+                self._send(M.SubmitSharesSuccess(msg.channel_id, msg.sequence_number, 1, max(int(v.difficulty), 1)))
+                new = self.pool.after_accept(w)
+                if new is not None:
+                    self._send(M.SetTarget(msg.channel_id, target_from_difficulty(new, self.pool.algo.diff1)))
+            else:
+                self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, v.reason))
+        elif isinstance(msg, M.UpdateChannel):
+            ent = self.channels.get(msg.channel_id)
+            if ent is not None and msg.nominal_hashrate > 0:
+                w = ent[0]
+                w.prev_difficulty, w.retarget_at = w.vd.difficulty, time.monotonic()
+                w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
+                self._send(M.SetTarget(msg.channel_id, target_from_difficulty(w.vd.difficulty, self.pool.algo.diff1)))
+        elif isinstance(msg, M.CloseChannel):
+            self.channels.pop(msg.channel_id, None)

@@ -1,0 +1,86 @@
+"""Per-connection variable difficulty. [NO REFERENCE CODE]
+
+The only related reference code is the share-interval estimate
+``interval = D * 2^32 / H`` (internal/engine/stats.go:502-513, publishDifficulty);
+vardiff inverts it: every retarget window the observed share interval moves the
+difficulty toward ``target_share_seconds``, bounded per step (x4 / /4) and
+globally (min/max), with a 10% dead band so it does not flap.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+
+@dataclass
+class VardiffConfig:
+    target_share_seconds: float = 10.0
+    retarget_seconds: float = 30.0
+    min_difficulty: float = 1e-6
+    max_difficulty: float = 1e15
+    max_step: float = 4.0
+    dead_band: float = 0.10
+    min_shares: int = 4             # retarget early once this many shares arrived faster than target
+
+
+@dataclass
+class VardiffState:
+    difficulty: float
+    window_start: float = field(default_factory=time.monotonic)
+    shares: int = 0
+    accepted_work: float = 0.0      # sum of share difficulties in the window
+    total_shares: int = 0
+
+    def hashes_per_diff1(self, diff1_hashes: float) -> float:
+        return diff1_hashes
+
+
+class Vardiff:
+    def __init__(self, cfg: VardiffConfig | None = None, diff1_hashes: float = 2.0 ** 32, clock=time.monotonic):
+        self.cfg = cfg or VardiffConfig()
+        self.diff1_hashes = diff1_hashes  # expected hashes per difficulty-1 share
+        self.clock = clock
+
+    def new_state(self, difficulty: float) -> VardiffState:
+        return VardiffState(self.clamp(difficulty), self.clock())
+
+    def clamp(self, d: float) -> float:
+        return min(max(d, self.cfg.min_difficulty), self.cfg.max_difficulty)
+
+    def on_share(self, st: VardiffState) -> float | None:
+        """Record an accepted share; returns a new difficulty when a retarget fires."""
+        st.shares += 1
+        st.total_shares += 1
+        st.accepted_work += st.difficulty
+        return self.maybe_retarget(st)
+
+    def maybe_retarget(self, st: VardiffState) -> float | None:
+        now = self.clock()
+        elapsed = now - st.window_start
+        c = self.cfg
+        early = st.shares >= c.min_shares and elapsed < c.target_share_seconds * st.shares / 2
+        if elapsed < c.retarget_seconds and not early:
+            return None
+        if st.shares == 0:
+            ratio = 1.0 / c.max_step if elapsed >= 2 * c.retarget_seconds else 0.5
+        else:
+            observed = elapsed / st.shares
+            ratio = c.target_share_seconds / max(observed, 1e-9)
+        ratio = min(max(ratio, 1.0 / c.max_step), c.max_step)
+        st.window_start, st.shares, st.accepted_work = now, 0, 0.0
+        new = self.clamp(st.difficulty * ratio)
+        if abs(new - st.difficulty) <= c.dead_band * st.difficulty:
+            return None
+        st.difficulty = new
+        return new
+
+    def estimated_hashrate(self, st: VardiffState) -> float:
+        """H/s implied by the window's accepted work (D * diff1_hashes / interval)."""
+        elapsed = max(self.clock() - st.window_start, 1e-9)
+        return st.accepted_work * self.diff1_hashes / elapsed
+
+    def difficulty_for_hashrate(self, hashrate: float) -> float:
+        """Inverse of interval = D * diff1_hashes / H for the target interval."""
+        if hashrate <= 0:
+            return self.clamp(1.0)
+        return self.clamp(hashrate * self.cfg.target_share_seconds / self.diff1_hashes)

@@ -1,0 +1,137 @@
+"""Stratum V2 binary framing.
+
+Parity: internal/stratum/frame.go
+  * 6-byte header: u16 extension_type (bit 15 = channel_msg) | u8 msg_type |
+    u24 msg_length, little-endian ...................... frame.go:57-86,172-186
+  * Header.validate (U24 bound, channel payload >= 4) ... frame.go:108-136
+  * Frame.channel_id ................................... frame.go:153-161
+  * encode_frame / decode_header ....................... frame.go:194-231
+  * Decoder: max frame (16 MiB) checked BEFORE
+    allocating the payload (anti-DoS) .................. frame.go:238-302
+An asyncio reader (``read_frame_async``) is provided for the client/pool loops.
+"""
+from __future__ import annotations
+
+import asyncio
+import struct
+from dataclasses import dataclass
+from typing import BinaryIO
+
+HEADER_SIZE = 6
+MAX_MESSAGE_LENGTH = (1 << 24) - 1
+DEFAULT_MAX_FRAME_SIZE = 16 * 1024 * 1024
+MINIMUM_CHANNEL_PAYLOAD = 4
+CHANNEL_MSG_BIT = 0x8000
+
+
+class FrameError(ValueError):
+    pass
+
+
+@dataclass(frozen=True)
+class Header:
+    extension_type: int = 0
+    msg_type: int = 0
+    msg_length: int = 0
+
+    @property
+    def channel_msg(self) -> bool:
+        return bool(self.extension_type & CHANNEL_MSG_BIT)
+
+    @property
+    def extension_id(self) -> int:
+        return self.extension_type & ~CHANNEL_MSG_BIT & 0xFFFF
+
+    def validate(self) -> None:
+        if self.msg_length > MAX_MESSAGE_LENGTH:
+            raise FrameError(f"stratum: MsgLength {self.msg_length} exceeds U24 maximum {MAX_MESSAGE_LENGTH}")
+        if self.channel_msg and self.msg_length < MINIMUM_CHANNEL_PAYLOAD:
+            raise FrameError(f"stratum: channel message requires payload >= {MINIMUM_CHANNEL_PAYLOAD} bytes, "
+                             f"got {self.msg_length}")
+
+    def encode(self) -> bytes:
+        self.validate()
+        n = self.msg_length
+        return struct.pack("<HB", self.extension_type & 0xFFFF, self.msg_type & 0xFF) + bytes(
+            (n & 0xFF, (n >> 8) & 0xFF, (n >> 16) & 0xFF))
+
+
+@dataclass(frozen=True)
+class Frame:
+    header: Header
+    payload: bytes
+
+    def channel_id(self) -> int:
+        if not self.header.channel_msg:
+            raise FrameError("stratum: frame is not a channel message")
+        if len(self.payload) < MINIMUM_CHANNEL_PAYLOAD:
+            raise FrameError(f"stratum: channel message payload is {len(self.payload)} bytes, need at least "
+                             f"{MINIMUM_CHANNEL_PAYLOAD}")
+        return struct.unpack_from("<I", self.payload, 0)[0]
+
+
+def decode_header(src: bytes) -> Header:
+    if len(src) < HEADER_SIZE:
+        raise FrameError(f"stratum: header truncated: need {HEADER_SIZE} bytes, got {len(src)}")
+    ext, mt = struct.unpack_from("<HB", src, 0)
+    return Header(ext, mt, src[3] | (src[4] << 8) | (src[5] << 16))
+
+
+def encode_frame(f: Frame) -> bytes:
+    if len(f.payload) > MAX_MESSAGE_LENGTH:
+        raise FrameError(f"stratum: payload length {len(f.payload)} exceeds U24 maximum {MAX_MESSAGE_LENGTH}")
+    h = Header(f.header.extension_type, f.header.msg_type, len(f.payload))
+    return h.encode() + bytes(f.payload)
+
+
+def _check_size(h: Header, max_frame: int) -> None:
+    h.validate()
+    total = HEADER_SIZE + h.msg_length
+    if total > max_frame:
+        raise FrameError(f"stratum: frame size {total} exceeds MaxFrameSize {max_frame}")
+
+
+class Decoder:
+    """Blocking frame reader over a file-like object (reads exactly)."""
+
+    def __init__(self, r: BinaryIO, max_frame_size: int = DEFAULT_MAX_FRAME_SIZE):
+        self.r = r
+        self.max_frame_size = max_frame_size
+
+    def _read_exact(self, n: int) -> bytes:
+        buf = bytearray()
+        while len(buf) < n:
+            chunk = self.r.read(n - len(buf))
+            if not chunk:
+                raise EOFError("unexpected EOF" if buf else "EOF")
+            buf += chunk
+        return bytes(buf)
+
+    def read_frame(self) -> Frame:
+        if self.max_frame_size <= 0:
+            raise FrameError("stratum: Decoder.MaxFrameSize must be positive")
+        h = decode_header(self._read_exact(HEADER_SIZE))
+        _check_size(h, self.max_frame_size)
+        payload = self._read_exact(h.msg_length) if h.msg_length else b""
+        return Frame(h, payload)
+
+
+async def read_frame_async(reader: asyncio.StreamReader, max_frame_size: int = DEFAULT_MAX_FRAME_SIZE) -> Frame:
+    raw = await reader.readexactly(HEADER_SIZE)
+    h = decode_header(raw)
+    _check_size(h, max_frame_size)
+    payload = await reader.readexactly(h.msg_length) if h.msg_length else b""
+    return Frame(h, payload)
+
+
+def iter_frames(buf: bytes, max_frame_size: int = DEFAULT_MAX_FRAME_SIZE):
+    """Parse back-to-back frames from a byte string (tests / fuzzing)."""
+    off = 0
+    while off < len(buf):
+        h = decode_header(buf[off:off + HEADER_SIZE])
+        _check_size(h, max_frame_size)
+        end = off + HEADER_SIZE + h.msg_length
+        if end > len(buf):
+            raise EOFError("unexpected EOF")
+        yield Frame(h, bytes(buf[off + HEADER_SIZE:end]))
+        off = end

@@ -1,0 +1,156 @@
+"""Loopback pool server <-> V1 / V2 client sessions, with real share validation
+(mirrors engine/integration_test.go's mock pool, but the pool re-hashes every
+share — the reference fakes never do)."""
+import asyncio
+import struct
+
+import pytest
+
+from otedama_amd.models.header import hash_to_int, sha256d
+from otedama_amd.ops.native import require_native
+from otedama_amd.pool.server import PoolOptions, PoolServer
+from otedama_amd.poolproto import Credentials, ShareSubmission
+from otedama_amd.poolproto.stratumv1 import V1Dialer
+from otedama_amd.poolproto.stratumv2 import V2Dialer
+
+N = require_native()
+ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
+
+
+def _find_share(job, max_variants=64):
+    """Mine a share for a poolproto Job on the CPU through the native runtime."""
+    t = job.template()
+    for v in range(max_variants):
+        hdr, ver, nt, en2 = N.variant_header(t, v)
+        hits = N.cpu_scan_sha256d(hdr, t["target"], 0, 1 << 20)
+        if hits:
+            return hits[0], ver, nt, en2, hdr
+    raise AssertionError("no share found")
+
+
+async def _with_pool(fn, **kw):
+    opts = PoolOptions(initial_difficulty=kw.pop("diff", 2e-5), payout_address=ADDR, **kw)
+    pool = PoolServer(opts)
+    await pool.start()
+    try:
+        return await fn(pool)
+    finally:
+        await pool.stop()
+
+
+@pytest.mark.parametrize("rolling", [True, False])
+def test_sv2_share_accept_duplicate_lowdiff(rolling):
+    async def body(pool):
+        s = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR, version_rolling=rolling))
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        assert job is not None and job.merkle_root is not None
+        assert (job.version_mask != 0) == rolling
+        nonce, ver, nt, _en2, hdr = _find_share(job)
+        h = sha256d(hdr[:76] + struct.pack("<I", nonce))
+        assert hash_to_int(h) <= hash_to_int(job.target)
+        r = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver))
+        assert r.accepted, r
+        r2 = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver))
+        assert not r2.accepted and "duplicate" in r2.reason
+        # a nonce that fails the target
+        bad = next(n for n in range(1000) if hash_to_int(sha256d(hdr[:76] + struct.pack("<I", n)))
+                   > hash_to_int(job.target))
+        r3 = await s.submit(ShareSubmission(job.job_id, bad, nt, ver))
+        assert not r3.accepted and "difficulty" in r3.reason
+        r4 = await s.submit(ShareSubmission("65535", nonce, nt, ver))
+        assert not r4.accepted and "stale" in r4.reason
+        assert pool.accepted == 1 and pool.rejected == 3
+        await s.close()
+
+    asyncio.run(_with_pool(body))
+
+
+def test_v1_coinbase_extranonce2_share():
+    async def body(pool):
+        s = await V1Dialer().dial(f"stratum+tcp://{pool.addr_v1}", Credentials(user=ADDR + ".rig1"))
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        assert job.coinb1 and job.coinb2 and len(job.merkle_branches) == 3  # 7 fake txs + coinbase
+        assert job.extranonce2_size == 4 and len(job.extranonce1) == 4
+        nonce, ver, nt, en2, hdr = _find_share(job)
+        # the pool rebuilds the same header from coinb1 | en1 | en2 | coinb2
+        cb = job.coinb1 + job.extranonce1 + en2.to_bytes(4, "little") + job.coinb2
+        root = sha256d(cb)
+        for b in job.merkle_branches:
+            root = sha256d(root + b)
+        assert hdr[36:68] == root
+        r = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, en2.to_bytes(4, "little")))
+        assert r.accepted, r
+        r2 = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, en2.to_bytes(4, "little")))
+        assert not r2.accepted and "duplicate" in r2.reason
+        await s.close()
+
+    asyncio.run(_with_pool(body))
+
+
+def test_v1_version_rolling_share():
+    async def body(pool):
+        s = await V1Dialer().dial(f"stratum+tcp://{pool.addr_v1}", Credentials(user=ADDR))
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        assert job.version_mask == 0x1FFFE000
+        t = dict(job.template())
+        # force version rolling (no extranonce2 rolling): fixed en2 = 0 via a 1-variant coinbase space
+        for v in range(1, 200):
+            hdr, ver, nt, en2 = N.variant_header({**t, "extranonce2_size": 0}, v)
+            if ver == job.version:
+                continue
+            # pool builds coinbase with en2 = 4 zero bytes; make the header match
+            cb = job.coinb1 + job.extranonce1 + bytes(4) + job.coinb2
+            root = sha256d(cb)
+            for b in job.merkle_branches:
+                root = sha256d(root + b)
+            hdr = hdr[:36] + root + hdr[68:]
+            hits = N.cpu_scan_sha256d(hdr, t["target"], 0, 1 << 20)
+            if hits:
+                r = await s.submit(ShareSubmission(job.job_id, hits[0], nt, ver, bytes(4)))
+                assert r.accepted, r
+                break
+        else:
+            raise AssertionError("no rolled share found")
+        await s.close()
+
+    asyncio.run(_with_pool(body))
+
+
+def test_vardiff_retarget_sends_set_target():
+    async def body(pool):
+        s = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR))
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        t0 = s.share_target
+        accepted = 0
+        for v in range(40):
+            hdr, ver, nt, _ = N.variant_header(job.template(), v)
+            for n in N.cpu_scan_sha256d(hdr, job.target, 0, 1 << 20)[:2]:
+                r = await s.submit(ShareSubmission(job.job_id, n, nt, ver))
+                accepted += r.accepted
+            if s.share_target != t0:
+                break
+        assert accepted >= 4
+        # shares arrive far faster than the 10 s target -> difficulty goes up, target down
+        assert hash_to_int(s.share_target) < hash_to_int(t0)
+        await s.close()
+
+    asyncio.run(_with_pool(body, retarget_seconds=0.5))
+
+
+def test_setup_connection_error_is_fatal():
+    from otedama_amd.poolproto import FatalPoolError
+    from otedama_amd.stratum import messages as M
+
+    async def body(pool):
+        async def serve(reader, writer):
+            await reader.read(100)
+            writer.write(M.encode_message(M.SetupConnectionError(0, "unsupported-feature-flags")))
+            await writer.drain()
+
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        with pytest.raises(FatalPoolError):
+            await V2Dialer().dial(f"stratum+v2://127.0.0.1:{port}", Credentials(user=ADDR))
+        srv.close()
+
+    asyncio.run(_with_pool(body))
