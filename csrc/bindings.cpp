@@ -91,6 +91,7 @@ py::list shares_to_list(std::vector<ShareRecord>&& v) {
     d["extranonce2_size"] = s.extranonce2_size;
     d["hash"] = to_bytes(s.hash, 32);
     d["device_id"] = s.device_id;
+    d["found_at"] = s.found_at;
     out.append(d);
   }
   return out;

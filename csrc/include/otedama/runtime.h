@@ -62,6 +62,7 @@ struct ShareRecord {
   uint32_t extranonce2_size;
   uint8_t hash[32];
   std::string device_id;
+  double found_at = 0;  // CLOCK_MONOTONIC seconds when the host verified the share
 };
 
 struct MinerStats {
@@ -114,7 +115,8 @@ class MinerBase {
   std::mutex job_mu_;
   std::condition_variable job_cv_;
   std::shared_ptr<const JobTemplate> job_;
-  uint64_t job_gen_ = 0;
+  std::shared_ptr<const JobTemplate> last_work_;  // last non-null job (work identity)
+  uint64_t job_gen_ = 0;                          // bumps only when the search space changes
   std::atomic<bool> running_{false};
   std::mutex stats_mu_;
   MinerStats stats_;
@@ -155,5 +157,8 @@ class CpuMiner : public MinerBase {
 // Returns the nonces (header byte order) whose SHA-256d meets the target.
 std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
                                        uint64_t count);
+
+// Seconds on CLOCK_MONOTONIC (same clock as Python time.monotonic()).
+double monotonic_seconds();
 
 }  // namespace otedama

@@ -121,6 +121,7 @@ void GpuMiner::loop() {
       r.epoch = s.job->epoch; r.job_id = s.job->job_id; r.channel_id = s.job->channel_id;
       r.nonce = nonce; r.ntime = s.ntime; r.version = s.version; r.extranonce2 = s.en2;
       r.extranonce2_size = s.job->extranonce2_size; r.device_id = device_id_;
+      r.found_at = monotonic_seconds();
       queue_.push(std::move(r));
       ++good;
     }

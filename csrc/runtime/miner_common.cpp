@@ -183,11 +183,25 @@ size_t ShareQueue::size() {
 
 // --------------------------------------------------------------- miner base
 
+// Two templates describe the same search space when everything that feeds a
+// header is equal (target / epoch / job id may differ). Re-issuing the same work
+// (SV2 SetTarget, V1 set_difficulty, curtail/arbitration pause -> resume) must
+// NOT restart the nonce cursor, or the device re-finds shares it already
+// submitted and the pool rejects them as duplicates.
+static bool same_work(const JobTemplate& a, const JobTemplate& b) {
+  return a.algo == b.algo && std::memcmp(a.header, b.header, 76) == 0 && a.version_mask == b.version_mask &&
+         a.ntime_roll == b.ntime_roll && a.has_coinbase == b.has_coinbase && a.coinb1 == b.coinb1 &&
+         a.coinb2 == b.coinb2 && a.extranonce1 == b.extranonce1 && a.extranonce2_size == b.extranonce2_size &&
+         a.merkle_branches == b.merkle_branches && a.variant_start == b.variant_start &&
+         a.variant_stride == b.variant_stride;
+}
+
 void MinerBase::set_job(std::shared_ptr<const JobTemplate> job) {
   {
     std::lock_guard<std::mutex> g(job_mu_);
+    if (job && !(last_work_ && same_work(*last_work_, *job))) ++job_gen_;
+    if (job) last_work_ = job;
     job_ = std::move(job);
-    ++job_gen_;
   }
   job_cv_.notify_all();
 }
@@ -304,6 +318,7 @@ void CpuMiner::loop(int /*tid*/) {
       s.epoch = job->epoch; s.job_id = job->job_id; s.channel_id = job->channel_id;
       s.nonce = n; s.ntime = nt; s.version = ver; s.extranonce2 = en2;
       s.extranonce2_size = job->extranonce2_size; s.device_id = device_id_;
+      s.found_at = monotonic_seconds();
       store_le32(hdr + 76, n);
       sha256d(hdr, 80, s.hash);
       queue_.push(std::move(s));
@@ -316,4 +331,12 @@ void CpuMiner::loop(int /*tid*/) {
   }
 }
 
+}  // namespace otedama
+
+namespace otedama {
+double monotonic_seconds() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return double(ts.tv_sec) + double(ts.tv_nsec) * 1e-9;
+}
 }  // namespace otedama

@@ -1,0 +1,654 @@
+"""Top-level orchestrator: devices -> miners -> pool session -> shares -> metrics.
+
+Parity: internal/engine/run.go + setup.go + arbitrate.go + fanin.go
+  * Options (config, clock, output, logger func(level,msg), no_tui, stats
+    interval, max reconnect attempts, wallet passphrases, metrics, on_ready) run.go:71-108
+  * curtail_decision (never on stale/fallback price) ............... run.go:123-135
+  * Run phases: metrics + uptime ticker, wallet, device detection,
+    miner start, rates (fallback 95000, 5 min), curtail loop (30 s),
+    providers, arbitration loop, TUI, reconnect loop ................ run.go:140-339
+  * reconnect loop: pool failover immediately, payout-address
+    failover only if the address never connected, backoff 1 s x2 ->
+    64 s, fatal errors stop, MaxReconnectAttempts ................... run.go:343-521
+  * session loop (stats tick: windowed hashrate, drops, stall
+    detection, sats, productive seconds, power/J-per-TH, acceptance
+    warning >= 20 judged & < 97%, latency p50/95/99) ................. run.go:610-961
+  * arbitration glue (quotes -> streams, 3 min staleness prune,
+    Decide every 30 s, pause devices moved to AI / idle) ............. arbitrate.go:62-299
+  * pool_urls / payout_addresses / session_user / mask_addr .......... setup.go:213-270
+
+Differences: one pool-agnostic session loop drives both
+Stratum V1 and V2 (both through otedama_amd.poolproto, with real verdicts);
+stream yields use NET sats/s (the reference uses gross, arbitrate.go:187-195);
+the simulated AI provider is opt-in because on MI355X it would idle real GPU
+mining for a simulated quote; GPU faults drop the device's stripe and
+rebalance the rest.
+"""
+from __future__ import annotations
+
+import asyncio
+import sys
+import time
+from dataclasses import dataclass
+from typing import Callable, TextIO
+
+from otedama_amd import arbitration as arb
+from otedama_amd import hal
+from otedama_amd.config import DEFAULT_POOL_URL, Config
+from otedama_amd.engine.metrics import EngineMetrics
+from otedama_amd.engine.miners import MinerSet
+from otedama_amd.engine.stats import (
+    HashrateMonitor,
+    HashrateWindow,
+    LatencyTracker,
+    SatsAccountant,
+    UptimeAccountant,
+    effective_yield,
+    hashrate_string,
+    publish_btc_rate,
+    publish_difficulty,
+    reject_class,
+)
+from otedama_amd.metrics import Registry, runtime_collector
+from otedama_amd.models.algorithms import get as get_algorithm
+from otedama_amd.poolproto import Credentials, FatalPoolError, Job, ShareSubmission
+from otedama_amd.poolproto.base import from_url, lookup
+from otedama_amd.provider import AkashProvider, MiningProvider
+from otedama_amd.utils.clock import SYSTEM, Clock
+
+RECONNECT_BACKOFF_INITIAL = 1.0
+RECONNECT_BACKOFF_MAX = 64.0
+STREAM_STALE_TIMEOUT = 180.0
+DEFAULT_HYSTERESIS = 0.05
+SHARE_POLL_INTERVAL = 0.005
+
+
+@dataclass
+class Options:
+    config: Config
+    clock: Clock = SYSTEM
+    output: TextIO | None = None
+    logger: Callable[[str, str], None] | None = None
+    no_tui: bool = True
+    stats_interval: float = 10.0
+    max_reconnect_attempts: int = 0
+    wallet_passphrase: str = ""
+    wallet_mnemonic_passphrase: str = ""
+    metrics: Registry | None = None
+    on_ready: Callable[[bool], None] | None = None
+    devices: list | None = None              # test seam: skip HAL detection
+    rate_fetcher: object | None = None       # test seam
+    enable_ai_provider: bool = False
+    arbitration_interval: float = 30.0
+    curtail_interval: float = 30.0
+    rates_interval: float = 300.0
+    fetch_rates: bool = True
+    dashboard: object | None = None
+
+
+def curtail_decision(curr: bool, rate: float, fresh: bool, threshold: float) -> tuple[bool, bool]:
+    if threshold <= 0 or not fresh or rate <= 0:
+        return curr, False
+    if rate < threshold and not curr:
+        return True, True
+    if rate >= threshold and curr:
+        return False, True
+    return curr, False
+
+
+def pool_urls(cfg: Config) -> list[str]:
+    return [p.url for p in cfg.pools] if cfg.pools else [DEFAULT_POOL_URL]
+
+
+def payout_addresses(cfg: Config) -> list[str]:
+    seen, out = set(), []
+    for a in [cfg.bitcoin_address, *cfg.bitcoin_addresses]:
+        if a and a not in seen:
+            seen.add(a)
+            out.append(a)
+    return out
+
+
+def session_user(pool_user: str, addr: str, worker: str) -> str:
+    if pool_user:
+        return pool_user
+    return f"{addr}.{worker}" if worker else addr
+
+
+def mask_addr(a: str) -> str:
+    return a if len(a) <= 12 else a[:6] + "…" + a[-4:]
+
+
+class Engine:
+    def __init__(self, opts: Options):
+        self.opts = opts
+        self.cfg = opts.config
+        self.log = opts.logger or (lambda level, msg: None)
+        self.registry = opts.metrics or Registry()
+        self.m = EngineMetrics(self.registry)
+        self.registry.register_collector(runtime_collector())
+        self.algorithm = get_algorithm(self.cfg.mining.algorithm)
+        self.start_time = opts.clock.now()
+        self.devices: list = []
+        self.miners: MinerSet | None = None
+        self.curtailed = False
+        self.latency = LatencyTracker(256)           # submit -> accept (reference semantics)
+        self.pipeline_latency = LatencyTracker(4096)  # host-verified hit -> accept
+        self.hash_window = HashrateWindow()
+        self.current_hashrate = 0.0
+        self.device_hashrates: dict[str, float] = {}
+        self.pool_url = ""
+        self.connected = False
+        self.stalled = False
+        self.est_sats = 0.0
+        self.wallet_fingerprint = ""
+        self.activity: dict[str, float] = {}
+        self._active_job: Job | None = None
+        self._valid_jobs: set[str] = set()
+        self._submitted: set = set()
+        self._session = None
+        self._providers: list = []
+        self._rate_fetcher = opts.rate_fetcher
+        self._tasks: list[asyncio.Task] = []
+        self._submit_tasks: set[asyncio.Task] = set()
+        self._hashmon = HashrateMonitor(0, 3, self.log)
+        self._uptime = UptimeAccountant()
+        self._sats = SatsAccountant()
+        self._last_dropped = 0
+        self.dashboard = opts.dashboard
+
+    # ---------------------------------------------------------------- API
+    def stats(self) -> dict:
+        return {
+            "hashrate": self.current_hashrate, "hashrate_str": hashrate_string(self.current_hashrate),
+            "devices": {k: v for k, v in self.device_hashrates.items()},
+            "shares_found": self.m.shares_found.value(), "shares_submitted": self.m.shares_submitted.value(),
+            "accepted": self.m.shares_accepted.value(), "rejected": self.m.shares_rejected.value(),
+            "latency_p50_ms": self.latency.quantile(0.5), "latency_p95_ms": self.latency.quantile(0.95),
+            "pool": self.pool_url, "connected": self.connected, "curtailed": self.curtailed,
+            "stalled": self.stalled, "uptime": self.opts.clock.now() - self.start_time,
+            "algorithm": self.algorithm.name, "wallet": self.wallet_fingerprint,
+            "est_sats": self.est_sats, "activity": dict(self.activity),
+        }
+
+    def device_list(self) -> list[dict]:
+        return [{"id": d.identity().id, "family": d.identity().family.value, "vendor": d.identity().vendor,
+                 "model": d.identity().model, "capabilities": d.capabilities().__dict__} for d in self.devices]
+
+    # ---------------------------------------------------------------- run
+    async def run(self) -> None:
+        cfg = self.cfg
+        self.m.uptime.set(0)
+        self.m.start_time.set(self.start_time)
+        if cfg.power_watts > 0 and cfg.electricity_price_per_kwh > 0:
+            self.m.power_cost_usd_per_hour.set(cfg.power_watts / 1000 * cfg.electricity_price_per_kwh)
+        self._tasks.append(asyncio.ensure_future(self._uptime_loop()))
+        try:
+            self.wallet_fingerprint = self._setup_wallet()
+            self.devices = self.opts.devices if self.opts.devices is not None else await asyncio.to_thread(
+                self._detect_devices)
+            self.log("info", f"engine: detected {len(self.devices)} device(s)")
+            for d in self.devices:
+                self.log("info", f"engine: device {d.identity()} caps={d.capabilities()}")
+            self.miners = MinerSet(self.devices, self.algorithm.name, cfg.mining.batch_nonces, cfg.mining.cpu_threads,
+                                   log=self.log)
+            if len(self.miners) == 0:
+                raise RuntimeError(f"engine: no device can mine {self.algorithm.name}")
+            self.miners.start()
+            if self._rate_fetcher is None:
+                from otedama_amd.rates import Fetcher
+
+                self._rate_fetcher = Fetcher(95_000.0, log=lambda msg: self.log("warn", msg))
+                if self.opts.fetch_rates:
+                    self._rate_fetcher.start_background(self.opts.rates_interval)
+            self._tasks.append(asyncio.ensure_future(self._curtail_loop()))
+            self._start_providers()
+            self._tasks.append(asyncio.ensure_future(self._arbitration_loop()))
+            if self.dashboard is not None:
+                self.dashboard.start()
+            await self._reconnect_loop()
+        finally:
+            for t in self._tasks:
+                t.cancel()
+            for p in self._providers:
+                await p.stop()
+            if self.miners is not None:
+                self.miners.stop()
+            if self.dashboard is not None:
+                self.dashboard.stop()
+            if self._rate_fetcher is not None and hasattr(self._rate_fetcher, "stop"):
+                self._rate_fetcher.stop()
+            if self.opts.on_ready:
+                self.opts.on_ready(False)
+
+    def _detect_devices(self) -> list:
+        reg = hal.default_registry(self.cfg.mining.cpu_threads)
+        devs = hal.Detector(reg, lambda drv, msg, err: self.log("warn", f"hal: {drv}: {msg}: {err}")).detect()
+        sel = self.cfg.mining.gpus.strip().lower()
+        if sel == "none":
+            devs = [d for d in devs if d.identity().family != hal.Family.GPU]
+        elif sel not in ("", "all"):
+            keep = {int(x) for x in sel.split(",") if x.strip().isdigit()}
+            devs = [d for d in devs if d.identity().family != hal.Family.GPU or d.index in keep]
+        return devs
+
+    def _setup_wallet(self) -> str:
+        if not self.opts.wallet_passphrase or not self.cfg.data_dir:
+            return ""
+        try:
+            from otedama_amd.lightning.wallet import WalletManager, recovery_phrase_banner
+        except ImportError:
+            return ""
+        try:
+            wm = WalletManager(self.cfg.data_dir, self.opts.wallet_passphrase,
+                               mnemonic_passphrase=self.opts.wallet_mnemonic_passphrase)
+        except Exception as exc:  # noqa: BLE001
+            self.log("warn", f"wallet: {exc}")
+            return ""
+        if wm.is_new:
+            self.log("info", "wallet: new wallet created — back up your recovery phrase")
+            out = self.opts.output or sys.stdout
+            out.write(recovery_phrase_banner(wm.mnemonic, wm.fingerprint))
+            out.flush()
+        self.log("info", f"wallet: fingerprint {wm.fingerprint}")
+        return wm.fingerprint
+
+    async def _uptime_loop(self) -> None:
+        while True:
+            await asyncio.sleep(1.0)
+            self.m.uptime.set(self.opts.clock.now() - self.start_time)
+
+    # ---------------------------------------------------------- curtail
+    async def _curtail_loop(self) -> None:
+        while True:
+            publish_btc_rate(self.m, self._rate_fetcher)
+            threshold = self.cfg.curtail_below_btc_usd
+            rate, fresh = self._rate_fetcher.btc_usd_rate()
+            nxt, changed = curtail_decision(self.curtailed, rate, fresh, threshold)
+            if changed:
+                self.curtailed = nxt
+                if nxt:
+                    self.miners.pause_all()
+                    self.m.curtailed.set(1)
+                    self.log("info", f"engine: curtailed — BTC/USD ${rate:.0f} below threshold ${threshold:.0f}; "
+                                     "hashing paused")
+                else:
+                    self.m.curtailed.set(0)
+                    self.log("info", f"engine: uncurtailed — BTC/USD ${rate:.0f} above threshold "
+                                     f"${threshold:.0f}; hashing resumes")
+                    if self._active_job is not None:
+                        self.miners.set_job(self._active_job.template())
+            await asyncio.sleep(self.opts.curtail_interval)
+
+    # ---------------------------------------------------------- providers / arbitration
+    def _start_providers(self) -> None:
+        url = pool_urls(self.cfg)[0]
+        mp = MiningProvider(url, self._rate_fetcher, hashrate_func=lambda dev: self.device_hashrates.get(dev, 0.0),
+                            algorithm=self.algorithm.name)
+        mp.start(self.devices)
+        self._providers.append(mp)
+        if self.opts.enable_ai_provider:
+            ap = AkashProvider(self._rate_fetcher)
+            ap.start(self.devices)
+            self._providers.append(ap)
+
+    async def _next_quote(self):
+        gets = [asyncio.ensure_future(p.quotes.get()) for p in self._providers]
+        try:
+            done, pending = await asyncio.wait(gets, return_when=asyncio.FIRST_COMPLETED)
+        finally:
+            for g in gets:
+                if not g.done():
+                    g.cancel()
+        return [d.result() for d in done]
+
+    async def _arbitration_loop(self) -> None:
+        dev_refs = [arb.DeviceRef(d.identity(), d.capabilities()) for d in self.devices]
+        streams: dict[str, arb.Stream] = {}
+        last_quote: dict[str, float] = {}
+        prev: arb.Allocation | None = None
+        margin = self.cfg.arbitration_hysteresis_pct or DEFAULT_HYSTERESIS
+        deadline = time.monotonic() + self.opts.arbitration_interval
+        while True:
+            timeout = max(deadline - time.monotonic(), 0)
+            try:
+                quotes = await asyncio.wait_for(self._next_quote(), timeout)
+            except asyncio.TimeoutError:
+                quotes = None
+            for q in quotes or []:
+                key = update_stream(streams, q)
+                last_quote[key] = q.at or time.time()
+            if time.monotonic() < deadline:
+                continue
+            deadline = time.monotonic() + self.opts.arbitration_interval
+            now = time.time()
+            for key in [k for k, t in last_quote.items() if now - t > STREAM_STALE_TIMEOUT]:
+                streams.pop(key, None)
+                last_quote.pop(key, None)
+                self.log("info", f"arbitration: stream {key!r} expired (no quote in 3m0s); no longer routing to it")
+            merged = streams_slice(streams)
+            self.m.active_streams.set(len(merged))
+            try:
+                alloc = arb.decide(arb.Input(dev_refs, merged, prev, arb.Policy.MAXIMIZE_EARNINGS, margin,
+                                             self.cfg.min_yield_sats_per_sec))
+            except arb.ArbitrationError as exc:
+                self.log("warn", f"arbitration: {exc}")
+                continue
+            prev_skipped = prev.skipped_device if prev else 0
+            prev = alloc
+            foregone = 0.0
+            for a in alloc.assignments:
+                if a.switched_from_id:
+                    self.m.arbitration_switches.inc()
+                if a.held:
+                    self.m.arbitration_holds.inc()
+                foregone += a.foregone_sats_per_sec
+            self.m.arbitration_foregone.set(foregone)
+            self.m.arbitration_expected_yield.set(alloc.total_yield)
+            self.m.devices_idle.set(alloc.skipped_device)
+            self.activity = {}
+            for a in alloc.assignments:
+                if not a.idle():
+                    self.activity[a.stream] = self.activity.get(a.stream, 0.0) + a.expected_yield
+            if alloc.skipped_device != prev_skipped:
+                if alloc.skipped_device:
+                    self.log("info", f"arbitration: {alloc.skipped_device} device(s) now idle (no viable stream, "
+                                     "or below min_yield_sats_per_sec floor)")
+                else:
+                    self.log("info", "arbitration: all devices now have a viable stream")
+            self._apply_allocation(alloc)
+
+    def _apply_allocation(self, alloc: arb.Allocation) -> None:
+        for a in alloc.assignments:
+            mining = (not a.idle()) and not a.stream.startswith("ai.")
+            changed = self.miners.pause_device(a.device_id, paused=not mining)
+            if a.idle():
+                self.log("info", f"arbitration: {a.device_id} idle ({a.reason or 'no compatible stream'})")
+            elif a.switched_from_id:
+                was_ai, now_ai = a.switched_from_id.startswith("ai."), a.stream.startswith("ai.")
+                if not was_ai and now_ai:
+                    self.log("info", f"arbitration: {a.device_id} → AI inference ({a.expected_yield:.0f} sat/s)")
+                elif was_ai and not now_ai:
+                    self.log("info", f"arbitration: {a.device_id} → mining ({a.expected_yield:.0f} sat/s)")
+                else:
+                    self.log("info", f"arbitration: {a.device_id} switched to {a.stream} "
+                                     f"({a.expected_yield:.0f} sat/s)")
+            del changed
+
+    # ---------------------------------------------------------- reconnect loop
+    async def _reconnect_loop(self) -> None:
+        pools = pool_urls(self.cfg)
+        addrs = payout_addresses(self.cfg) or [""]
+        pool_idx = addr_idx = attempt = 0
+        addr_connected = False
+        backoff = RECONNECT_BACKOFF_INITIAL
+        while True:
+            attempt += 1
+            if self.opts.max_reconnect_attempts > 0 and attempt > self.opts.max_reconnect_attempts:
+                raise RuntimeError(f"engine: exceeded {self.opts.max_reconnect_attempts} reconnect attempts")
+            url = pools[pool_idx]
+            pc = self.cfg.pools[pool_idx] if pool_idx < len(self.cfg.pools) else None
+            user = session_user(pc.user if pc else "", addrs[addr_idx], self.cfg.workers.name)
+            loc = f"attempt {attempt}"
+            if len(pools) > 1:
+                loc += f", pool {pool_idx + 1}/{len(pools)}"
+            if len(addrs) > 1:
+                loc += f", address {addr_idx + 1}/{len(addrs)}"
+            self.log("info", f"engine: connecting to {url} ({loc})")
+            self.m.pool_connect_attempts.inc()
+            self.m.pool_active_index.set(pool_idx)
+            self.m.payout_active_index.set(addr_idx)
+            if addrs[addr_idx]:
+                self.m.set_active_payout(mask_addr(addrs[addr_idx]))
+            self.m.pool_connection_state.set(1)
+            self.pool_url = url
+
+            def on_connected():
+                nonlocal addr_connected
+                addr_connected = True
+                if self.opts.on_ready:
+                    self.opts.on_ready(True)
+
+            err: BaseException | None = None
+            try:
+                await self._run_session(url, user, pc, on_connected)
+            except asyncio.CancelledError:
+                raise
+            except BaseException as exc:  # noqa: BLE001
+                err = exc
+            if err is not None:
+                self.m.pool_connect_failures.inc()
+            self.m.pool_connection_state.set(0)
+            self.connected = False
+            if self.opts.on_ready:
+                self.opts.on_ready(False)
+            if isinstance(err, FatalPoolError):
+                raise err
+            if len(pools) > 1:
+                pool_idx = (pool_idx + 1) % len(pools)
+                if pool_idx != 0:
+                    self.log("warn", f"engine: session ended: {err}; failing over to next pool")
+                    continue
+            if not addr_connected and len(addrs) > 1:
+                prev_i = addr_idx
+                addr_idx = (addr_idx + 1) % len(addrs)
+                pool_idx = 0
+                if addr_idx != 0:
+                    self.log("warn", f"engine: payout address {mask_addr(addrs[prev_i])} ({prev_i + 1}/{len(addrs)}) "
+                                     f"could not establish a session on any pool; failing over to "
+                                     f"{mask_addr(addrs[addr_idx])} ({addr_idx + 1}/{len(addrs)})")
+                    continue
+                addr_connected = False
+                self.log("warn", f"engine: none of the {len(addrs)} configured payout addresses could connect; "
+                                 f"backing off {backoff:.0f}s and retrying from the primary")
+            elif len(pools) > 1:
+                self.log("warn", f"engine: all {len(pools)} pools failed; backing off {backoff:.0f}s")
+            else:
+                self.log("warn", f"engine: session ended: {err}; reconnecting in {backoff:.0f}s")
+            await asyncio.sleep(backoff)
+            if backoff < RECONNECT_BACKOFF_MAX:
+                backoff *= 2
+
+    # ---------------------------------------------------------- session
+    async def _dial(self, url: str, creds: Credentials):
+        proto = from_url(url)
+        d = lookup(proto)
+        kw = {"algorithm": self.algorithm.name}
+        if proto.value.startswith("stratum-v2"):
+            kw["log"] = self.log
+        return await d.dial(url, creds, **kw)
+
+    async def _run_session(self, url: str, user: str, pc, on_connected) -> None:
+        ca = b""
+        if pc is not None and pc.tls_ca_file:
+            with open(pc.tls_ca_file, "rb") as f:
+                ca = f.read()
+        gpu = any(d.identity().family == hal.Family.GPU for d in self.devices)
+        creds = Credentials(user=user, password=(pc.password if pc else "") or "x", tls_root_cas_pem=ca,
+                            worker=user, version_rolling=self.cfg.mining.version_rolling,
+                            device="gfx950" if gpu else "cpu", hardware="v3.0.0",
+                            nominal_hashrate=self.current_hashrate)
+        session = await self._dial(url, creds)
+        self._session = session
+        self.connected = True
+        self.m.pool_connection_state.set(2)
+        self.log("info", f"engine: connected to {url} ({session.protocol.value})")
+        on_connected()
+        tasks = [asyncio.ensure_future(self._job_pump(session)), asyncio.ensure_future(self._share_pump(session)),
+                 asyncio.ensure_future(self._stats_loop(session)), asyncio.ensure_future(self._notice_pump(session))]
+        try:
+            closed = asyncio.ensure_future(session.wait_closed())
+            done, _ = await asyncio.wait(tasks + [closed], return_when=asyncio.FIRST_COMPLETED)
+            for t in done:
+                if t is not closed and t.exception() is not None:
+                    raise t.exception()
+            raise ConnectionError("engine: pool closed connection")
+        finally:
+            for t in tasks:
+                t.cancel()
+            await session.close()
+            self._session = None
+            self.miners.pause_all()
+            self._active_job = None
+            self._valid_jobs.clear()
+
+    async def _notice_pump(self, session) -> None:
+        while True:
+            n = await session.notices.get()
+            self.log("info", f"engine: pool notice: {n}")
+
+    async def _job_pump(self, session) -> None:
+        while True:
+            job = await session.jobs.get()
+            self.m.last_job_received.set(time.time())
+            if job is None:
+                self._active_job = None
+                self._valid_jobs.clear()
+                self.miners.pause_all()
+                continue
+            if job.clean_jobs:
+                if job.job_id not in self._valid_jobs:
+                    self._submitted.clear()
+                self._valid_jobs = {job.job_id}
+            else:
+                self._valid_jobs.add(job.job_id)
+            self._active_job = job
+            publish_difficulty(self.m, session.suggested_difficulty(), self.current_hashrate,
+                               float(2 ** 256) / self.algorithm.diff1)
+            if self.curtailed:
+                self.log("debug", f"engine: job {job.job_id} ignored (curtailed)")
+                continue
+            self.miners.set_job(job.template())
+            self.log("info", f"engine: job {job.job_id} version=0x{job.version:08X} active")
+
+    async def _share_pump(self, session) -> None:
+        while True:
+            shares = self.miners.poll(256)  # native queue drain; releases the GIL, never blocks
+            if not shares:
+                await asyncio.sleep(SHARE_POLL_INTERVAL)
+                continue
+            for s in shares:
+                self.m.shares_found.inc()
+                self.m.inc_shares_found_for_device(s["device_id"])
+                if s["job_id"] not in self._valid_jobs:
+                    self.m.stale_skipped.inc()
+                    continue
+                en2 = s["extranonce2"].to_bytes(8, "little")[: s["extranonce2_size"]] if s["extranonce2_size"] else b""
+                key = (s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
+                if key in self._submitted:  # defence in depth: never send a pool a duplicate
+                    continue
+                self._submitted.add(key)
+                sub = ShareSubmission(s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
+                t = asyncio.ensure_future(self._submit(session, sub, s.get("found_at", 0.0)))
+                self._submit_tasks.add(t)
+                t.add_done_callback(self._submit_tasks.discard)
+
+    async def _submit(self, session, sub: ShareSubmission, found_at: float = 0.0) -> None:
+        self.m.shares_submitted.inc()
+        try:
+            res = await session.submit(sub)
+        except Exception as exc:  # noqa: BLE001
+            self.log("warn", f"engine: submit share: {exc}")
+            return
+        if res.accepted:
+            self.m.shares_accepted.inc()
+            self.latency.record(res.latency_ms)
+            if found_at > 0:  # device verify -> pool accept (native queue + submit + pool validation)
+                self.pipeline_latency.record((time.monotonic() - found_at) * 1e3)
+            self.log("info", f"engine: share accepted job={sub.job_id} nonce=0x{sub.nonce:08X} "
+                             f"({res.latency_ms:.1f} ms)")
+        else:
+            cat, diag = reject_class(res.reason)
+            self.m.shares_rejected.inc()
+            self.m.reject_reason(cat).inc()
+            self.m.touch_last_reject(cat, time.time())
+            self.log("warn", f"engine: share rejected: {res.reason} ({diag})")
+
+    async def _stats_loop(self, session) -> None:
+        while True:
+            await asyncio.sleep(self.opts.stats_interval)
+            self.tick_stats(session)
+
+    def tick_stats(self, session=None) -> None:
+        now = self.opts.clock.now()
+        total = self.miners.total_hashes()
+        rate = self.hash_window.observe(total, now)
+        self.current_hashrate = rate
+        self.device_hashrates = self.miners.update_hashrates()
+        for dev, r in self.device_hashrates.items():
+            self.m.set_device_hashrate(dev, r)
+        shares = self.m.shares_found.value()
+        self.log("info", f"engine: hashrate={hashrate_string(rate)} shares={shares}")
+        dropped = self.miners.total_dropped()
+        if dropped > self._last_dropped:
+            self.log("warn", f"engine: dropped {dropped - self._last_dropped} found share(s) — share submission is "
+                             "not keeping up with discovery")
+            self._last_dropped = dropped
+        for dev, err in self.miners.faulted():
+            self.log("error", f"engine: device {dev} faulted: {err}")
+        if self.curtailed:
+            self.m.up.set(1)
+            self.stalled = False
+        else:
+            self._hashmon.observe(rate)
+            self.stalled = self._hashmon.stalled()
+            self.m.up.set(0 if self.stalled else 1)
+        self.est_sats = self._sats.observe(now, self.m.arbitration_expected_yield.value(), rate > 0 and not self.stalled)
+        self.m.hashrate.set(rate)
+        self._uptime.observe(now, rate > 0 and not self.stalled, self.m.productive_seconds)
+        self.m.effective_yield.set(effective_yield(self.m.arbitration_expected_yield.value(),
+                                                   float(self.m.productive_seconds.value()), self.m.uptime.value()))
+        if self.cfg.power_watts > 0:
+            self.m.power_watts.set(self.cfg.power_watts)
+            if rate > 0:
+                self.m.joules_per_terahash.set(self.cfg.power_watts * 1e12 / rate)
+        acc_rate, judged = self.m.update_share_rates()
+        if judged >= 20 and acc_rate < 0.97:
+            self.log("warn", f"engine: share acceptance {acc_rate * 100:.1f}% ({self.m.shares_accepted.value()}/"
+                             f"{judged}) — check the reject-reason breakdown")
+        p95 = self.latency.quantile(0.95)
+        if p95 > 0:
+            p50, p99 = self.latency.quantile(0.5), self.latency.quantile(0.99)
+            self.log("info", f"engine: submit latency p50={p50:.0f}ms p95={p95:.0f}ms p99={p99:.0f}ms")
+            self.m.submit_latency_p50.set(p50)
+            self.m.submit_latency_p95.set(p95)
+            self.m.submit_latency_p99.set(p99)
+        if session is not None:
+            publish_difficulty(self.m, session.suggested_difficulty(), rate, float(2 ** 256) / self.algorithm.diff1)
+        if self.dashboard is not None:
+            self.dashboard.update(self.stats())
+
+
+def update_stream(streams: dict[str, arb.Stream], q) -> str:
+    """Quote -> stream keyed provider:device; NET yield (fixes arbitrate.go:187-195)."""
+    key = f"{q.provider_id}:{q.device_id}"
+    s = streams.get(key) or arb.Stream(id=q.provider_id)
+    s.id = q.provider_id
+    s.accepts_families = list(q.accepted_families)
+    y = arb.Yield(q.yield_.net_sats_per_second, q.yield_.confidence)
+    if q.device_id:
+        s.yield_per_device[q.device_id] = y
+    s.default_yield = y
+    s.is_bitcoin_mining = q.provider_id == "mining.stratum"
+    streams[key] = s
+    return key
+
+
+def streams_slice(streams: dict[str, arb.Stream]) -> list[arb.Stream]:
+    merged: dict[str, arb.Stream] = {}
+    for s in streams.values():
+        rep = merged.get(s.id)
+        if rep is not None:
+            rep.yield_per_device.update(s.yield_per_device)
+        else:
+            merged[s.id] = arb.Stream(s.id, list(s.accepts_families), dict(s.yield_per_device), s.default_yield,
+                                      s.privacy_rating, s.environmental_rating, s.is_bitcoin_mining)
+    return list(merged.values())
+
+
+async def run(opts: Options) -> None:
+    await Engine(opts).run()
+
+
+__all__ = ["Engine", "Options", "curtail_decision", "mask_addr", "payout_addresses", "pool_urls", "run",
+           "session_user", "streams_slice", "update_stream"]

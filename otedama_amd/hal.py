@@ -1,0 +1,293 @@
+"""Hardware abstraction: device identities, capabilities, drivers, detection.
+
+Parity: internal/hal/{device,registry,gpu_linux}.go
+  * Family (asic|gpu|cpu), Identity(+validate), Capabilities ...... device.go:50-148
+  * Device / Driver / Detector contracts ........................... device.go:155-217
+  * Registry (sorted drivers, duplicate guard) ..................... registry.go:25-105
+  * Detect: every driver in parallel, identity validation,
+    partial-failure tolerant ....................................... registry.go:138-201
+  * GPULinuxDriver: /sys/class/drm/renderD* presence detection,
+    vendor 0x1002 = AMD, id "gpu-renderD128" ....................... gpu_linux.go:61-189
+
+MI355X-native difference: the reference hard-codes ``SHA256d = False`` for
+every GPU (gpu_linux.go:131) because it has no GPU compute. Here the HIP driver
+enumerates devices through the native runtime and reports the kernels that
+exist for the device's ISA: gfx950 -> sha256d, scrypt, x11 all true. The DRM
+driver is kept for non-HIP render nodes (presence only, no hashing), and
+render nodes that the HIP driver already owns are not reported twice.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import threading
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import Callable, Protocol
+
+
+class Family(str, Enum):
+    ASIC = "asic"
+    GPU = "gpu"
+    CPU = "cpu"
+
+
+class HalError(ValueError):
+    pass
+
+
+@dataclass(frozen=True)
+class Identity:
+    id: str
+    family: Family
+    vendor: str = ""
+    model: str = ""
+
+    def __str__(self) -> str:
+        return f"{self.family.value}[{self.id}: {self.model or 'unknown'}]"
+
+    def validate(self) -> None:
+        if not self.id:
+            raise HalError("hal: Identity.ID must not be empty")
+        if not isinstance(self.family, Family):
+            raise HalError(f"hal: Identity.Family {self.family!r} is not a valid Family")
+        for ch in self.id:
+            if ch in " \t\n/":
+                raise HalError(f"hal: Identity.ID contains forbidden character {ch!r}")
+
+
+@dataclass(frozen=True)
+class Capabilities:
+    sha256d: bool = False
+    general_compute: bool = False
+    scrypt: bool = False
+    x11: bool = False
+
+    def supports(self, algorithm: str) -> bool:
+        return bool(getattr(self, algorithm, False))
+
+
+class Device(Protocol):
+    def identity(self) -> Identity: ...
+
+    def capabilities(self) -> Capabilities: ...
+
+    def shutdown(self) -> None: ...
+
+
+@dataclass
+class SimpleDevice:
+    ident: Identity
+    caps: Capabilities
+    index: int = -1                 # HIP ordinal for GPUs
+    threads: int = 0                # CPU threads
+    extra: dict = field(default_factory=dict)
+
+    def identity(self) -> Identity:
+        return self.ident
+
+    def capabilities(self) -> Capabilities:
+        return self.caps
+
+    def shutdown(self) -> None:
+        return None
+
+
+class Driver(Protocol):
+    def name(self) -> str: ...
+
+    def enumerate(self) -> list: ...
+
+
+class CPUDriver:
+    """The built-in CPU device (engine/setup.go:274-297): SHA256d + general compute."""
+
+    def __init__(self, threads: int = 0):
+        self.threads = threads or (os.cpu_count() or 1)
+
+    def name(self) -> str:
+        return "cpu"
+
+    def enumerate(self) -> list:
+        model = _cpu_model()
+        return [SimpleDevice(Identity("cpu-0", Family.CPU, _cpu_vendor(), model),
+                             Capabilities(sha256d=True, general_compute=True, scrypt=True), threads=self.threads)]
+
+
+# ISA -> kernels compiled into the native extension (csrc/kernels)
+KERNEL_ISAS = {"gfx950": Capabilities(sha256d=True, general_compute=True, scrypt=True, x11=True)}
+
+
+class HIPDriver:
+    """GPU devices visible to the HIP runtime (one per ordinal)."""
+
+    def __init__(self, native_loader: Callable | None = None):
+        self._loader = native_loader
+
+    def name(self) -> str:
+        return "hip"
+
+    def enumerate(self) -> list:
+        try:
+            if self._loader is not None:
+                n = self._loader()
+            else:
+                from otedama_amd.ops.native import load
+
+                n = load(build_if_missing=False)
+        except Exception:  # noqa: BLE001
+            return []
+        if n is None:
+            return []
+        out = []
+        for i in range(n.gpu_device_count()):
+            arch = n.gpu_arch_name(i).split(":")[0]
+            caps = KERNEL_ISAS.get(arch, Capabilities(general_compute=True))
+            cus = n.gpu_cu_count(i)
+            model = "AMD Instinct MI355X" if arch == "gfx950" else f"AMD GPU ({arch})"
+            out.append(SimpleDevice(Identity(f"gpu-{i}", Family.GPU, "AMD", f"{model} {cus}CU {arch}"), caps,
+                                    index=i, extra={"arch": arch, "cus": cus}))
+        return out
+
+
+DRM_BASE_PATH = "/sys/class/drm"
+
+
+def infer_vendor_name(vendor_id: str) -> str:
+    return {"0x10de": "NVIDIA", "0x1002": "AMD", "0x8086": "Intel"}.get(vendor_id.strip(), "Unknown GPU vendor")
+
+
+def _read(path: str) -> str:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
+class GPULinuxDriver:
+    """Presence-only render-node detection (gpu_linux.go). Capability: general compute only."""
+
+    def __init__(self, base_path: str | None = None, skip_vendors: tuple[str, ...] = ()):
+        self.base_path = base_path or DRM_BASE_PATH
+        self.skip_vendors = skip_vendors
+
+    def name(self) -> str:
+        return "gpu_linux"
+
+    def enumerate(self) -> list:
+        try:
+            entries = sorted(os.listdir(self.base_path))
+        except OSError:
+            return []
+        seen, out = set(), []
+        for name in entries:
+            if not name.startswith("renderD"):
+                continue
+            dev_path = os.path.join(self.base_path, name, "device")
+            canonical = os.path.realpath(dev_path)
+            if canonical in seen:
+                continue
+            seen.add(canonical)
+            vendor_id = _read(os.path.join(canonical, "vendor"))
+            if vendor_id in self.skip_vendors:
+                continue
+            vendor = infer_vendor_name(vendor_id)
+            model = vendor + " GPU"
+            for line in _read(os.path.join(canonical, "uevent")).splitlines():
+                if line.startswith("PCI_ID="):
+                    model = f"{vendor} GPU ({line[7:]})"
+            ident = Identity(f"gpu-{name}", Family.GPU, vendor, model)
+            try:
+                ident.validate()
+            except HalError:
+                continue
+            out.append(SimpleDevice(ident, Capabilities(sha256d=False, general_compute=True)))
+        return out
+
+
+class Registry:
+    def __init__(self) -> None:
+        self._lock = threading.Lock()
+        self._drivers: dict[str, object] = {}
+
+    def register(self, d) -> None:
+        if d is None:
+            raise HalError("hal: cannot register nil driver")
+        name = d.name()
+        if not name:
+            raise HalError("hal: driver must have a non-empty name")
+        with self._lock:
+            if name in self._drivers:
+                raise HalError(f"hal: driver {name!r} is already registered")
+            self._drivers[name] = d
+
+    def drivers(self) -> list:
+        with self._lock:
+            return [self._drivers[k] for k in sorted(self._drivers)]
+
+    def lookup(self, name: str):
+        with self._lock:
+            return self._drivers.get(name)
+
+    def __len__(self) -> int:
+        return len(self._drivers)
+
+
+class Detector:
+    def __init__(self, registry: Registry | None = None, logger: Callable[[str, str, Exception], None] | None = None,
+                 timeout: float = 30.0):
+        self.registry = registry or Registry()
+        self.logger = logger
+        self.timeout = timeout
+
+    def detect(self) -> list:
+        drivers = self.registry.drivers()
+        if not drivers:
+            return []
+        out = []
+        with cf.ThreadPoolExecutor(max_workers=len(drivers)) as ex:
+            futs = {ex.submit(d.enumerate): d for d in drivers}
+            for fut in cf.as_completed(futs, timeout=self.timeout):
+                d = futs[fut]
+                try:
+                    devs = fut.result()
+                except Exception as exc:  # noqa: BLE001 - partial failure tolerated
+                    if self.logger:
+                        self.logger(d.name(), "enumerate failed", exc)
+                    continue
+                for dev in devs or []:
+                    try:
+                        dev.identity().validate()
+                    except HalError as exc:
+                        if self.logger:
+                            self.logger(d.name(), "device rejected due to invalid identity", exc)
+                        continue
+                    out.append(dev)
+        out.sort(key=lambda d: d.identity().id)
+        return out
+
+
+def default_registry(cpu_threads: int = 0, include_drm: bool = True) -> Registry:
+    r = Registry()
+    r.register(CPUDriver(cpu_threads))
+    r.register(HIPDriver())
+    if include_drm:
+        r.register(GPULinuxDriver(skip_vendors=("0x1002",)))  # AMD GPUs come from the HIP driver
+    return r
+
+
+def _cpu_model() -> str:
+    for line in _read("/proc/cpuinfo").splitlines():
+        if line.startswith("model name"):
+            return line.split(":", 1)[1].strip()
+    import platform
+
+    return platform.processor() or "CPU"
+
+
+def _cpu_vendor() -> str:
+    for line in _read("/proc/cpuinfo").splitlines():
+        if line.startswith("vendor_id"):
+            return line.split(":", 1)[1].strip()
+    return ""
