@@ -9,6 +9,7 @@
 #include <cstring>
 #include <stdexcept>
 
+#include "otedama/aead.h"
 #include "otedama/job.h"
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
@@ -133,6 +134,19 @@ PYBIND11_MODULE(_native, m) {
                 reinterpret_cast<const uint8_t*>(ms.data()), ms.size(), o);
     return to_bytes(o, 32);
   });
+  m.def("aead_seal", [](int kind, const py::bytes& key, const py::bytes& nonce, const py::bytes& plain,
+                        const py::bytes& aad) {
+    std::string out = aead_seal(static_cast<AeadKind>(kind), key, nonce, plain, aad);
+    return py::bytes(out);
+  }, py::arg("kind"), py::arg("key"), py::arg("nonce"), py::arg("plain"), py::arg("aad") = py::bytes());
+  m.def("aead_open", [](int kind, const py::bytes& key, const py::bytes& nonce, const py::bytes& sealed,
+                        const py::bytes& aad) -> py::object {
+    std::string out;
+    if (!aead_open(static_cast<AeadKind>(kind), key, nonce, sealed, aad, &out)) return py::none();
+    return py::bytes(out);
+  }, py::arg("kind"), py::arg("key"), py::arg("nonce"), py::arg("sealed"), py::arg("aad") = py::bytes());
+  m.attr("AEAD_AES256GCM") = 0;
+  m.attr("AEAD_CHACHA20POLY1305") = 1;
   m.def("scrypt_1024_1_1", [](const py::bytes& h) {
     std::string s = need(h, 80, "header"); uint8_t o[32];
     { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }

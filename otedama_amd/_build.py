@@ -33,6 +33,7 @@ CXX_SOURCES = [
     "cpu/sha256_cpu.cpp",
     "cpu/job_prepare.cpp",
     "cpu/x11_cpu.cpp",
+    "cpu/aead.cpp",
     "runtime/miner_common.cpp",
     "bindings.cpp",
 ]
@@ -107,7 +108,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         # which torch's bundled runtime also carries: ops.native imports torch
         # first, so the extension binds to the runtime already in the process
         # (two HIP/HSA runtimes in one process fail to enumerate the GPU).
-        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread"]
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread", "-lcrypto"]
         _compile(link, verbose)
         os.replace(tmp, out)
     return out

@@ -1,0 +1,112 @@
+"""``otedama pool`` — run the local validating Stratum pool [NO REFERENCE CODE].
+
+One process can serve several algorithms (``--algorithms sha256d,scrypt``):
+each gets its own SV2 + V1 listener pair (ports increment per algorithm), its
+own vardiff / diff1 constant and share journal, and all publish into one
+/metrics registry — the "mixed SHA-256d + scrypt workers" pool of BASELINE.json
+config 5.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import signal
+from typing import TextIO
+
+from otedama_amd.cli.flags import FlagSet
+from otedama_amd.cli.main import EXIT_CONFIG, EXIT_OK, EXIT_RUNTIME, parse_subcommand
+
+
+def _bump(addr: str, k: int) -> str:
+    if not addr:
+        return ""
+    h, _, p = addr.rpartition(":")
+    return f"{h}:{int(p) + k}" if p and int(p) else addr
+
+
+def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
+    fs = FlagSet("pool", stderr)
+    fs.string("algorithms", "sha256d", "Comma-separated algorithms to serve (sha256d, scrypt).")
+    fs.string("listen-sv2", "127.0.0.1:3336", "Stratum V2 listen address (port +1 per extra algorithm).")
+    fs.string("listen-v1", "127.0.0.1:3333", "Stratum V1 listen address (port +1 per extra algorithm).")
+    fs.string("payout-address", "", "Operator address paid by the coinbase (empty = OP_RETURN).")
+    fs.float("difficulty", 1.0, "Initial share difficulty.")
+    fs.float("share-seconds", 10.0, "Vardiff target seconds between shares per connection.")
+    fs.float("retarget-seconds", 30.0, "Vardiff retarget window.")
+    fs.float("block-interval", 600.0, "Seconds between synthetic network blocks.")
+    fs.float("job-interval", 30.0, "Seconds between job refreshes (new ntime).")
+    fs.string("journal", "", "SQLite share journal path (empty = in-memory).")
+    fs.string("payout-scheme", "pplns", "Block payout accounting: pplns | prop.")
+    fs.string("http-addr", "", "Address for /metrics /healthz /api/v1/pool (empty disables).")
+    fs.string("dialect", "reference", "SV2 wire dialect: reference | spec.")
+    fs.float("duration", 0.0, "Stop after this many seconds (0 = run until signalled).")
+    rc = parse_subcommand(fs, args, stdout, stderr)
+    if rc is not None:
+        return rc
+    algos = [a.strip() for a in fs["algorithms"].split(",") if a.strip()]
+    for a in algos:
+        if a not in ("sha256d", "scrypt"):
+            stderr.write(f"pool: unsupported algorithm {a!r} (sha256d, scrypt)\n")
+            return EXIT_CONFIG
+    if fs["payout-address"]:
+        from otedama_amd.config import validate_bitcoin_address
+
+        err = validate_bitcoin_address(fs["payout-address"])
+        if err:
+            stderr.write(f"pool: payout address invalid: {err}\n")
+            return EXIT_CONFIG
+    try:
+        return asyncio.run(_serve(fs, algos, stdout))
+    except OSError as exc:
+        stderr.write(f"pool: {exc}\n")
+        return EXIT_RUNTIME
+
+
+async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
+    from otedama_amd.httpserver import HTTPServer
+    from otedama_amd.metrics import Registry
+    from otedama_amd.pool.server import PoolOptions, PoolServer
+
+    reg = Registry()
+    pools = []
+    for k, algo in enumerate(algos):
+        journal = fs["journal"]
+        if journal and len(algos) > 1:
+            journal = journal.replace(".db", f".{algo}.db") if journal.endswith(".db") else f"{journal}.{algo}"
+        opts = PoolOptions(algorithm=algo, listen_sv2=_bump(fs["listen-sv2"], k), listen_v1=_bump(fs["listen-v1"], k),
+                           payout_address=fs["payout-address"] or None, initial_difficulty=fs["difficulty"],
+                           target_share_seconds=fs["share-seconds"], retarget_seconds=fs["retarget-seconds"],
+                           block_interval=fs["block-interval"], job_interval=fs["job-interval"],
+                           journal_path=journal or ":memory:", payout_scheme=fs["payout-scheme"],
+                           dialect=fs["dialect"])
+
+        def log(level, msg):
+            stdout.write(f"[{level}] {msg}\n")
+            stdout.flush()
+
+        p = PoolServer(opts, reg, log)
+        await p.start()
+        pools.append(p)
+    srv = None
+    if fs["http-addr"]:
+        srv = HTTPServer(fs["http-addr"], reg, api={"pool": lambda: [p.stats() for p in pools],
+                                                    "stats": lambda: [p.stats() for p in pools]})
+        srv.start()
+        srv.set_ready(True)
+        stdout.write(f"[info] http: listening on {srv.addr}\n")
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    if fs["duration"] > 0:
+        loop.call_later(fs["duration"], stop.set)
+    await stop.wait()
+    for p in pools:
+        stdout.write(json.dumps(p.stats()) + "\n")
+        await p.stop()
+    if srv:
+        srv.stop()
+    return EXIT_OK

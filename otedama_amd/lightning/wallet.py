@@ -1,0 +1,130 @@
+"""WalletManager: create-or-unlock the encrypted seed under the data directory.
+
+Parity: internal/lightning/wallet.go
+  * NewWalletManager: dataDir/passphrase required, dir 0700, create on first
+    run else decrypt ........................................... wallet.go:108-150
+  * Seed / Fingerprint / Mnemonic (first run only) / IsNew ....... wallet.go:153-170
+  * createNew: 256-bit entropy → mnemonic → seed, wallet.fingerprint
+    written best-effort ......................................... wallet.go:175-203
+  * loadExisting: opaque unlock error ............................ wallet.go:206-225
+  * save: temp file → fsync → chmod 0600 → rename ................ wallet.go:228-277
+  * ChangePassphrase ............................................. wallet.go:282-303
+Also the one-time recovery-phrase banner the engine prints
+(internal/engine/setup.go:175-197): written to the console stream, never a log.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+from pathlib import Path
+
+from otedama_amd.lightning import seed as S
+from otedama_amd.lightning import seedstore as SS
+
+WALLET_FILE = "wallet.dat"
+FINGERPRINT_FILE = "wallet.fingerprint"
+
+
+class WalletError(S.SeedError):
+    pass
+
+
+class WalletManager:
+    def __init__(self, data_dir: str, passphrase: str, reader: S.Reader | None = None,
+                 wordlist: S.WordList | None = None, mnemonic_passphrase: str = ""):
+        if not data_dir:
+            raise WalletError("lightning: dataDir must not be empty")
+        if not passphrase:
+            raise WalletError("lightning: passphrase must not be empty")
+        self.data_dir = Path(data_dir)
+        self.wordlist = wordlist or S.english_wordlist()
+        self._seed = b""
+        self._mnemonic: list[str] | None = None
+        self.data_dir.mkdir(mode=0o700, parents=True, exist_ok=True)
+        if not (self.data_dir / WALLET_FILE).exists():
+            self._create(passphrase, mnemonic_passphrase, reader)
+        else:
+            self._load(passphrase)
+
+    @property
+    def seed(self) -> bytes:
+        return self._seed
+
+    @property
+    def fingerprint(self) -> str:
+        return S.fingerprint(self._seed)
+
+    @property
+    def mnemonic(self) -> list[str] | None:
+        return self._mnemonic
+
+    @property
+    def is_new(self) -> bool:
+        return self._mnemonic is not None
+
+    def _create(self, passphrase: str, mnemonic_passphrase: str, reader) -> None:
+        entropy = S.generate_entropy(S.DEFAULT_ENTROPY_BITS, reader)
+        words = S.entropy_to_mnemonic(entropy, self.wordlist)
+        seed = S.mnemonic_to_seed(words, mnemonic_passphrase)
+        self._seed, self._mnemonic = seed, words
+        self._save(seed, passphrase, reader)
+        try:
+            fp = self.data_dir / FINGERPRINT_FILE
+            fp.write_text(S.fingerprint(seed))
+            os.chmod(fp, 0o600)
+        except OSError:
+            pass  # UI convenience only; recomputable from the seed
+
+    def _read(self) -> SS.EncryptedSeed:
+        try:
+            raw = (self.data_dir / WALLET_FILE).read_bytes()
+        except OSError as exc:
+            raise WalletError(f"lightning: read wallet file: {exc}") from exc
+        try:
+            return SS.unmarshal(raw)
+        except S.SeedError as exc:
+            raise WalletError(f"lightning: unmarshal wallet: {exc}") from exc
+
+    def _load(self, passphrase: str) -> None:
+        try:
+            self._seed = SS.decrypt_seed(self._read(), passphrase)
+        except S.SeedError:
+            raise WalletError("lightning: wallet unlock failed — check your passphrase") from None
+
+    def _save(self, seed: bytes, passphrase: str, reader) -> None:
+        raw = SS.encrypt_seed(seed, passphrase, reader).marshal()
+        fd, tmp = tempfile.mkstemp(prefix=".wallet-", suffix=".tmp", dir=self.data_dir)
+        try:
+            with os.fdopen(fd, "wb") as f:
+                f.write(raw)
+                f.flush()
+                os.fsync(f.fileno())
+            os.chmod(tmp, 0o600)
+            os.replace(tmp, self.data_dir / WALLET_FILE)
+        except BaseException:
+            try:
+                os.unlink(tmp)
+            except OSError:
+                pass
+            raise
+
+    def change_passphrase(self, old: str, new: str, reader: S.Reader | None = None) -> None:
+        if not new:
+            raise WalletError("lightning: new passphrase must not be empty")
+        try:
+            seed = SS.decrypt_seed(self._read(), old)
+        except SS.WrongPassphrase:
+            raise WalletError("lightning: incorrect old passphrase") from None
+        self._save(seed, new, reader)
+
+
+def recovery_phrase_banner(mnemonic: list[str] | None, fingerprint: str) -> str:
+    if not mnemonic:
+        return ""
+    bar = "=" * 72
+    return (f"\n{bar}\n  WALLET RECOVERY PHRASE — SHOWN ONCE, NEVER AGAIN\n{bar}\n\n"
+            f"  {' '.join(mnemonic)}\n\n  Fingerprint: {fingerprint}\n\n"
+            f"  Write these {len(mnemonic)} words on paper, in order, and keep them\n"
+            "  offline. They are the ONLY way to recover the wallet if wallet.dat\n"
+            "  is lost. Otedama will not display them again.\n"
+            f"{bar}\n\n")
