@@ -98,7 +98,7 @@ def main() -> int:
         hdr, params = variant_params(i)
         r = search.launch(params, 0, 1 << 32)  # K1: full 2^32 nonce space
         if world > 1:  # R2: on-device hit buffers, gathered on the comm stream
-            comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered, r.buf))
+            comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered.view(-1), r.buf.view(-1)))
         else:
             gathered[0].copy_(r.buf)
         counters_hashes += 1 << 32

@@ -98,17 +98,54 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     if fs["dry-run"]:
         stdout.write("dry-run: configuration is valid; would start run\n")
         return EXIT_OK
+    node = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # torchrun node mode: one rank per GPU; rank 0 is the pool-facing engine
+        from otedama_amd.parallel.comm import NodeComm, init_from_env
+
+        info = init_from_env()
+        cfg.mining.gpus = str(info.local_rank)
+        cfg.mining.cpu_threads = 0  # equal device count per rank keeps the stripes disjoint
+        if info.rank > 0:
+            return _run_node_worker(cfg, info, NodeComm(info), stdout)
+        node = NodeComm(info)
+        no_tui = True
     logln("info", i18n.STARTUP_READY)
     pool_url = cfg.pools[0].url if cfg.pools else C.DEFAULT_POOL_URL
     logln("info", i18n.STARTUP_POOL_CONNECTING, {"url": pool_url})
     structlog, close_log = build_logger(no_tui, fs["log-file"], cfg, stdout)
     try:
-        return asyncio.run(_run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, stdout, stderr, logln))
+        return asyncio.run(_run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, stdout, stderr, logln,
+                                      node))
     finally:
         close_log()
+        if node is not None:
+            from otedama_amd.parallel.comm import shutdown
+
+            shutdown(node.info)
 
 
-async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, stdout, stderr, logln) -> int:
+def _run_node_worker(cfg, info, comm, stdout) -> int:
+    """Ranks > 0 of a torchrun node: mine rank 0's jobs on the local GPU until rank 0 stops."""
+    from otedama_amd import hal
+    from otedama_amd.engine.miners import MinerSet
+    from otedama_amd.parallel.comm import shutdown
+    from otedama_amd.parallel.node import NodeWorker
+
+    devs = hal.Detector(hal.default_registry(0)).detect()
+    devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == info.local_rank]
+    local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0, rank=info.rank,
+                     world_size=info.world_size)
+    stdout.write(f"[info] node: rank {info.rank}/{info.world_size} mining on GPU {info.local_rank} "
+                 f"({len(local)} device(s))\n")
+    try:
+        NodeWorker(local, comm).run()
+    finally:
+        shutdown(info)
+    return EXIT_OK
+
+
+async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, stdout, stderr, logln, node=None) -> int:
     from otedama_amd.engine.run import Engine, Options
     from otedama_amd.httpserver import HTTPServer
     from otedama_amd.metrics import Registry
@@ -135,7 +172,7 @@ async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, std
     engine = Engine(Options(config=cfg, output=stdout, logger=structlog.adapter(), no_tui=no_tui,
                             wallet_passphrase=wallet_pass, wallet_mnemonic_passphrase=mnemonic_pass, metrics=reg,
                             on_ready=(srv.set_ready if srv else None), enable_ai_provider=fs["enable-ai-provider"],
-                            dashboard=dashboard))
+                            dashboard=dashboard, node_comm=node))
     eng_holder["e"] = engine
     loop = asyncio.get_running_loop()
     task = asyncio.ensure_future(engine.run())

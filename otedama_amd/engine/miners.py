@@ -72,10 +72,12 @@ class MinerSet:
         for m in self.miners:
             m.native.stop()
 
-    def set_job(self, template: dict | None) -> int:
-        """Hand a job template to every non-paused device; returns the new epoch."""
+    def set_job(self, template: dict | None, epoch: int | None = None) -> int:
+        """Hand a job template to every non-paused device; returns the new epoch.
+
+        ``epoch`` is given by node workers so hits map back to rank 0's job table."""
         with self._lock:
-            self._epoch += 1
+            self._epoch = epoch if epoch is not None else self._epoch + 1
             self._template = dict(template) if template is not None else None
             for m in self.miners:
                 self._apply(m)

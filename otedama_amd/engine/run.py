@@ -84,6 +84,7 @@ class Options:
     rates_interval: float = 300.0
     fetch_rates: bool = True
     dashboard: object | None = None
+    node_comm: object | None = None          # parallel.comm.NodeComm when launched under torchrun
 
 
 def curtail_decision(curr: bool, rate: float, fresh: bool, threshold: float) -> tuple[bool, bool]:
@@ -190,8 +191,15 @@ class Engine:
             self.log("info", f"engine: detected {len(self.devices)} device(s)")
             for d in self.devices:
                 self.log("info", f"engine: device {d.identity()} caps={d.capabilities()}")
+            node = self.opts.node_comm
+            world = node.info.world_size if node is not None else 1
             self.miners = MinerSet(self.devices, self.algorithm.name, cfg.mining.batch_nonces, cfg.mining.cpu_threads,
-                                   log=self.log)
+                                   rank=0, world_size=world, log=self.log)
+            if node is not None and world > 1:
+                from otedama_amd.parallel.node import NodeMinerSet
+
+                self.miners = NodeMinerSet(self.miners, node, log=self.log)
+                self.log("info", f"engine: node mode, {world} ranks over {node.info.backend}")
             if len(self.miners) == 0:
                 raise RuntimeError(f"engine: no device can mine {self.algorithm.name}")
             self.miners.start()

@@ -26,7 +26,8 @@ import torch.distributed as dist
 
 JOB_BLOB_BYTES = 4096
 SHARE_SLOTS = 64
-SHARE_WORDS = 8  # epoch_lo, epoch_hi, nonce, ntime, version, en2_lo, en2_hi, device
+SHARE_WORDS = 9  # epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_hi, rank|device, found_at_us
+COUNTER_WORDS = 4  # hashes, shares, dropped, faulted
 
 
 @dataclass
@@ -85,7 +86,9 @@ class NodeComm:
         self._job = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8, device=dev)
         self._slots = torch.zeros(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
         self._gathered = torch.zeros(info.world_size, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
-        self._counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        self._counters = torch.zeros(COUNTER_WORDS, dtype=torch.int64, device=dev)
+        self._counter_rows = torch.zeros(info.world_size, COUNTER_WORDS, dtype=torch.int64, device=dev)
+        self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)
         self.stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
 
     # ---------------------------------------------------------------- R1
@@ -117,10 +120,11 @@ class NodeComm:
             host[i] = torch.tensor([
                 e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
                 en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
+                int(s.get("found_at", 0.0) * 1e6),
             ], dtype=torch.int64)
         self._slots.copy_(host)
         if self.info.world_size > 1:
-            self._run(lambda: dist.all_gather_into_tensor(self._gathered, self._slots))
+            self._run(lambda: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots))
         else:
             self._gathered[0].copy_(self._slots)
         out = []
@@ -133,7 +137,7 @@ class NodeComm:
                     "epoch": rec[0] | ((rec[1] & 0x7FFFFFFF) << 32), "nonce": rec[2] & 0xFFFFFFFF,
                     "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
                     "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
-                    "device_index": rec[7] & 0xFFFF,
+                    "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6,
                 })
         return out
 
@@ -143,6 +147,24 @@ class NodeComm:
         if self.info.world_size > 1:
             self._run(lambda: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM))
         return tuple(int(x) for x in self._counters.cpu().tolist())
+
+    def gather_counters(self, values: list[int]) -> list[list[int]]:
+        """R3 variant for per-device stats: every rank's COUNTER_WORDS counters (all_gather, 32 B/rank)."""
+        mine = torch.tensor(list(values)[:COUNTER_WORDS] + [0] * (COUNTER_WORDS - len(values)), dtype=torch.int64)
+        self._counters.copy_(mine)
+        if self.info.world_size > 1:
+            self._run(lambda: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters))
+        else:
+            self._counter_rows[0].copy_(self._counters)
+        return self._counter_rows.cpu().tolist()
+
+    def broadcast_control(self, words: list[int]) -> list[int]:
+        """R1 control word (seq, stop, ...): 4 int64, every tick; the job blob follows only on change."""
+        if self.info.is_primary:
+            self._ctl.copy_(torch.tensor(list(words)[:4] + [0] * (4 - len(words)), dtype=torch.int64))
+        if self.info.world_size > 1:
+            self._run(lambda: dist.broadcast(self._ctl, src=0))
+        return self._ctl.cpu().tolist()
 
     def allreduce_max(self, value: float) -> float:
         t = torch.tensor([value], dtype=torch.float64, device=self.info.device)

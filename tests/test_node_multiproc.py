@@ -1,0 +1,113 @@
+"""Multi-process node (world_size 2, gloo on CPU): R1 job fan-out, R2 share fan-in,
+R3 counters, disjoint stripes, remote pause and clean stop.
+
+Same code path as the RCCL node on MI355X (parallel/node.py); only the
+backend and the miner (native CpuMiner instead of GpuMiner) differ.
+"""
+import json
+import os
+import socket
+import time
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from otedama_amd import hal
+from otedama_amd.models.header import int_to_hash, sha256d
+
+WORLD = 2
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _job() -> dict:
+    hdr = bytes([1, 0, 0, 0]) + bytes(range(32)) + bytes(range(32, 64)) + (1700000000).to_bytes(4, "little") + \
+        bytes.fromhex("ffff001d") + bytes(4)
+    return {"header": hdr, "target": int_to_hash(1 << 240), "job_id": "job-A", "algo": "sha256d",
+            "version_mask": 0x1FFFE000}
+
+
+def _worker(rank: int, port: int, out_path: str) -> None:
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from otedama_amd.engine.miners import MinerSet
+    from otedama_amd.parallel.comm import NodeComm, init_from_env, shutdown
+    from otedama_amd.parallel.node import NodeMinerSet, NodeWorker
+
+    info = init_from_env(backend="gloo", use_gpu=False)
+    dev = [hal.SimpleDevice(hal.Identity(f"cpu-{rank}", hal.Family.CPU, "t", "cpu"),
+                            hal.Capabilities(sha256d=True, general_compute=True), threads=1)]
+    local = MinerSet(dev, "sha256d", rank=info.rank, world_size=info.world_size)
+    comm = NodeComm(info)
+    if rank > 0:
+        NodeWorker(local, comm, tick=0.005).run()
+        shutdown(info)
+        return
+    node = NodeMinerSet(local, comm, tick=0.005)
+    node.start()
+    ep = node.set_job(_job())
+    shares, deadline = [], time.monotonic() + 20
+    while time.monotonic() < deadline:
+        shares += node.poll(256)
+        if sum(1 for s in shares if s["device_id"] == "rank1") >= 3 and len(shares) >= 6:
+            break
+        time.sleep(0.02)
+    node.update_hashrates()
+    stats = node.device_stats()
+    total = node.total_hashes()
+    # pause the remote rank, wait for its counter to freeze
+    node.pause_device("rank1", True)
+    time.sleep(0.3)
+    h1 = node.device_stats()["rank1"]["hashes"]
+    time.sleep(0.3)
+    h2 = node.device_stats()["rank1"]["hashes"]
+    node.stop()
+    shutdown(info)
+    with open(out_path, "w") as f:
+        json.dump({"epoch": ep, "shares": shares, "stats": stats, "total": total, "paused_delta": h2 - h1,
+                   "len": len(node)}, f, default=str)
+
+
+def test_node_two_ranks(tmp_path):
+    out = tmp_path / "out.json"
+    mp.start_processes(_worker, args=(_port(), str(out)), nprocs=WORLD, join=True, start_method="spawn")
+    res = json.loads(out.read_text())
+    shares = res["shares"]
+    remote = [s for s in shares if s["device_id"] == "rank1"]
+    local = [s for s in shares if s["device_id"] != "rank1"]
+    assert len(remote) >= 3 and local
+    assert res["len"] == 2 and "rank1" in res["stats"] and res["stats"]["rank1"]["hashes"] > 0
+    assert res["total"] >= res["stats"]["rank1"]["hashes"]
+    job = _job()
+    for s in shares:
+        assert s["job_id"] == "job-A" and int(s["epoch"]) == res["epoch"]
+        hdr = bytearray(job["header"])
+        hdr[0:4] = int(s["version"]).to_bytes(4, "little")
+        hdr[68:72] = int(s["ntime"]).to_bytes(4, "little")
+        hdr[76:80] = int(s["nonce"]).to_bytes(4, "little")
+        assert int.from_bytes(sha256d(bytes(hdr)), "little") <= 1 << 240
+        # disjoint stripes: variant parity (lowest rolled version bit 13) == rank
+        rank = 1 if s["device_id"] == "rank1" else 0
+        assert (int(s["version"]) >> 13) & 1 == rank
+    assert res["paused_delta"] == 0
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1])
+def test_nodecomm_single_rank_paths(n):
+    from otedama_amd.parallel.comm import DistInfo, NodeComm
+
+    c = NodeComm(DistInfo())
+    assert c.broadcast_control([5, 0, 9]) == [5, 0, 9, 0]
+    assert c.gather_counters([1, 2, 3, 4]) == [[1, 2, 3, 4]]
+    got = c.gather_shares([{"epoch": 3, "nonce": 7, "ntime": 1, "version": 2, "extranonce2": 1 << 40,
+                            "found_at": 12.5}])
+    assert got[0]["extranonce2"] == 1 << 40 and got[0]["found_at"] == 12.5 and got[0]["epoch"] == 3
