@@ -218,8 +218,10 @@ def resolve_with_origins(from_file: Config, env: dict[str, str] | None, flags: F
         cfg.pools, o["pools"] = list(f.pools), ValueOrigin.FILE
     if f.workers.name:
         cfg.workers.name, o["worker_name"] = f.workers.name, ValueOrigin.FILE
+    file_keys = getattr(f, "_file_keys", None)
     for name in ("language", "log_level", "log_format", "data_dir", "http_addr"):
-        if getattr(f, name):
+        set_in_file = name in file_keys if file_keys is not None else getattr(f, name) != getattr(cfg, name)
+        if getattr(f, name) and set_in_file:
             setattr(cfg, name, getattr(f, name))
             o[name] = ValueOrigin.FILE
     # zero-value caveat: a numeric 0 in the file means "unset" (config.go:427-457)
@@ -350,7 +352,10 @@ def _decode_strict(cls, data, path: str):
 
 def parse_config_yaml(text: str) -> Config:
     data = yaml.safe_load(text) if text.strip() else None
-    return _decode_strict(Config, data, "")
+    cfg = _decode_strict(Config, data, "")
+    # keys the file actually set (Go decodes into zero values, so only these count as FILE origin)
+    cfg._file_keys = set(data) if isinstance(data, dict) else set()
+    return cfg
 
 
 def load_config_file(path: str | os.PathLike | None) -> tuple[Config, str | None]:
