@@ -61,6 +61,7 @@ def main() -> int:
     ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
+    ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
     ap.add_argument("--no-latency", action="store_true")
     args = ap.parse_args()
 
@@ -141,7 +142,7 @@ def main() -> int:
         from otedama_amd.models.algorithms import ALGORITHMS
         from otedama_amd.models.header import int_to_hash
 
-        sc = ScryptSearch(dev, gap=args.scrypt_gap)
+        sc = ScryptSearch(dev, gap=args.scrypt_gap, kernel=args.scrypt_kernel)
         starget = int_to_hash(ALGORITHMS["scrypt"].diff1)
         hdr, _, _, _ = N.variant_header(job, stripe.start)
         sparams = N.scrypt_prepare(hdr, starget)
@@ -158,7 +159,7 @@ def main() -> int:
         selapsed = comm.allreduce_max(time.perf_counter() - t0)
         stotal = comm.allreduce_counters(ssteps * sc.batch)[0] if world > 1 else ssteps * sc.batch
         scrypt_hps = stotal / selapsed
-        scrypt_info = {"lookup_gap": sc.gap, "lanes": sc.batch, "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2)}
+        scrypt_info = {"kernel": sc.kernel, "lookup_gap": 1 if sc.kernel == "coop" else sc.gap, "lanes": sc.batch, "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2)}
         del sc
         torch.cuda.empty_cache()
 

@@ -191,6 +191,102 @@ __device__ __forceinline__ void scrypt_romix(uint32_t X[32], uint4* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lane-cooperative ROMix (GAP 1). Measured on the per-lane kernel above
+// (profiles/r1): the texture path is ~95% busy and L2 sees ~3 read requests per
+// 128-byte lookup, because every vector-memory instruction carries 64 lanes x
+// 16 B of 64 unrelated lines - the 8 partial-line loads of an entry thrash the
+// L1 between instructions, and the 8 partial-line stores of the write phase
+// cost the same address/tag work. Here every pad access is full-line: the 8
+// lanes of an octet move ONE 128-byte entry (lane `slot` handles chunk
+// slot ^ swz(owner)), and entries change hands through a wave-private 4 KiB LDS
+// tile (32 owner rows of 8 chunks; owner s's chunk c at s*8 + (c ^ swz(s)), so
+// owner-side ds_*_b128 and the lane-linear octet side are both conflict-free).
+//   write phase: owners stage X into the tile, octets store full lines (2 halves)
+//   read phase : owners 0..31 by LDS-DMA (buffer_load ... lds), owners 32..63
+//                register-staged, ONE vmcnt wait per lookup, then the staged
+//                half is written to the tile after the first half is consumed.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void glds_lptr_t;
+typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t coop_swz(uint32_t s_local) {
+  return ((s_local >> 1) & 3u) | (((s_local >> 3) & 1u) << 2);
+}
+
+// tile: this wave's 4 KiB LDS tile (wave-uniform). rs: buffer descriptor over this wave's 8 MiB pad.
+__device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
+                                                  uint32_t lane) {
+  char* tb = reinterpret_cast<char*>(tile);
+  for (int i = 0; i < 1024; ++i) {
+    // Lane-derived constants are recomputed each iteration (a few VALU) rather than hoisted into
+    // loop-invariant VGPRs that would stay live through BlockMix and cost occupancy.
+    uint32_t ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t slot = ln & 7u, octet = ln >> 3, own = ln & 31u;
+    const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);  // owner row, swizzled chunk 0 (bytes)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous reads of the tile retired
+      if ((ln >> 5) == uint32_t(h)) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          *reinterpret_cast<uint4*>(tb + (rd ^ (uint32_t(c) << 4))) =
+              make_uint4(X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint4 v = tile[64 * r + ln];
+        const uint32_t owner = uint32_t(32 * h + 8 * r) + octet;
+        const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));  // slot ^ swz(8r+octet)
+        const coop_v4u vv = {v.x, v.y, v.z, v.w};
+        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (uint32_t(i) << 13) | (owner << 7) | (chunk << 4), 0, 0);
+      }
+    }
+    blockmix(X);
+  }
+  for (int i = 0; i < 1024; ++i) {
+    uint32_t ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t slot = ln & 7u, octet = ln >> 3, own = ln & 31u;
+    const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);
+    const uint32_t j = X[16] & 1023u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile free (previous iteration's reads retired)
+    coop_v4u R[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));
+      const uint32_t o0 = uint32_t(8 * r) + octet, o1 = o0 + 32u;
+      const uint32_t j0 = uint32_t(__shfl(int(j), int(o0), 64));
+      const uint32_t j1 = uint32_t(__shfl(int(j), int(o1), 64));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (glds_lptr_t*)(tile + 64 * r), 16, (j0 << 13) | (o0 << 7) | (chunk << 4),
+                                               0, 0, 0);
+      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j1 << 13) | (o1 << 7) | (chunk << 4), 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ln < 32u) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
+        X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[64 * r + ln] = make_uint4(R[r].x, R[r].y, R[r].z, R[r].w);
+    __builtin_amdgcn_wave_barrier();
+    if (ln >= 32u) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
+        X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
+      }
+    }
+    blockmix(X);
+  }
+}
+
 }  // namespace
 
 // The three stages are separate launches so the ROMix kernel is register-lean
@@ -221,6 +317,46 @@ __global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* _
   }
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop(uint32_t count, uint4* __restrict__ xbuf,
+                                                             uint4* __restrict__ V) {
+  __shared__ uint4 tiles[4 * 256];  // 4 waves x 4 KiB half-tiles
+  const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
+  const uint32_t lane = uint32_t(slot & 63u);
+  // Wave-uniform values made provably uniform (readfirstlane) so the pad descriptor and the LDS-DMA base
+  // (M0) live in SGPRs.
+  const uint64_t wave = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot >> 32))) << 26) |
+                        uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot) >> 6));
+  uint4* Vw = V + wave * (1024ull * 64u * 8u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Vw, (short)0, 1024 * 64 * 128, 0x00020000);
+  (void)Vw;
+  uint4* tile = tiles + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256;
+  // count is a multiple of 64 (launcher rounds up), so whole waves iterate together and every lane of a wave
+  // reaches the cooperative loads and __shfl.
+  for (uint64_t i = slot; i < count; i += nslots) {
+    uint32_t X[32];
+    load_entry(xbuf + (i << 3), X);
+    scrypt_romix_coop(X, rs, tile, lane);
+    store_entry(xbuf + (i << 3), X);
+  }
+}
+
+// Same per-lane ROMix (gap 1) pinned to 8 waves/SIMD (64 VGPRs, no spill) for A/B against the
+// compiler's default 67-VGPR / 7-wave allocation.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_w8(
+    uint32_t count, uint4* __restrict__ xbuf, uint4* __restrict__ V) {
+  const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
+  uint4* Vw = V + (slot >> 6) * (1024ull * 64u * 8u);
+  const uint32_t lane = uint32_t(slot & 63u);
+  for (uint64_t i = slot; i < count; i += nslots) {
+    uint32_t X[32];
+    load_entry(xbuf + (i << 3), X);
+    scrypt_romix<1>(X, Vw, lane);
+    store_entry(xbuf + (i << 3), X);
+  }
+}
+
 // out[0]: candidate count; out[1..cap]: nonces.
 extern "C" __global__ __launch_bounds__(256) void otd_scrypt_pbkdf_out(const otedama::ScryptParams p, uint32_t base,
                                                                        uint32_t count, const uint4* __restrict__ xbuf,
@@ -244,17 +380,28 @@ namespace otedama {
 
 // Scratchpad bytes for `grid` ROMix blocks of 256 lane slots at lookup gap `gap`.
 uint64_t scrypt_scratch_bytes(int grid, int gap) {
+  if (gap == kScryptCoop || gap == kScryptLaneW8) gap = 1;
   return uint64_t(grid) * 256ull * (1024ull / uint64_t(gap)) * 128ull;
 }
 
 // xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
+// gap: 1/2/4 = per-lane ROMix with that lookup gap; kScryptCoop = lane-cooperative ROMix (gap 1).
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
                                 int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream) {
   uint4* X = static_cast<uint4*>(xbuf);
   uint4* V = static_cast<uint4*>(scratch);
   const int eg = int((count + 255) / 256);
+  // The cooperative kernel runs whole waves (shfl + octet loads): round its count up to 64 lanes. xbuf is
+  // allocated in multiples of 256 lanes, and lanes past `count` are ignored by pbkdf_out.
+  const uint32_t count64 = (count + 63u) & ~63u;
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
+    case kScryptCoop:
+      hipLaunchKernelGGL(otd_scrypt_romix_coop, dim3(grid), dim3(256), 0, stream, count64, X, V);
+      break;
+    case kScryptLaneW8:
+      hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);
+      break;
     case 1: hipLaunchKernelGGL(otd_scrypt_romix<1>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
     case 2: hipLaunchKernelGGL(otd_scrypt_romix<2>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
     case 4: hipLaunchKernelGGL(otd_scrypt_romix<4>, dim3(grid), dim3(256), 0, stream, count, X, V); break;

@@ -82,8 +82,16 @@ class ScryptSearch:
     """scrypt(1024,1,1) search: PBKDF2-in -> ROMix (HBM scratchpad) -> PBKDF2-out."""
 
     def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, gap: int = 1,
-                 lanes_per_slot: int = 1):
+                 lanes_per_slot: int = 1, kernel: str = "coop"):
+        """kernel="coop": lane-cooperative full-line ROMix (gap 1 only, the fast path);
+        kernel="lane": one lane per hash with lookup gap 1/2/4. Raw native codes
+        (SCRYPT_COOP / SCRYPT_LANE_W8) may also be passed as ``gap``."""
         self.native = require_native()
+        if kernel not in ("coop", "lane"):
+            raise ValueError(f"kernel must be 'coop' or 'lane', got {kernel!r}")
+        if kernel == "coop" and gap == 1:
+            gap = self.native.SCRYPT_COOP
+        self.kernel = "coop" if gap == self.native.SCRYPT_COOP else "lane"
         self.device = torch.device(device)
         self.cap = cap
         self.gap = gap

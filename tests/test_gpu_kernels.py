@@ -91,14 +91,18 @@ def test_sha256d_wraps_nonce_space():
     assert got == ref
 
 
-@pytest.mark.parametrize("gap", [1, 2, 4])
-def test_scrypt_matches_hashlib(gap):
+# kernel "coop" = lane-cooperative full-line ROMix (gap 1); "lane" = one lane per hash at gap 1/2/4, and
+# native code 9 = per-lane gap 1 pinned to 8 waves/SIMD. n = 200 is not a multiple of 64 (the cooperative
+# kernel rounds its wave count up).
+@pytest.mark.parametrize("gap,n,kernel", [(1, 192, "lane"), (2, 192, "lane"), (4, 192, "lane"), (1, 192, "coop"),
+                                          (1, 200, "coop"), (9, 200, "lane")])
+def test_scrypt_matches_hashlib(gap, n, kernel):
     from otedama_amd.models.header import int_to_hash
     from otedama_amd.ops.search import ScryptSearch
 
     hdr = os.urandom(76) + bytes(4)
-    sc = ScryptSearch("cuda:0", grid=8, gap=gap, cap=1024)
-    n = 192
+    sc = ScryptSearch("cuda:0", grid=8, gap=gap, cap=1024, kernel=kernel)
+    assert sc.kernel == kernel
     # target: ~1/4 of hashes pass -> checks filtering as well as hashing
     target_int = (1 << 254) - 1
     got = sorted(sc.search(hdr, int_to_hash(target_int), 5000, n))
@@ -111,15 +115,20 @@ def test_scrypt_matches_hashlib(gap):
     assert got == ref and 0 < len(ref) < n
 
 
-def test_scrypt_more_lanes_than_slots():
-    """count > grid*256 exercises the grid-stride reuse of a scratchpad slot."""
+@pytest.mark.parametrize("kernel", ["lane", "coop"])
+def test_scrypt_more_lanes_than_slots(kernel):
+    """count > grid*256 exercises the grid-stride reuse of a scratchpad slot (hashes checked, not just counted)."""
     from otedama_amd.models.header import int_to_hash
     from otedama_amd.ops.search import ScryptSearch
 
     hdr = os.urandom(76) + bytes(4)
-    sc = ScryptSearch("cuda:0", grid=1, gap=1, lanes_per_slot=2, cap=1024)
-    got = sorted(sc.search(hdr, int_to_hash((1 << 256) - 1), 0, 512))
-    assert got == list(range(512))
+    sc = ScryptSearch("cuda:0", grid=1, lanes_per_slot=2, cap=1024, kernel=kernel)
+    target_int = (1 << 255) - 1
+    got = sorted(sc.search(hdr, int_to_hash(target_int), 0, 512))
+    ref = [n for n in range(512) if int.from_bytes(hashlib.scrypt(
+        hdr[:76] + struct.pack("<I", n), salt=hdr[:76] + struct.pack("<I", n), n=1024, r=1, p=1, dklen=32),
+        "little") <= target_int]
+    assert got == ref and 100 < len(ref) < 412
 
 
 def test_gpu_miner_runtime_shares():
