@@ -157,6 +157,9 @@ async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, std
         from otedama_amd.tui import Dashboard
 
         dashboard = Dashboard(stdout)
+        import shutil
+
+        dashboard.set_width(shutil.get_terminal_size((80, 24)).columns)  # not pinned to 80 (tui/dashboard.go:545)
     eng_holder: dict = {}
     if cfg.http_addr:
         srv = HTTPServer(cfg.http_addr, reg, fs["pprof"], api={
@@ -166,6 +169,7 @@ async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, std
         try:
             srv.start()
             stdout.write(f"[info] http: listening on {srv.addr}\n")
+            stdout.flush()
         except OSError as exc:
             stderr.write(f"warning: cannot start HTTP server: {exc}\n")
             srv = None
