@@ -210,11 +210,20 @@ __device__ __forceinline__ void scrypt_romix(uint32_t X[32], uint4* __restrict__
 typedef __attribute__((address_space(3))) void glds_lptr_t;
 typedef unsigned coop_v4u __attribute__((ext_vector_type(4)));
 
+// Pad stores are streaming (nt): the write phase is store-only traffic that is read back at most once,
+// much later. tools/bench_hbm.hip: sequential full-line stores 3.3 TB/s plain vs 5.8 TB/s nt.
+#ifndef OTD_SCRYPT_STORE_CPOL
+#define OTD_SCRYPT_STORE_CPOL 2  // gfx950 cache policy bits: 1 = sc0, 2 = nt, 16 = sc1
+#endif
+constexpr int kStoreNT = OTD_SCRYPT_STORE_CPOL;
+
 __device__ __forceinline__ uint32_t coop_swz(uint32_t s_local) {
   return ((s_local >> 1) & 3u) | (((s_local >> 3) & 1u) << 2);
 }
 
 // tile: this wave's 4 KiB LDS tile (wave-uniform). rs: buffer descriptor over this wave's 8 MiB pad.
+// LCPOL: cache policy of the lookup loads (0 = default, 2 = nt).
+template <int LCPOL>
 __device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
                                                   uint32_t lane) {
   char* tb = reinterpret_cast<char*>(tile);
@@ -241,7 +250,8 @@ __device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffe
         const uint32_t owner = uint32_t(32 * h + 8 * r) + octet;
         const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));  // slot ^ swz(8r+octet)
         const coop_v4u vv = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (uint32_t(i) << 13) | (owner << 7) | (chunk << 4), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (uint32_t(i) << 13) | (owner << 7) | (chunk << 4), 0,
+                                               kStoreNT);
       }
     }
     blockmix(X);
@@ -261,8 +271,8 @@ __device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffe
       const uint32_t j0 = uint32_t(__shfl(int(j), int(o0), 64));
       const uint32_t j1 = uint32_t(__shfl(int(j), int(o1), 64));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (glds_lptr_t*)(tile + 64 * r), 16, (j0 << 13) | (o0 << 7) | (chunk << 4),
-                                               0, 0, 0);
-      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j1 << 13) | (o1 << 7) | (chunk << 4), 0, 0);
+                                               0, 0, LCPOL);
+      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j1 << 13) | (o1 << 7) | (chunk << 4), 0, LCPOL);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (ln < 32u) {
@@ -317,6 +327,7 @@ __global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* _
   }
 }
 
+template <int LCPOL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop(uint32_t count, uint4* __restrict__ xbuf,
                                                              uint4* __restrict__ V) {
   __shared__ uint4 tiles[4 * 256];  // 4 waves x 4 KiB half-tiles
@@ -336,7 +347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (uint64_t i = slot; i < count; i += nslots) {
     uint32_t X[32];
     load_entry(xbuf + (i << 3), X);
-    scrypt_romix_coop(X, rs, tile, lane);
+    scrypt_romix_coop<LCPOL>(X, rs, tile, lane);
     store_entry(xbuf + (i << 3), X);
   }
 }
@@ -396,8 +407,8 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   const uint32_t count64 = (count + 63u) & ~63u;
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
-    case kScryptCoop:
-      hipLaunchKernelGGL(otd_scrypt_romix_coop, dim3(grid), dim3(256), 0, stream, count64, X, V);
+    case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
+      hipLaunchKernelGGL(otd_scrypt_romix_coop<2>, dim3(grid), dim3(256), 0, stream, count64, X, V);
       break;
     case kScryptLaneW8:
       hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);

@@ -24,6 +24,7 @@ hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
                                 int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
 uint64_t scrypt_scratch_bytes(int grid, int gap);
+int gpu_cu_count(int device);
 
 #define OTD_HIP(call)                                                                              \
   do {                                                                                             \
@@ -94,10 +95,10 @@ void GpuMiner::loop() {
   // scrypt scratch (allocated lazily on the first scrypt job)
   void* scratch = nullptr;
   void* xbuf = nullptr;
-  // Lane-cooperative full-line ROMix (gap 1, 8 blocks/CU): 16.1 MH/s vs 13.6-14.0 for the per-lane
-  // kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md). One pad slot per lane (48-64 GiB of HBM).
+  // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
+  // 13.6-14.0 for the per-lane kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md).
   const int scrypt_gap = kScryptCoop;
-  const int scrypt_grid = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 8;
+  const int scrypt_grid = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
 
   uint64_t cur_gen = ~0ull;

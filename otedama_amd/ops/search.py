@@ -20,7 +20,7 @@ from otedama_amd.ops.native import require_native
 # Blocks of 256 lanes per CU that stay resident for the SHA-256d kernel
 # (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
 SHA256D_BLOCKS_PER_CU = 6
-SCRYPT_BLOCKS_PER_CU = 8
+SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
 
 
 def _device_index(device) -> int:

@@ -157,3 +157,31 @@ def test_gpu_miner_runtime_shares():
         d = hashlib.sha256(hashlib.sha256(bytes(h80)).digest()).digest()
         assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
         assert s["epoch"] == 3 and s["job_id"] == "j1"
+
+
+def test_gpu_miner_runtime_scrypt_shares():
+    """Production scrypt path: native GpuMiner thread + lane-cooperative ROMix, hits re-verified by hashlib."""
+    from otedama_amd.models.header import int_to_hash
+
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    tgt = int_to_hash((1 << 248) - 1)  # ~1 per 256 hashes
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 20)
+    m.set_job({"header": hdr, "target": tgt, "epoch": 5, "job_id": "s1", "algo": "scrypt"})
+    m.start()
+    deadline = time.time() + 30
+    shares = []
+    while time.time() < deadline and len(shares) < 50:
+        shares += m.poll(256)
+        time.sleep(0.02)
+    m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert len(shares) >= 20, st
+    for s in shares[:50]:
+        h80 = bytearray(hdr)
+        struct.pack_into("<I", h80, 0, s["version"])
+        struct.pack_into("<I", h80, 76, s["nonce"])
+        d = hashlib.scrypt(bytes(h80), salt=bytes(h80), n=1024, r=1, p=1, dklen=32)
+        assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
+        assert s["epoch"] == 5 and s["job_id"] == "s1"

@@ -64,7 +64,7 @@ def main() -> int:
         params = N.scrypt_prepare(hdr, bytes(28) + b"\xff\xff\x00\x00")
         for g in grids:
             for gap in gaps:
-                sc = ScryptSearch("cuda:0", grid=g, gap=gap, kernel="lane" if gap in (2, 4) else "coop")
+                sc = ScryptSearch("cuda:0", grid=g, gap=gap, kernel="lane" if gap in (2, 4, 9) else "coop")
                 sc.launch(params, 0)
                 ts = []
                 for _ in range(args.rounds * args.reps):
