@@ -20,10 +20,10 @@ ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
 
 
 class _PoolThread:
-    def __init__(self, difficulty: float):
+    def __init__(self, difficulty: float, algorithm: str = "sha256d"):
         from otedama_amd.pool.server import PoolOptions, PoolServer
 
-        self.pool = PoolServer(PoolOptions(initial_difficulty=difficulty, payout_address=ADDR,
+        self.pool = PoolServer(PoolOptions(algorithm=algorithm, initial_difficulty=difficulty, payout_address=ADDR,
                                            target_share_seconds=0.2, retarget_seconds=5))
         self.loop = asyncio.new_event_loop()
         self.ready = threading.Event()
@@ -52,12 +52,15 @@ def _metric(body: str, name: str, labels: str = "") -> float | None:
 
 
 @pytest.mark.gpu
-def test_cli_run_mines_against_local_pool(tmp_path):
-    # ~16 GH/s per GPU: difficulty 0.25 -> ~15 shares/s before vardiff settles
-    with _PoolThread(0.25) as pool:
+@pytest.mark.parametrize("algorithm,difficulty,min_hashrate", [
+    ("sha256d", 0.25, 1e9),   # ~16 GH/s per GPU: ~15 shares/s before vardiff settles
+    ("scrypt", 16.0, 1e6),    # ~16.7 MH/s per GPU, scrypt diff1 = 0xffff << 224: ~16 shares/s
+])
+def test_cli_run_mines_against_local_pool(tmp_path, algorithm, difficulty, min_hashrate):
+    with _PoolThread(difficulty, algorithm) as pool:
         cfg = tmp_path / "config.yaml"
         cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: stratum+v2://{pool.addr_sv2}\n"
-                       "mining:\n  batch_nonces: 134217728\n")
+                       f"mining:\n  algorithm: {algorithm}\n  batch_nonces: 134217728\n")
         env = dict(os.environ, HOME=str(tmp_path), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(tmp_path / "d"))
         proc = subprocess.Popen([sys.executable, "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
                                  "--http-addr", "127.0.0.1:0", "--gpus", "0"],
@@ -84,10 +87,10 @@ def test_cli_run_mines_against_local_pool(tmp_path):
                 acc = _metric(body, "otedama_shares_total", '{status="accepted"}') or 0
                 p50 = _metric(body, "otedama_submit_latency_milliseconds", '{quantile="0.5"}') or 0
                 hr = _metric(body, "otedama_hashrate_hashes_per_second") or 0
-                if acc >= 10 and p50 > 0 and hr > 1e9:
+                if acc >= 10 and p50 > 0 and hr > min_hashrate:
                     break
             assert acc >= 10 and p50 > 0, body + "".join(lines[-40:])
-            assert hr > 1e9, f"hashrate {hr}"
+            assert hr > min_hashrate, f"hashrate {hr}"
             with urllib.request.urlopen(f"http://{http}/readyz", timeout=5) as r:
                 assert r.status == 200
             assert pool.m_accepted.value() >= acc  # every engine-side accept was validated by the pool
