@@ -41,6 +41,7 @@ void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], Scry
 // `gap` selector for launch_scrypt_search: 1/2/4 = per-lane ROMix with that lookup gap,
 // kScryptCoop = lane-cooperative ROMix (full-line octet lookups, gap 1).
 constexpr int kScryptCoop = 8;
-constexpr int kScryptLaneW8 = 9;  // per-lane ROMix, gap 1, pinned to 8 waves/SIMD
+constexpr int kScryptLaneW8 = 9;   // per-lane ROMix, gap 1, pinned to 8 waves/SIMD
+constexpr int kScryptCoop2 = 11;   // cooperative ROMix, two software-pipelined hashes per lane (gap 1)
 
 }  // namespace otedama

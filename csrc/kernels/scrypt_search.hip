@@ -223,77 +223,124 @@ __device__ __forceinline__ uint32_t coop_swz(uint32_t s_local) {
 
 // tile: this wave's 4 KiB LDS tile (wave-uniform). rs: buffer descriptor over this wave's 8 MiB pad.
 // LCPOL: cache policy of the lookup loads (0 = default, 2 = nt).
+// Cooperative store of pad entry i (X of all 64 lanes) as 64 full-line nt stores (two halves through the tile).
+__device__ __forceinline__ void coop_store_entry(const uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
+                                                 uint32_t lane, uint32_t i) {
+  char* tb = reinterpret_cast<char*>(tile);
+  // Lane-derived constants are recomputed per call (a few VALU) rather than hoisted into loop-invariant
+  // VGPRs that would stay live through BlockMix and cost occupancy.
+  uint32_t ln = lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t slot = ln & 7u, octet = ln >> 3, own = ln & 31u;
+  const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);  // owner row, swizzled chunk 0 (bytes)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous reads of the tile retired
+    if ((ln >> 5) == uint32_t(h)) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        *reinterpret_cast<uint4*>(tb + (rd ^ (uint32_t(c) << 4))) =
+            make_uint4(X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint4 v = tile[64 * r + ln];
+      const uint32_t owner = uint32_t(32 * h + 8 * r) + octet;
+      const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));  // slot ^ swz(8r+octet)
+      const coop_v4u vv = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (i << 13) | (owner << 7) | (chunk << 4), 0, kStoreNT);
+    }
+  }
+}
+
+// Issue the cooperative lookup V[X[16] & 1023] for all 64 lanes: owners 0..31 by LDS-DMA into the tile,
+// owners 32..63 into R (register staging). Completed by coop_consume.
+template <int LCPOL>
+__device__ __forceinline__ void coop_issue(const uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
+                                           uint32_t lane, coop_v4u R[4]) {
+  uint32_t ln = lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t slot = ln & 7u, octet = ln >> 3;
+  const uint32_t j = X[16] & 1023u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile free (previous consumer's reads retired)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));
+    const uint32_t o0 = uint32_t(8 * r) + octet, o1 = o0 + 32u;
+    const uint32_t j0 = uint32_t(__shfl(int(j), int(o0), 64));
+    const uint32_t j1 = uint32_t(__shfl(int(j), int(o1), 64));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (glds_lptr_t*)(tile + 64 * r), 16, (j0 << 13) | (o0 << 7) | (chunk << 4),
+                                             0, 0, LCPOL);
+    R[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j1 << 13) | (o1 << 7) | (chunk << 4), 0, LCPOL);
+  }
+}
+
+// X ^= the looked-up entry (one vmcnt wait; the register-staged half goes through the tile second).
+__device__ __forceinline__ void coop_consume(uint32_t X[32], uint4* __restrict__ tile, uint32_t lane,
+                                             const coop_v4u R[4]) {
+  const char* tb = reinterpret_cast<const char*>(tile);
+  uint32_t ln = lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t own = ln & 31u;
+  const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (ln < 32u) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
+      X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[64 * r + ln] = make_uint4(R[r].x, R[r].y, R[r].z, R[r].w);
+  __builtin_amdgcn_wave_barrier();
+  if (ln >= 32u) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
+      X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
+    }
+  }
+}
+
 template <int LCPOL>
 __device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
                                                   uint32_t lane) {
-  char* tb = reinterpret_cast<char*>(tile);
-  for (int i = 0; i < 1024; ++i) {
-    // Lane-derived constants are recomputed each iteration (a few VALU) rather than hoisted into
-    // loop-invariant VGPRs that would stay live through BlockMix and cost occupancy.
-    uint32_t ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint32_t slot = ln & 7u, octet = ln >> 3, own = ln & 31u;
-    const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);  // owner row, swizzled chunk 0 (bytes)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous reads of the tile retired
-      if ((ln >> 5) == uint32_t(h)) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          *reinterpret_cast<uint4*>(tb + (rd ^ (uint32_t(c) << 4))) =
-              make_uint4(X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3]);
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint4 v = tile[64 * r + ln];
-        const uint32_t owner = uint32_t(32 * h + 8 * r) + octet;
-        const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));  // slot ^ swz(8r+octet)
-        const coop_v4u vv = {v.x, v.y, v.z, v.w};
-        __builtin_amdgcn_raw_buffer_store_b128(vv, rs, (uint32_t(i) << 13) | (owner << 7) | (chunk << 4), 0,
-                                               kStoreNT);
-      }
-    }
+  for (uint32_t i = 0; i < 1024; ++i) {
+    coop_store_entry(X, rs, tile, lane, i);
     blockmix(X);
   }
   for (int i = 0; i < 1024; ++i) {
-    uint32_t ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint32_t slot = ln & 7u, octet = ln >> 3, own = ln & 31u;
-    const uint32_t rd = (own << 7) ^ (coop_swz(own) << 4);
-    const uint32_t j = X[16] & 1023u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile free (previous iteration's reads retired)
     coop_v4u R[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t chunk = slot ^ (((octet >> 1) & 3u) | (uint32_t(r & 1) << 2));
-      const uint32_t o0 = uint32_t(8 * r) + octet, o1 = o0 + 32u;
-      const uint32_t j0 = uint32_t(__shfl(int(j), int(o0), 64));
-      const uint32_t j1 = uint32_t(__shfl(int(j), int(o1), 64));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (glds_lptr_t*)(tile + 64 * r), 16, (j0 << 13) | (o0 << 7) | (chunk << 4),
-                                               0, 0, LCPOL);
-      R[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j1 << 13) | (o1 << 7) | (chunk << 4), 0, LCPOL);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (ln < 32u) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
-        X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tile[64 * r + ln] = make_uint4(R[r].x, R[r].y, R[r].z, R[r].w);
-    __builtin_amdgcn_wave_barrier();
-    if (ln >= 32u) {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint4 t = *reinterpret_cast<const uint4*>(tb + (rd ^ (uint32_t(c) << 4)));
-        X[4 * c] ^= t.x; X[4 * c + 1] ^= t.y; X[4 * c + 2] ^= t.z; X[4 * c + 3] ^= t.w;
-      }
-    }
+    coop_issue<LCPOL>(X, rs, tile, lane, R);
+    coop_consume(X, tile, lane, R);
     blockmix(X);
+  }
+}
+
+// Two hashes per lane (A, B), software-pipelined so each stream's BlockMix runs while the other stream's
+// lookup is in flight; the wave only waits when a lookup outlives a whole BlockMix. One tile and one R are
+// shared: at most one lookup is outstanding per wave at any time.
+template <int LCPOL>
+__device__ __forceinline__ void scrypt_romix_coop2(uint32_t XA[32], uint32_t XB[32], __amdgpu_buffer_rsrc_t rsA,
+                                                   __amdgpu_buffer_rsrc_t rsB, uint4* __restrict__ tile, uint32_t lane) {
+  for (uint32_t i = 0; i < 1024; ++i) {
+    coop_store_entry(XA, rsA, tile, lane, i);
+    blockmix(XA);
+    coop_store_entry(XB, rsB, tile, lane, i);
+    blockmix(XB);
+  }
+  coop_v4u R[4];
+  coop_issue<LCPOL>(XA, rsA, tile, lane, R);
+  for (int i = 0; i < 1024; ++i) {
+    coop_consume(XA, tile, lane, R);
+    coop_issue<LCPOL>(XB, rsB, tile, lane, R);
+    blockmix(XA);
+    coop_consume(XB, tile, lane, R);
+    if (i < 1023) coop_issue<LCPOL>(XA, rsA, tile, lane, R);
+    blockmix(XB);
   }
 }
 
@@ -352,6 +399,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
+// Two-stream cooperative ROMix: wave w owns hashes [128w, 128w+128) (lane l: 128w+l and 128w+64+l) and a
+// 16 MiB pad region (8 MiB per stream). count is a multiple of 128 (launcher rounds up).
+template <int LCPOL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void otd_scrypt_romix_coop2(
+    uint32_t count, uint4* __restrict__ xbuf, uint4* __restrict__ V) {
+  __shared__ uint4 tiles[4 * 256];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave0 = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = (uint64_t(gridDim.x) * blockDim.x) >> 6;
+  const uint64_t wslot = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(wave0 >> 32))) << 32) |
+                         uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(wave0)));
+  uint4* VA = V + wslot * (2ull * 1024 * 64 * 8);
+  uint4* VB = VA + 1024ull * 64 * 8;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(VA, (short)0, 1024 * 64 * 128, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(VB, (short)0, 1024 * 64 * 128, 0x00020000);
+  uint4* tile = tiles + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256;
+  for (uint64_t w = wslot; w * 128 < count; w += nwaves) {
+    const uint64_t ia = w * 128 + lane, ib = ia + 64;
+    uint32_t XA[32], XB[32];
+    load_entry(xbuf + (ia << 3), XA);
+    load_entry(xbuf + (ib << 3), XB);
+    scrypt_romix_coop2<LCPOL>(XA, XB, rsA, rsB, tile, lane);
+    store_entry(xbuf + (ia << 3), XA);
+    store_entry(xbuf + (ib << 3), XB);
+  }
+}
+
 // Same per-lane ROMix (gap 1) pinned to 8 waves/SIMD (64 VGPRs, no spill) for A/B against the
 // compiler's default 67-VGPR / 7-wave allocation.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_w8(
@@ -391,6 +465,7 @@ namespace otedama {
 
 // Scratchpad bytes for `grid` ROMix blocks of 256 lane slots at lookup gap `gap`.
 uint64_t scrypt_scratch_bytes(int grid, int gap) {
+  if (gap == kScryptCoop2) return uint64_t(grid) * 512ull * 1024ull * 128ull;  // 2 hashes per lane slot
   if (gap == kScryptCoop || gap == kScryptLaneW8) gap = 1;
   return uint64_t(grid) * 256ull * (1024ull / uint64_t(gap)) * 128ull;
 }
@@ -412,6 +487,9 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
       break;
     case kScryptLaneW8:
       hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);
+      break;
+    case kScryptCoop2:
+      hipLaunchKernelGGL(otd_scrypt_romix_coop2<2>, dim3(grid), dim3(256), 0, stream, (count + 127u) & ~127u, X, V);
       break;
     case 1: hipLaunchKernelGGL(otd_scrypt_romix<1>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
     case 2: hipLaunchKernelGGL(otd_scrypt_romix<2>, dim3(grid), dim3(256), 0, stream, count, X, V); break;

@@ -84,19 +84,20 @@ class ScryptSearch:
     def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, gap: int = 1,
                  lanes_per_slot: int = 1, kernel: str = "coop"):
         """kernel="coop": lane-cooperative full-line ROMix (gap 1 only, the fast path);
+        kernel="coop2": the same with two software-pipelined hashes per lane;
         kernel="lane": one lane per hash with lookup gap 1/2/4. Raw native codes
-        (SCRYPT_COOP / SCRYPT_LANE_W8) may also be passed as ``gap``."""
+        (SCRYPT_COOP / SCRYPT_COOP2 / SCRYPT_LANE_W8) may also be passed as ``gap``."""
         self.native = require_native()
-        if kernel not in ("coop", "lane"):
-            raise ValueError(f"kernel must be 'coop' or 'lane', got {kernel!r}")
-        if kernel == "coop" and gap == 1:
-            gap = self.native.SCRYPT_COOP
-        self.kernel = "coop" if gap == self.native.SCRYPT_COOP else "lane"
+        if kernel not in ("coop", "coop2", "lane"):
+            raise ValueError(f"kernel must be 'coop', 'coop2' or 'lane', got {kernel!r}")
+        if kernel in ("coop", "coop2") and gap == 1:
+            gap = self.native.SCRYPT_COOP if kernel == "coop" else self.native.SCRYPT_COOP2
+        self.kernel = {self.native.SCRYPT_COOP: "coop", self.native.SCRYPT_COOP2: "coop2"}.get(gap, "lane")
         self.device = torch.device(device)
         self.cap = cap
         self.gap = gap
-        self.grid = grid or default_grid(self.device, SCRYPT_BLOCKS_PER_CU)
-        self.batch = self.grid * 256 * lanes_per_slot
+        self.grid = grid or default_grid(self.device, SCRYPT_BLOCKS_PER_CU // (2 if self.kernel == "coop2" else 1))
+        self.batch = self.grid * 256 * lanes_per_slot * (2 if self.kernel == "coop2" else 1)
         nbytes = self.native.scrypt_scratch_bytes(self.grid, gap)
         self.scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.xbuf = torch.empty(self.batch * 128, dtype=torch.uint8, device=self.device)

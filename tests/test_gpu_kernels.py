@@ -95,7 +95,7 @@ def test_sha256d_wraps_nonce_space():
 # native code 9 = per-lane gap 1 pinned to 8 waves/SIMD. n = 200 is not a multiple of 64 (the cooperative
 # kernel rounds its wave count up).
 @pytest.mark.parametrize("gap,n,kernel", [(1, 192, "lane"), (2, 192, "lane"), (4, 192, "lane"), (1, 192, "coop"),
-                                          (1, 200, "coop"), (9, 200, "lane")])
+                                          (1, 200, "coop"), (9, 200, "lane"), (1, 192, "coop2"), (1, 200, "coop2")])
 def test_scrypt_matches_hashlib(gap, n, kernel):
     from otedama_amd.models.header import int_to_hash
     from otedama_amd.ops.search import ScryptSearch
@@ -115,7 +115,7 @@ def test_scrypt_matches_hashlib(gap, n, kernel):
     assert got == ref and 0 < len(ref) < n
 
 
-@pytest.mark.parametrize("kernel", ["lane", "coop"])
+@pytest.mark.parametrize("kernel", ["lane", "coop", "coop2"])
 def test_scrypt_more_lanes_than_slots(kernel):
     """count > grid*256 exercises the grid-stride reuse of a scratchpad slot (hashes checked, not just counted)."""
     from otedama_amd.models.header import int_to_hash
