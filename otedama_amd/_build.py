@@ -26,13 +26,11 @@ ARCH = os.environ.get("OTEDAMA_OFFLOAD_ARCH", "gfx950")
 HIP_SOURCES = [
     "kernels/sha256d_search.hip",
     "kernels/scrypt_search.hip",
-    "kernels/x11_search.hip",
     "runtime/gpu_miner.hip",
 ]
 CXX_SOURCES = [
     "cpu/sha256_cpu.cpp",
     "cpu/job_prepare.cpp",
-    "cpu/x11_cpu.cpp",
     "cpu/aead.cpp",
     "runtime/miner_common.cpp",
     "bindings.cpp",

@@ -12,7 +12,7 @@ Parity: internal/hal/{device,registry,gpu_linux}.go
 MI355X-native difference: the reference hard-codes ``SHA256d = False`` for
 every GPU (gpu_linux.go:131) because it has no GPU compute. Here the HIP driver
 enumerates devices through the native runtime and reports the kernels that
-exist for the device's ISA: gfx950 -> sha256d, scrypt, x11 all true. The DRM
+exist for the device's ISA: gfx950 -> sha256d and scrypt. The DRM
 driver is kept for non-HIP render nodes (presence only, no hashing), and
 render nodes that the HIP driver already owns are not reported twice.
 """
@@ -111,11 +111,11 @@ class CPUDriver:
     def enumerate(self) -> list:
         model = _cpu_model()
         return [SimpleDevice(Identity("cpu-0", Family.CPU, _cpu_vendor(), model),
-                             Capabilities(sha256d=True, general_compute=True, scrypt=True), threads=self.threads)]
+                             Capabilities(sha256d=True, general_compute=True), threads=self.threads)]
 
 
 # ISA -> kernels compiled into the native extension (csrc/kernels)
-KERNEL_ISAS = {"gfx950": Capabilities(sha256d=True, general_compute=True, scrypt=True, x11=True)}
+KERNEL_ISAS = {"gfx950": Capabilities(sha256d=True, general_compute=True, scrypt=True)}
 
 
 class HIPDriver:
@@ -190,7 +190,9 @@ class GPULinuxDriver:
                 continue
             seen.add(canonical)
             vendor_id = _read(os.path.join(canonical, "vendor"))
-            if vendor_id in self.skip_vendors:
+            # Unreadable vendor = a node this process cannot use (e.g. another GPU's partition exposed in
+            # a container's sysfs): reporting it would hand arbitration phantom devices.
+            if not vendor_id or vendor_id in self.skip_vendors:
                 continue
             vendor = infer_vendor_name(vendor_id)
             model = vendor + " GPU"

@@ -6,7 +6,7 @@ the gfx950 search op that mines it.
 
   sha256d  Bitcoin double SHA-256      reference: internal/miner/sha256d.go:107-117
   scrypt   Litecoin scrypt(1024,1,1)   [NO REFERENCE CODE] (removed in v3, CHANGELOG.md:6623)
-  x11      Dash 11-hash chain          [NO REFERENCE CODE]
+  x11      Dash 11-hash chain          not offered (no validatable known-answer source; see ALGORITHMS)
 """
 from __future__ import annotations
 
@@ -22,12 +22,6 @@ def scrypt_hash(header80: bytes) -> bytes:
     return hashlib.scrypt(header80, salt=header80, n=1024, r=1, p=1, dklen=32)
 
 
-def _x11_hash(header80: bytes) -> bytes:
-    from otedama_amd.ops.native import require_native
-
-    return require_native().x11_hash(header80)
-
-
 @dataclass(frozen=True)
 class PowAlgorithm:
     name: str
@@ -41,7 +35,8 @@ ALGORITHMS: dict[str, PowAlgorithm] = {
     "sha256d": PowAlgorithm("sha256d", DIFF1_TARGET_INT, sha256d, True, "Bitcoin SHA-256d"),
     # Litecoin-family pools define share difficulty 1 as 2^16 easier than Bitcoin's.
     "scrypt": PowAlgorithm("scrypt", 0xFFFF << 224, scrypt_hash, True, "Litecoin scrypt N=1024 r=1 p=1"),
-    "x11": PowAlgorithm("x11", DIFF1_TARGET_INT, _x11_hash, True, "Dash X11 (11 chained 512-bit hashes)"),
+    # X11 (Dash) is not offered: its eleven 512-bit hashes have no offline known-answer source here, so a
+    # kernel could not be validated. Asking for it fails in get() with a clear error.
 }
 
 

@@ -222,3 +222,41 @@ def test_daemon_unit_generation(tmp_path, monkeypatch):
     with pytest.raises(daemon.DaemonError):
         m.install()
     assert daemon.quote_token('a"b c') == '"a\\"b c"'
+
+
+# ------------------------------------------------------------------ HAL
+def test_hal_drm_driver_filters(tmp_path):
+    """gpu_linux.go parity: render nodes are reported once, AMD nodes are left to the HIP driver, and a node
+    whose vendor cannot be read (another partition's node in a container) is not reported at all."""
+    from otedama_amd import hal
+
+    def node(name, vendor, pci="PCI_ID=10DE:2684"):
+        dev = tmp_path / "devices" / name
+        dev.mkdir(parents=True)
+        if vendor is not None:
+            (dev / "vendor").write_text(vendor + "\n")
+        (dev / "uevent").write_text(pci + "\n")
+        (tmp_path / "drm" / name).mkdir(parents=True)
+        (tmp_path / "drm" / name / "device").symlink_to(dev)
+
+    node("renderD128", "0x10de")
+    node("renderD129", "0x1002", "PCI_ID=1002:75A3")
+    node("renderD130", None)
+    drv = hal.GPULinuxDriver(str(tmp_path / "drm"), skip_vendors=("0x1002",))
+    devs = drv.enumerate()
+    assert [d.identity().id for d in devs] == ["gpu-renderD128"]
+    assert devs[0].identity().vendor == "NVIDIA" and not devs[0].capabilities().sha256d
+    assert devs[0].capabilities().general_compute
+
+
+def test_hal_capabilities_match_kernels():
+    from otedama_amd import hal
+    from otedama_amd.models import algorithms
+
+    cpu = hal.CPUDriver(2).enumerate()[0]
+    assert cpu.capabilities().sha256d and not cpu.capabilities().scrypt  # CpuMiner is SHA-256d only
+    gfx950 = hal.KERNEL_ISAS["gfx950"]
+    assert gfx950.sha256d and gfx950.scrypt and not gfx950.x11
+    assert set(algorithms.ALGORITHMS) == {"sha256d", "scrypt"}
+    with pytest.raises(ValueError, match="unknown algorithm"):
+        algorithms.get("x11")
