@@ -128,7 +128,9 @@ void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]) {
   pbkdf2_sha256(header80, 80, header80, 80, 1, b, 128);
   uint32_t X[32];
   for (int i = 0; i < 32; ++i) X[i] = load_le32(b + 4 * i);
-  std::vector<uint32_t> V(32 * 1024);
+  // Per-thread pad: a fresh 128 KiB vector sits at glibc's mmap threshold, and the mmap/munmap pair per
+  // hash serialised concurrent verifiers on the kernel mm lock (4 threads ran at 0.93x of one).
+  thread_local std::vector<uint32_t> V(32 * 1024);
   for (int i = 0; i < 1024; ++i) {
     std::memcpy(&V[32 * i], X, 128);
     for (int k = 0; k < 16; ++k) X[k] ^= X[16 + k];

@@ -22,6 +22,7 @@ The reject strings land in the engine's reject taxonomy (engine/stats.go:263-277
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 import json
 import os
 import struct
@@ -31,7 +32,7 @@ from dataclasses import dataclass, field
 
 from otedama_amd.metrics import Registry
 from otedama_amd.models import algorithms
-from otedama_amd.models.header import hash_to_int, target_from_difficulty, target_from_nbits
+from otedama_amd.models.header import TargetError, hash_to_int, target_from_difficulty, target_from_nbits
 from otedama_amd.pool.journal import Journal, ShareRow
 from otedama_amd.pool.template import BlockTemplate, TemplateSource, merkle_root_from_branches
 from otedama_amd.pool.vardiff import Vardiff, VardiffConfig, VardiffState
@@ -116,6 +117,17 @@ class PoolServer:
                                              min_difficulty=self.opts.min_difficulty),
                                diff1_hashes=float(2 ** 256) / self.algo.diff1)
         self.journal = Journal(self.opts.journal_path)
+        # share-hash workers for slow PoW (scrypt); sized to the host, never more than 8 threads
+        self._hash_pool = concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1),
+                                                                thread_name_prefix="otedama-pool-hash")
+        # hashlib.scrypt holds the GIL; the native C++ scrypt releases it, so the workers run in parallel
+        self._slow_hash = self.algo.hash
+        if self.algo.name == "scrypt":
+            from otedama_amd.ops.native import load
+
+            n = load(build_if_missing=False)
+            if n is not None:
+                self._slow_hash = n.scrypt_1024_1_1
         self.block: BlockTemplate | None = None
         self.jobs: "OrderedDict[str, PoolJob]" = OrderedDict()
         self._job_counter = 0
@@ -181,6 +193,7 @@ class PoolServer:
                 await asyncio.wait_for(s.wait_closed(), 2)
             except asyncio.TimeoutError:
                 pass
+        self._hash_pool.shutdown(wait=False, cancel_futures=True)
         self.journal.close()
 
     async def _refresh_loop(self) -> None:
@@ -247,6 +260,34 @@ class PoolServer:
     # ------------------------------------------------------------ validation
     def validate(self, worker: _Worker, job_id: str, extranonce: bytes, ntime: int, nonce: int,
                  version: int) -> Verdict:
+        pre = self._precheck(worker, job_id, extranonce, ntime, nonce, version)
+        if isinstance(pre, Verdict):
+            return pre
+        job, key, hdr = pre
+        return self._finish(worker, job_id, job, key, self.algo.hash(hdr))
+
+    async def validate_async(self, worker: _Worker, job_id: str, extranonce: bytes, ntime: int, nonce: int,
+                             version: int) -> Verdict:
+        """validate() with the header hash off the event loop for slow algorithms (scrypt: ~ms per share,
+        GIL released), so a burst of shares from many GPUs does not stall every other connection."""
+        pre = self._precheck(worker, job_id, extranonce, ntime, nonce, version)
+        if isinstance(pre, Verdict):
+            return pre
+        job, key, hdr = pre
+        if self.algo.name == "sha256d":
+            h = self.algo.hash(hdr)  # ~1 us: cheaper inline than a thread hop
+        else:
+            h = await asyncio.get_running_loop().run_in_executor(self._hash_pool, self._slow_hash, hdr)
+        return self._finish(worker, job_id, job, key, h)
+
+    def share_target(self, difficulty: float) -> bytes:
+        """Share target for a difficulty, clamped to 2^256-1 (below ~diff1/2^256 the target would overflow)."""
+        try:
+            return target_from_difficulty(difficulty, self.algo.diff1)
+        except TargetError:
+            return b"\xff" * 32
+
+    def _precheck(self, worker: _Worker, job_id: str, extranonce: bytes, ntime: int, nonce: int, version: int):
         job = self.jobs.get(job_id)
         if job is None or job.block is not self.block:
             return self._reject(worker, job_id, "stale-job")
@@ -257,13 +298,19 @@ class PoolServer:
         key = (job_id, extranonce, ntime, nonce, version)
         if key in self._seen:
             return self._reject(worker, job_id, "duplicate-share")
-        hdr = self.header_for(job, extranonce, version, ntime, nonce)
-        h = self.algo.hash(hdr)
+        return job, key, self.header_for(job, extranonce, version, ntime, nonce)
+
+    def _finish(self, worker: _Worker, job_id: str, job: PoolJob, key: tuple, h: bytes) -> Verdict:
+        # re-checked after the (possibly off-loop) hash: a new block or an identical concurrent submit
+        if job.block is not self.block:
+            return self._reject(worker, job_id, "stale-job")
+        if key in self._seen:
+            return self._reject(worker, job_id, "duplicate-share")
         hv = hash_to_int(h)
         diff = worker.vd.difficulty
-        if hv > hash_to_int(target_from_difficulty(diff, self.algo.diff1)):
+        if hv > hash_to_int(self.share_target(diff)):
             grace = time.monotonic() - worker.retarget_at < RETARGET_GRACE
-            if grace and hv <= hash_to_int(target_from_difficulty(worker.prev_difficulty, self.algo.diff1)):
+            if grace and hv <= hash_to_int(self.share_target(worker.prev_difficulty)):
                 diff = worker.prev_difficulty
             else:
                 return self._reject(worker, job_id, "low-difficulty-share", h)
@@ -444,7 +491,7 @@ class _V1Conn:
             except (ValueError, TypeError, IndexError):
                 self._write({"id": mid, "result": None, "error": [20, "invalid submit parameters", None]})
                 return
-            v = self.pool.validate(self.worker, str(job_id), self.en1 + en2, ntime, nonce, version)
+            v = await self.pool.validate_async(self.worker, str(job_id), self.en1 + en2, ntime, nonce, version)
             if v.accepted:
                 self._write({"id": mid, "result": True, "error": None})
                 if self.pool.after_accept(self.worker) is not None:
@@ -531,7 +578,7 @@ class _V2Conn:
                 w.prev_difficulty = w.vd.difficulty
             self.channels[ch] = (w, prefix)
             self._send(M.OpenMiningChannelSuccess(
-                msg.req_id, ch, target_from_difficulty(w.vd.difficulty, self.pool.algo.diff1), prefix,
+                msg.req_id, ch, self.pool.share_target(w.vd.difficulty), prefix,
                 extranonce2_size=0))
             if self.pool.jobs:
                 for m in self._job_msgs(ch, next(reversed(self.pool.jobs.values())), prefix, future=True):
@@ -542,12 +589,12 @@ class _V2Conn:
                 self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, "invalid-channel-id"))
                 return
             w, prefix = ent
-            v = self.pool.validate(w, f"{msg.job_id:x}", prefix, msg.ntime, msg.nonce, msg.nversion)
+            v = await self.pool.validate_async(w, f"{msg.job_id:x}", prefix, msg.ntime, msg.nonce, msg.nversion)
             if v.accepted:
                 self._send(M.SubmitSharesSuccess(msg.channel_id, msg.sequence_number, 1, max(int(v.difficulty), 1)))
                 new = self.pool.after_accept(w)
                 if new is not None:
-                    self._send(M.SetTarget(msg.channel_id, target_from_difficulty(new, self.pool.algo.diff1)))
+                    self._send(M.SetTarget(msg.channel_id, self.pool.share_target(new)))
             else:
                 self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, v.reason))
         elif isinstance(msg, M.UpdateChannel):
@@ -556,6 +603,6 @@ class _V2Conn:
                 w = ent[0]
                 w.prev_difficulty, w.retarget_at = w.vd.difficulty, time.monotonic()
                 w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
-                self._send(M.SetTarget(msg.channel_id, target_from_difficulty(w.vd.difficulty, self.pool.algo.diff1)))
+                self._send(M.SetTarget(msg.channel_id, self.pool.share_target(w.vd.difficulty)))
         elif isinstance(msg, M.CloseChannel):
             self.channels.pop(msg.channel_id, None)
