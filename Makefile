@@ -12,7 +12,7 @@ VERSION     := $(shell $(PYTHON) -c "from otedama_amd.version import VERSION; pr
 export PYTHONPATH := $(CURDIR)$(if $(PYTHONPATH),:$(PYTHONPATH))
 
 .PHONY: help build rebuild test test-unit test-gpu test-multiproc bench bench-cpu profile fuzz lint docs \
-        docker-build docker-run release-check clean smoke doctor
+        docker-build docker-run release-check clean smoke doctor sanitize
 
 help: ## Display this help message
 	@grep -E '^[a-zA-Z_-]+:.*?## ' $(MAKEFILE_LIST) | awk 'BEGIN {FS = ":.*?## "}; {printf "  %-16s %s\n", $$1, $$2}'
@@ -46,6 +46,9 @@ profile: build ## rocprofv3 kernel trace + SQ counters (writes gpurun_out/prof*)
 
 fuzz: ## Property/fuzz tests for the SV2 frame codec and message decoders
 	$(PYTHON) -m pytest tests -q -k "fuzz or frame"
+
+sanitize: ## Host-only TSan + ASan/UBSan builds of the C++ runtime + job-epoch race stress
+	bash tools/sanitize/run.sh 4
 
 lint: ## Byte-compile everything (no third-party linters in the image)
 	$(PYTHON) -m compileall -q otedama_amd tests bench.py __graft_entry__.py

@@ -105,17 +105,20 @@ static void sha256_compress_shani(uint32_t state[8], const uint8_t block[64]) {
   _mm_storeu_si128((__m128i*)&state[4], STATE1);
 }
 
+static bool detect_sha_ni() {
+  unsigned a, b, c, d;
+  bool ok = false;
+  if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) ok = (b >> 29) & 1;  // EBX bit 29 = SHA
+  unsigned a1, b1, c1, d1;
+  if (ok && __get_cpuid(1, &a1, &b1, &c1, &d1)) ok = (c1 >> 19) & 1;  // SSE4.1
+  return ok;
+}
+
 bool cpu_has_sha_ni() {
-  static int cached = -1;
-  if (cached < 0) {
-    unsigned a, b, c, d;
-    bool ok = false;
-    if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) ok = (b >> 29) & 1;  // EBX bit 29 = SHA
-    unsigned a1, b1, c1, d1;
-    if (ok && __get_cpuid(1, &a1, &b1, &c1, &d1)) ok = (c1 >> 19) & 1;  // SSE4.1
-    cached = ok ? 1 : 0;
-  }
-  return cached == 1;
+  // Function-local static: thread-safe one-time init (a plain lazily-written int raced
+  // across miner threads; found by tools/sanitize under TSan).
+  static const bool cached = detect_sha_ni();
+  return cached;
 }
 
 void sha256_compress(uint32_t state[8], const uint8_t block[64]) {
@@ -149,7 +152,7 @@ void sha256d(const uint8_t* data, size_t len, uint8_t out[32]) {
 void hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen, uint8_t out[32]) {
   uint8_t k[64] = {0};
   if (klen > 64) sha256(key, klen, k);
-  else std::memcpy(k, key, klen);
+  else if (klen) std::memcpy(k, key, klen);  // key may be null when klen == 0
   uint8_t ipad[64], opad[64];
   for (int i = 0; i < 64; ++i) { ipad[i] = k[i] ^ 0x36; opad[i] = k[i] ^ 0x5c; }
   // inner = H(ipad || msg)
@@ -160,7 +163,7 @@ void hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* msg, size_t mle
   while (mlen - off >= 64) { sha256_compress(st, msg + off); off += 64; }
   uint8_t tail[128] = {0};
   size_t rem = mlen - off;
-  std::memcpy(tail, msg + off, rem);
+  if (rem) std::memcpy(tail, msg + off, rem);
   tail[rem] = 0x80;
   size_t tl = (rem + 9 <= 64) ? 64 : 128;
   uint64_t bits = uint64_t(64 + mlen) * 8;
@@ -185,7 +188,7 @@ void pbkdf2_sha256(const uint8_t* pw, size_t pwlen, const uint8_t* salt, size_t 
                    uint32_t iters, uint8_t* out, size_t outlen) {
   uint8_t buf[1024];
   uint8_t* msg = saltlen + 4 <= sizeof buf ? buf : new uint8_t[saltlen + 4];
-  std::memcpy(msg, salt, saltlen);
+  if (saltlen) std::memcpy(msg, salt, saltlen);
   uint32_t blockno = 1;
   size_t done = 0;
   while (done < outlen) {

@@ -149,7 +149,7 @@ class CpuMiner : public MinerBase {
   int threads_;
   std::vector<std::thread> ths_;
   std::atomic<uint64_t> cursor_{0};
-  std::atomic<uint64_t> cursor_gen_{~0ull};
+  std::atomic<uint64_t> cursor_gen_{0};  // job_gen_ of the cursor; first job is gen 1
   std::mutex cursor_mu_;
 };
 

@@ -294,9 +294,19 @@ void CpuMiner::loop(int /*tid*/) {
       continue;
     }
     uint64_t claim;
+#ifdef OTEDAMA_STRESS_HOOKS
+    // tools/sanitize: widen the snapshot -> claim window so job switches land inside it.
+    std::this_thread::sleep_for(std::chrono::microseconds(std::hash<std::thread::id>{}(
+        std::this_thread::get_id()) % 400));
+#endif
     {
       std::lock_guard<std::mutex> g(cursor_mu_);
-      if (cursor_gen_.load() != gen) { cursor_gen_.store(gen); cursor_.store(0); }
+      // Generations only move forward. A thread still holding a superseded snapshot must drop
+      // it, not rewind the shared cursor to its own generation: that would rescan chunks of the
+      // old work already searched and emit duplicate shares.
+      const uint64_t cg = cursor_gen_.load();
+      if (gen < cg) continue;
+      if (gen > cg) { cursor_gen_.store(gen); cursor_.store(0); }
       claim = cursor_.fetch_add(kChunk);
     }
     // claim indexes (variant-stripe slot k, nonce chunk)
