@@ -50,6 +50,14 @@ class EngineMetrics:
         self.devices_idle = G("otedama_devices_idle",
                               "Number of devices left idle this arbitration cycle (no compatible stream above the "
                               "yield floor).")
+        self.devices_active = G("otedama_devices_active",
+                                "Local devices hashing: not retired after a fault and not stalled.")
+        self.devices_faulted = G("otedama_devices_faulted",
+                                 "Devices whose miner thread died on a HIP error (retired; survivors re-split "
+                                 "their search stripe at the next job).")
+        self.devices_stalled = G("otedama_devices_stalled",
+                                 "Live devices with work assigned whose hash counter stopped advancing for "
+                                 "several stats ticks.")
         self.btc_usd_rate = G("otedama_btc_usd_rate", "Current BTC/USD rate from provider consensus.")
         self.uptime = G("otedama_uptime_seconds", "Seconds since engine start.")
         self.start_time = G("otedama_start_time_seconds", "Unix timestamp at which engine started.")

@@ -592,8 +592,12 @@ class Engine:
             self.log("warn", f"engine: dropped {dropped - self._last_dropped} found share(s) — share submission is "
                              "not keeping up with discovery")
             self._last_dropped = dropped
-        for dev, err in self.miners.faulted():
+        for dev, err in self.miners.retire_faulted():
             self.log("error", f"engine: device {dev} faulted: {err}")
+        stalled_devs = self.miners.stalled()
+        self.m.devices_faulted.set(sum(1 for s in self.miners.device_stats().values() if s["faulted"]))
+        self.m.devices_stalled.set(len(stalled_devs))
+        self.m.devices_active.set(len(self.miners.live()) - len(stalled_devs))
         if self.curtailed:
             self.m.up.set(1)
             self.stalled = False

@@ -11,8 +11,8 @@ lockstep by a tick thread on every rank:
          R2  all_gather share slots   64 × 9 int64 per rank       4.6 KiB/rank
          R3  all_gather counters      [hashes, shares, dropped, faulted]
 
-Each rank's native miner searches the disjoint variant stripe
-``rank*local + i (mod world*local)`` (parallel/partition.py), so nothing but
+Each rank's native miners search the disjoint variant stripes
+``rank + world*i (mod world*live)`` (parallel/partition.py), so nothing but
 jobs, hits and counters ever crosses xGMI. The tick (default 10 ms) bounds the
 extra share latency of non-primary ranks; hashing never waits on it because
 kernels run on the miners' own HIP streams and the collectives on NodeComm's
@@ -86,6 +86,8 @@ class NodeMinerSet:
         self._rates: dict[str, float] = {}
         self._t_last = time.monotonic()
         self.remote_ids = [f"rank{r}" for r in range(1, comm.info.world_size)]
+        self._remote_faults = [0] * comm.info.world_size   # faulted-device count already reported
+        self._remote_idle = [0] * comm.info.world_size     # ticks without hash progress
 
     # MinerSet API ------------------------------------------------------------
     def __len__(self) -> int:
@@ -177,14 +179,36 @@ class NodeMinerSet:
                 if self._last_rows[r][3]]
         return out
 
+    def retire_faulted(self) -> list[tuple[str, str]]:
+        """Local faults are retired here; a remote rank retires its own devices (NodeWorker) and
+        re-splits its variant class, so rank 0 only reports the new fault count once."""
+        out = self.local.retire_faulted()
+        for r, rid in enumerate(self.remote_ids, start=1):
+            n = self._last_rows[r][3]
+            if n > self._remote_faults[r]:
+                out.append((rid, f"{n - self._remote_faults[r]} device(s) faulted on {rid}"))
+                self._remote_faults[r] = n
+        return out
+
+    def stalled(self) -> list[str]:
+        stall = self.local.stall_samples
+        return self.local.stalled() + [rid for r, rid in enumerate(self.remote_ids, start=1)
+                                       if self._remote_idle[r] >= stall]
+
+    def live(self):
+        return self.local.live()
+
     def update_hashrates(self) -> dict[str, float]:
         rates = self.local.update_hashrates()
         now = time.monotonic()
         dt = max(now - self._t_last, 1e-6)
         self._t_last = now
         prev = getattr(self, "_prev_rows", None) or [[0, 0, 0, 0] for _ in self._last_rows]
+        working = self._blob is not None and self._blob.get("job") is not None
         for r, rid in enumerate(self.remote_ids, start=1):
             rates[rid] = max(self._last_rows[r][0] - prev[r][0], 0) / dt
+            idle = working and rid not in self._paused and self._last_rows[r][0] == prev[r][0]
+            self._remote_idle[r] = self._remote_idle[r] + 1 if idle else 0
         self._prev_rows = [list(x) for x in self._last_rows]
         self._rates = rates
         return rates
@@ -232,11 +256,13 @@ class NodeWorker:
         self.link = _Link(local, comm, tick)
         self.log = log or (lambda level, msg: None)
         self.rank_id = f"rank{comm.info.rank}"
+        self.health_every = max(1, int(1.0 / max(tick, 1e-3)))  # fault check about once a second
 
     def run(self) -> None:
         self.local.start()
         try:
             pending: list[dict] = []
+            n = 0
             while True:
                 pending.extend(self.local.poll(256))
                 out, pending = pending[:64], pending[64:]
@@ -245,6 +271,9 @@ class NodeWorker:
                     self._apply(blob)
                 if stop:
                     return
+                n += 1
+                if n % self.health_every == 0:
+                    self.local.retire_faulted()  # survivors re-split this rank's class on the next job
                 time.sleep(self.link.tick)
         finally:
             self.local.stop()

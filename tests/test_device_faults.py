@@ -1,0 +1,130 @@
+"""GPU-fault handling and per-device stall detection.
+
+A faulted device is retired and its rank's variant class (parallel/partition.py) is re-split among
+the survivors at the next NEW work, never mid-job (that would re-search variants and re-submit
+duplicates). A live device with work whose hash counter stops is reported as stalled."""
+from types import SimpleNamespace
+
+import pytest
+
+from otedama_amd.engine import miners as miners_mod
+from otedama_amd.engine.miners import DeviceMiner, MinerSet
+from otedama_amd.parallel.partition import stripe_for
+
+
+class FakeNative:
+    def __init__(self):
+        self.jobs, self.hashes, self.fault, self.stopped = [], 0, "", False
+
+    def start(self):
+        pass
+
+    def stop(self):
+        self.stopped = True
+
+    def set_job(self, t):
+        self.jobs.append(t)
+
+    def poll(self, n):
+        return []
+
+    def stats(self):
+        return {"hashes": self.hashes, "shares": 0, "dropped": 0, "faulted": bool(self.fault), "error": self.fault,
+                "candidates": 0, "launches": 0}
+
+
+def _dev(name):
+    return SimpleNamespace(identity=lambda: SimpleNamespace(id=name))
+
+
+def _set(n, rank=0, world=1, log=None):
+    ms = MinerSet.__new__(MinerSet)
+    ms.algorithm, ms.log = "sha256d", log or (lambda lvl, msg: None)
+    ms.miners = [DeviceMiner(_dev(f"gpu{i}"), FakeNative()) for i in range(n)]
+    ms.rank, ms.world_size, ms.stall_samples, ms._restripe_pending = rank, world, 3, False
+    ms._restripe()
+    import threading
+    import time
+    ms._lock, ms._epoch, ms._template, ms._t_last = threading.Lock(), 0, None, time.monotonic()
+    return ms
+
+
+def _covered(stripes, n):
+    seen = []
+    for st in stripes:
+        seen += [v for v in st.variants(n) if v < n]
+    return sorted(seen)
+
+
+@pytest.mark.parametrize("world,local", [(1, 1), (1, 4), (2, 3), (8, 1), (4, 2)])
+def test_two_level_stripes_are_a_partition(world, local):
+    n = 240
+    stripes = [stripe_for(r, world, i, local) for r in range(world) for i in range(local)]
+    assert _covered(stripes, n) == list(range(n))  # disjoint (no repeats) and complete
+
+
+def test_rank_resplits_its_own_class_after_a_fault():
+    world, n = 4, 400
+    plan = {r: [stripe_for(r, world, i, 3) for i in range(3)] for r in range(world)}
+    plan[2] = [stripe_for(2, world, i, 2) for i in range(2)]  # rank 2 lost one of 3 devices
+    assert _covered([s for ss in plan.values() for s in ss], n) == list(range(n))
+
+
+def _tmpl(prev=b"\x01", target="ff" * 32, job="j1"):
+    return {"algo": "sha256d", "header": (prev * 80)[:80].hex(), "target": target, "job_id": job}
+
+
+def test_faulted_device_retired_and_stripe_resplit_on_next_new_work():
+    logs = []
+    ms = _set(3, log=lambda lvl, msg: logs.append((lvl, msg)))
+    ms.set_job(_tmpl())
+    assert [(m.native.jobs[-1]["variant_start"], m.native.jobs[-1]["variant_stride"]) for m in ms.miners] == \
+        [(0, 3), (1, 3), (2, 3)]
+    ms.miners[1].native.fault = "hipErrorLaunchFailure"
+    assert ms.retire_faulted() == [("gpu1", "hipErrorLaunchFailure")]
+    assert ms.miners[1].native.stopped and ms.miners[1].retired
+    assert ms.retire_faulted() == []                     # reported once
+    assert any("retired" in m for _, m in logs)
+    n1 = len(ms.miners[1].native.jobs)
+    # same work, new target (SetTarget): stripes must NOT move (cursor keeps going, no duplicates)
+    ms.set_job(_tmpl(target="7f" + "ff" * 31, job="j2"))
+    assert [(m.native.jobs[-1]["variant_start"], m.native.jobs[-1]["variant_stride"]) for m in (ms.miners[0],
+            ms.miners[2])] == [(0, 3), (2, 3)]
+    # new work: survivors take the whole class
+    ms.set_job(_tmpl(prev=b"\x02", job="j3"))
+    assert [(m.native.jobs[-1]["variant_start"], m.native.jobs[-1]["variant_stride"]) for m in (ms.miners[0],
+            ms.miners[2])] == [(0, 2), (1, 2)]
+    assert len(ms.miners[1].native.jobs) == n1           # retired device gets no more work
+    assert ms.stripe_total == 2 and [m.id for m in ms.live()] == ["gpu0", "gpu2"]
+
+
+def test_per_device_stall_detection():
+    logs = []
+    ms = _set(2, log=lambda lvl, msg: logs.append((lvl, msg)))
+    for _ in range(5):                                   # no work: idle is not a stall
+        ms.update_hashrates()
+    assert ms.stalled() == []
+    ms.set_job(_tmpl())
+    for k in range(3):
+        ms.miners[0].native.hashes += 1 << 29             # gpu0 progresses, gpu1 is hung
+        ms.update_hashrates()
+    assert ms.stalled() == ["gpu1"]
+    assert sum("no hash progress" in m for _, m in logs) == 1
+    ms.pause_device("gpu1", True)
+    ms.update_hashrates()
+    assert ms.stalled() == []                            # paused on purpose
+    ms.pause_device("gpu1", False)
+    ms.miners[1].native.hashes += 5
+    ms.update_hashrates()
+    assert ms.stalled() == []
+
+
+def test_engine_metrics_track_device_health():
+    from otedama_amd.engine.metrics import EngineMetrics
+    from otedama_amd.metrics import Registry
+
+    m = EngineMetrics(Registry())
+    m.devices_active.set(7)
+    m.devices_faulted.set(1)
+    assert m.devices_active.value() == 7 and m.devices_faulted.value() == 1
+    assert miners_mod._work_key(_tmpl(target="00" * 32)) == miners_mod._work_key(_tmpl())
