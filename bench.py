@@ -68,6 +68,7 @@ def main() -> int:
     from otedama_amd.ops import native
     from otedama_amd.ops.search import ScryptSearch, Sha256dSearch
     from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
+    from otedama_amd.utils.trace import span
 
     if not torch.cuda.is_available():
         print("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU config",
@@ -93,6 +94,10 @@ def main() -> int:
     hits_log: list[tuple[bytes, torch.Tensor]] = []
 
     def step(i: int, record: bool) -> None:
+        with span("otd.bench.sha256d_step"):
+            _step(i, record)
+
+    def _step(i: int, record: bool) -> None:
         nonlocal counters_hashes
         if world > 1:  # R1: job blob fan-out (kept on device; decoded only on job change)
             comm._run(lambda: torch.distributed.broadcast(comm._job, src=0))

@@ -12,6 +12,7 @@
 #include "otedama/aead.h"
 #include "otedama/job.h"
 #include "otedama/runtime.h"
+#include "otedama/trace.h"
 #include "otedama/sha256.h"
 
 namespace py = pybind11;
@@ -192,6 +193,10 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   });
 
+  // roctx ranges for Python-side spans (node collectives, share submit, bench steps): SURVEY §5.1.
+  m.def("trace_push", [](const std::string& name) { trace_push(name.c_str()); });
+  m.def("trace_pop", [] { trace_pop(); });
+  m.def("trace_mark", [](const std::string& name) { trace_mark(name.c_str()); });
   m.def("gpu_device_count", &gpu_device_count);
   m.def("gpu_arch_name", &gpu_arch_name);
   m.def("gpu_cu_count", &gpu_cu_count);

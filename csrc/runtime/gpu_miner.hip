@@ -10,12 +10,14 @@
 
 #include <chrono>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 
 #include "otedama/job.h"
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
+#include "otedama/trace.h"
 
 namespace otedama {
 
@@ -48,6 +50,7 @@ struct Slot {
   uint8_t header[80];
   uint32_t version = 0, ntime = 0;
   uint64_t en2 = 0;
+  TraceId range = 0;  // roctx: enqueue -> host verification of this batch
 };
 }  // namespace
 
@@ -82,19 +85,37 @@ void GpuMiner::stop() {
 }
 
 void GpuMiner::loop() {
+  trace_name_thread(("otedama-" + device_id_).c_str());
   OTD_HIP(hipSetDevice(device_));
-  hipStream_t stream;
-  OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  hipStream_t stream = nullptr;
   Slot slots[2];
+  // scrypt scratch (allocated lazily on the first scrypt job)
+  void* scratch = nullptr;
+  void* xbuf = nullptr;
+  // Released on every exit, including a HIP error thrown mid-loop (device fault): in-flight
+  // batches are drained first so nothing is freed under a running kernel or copy.
+  struct Release {
+    std::function<void()> f;
+    ~Release() { f(); }
+  } release{[&] {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& s : slots) {
+      if (s.d_out) (void)hipFree(s.d_out);
+      if (s.h_out) (void)hipHostFree(s.h_out);
+      if (s.start) (void)hipEventDestroy(s.start);
+      if (s.done) (void)hipEventDestroy(s.done);
+    }
+    if (scratch) (void)hipFree(scratch);
+    if (xbuf) (void)hipFree(xbuf);
+    if (stream) (void)hipStreamDestroy(stream);
+  }};
+  OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto& s : slots) {
     OTD_HIP(hipMalloc(&s.d_out, (1 + 2 * kHitCap) * sizeof(uint32_t)));
     OTD_HIP(hipHostMalloc(&s.h_out, (1 + 2 * kHitCap) * sizeof(uint32_t), hipHostMallocDefault));
     OTD_HIP(hipEventCreate(&s.start));
     OTD_HIP(hipEventCreate(&s.done));
   }
-  // scrypt scratch (allocated lazily on the first scrypt job)
-  void* scratch = nullptr;
-  void* xbuf = nullptr;
   // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
   // 13.6-14.0 for the per-lane kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md).
   const int scrypt_gap = kScryptCoop;
@@ -109,9 +130,11 @@ void GpuMiner::loop() {
   auto finish = [&](Slot& s) {
     if (!s.busy) return;
     OTD_HIP(hipEventSynchronize(s.done));
+    trace_stop(s.range);
     float ms = 0;
     hipEventElapsedTime(&ms, s.start, s.done);
     const uint32_t n = s.h_out[0] < kHitCap ? s.h_out[0] : kHitCap;
+    TraceScope verify_scope("otd.verify_candidates");
     uint64_t good = 0, bad = 0;
     const bool multi = false;
     for (uint32_t i = 0; i < n; ++i) {
@@ -159,6 +182,7 @@ void GpuMiner::loop() {
     s.gen = gen;
     s.variant = v;
     job->variant_header(v, s.header, &s.version, &s.ntime, &s.en2);
+    s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch" : "otd.sha256d.batch");
     OTD_HIP(hipMemsetAsync(s.d_out, 0, sizeof(uint32_t), stream));
     OTD_HIP(hipEventRecord(s.start, stream));
     if (job->algo == Algo::kScrypt) {
@@ -188,15 +212,6 @@ void GpuMiner::loop() {
   }
   finish(slots[0]);
   finish(slots[1]);
-  for (auto& s : slots) {
-    hipFree(s.d_out);
-    hipHostFree(s.h_out);
-    hipEventDestroy(s.start);
-    hipEventDestroy(s.done);
-  }
-  if (scratch) hipFree(scratch);
-  if (xbuf) hipFree(xbuf);
-  hipStreamDestroy(stream);
 }
 
 // ------------------------------------------------------------- direct launches

@@ -93,7 +93,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         obj = BUILD / (rel.replace("/", "_") + ".o")
         objs.append(obj)
         if force or _stale(obj, src, deps):
-            tasks.append(["g++", *common, "-march=x86-64-v2", f"-I{py_inc}", f"-I{pybind11.get_include()}",
+            tasks.append(["g++", *common, "-march=x86-64-v2", "-I/opt/rocm/include", f"-I{py_inc}", f"-I{pybind11.get_include()}",
                           "-fvisibility=hidden", "-c", str(src), "-o", str(obj)])
     n = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
@@ -106,7 +106,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         # which torch's bundled runtime also carries: ops.native imports torch
         # first, so the extension binds to the runtime already in the process
         # (two HIP/HSA runtimes in one process fail to enumerate the GPU).
-        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread", "-lcrypto"]
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread", "-lcrypto",
+                "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx"]
         _compile(link, verbose)
         os.replace(tmp, out)
     return out

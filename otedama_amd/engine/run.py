@@ -55,6 +55,7 @@ from otedama_amd.poolproto import Credentials, FatalPoolError, Job, ShareSubmiss
 from otedama_amd.poolproto.base import from_url, lookup
 from otedama_amd.provider import AkashProvider, MiningProvider
 from otedama_amd.utils.clock import SYSTEM, Clock
+from otedama_amd.utils.trace import mark as trace_mark
 
 RECONNECT_BACKOFF_INITIAL = 1.0
 RECONNECT_BACKOFF_MAX = 64.0
@@ -553,11 +554,13 @@ class Engine:
 
     async def _submit(self, session, sub: ShareSubmission, found_at: float = 0.0) -> None:
         self.m.shares_submitted.inc()
+        trace_mark("otd.share.submit")
         try:
             res = await session.submit(sub)
         except Exception as exc:  # noqa: BLE001
             self.log("warn", f"engine: submit share: {exc}")
             return
+        trace_mark("otd.share.ack")
         if res.accepted:
             self.m.shares_accepted.inc()
             self.latency.record(res.latency_ms)

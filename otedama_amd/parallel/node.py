@@ -29,6 +29,7 @@ import time
 
 from otedama_amd.engine.miners import MinerSet
 from otedama_amd.parallel.comm import NodeComm
+from otedama_amd.utils.trace import span
 
 DEFAULT_TICK = 0.010
 
@@ -53,15 +54,20 @@ class _Link:
 
     def step(self, ctl_words: list[int] | None, job: dict | None, outgoing: list[dict]) -> tuple:
         """One tick; returns (stop, job_or_None_if_unchanged, changed, gathered_shares)."""
-        ctl =self.comm.broadcast_control(ctl_words or [0, 0, 0, 0])
-        seq, stop = ctl[0], ctl[1]
-        changed, new_job = False, None
-        if seq != self._seen_seq:
-            new_job = self.comm.broadcast_job(job)
-            self._seen_seq = seq
-            changed = True
-        shares = self.comm.gather_shares(outgoing)
-        self.rows = self.comm.gather_counters(self.local_counters())
+        with span("otd.node.tick"):
+            with span("otd.node.R1_control"):
+                ctl = self.comm.broadcast_control(ctl_words or [0, 0, 0, 0])
+            seq, stop = ctl[0], ctl[1]
+            changed, new_job = False, None
+            if seq != self._seen_seq:
+                with span("otd.node.R1_job"):
+                    new_job = self.comm.broadcast_job(job)
+                self._seen_seq = seq
+                changed = True
+            with span("otd.node.R2_shares"):
+                shares = self.comm.gather_shares(outgoing)
+            with span("otd.node.R3_counters"):
+                self.rows = self.comm.gather_counters(self.local_counters())
         return bool(stop), new_job, changed, shares
 
 

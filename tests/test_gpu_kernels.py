@@ -185,3 +185,51 @@ def test_gpu_miner_runtime_scrypt_shares():
         d = hashlib.scrypt(bytes(h80), salt=bytes(h80), n=1024, r=1, p=1, dklen=32)
         assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
         assert s["epoch"] == 5 and s["job_id"] == "s1"
+
+
+def test_gpu_fault_retires_device_and_survivor_takes_the_stripe():
+    """SURVEY §5.3 on real hardware: a GpuMiner on a HIP ordinal that does not exist faults in its
+    device thread; MinerSet retires it, and at the next new work the surviving MI355X takes the whole
+    variant class (stride 1) and keeps producing verified shares."""
+    import dataclasses
+
+    from otedama_amd.engine.miners import MinerSet
+    from otedama_amd.hal import HIPDriver, Identity
+    from otedama_amd.models.header import int_to_hash
+
+    N = _native()
+    gpu0 = HIPDriver().enumerate()[0]
+    dead = dataclasses.replace(gpu0, ident=dataclasses.replace(gpu0.ident, id="gpu-dead"),
+                               index=N.gpu_device_count() + 7)
+    logs = []
+    ms = MinerSet([gpu0, dead], batch_nonces=1 << 28, log=lambda lvl, msg: logs.append(msg))
+    tgt = int_to_hash((1 << 232) - 1)
+    hdr1 = os.urandom(76) + bytes(4)
+    ms.start()
+    try:
+        ms.set_job({"header": hdr1, "target": tgt, "job_id": "a", "version_mask": 0x1FFFE000})
+        deadline = time.time() + 10
+        retired = []
+        while time.time() < deadline and not retired:
+            retired = ms.retire_faulted()
+            time.sleep(0.05)
+        assert [d for d, _ in retired] == ["gpu-dead"], (retired, ms.device_stats())
+        assert "HIP error" in retired[0][1]
+        hdr2 = os.urandom(76) + bytes(4)
+        ep = ms.set_job({"header": hdr2, "target": tgt, "job_id": "b", "version_mask": 0x1FFFE000})
+        assert (ms.miners[0].stripe_index, ms.miners[0].stripe_stride) == (0, 1)
+        shares, deadline = [], time.time() + 20
+        while time.time() < deadline and len(shares) < 10:
+            shares += [s for s in ms.poll(256) if s["epoch"] == ep]
+            time.sleep(0.02)
+    finally:
+        ms.stop()
+    assert len(shares) >= 5 and all(s["device_id"] == "gpu-0" for s in shares)
+    for s in shares:
+        h80 = bytearray(hdr2)
+        struct.pack_into("<I", h80, 0, s["version"])
+        struct.pack_into("<I", h80, 76, s["nonce"])
+        d = hashlib.sha256(hashlib.sha256(bytes(h80)).digest()).digest()
+        assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
+    assert not ms.device_stats()["gpu-0"]["faulted"]
+    assert any("re-split" in m for m in logs)
