@@ -173,6 +173,40 @@ class Engine:
             "est_sats": self.est_sats, "activity": dict(self.activity),
         }
 
+    def debug_stats(self) -> dict:
+        """GET /debug/stats: raw native counters and the scheduler state behind them,
+        for diagnosing a device or node without attaching a profiler."""
+        import resource
+        import threading as _th
+
+        ms = self.miners
+        devs = {}
+        if ms is not None:
+            raw = ms.device_stats()
+            stalled = set(ms.stalled())
+            for m in ms.miners:
+                st = dict(raw.get(m.id, {}))
+                up = max(self.opts.clock.now() - self.start_time, 1e-9)
+                st.update({"stripe_start": m.stripe_index, "stripe_stride": m.stripe_stride, "paused": m.paused,
+                           "retired": m.retired, "stalled": m.id in stalled, "hashrate": m.hashrate,
+                           "idle_samples": m.idle_samples, "busy_ratio": st.get("busy_seconds", 0.0) / up})
+                devs[m.id] = st
+            for rid in getattr(ms, "remote_ids", []):
+                devs[rid] = dict(raw.get(rid, {}), hashrate=ms.hashrate_of(rid), stalled=rid in stalled)
+        link = getattr(ms, "link", None)
+        return {
+            "epoch": ms.epoch if ms is not None else 0,
+            "devices": devs,
+            "node": None if link is None else {"rank": link.rank, "world": link.world, "tick_s": link.tick,
+                                               "counter_rows": link.rows,
+                                               "error": str(link.error) if link.error else None},
+            "submit_tasks_inflight": len(self._submit_tasks),
+            "latency_ms": {"p50": self.latency.quantile(0.5), "p95": self.latency.quantile(0.95),
+                           "p99": self.latency.quantile(0.99)},
+            "process": {"threads": _th.active_count(),
+                        "max_rss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0},
+        }
+
     def device_list(self) -> list[dict]:
         return [{"id": d.identity().id, "family": d.identity().family.value, "vendor": d.identity().vendor,
                  "model": d.identity().model, "capabilities": d.capabilities().__dict__} for d in self.devices]

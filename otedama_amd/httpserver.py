@@ -6,6 +6,8 @@ Parity: internal/httpserver/server.go
     /metrics text/plain; version=0.0.4; / index; 404 elsewhere  server.go:172-206
   * pprof mount (opt-in) -> /debug/pprof/{,goroutine,profile,heap}
     (Python equivalents: thread stacks, cProfile sample, gc/tracemalloc)
+  * /debug/stats: raw native device counters + stripe/fault/stall state (JSON; MI355X
+    addition), served whenever the owner registers a ``debug_stats`` provider
   * timeouts: 5 s header read / 10 s read / 10 s write / 60 s idle
 Additions for the north star's "REST/WS API": GET /api/v1/{stats,devices,pool}
 (JSON from provider callbacks) and a minimal RFC 6455 WebSocket at /ws that
@@ -39,6 +41,7 @@ INDEX_HTML = """<!DOCTYPE html>
 <li><a href="/healthz">/healthz</a> &mdash; liveness probe</li>
 <li><a href="/readyz">/readyz</a> &mdash; readiness probe</li>
 <li><a href="/api/v1/stats">/api/v1/stats</a> &mdash; live stats (JSON); <code>/ws</code> streams them</li>
+<li><a href="/debug/stats">/debug/stats</a> &mdash; per-device native counters, stripes, faults, stalls</li>
 </ul>
 </body>
 </html>
@@ -99,6 +102,12 @@ class _Handler(BaseHTTPRequestHandler):
             return self._send(200, body, "application/json")
         if path == "/ws" and "stats" in app.api:
             return self._websocket(app.api["stats"])
+        if path == "/debug/stats" and "debug_stats" in app.api:
+            try:
+                body = json.dumps(app.api["debug_stats"](), default=_json_default).encode() + b"\n"
+            except Exception as exc:  # noqa: BLE001
+                return self._send(500, json.dumps({"error": str(exc)}).encode(), "application/json")
+            return self._send(200, body, "application/json")
         if app.pprof and path.startswith("/debug/pprof"):
             return self._pprof(path)
         return self._send(404, b"404 page not found\n", "text/plain; charset=utf-8")

@@ -68,7 +68,8 @@ def _get(url):
 def test_http_endpoints():
     reg = Registry()
     reg.new_gauge("otedama_hashrate", "H/s").set(5.0)
-    srv = HTTPServer("127.0.0.1:0", reg, api={"stats": lambda: {"hashrate": 5.0}})
+    srv = HTTPServer("127.0.0.1:0", reg, api={"stats": lambda: {"hashrate": 5.0},
+                                               "debug_stats": lambda: {"devices": {"gpu-0": {"faulted": False}}}})
     srv.start()
     base = f"http://{srv.addr}"
     try:
@@ -82,6 +83,8 @@ def test_http_endpoints():
         assert code == 200 and json.loads(body) == {"hashrate": 5.0}
         assert _get(base + "/api/v1/nope")[0] == 404
         assert _get(base + "/debug/pprof/")[0] == 404  # pprof off by default
+        code, body, ctype = _get(base + "/debug/stats")     # debug stats are not behind the pprof opt-in
+        assert code == 200 and json.loads(body)["devices"]["gpu-0"] == {"faulted": False} and "json" in ctype
         assert _get(base + "/nothing")[0] == 404
         # websocket upgrade handshake
         host, port = srv.addr.rsplit(":", 1)

@@ -54,6 +54,12 @@ def test_engine_mines_accepted_shares(scheme):
     assert "otedama_hashrate_hashes_per_second" in text
     assert eng.current_hashrate > 0
     assert eng.latency.quantile(0.5) > 0
+    dbg = eng.debug_stats()                      # GET /debug/stats payload
+    cpu = dbg["devices"]["cpu-0"]
+    assert cpu["hashes"] > 0 and cpu["shares"] >= 1 and not cpu["faulted"] and not cpu["retired"]
+    assert (cpu["stripe_start"], cpu["stripe_stride"]) == (0, 1) and 0 < cpu["busy_ratio"] <= 2.5
+    assert dbg["epoch"] >= 1 and dbg["node"] is None and dbg["process"]["threads"] >= 1
+    assert 'otedama_devices_active' in text
 
 
 def test_engine_reconnects_on_pool_failure():
