@@ -44,13 +44,19 @@ class DistInfo:
 
 
 def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> DistInfo:
-    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun)."""
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun).
+
+    One rank per GPU (LOCAL_RANK = HIP ordinal) over RCCL. ``OTEDAMA_DIST_BACKEND=gloo`` rehearses the
+    N-rank control flow on fewer GPUs than ranks (ranks share ordinals modulo the device count; RCCL
+    itself refuses two ranks on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    backend = backend or os.environ.get("OTEDAMA_DIST_BACKEND") or None
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
-    device = torch.device(f"cuda:{local}") if use_gpu else torch.device("cpu")
+    ordinal = local % max(1, torch.cuda.device_count()) if (use_gpu and backend == "gloo") else local
+    device = torch.device(f"cuda:{ordinal}") if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     if world <= 1:
