@@ -14,6 +14,7 @@
 #include "otedama/runtime.h"
 #include "otedama/trace.h"
 #include "otedama/sha256.h"
+#include "otedama/x11.h"
 
 namespace py = pybind11;
 using namespace otedama;
@@ -23,6 +24,10 @@ void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, ui
                        uintptr_t stream);
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
+void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
+                         uintptr_t out, uint32_t cap, uintptr_t stream);
+void py_launch_x11(const X11Params& p, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n, uintptr_t out,
+                   uint32_t cap, uintptr_t stream);
 uint64_t scrypt_scratch_bytes(int grid, int gap);
 int gpu_device_count();
 std::string gpu_arch_name(int device);
@@ -56,6 +61,7 @@ std::shared_ptr<JobTemplate> make_job(const py::dict& d) {
     auto a = d["algo"].cast<std::string>();
     if (a == "sha256d") j->algo = Algo::kSha256d;
     else if (a == "scrypt") j->algo = Algo::kScrypt;
+    else if (a == "x11") j->algo = Algo::kX11;
     else throw std::invalid_argument("unsupported algo for the native miner: " + a);
   }
   if (!get("version_mask").is_none()) j->version_mask = d["version_mask"].cast<uint32_t>();
@@ -156,6 +162,23 @@ PYBIND11_MODULE(_native, m) {
     { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }
     return to_bytes(o, 32);
   });
+  m.attr("X11_STAGES") = kX11StageCount;
+  m.def("x11", [](const py::bytes& msg) {
+    std::string s = msg; uint8_t o[32];
+    { py::gil_scoped_release r; x11::x11(reinterpret_cast<const uint8_t*>(s.data()), s.size(), o, nullptr); }
+    return to_bytes(o, 32);
+  }, py::arg("msg"));
+  m.def("x11_trace", [](const py::bytes& msg) {
+    std::string s = msg; uint8_t o[32], t[64 * kX11StageCount];
+    x11::x11(reinterpret_cast<const uint8_t*>(s.data()), s.size(), o, t);
+    return to_bytes(t, sizeof t);
+  }, py::arg("msg"), "The 11 intermediate 64-byte digests of the X11 chain, concatenated.");
+  m.def("x11_stage", [](int i, const py::bytes& msg) {
+    if (i < 0 || i >= kX11StageCount) throw std::invalid_argument("stage must be in [0, 11)");
+    std::string s = msg; uint8_t o[64];
+    x11::stage(i, reinterpret_cast<const uint8_t*>(s.data()), s.size(), o);
+    return to_bytes(o, 64);
+  }, py::arg("stage"), py::arg("msg"));
   m.def("cpu_scan_sha256d", [](const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     std::vector<uint32_t> hits;
@@ -193,6 +216,13 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   });
 
+  m.def("x11_prepare", [](const py::bytes& h, const py::bytes& t) {
+    std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
+    X11Params p;
+    x11_prepare(reinterpret_cast<const uint8_t*>(hs.data()), reinterpret_cast<const uint8_t*>(ts.data()), &p);
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
+  });
+
   // roctx ranges for Python-side spans (node collectives, share submit, bench steps): SURVEY §5.1.
   m.def("trace_push", [](const std::string& name) { trace_push(name.c_str()); });
   m.def("trace_pop", [] { trace_pop(); });
@@ -220,6 +250,24 @@ PYBIND11_MODULE(_native, m) {
     py_launch_scrypt(p, base, count, xbuf, scratch, gap, out, cap, grid, stream);
   }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("xbuf"), py::arg("scratch"), py::arg("gap"),
      py::arg("out"), py::arg("cap"), py::arg("grid"), py::arg("stream"));
+
+  m.def("launch_x11_stage", [](const py::bytes& params, int stage, uint32_t base, uintptr_t H, uint32_t stride,
+                               uint32_t n, uintptr_t out, uint32_t cap, uintptr_t stream) {
+    std::string ps = need(params, sizeof(X11Params), "params");
+    X11Params p; std::memcpy(&p, ps.data(), sizeof p);
+    if (stage < 0 || stage >= kX11StageCount) throw std::invalid_argument("stage must be in [0, 11)");
+    if (H == 0 || n == 0 || stride < n) throw std::invalid_argument("need H != 0, n > 0, stride >= n");
+    py_launch_x11_stage(p, stage, base, H, stride, n, out, cap, stream);
+  }, py::arg("params"), py::arg("stage"), py::arg("base"), py::arg("H"), py::arg("stride"), py::arg("n"),
+     py::arg("out") = 0, py::arg("cap") = 0, py::arg("stream") = 0);
+  m.def("launch_x11", [](const py::bytes& params, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
+                         uintptr_t out, uint32_t cap, uintptr_t stream) {
+    std::string ps = need(params, sizeof(X11Params), "params");
+    X11Params p; std::memcpy(&p, ps.data(), sizeof p);
+    if (H == 0 || n == 0 || stride < n) throw std::invalid_argument("need H != 0, n > 0, stride >= n");
+    py_launch_x11(p, base, H, stride, n, out, cap, stream);
+  }, py::arg("params"), py::arg("base"), py::arg("H"), py::arg("stride"), py::arg("n"), py::arg("out") = 0,
+     py::arg("cap") = 0, py::arg("stream") = 0);
 
   py::class_<MinerBase, std::shared_ptr<MinerBase>>(m, "Miner")
       .def("start", &MinerBase::start, py::call_guard<py::gil_scoped_release>())

@@ -49,3 +49,13 @@ void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], Scry
 }
 
 }  // namespace otedama
+
+namespace otedama {
+
+void x11_prepare(const uint8_t header80[80], const uint8_t target32[32], X11Params* p) {
+  for (int k = 0; k < 9; ++k) p->m[k] = (uint64_t(load_be32(header80 + 8 * k)) << 32) | load_be32(header80 + 8 * k + 4);
+  p->m9_hi = uint64_t(load_be32(header80 + 72)) << 32;
+  p->target_hi = (uint64_t(load_le32(target32 + 28)) << 32) | load_le32(target32 + 24);
+}
+
+}  // namespace otedama

@@ -12,6 +12,8 @@
 #include <cstdint>
 #include <cstring>
 
+#include "otedama/x11.h"
+
 namespace otedama {
 namespace x11 {
 
@@ -37,7 +39,7 @@ static inline void st32be(u8* p, u32 v) { for (int i = 3; i >= 0; --i) { p[i] = 
 static u8 SBOX[256];
 static bool sbox_ready = false;
 static inline u8 rotl8(u8 x, int n) { return (u8)((x << n) | (x >> (8 - n))); }
-static void init_sbox() {
+static void init_sbox_impl() {
     if (sbox_ready) return;
     u8 p = 1, q = 1;
     do {
@@ -49,6 +51,8 @@ static void init_sbox() {
     SBOX[0] = 0x63;
     sbox_ready = true;
 }
+// Thread-safe one-time init (miner threads verify shares concurrently).
+static void init_sbox() { static const bool once = (init_sbox_impl(), true); (void)once; }
 const u8* aes_sbox() { init_sbox(); return SBOX; }
 static inline u8 xt(u8 x) { return (u8)((x << 1) ^ ((x & 0x80) ? 0x1B : 0)); }
 static inline u8 gmul(u8 a, u8 b) {
@@ -449,7 +453,7 @@ static void jh_round(u8* e, int dim, const u8* cb) {
 }
 static u8 JH_C[42][256];  // round-constant bits, one per element
 static bool jh_ready = false;
-static void jh_init_constants() {
+static void jh_init_constants_impl() {
     if (jh_ready) return;
     // C0 = first 256 bits of the fractional part of sqrt(2)
     static const u8 C0[32] = {0x6a, 0x09, 0xe6, 0x67, 0xf3, 0xbc, 0xc9, 0x08, 0xb2, 0xfb, 0x13, 0x66, 0xea, 0x95, 0x7d, 0x3e,
@@ -464,6 +468,7 @@ static void jh_init_constants() {
     }
     jh_ready = true;
 }
+static void jh_init_constants() { static const bool once = (jh_init_constants_impl(), true); (void)once; }
 const u8* jh_round_constant_bits(int r) { jh_init_constants(); return JH_C[r]; }
 static void jh_E8(u8 H[128]) {
     auto bit = [&](int i) -> u8 { return (H[i >> 3] >> (7 - (i & 7))) & 1; };

@@ -38,6 +38,16 @@ struct ScryptParams {
 
 void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], ScryptParams* out);
 
+// X11 (Dash) job parameters. Stage 1 (BLAKE-512) sees the whole 80-byte header
+// as one padded block; only the low half of message word 9 carries the nonce.
+struct X11Params {
+  uint64_t m[9];       // header bytes 0..71 as big-endian 64-bit words
+  uint64_t m9_hi;      // header bytes 72..75 (nbits) in the high half of word 9
+  uint64_t target_hi;  // most-significant 64 bits of the LE share target (bytes 24..31)
+};
+
+void x11_prepare(const uint8_t header80[80], const uint8_t target32[32], X11Params* out);
+
 // `gap` selector for launch_scrypt_search: 1/2/4 = per-lane ROMix with that lookup gap,
 // kScryptCoop = lane-cooperative ROMix (full-line octet lookups, gap 1).
 constexpr int kScryptCoop = 8;

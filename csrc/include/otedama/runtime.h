@@ -23,7 +23,7 @@
 
 namespace otedama {
 
-enum class Algo : int { kSha256d = 0, kScrypt = 1 };
+enum class Algo : int { kSha256d = 0, kScrypt = 1, kX11 = 2 };
 
 // A pool job plus the rules for deriving header variants from it.
 struct JobTemplate {

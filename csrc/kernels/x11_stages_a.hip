@@ -1,0 +1,443 @@
+// X11 stages 1-6 on gfx950: BLAKE-512 (80-byte header), BMW-512, Groestl-512,
+// Skein-512, JH-512, Keccak-512 (64-byte inputs). One lane per nonce; the padding
+// blocks of the fixed-length inputs are folded into compile-time constants.
+// Bit-exact oracle: csrc/cpu/x11_cpu.cpp (tests/test_x11_gpu.py compares every stage).
+#include "x11_common.h"
+
+namespace otedama {
+namespace x11k {
+
+// ------------------------------------------------------------------ BLAKE-512
+__constant__ u64 c_blake_c[16] = {
+    0x243F6A8885A308D3ull, 0x13198A2E03707344ull, 0xA4093822299F31D0ull, 0x082EFA98EC4E6C89ull,
+    0x452821E638D01377ull, 0xBE5466CF34E90C6Cull, 0xC0AC29B7C97C50DDull, 0x3F84D5B5B5470917ull,
+    0x9216D5D98979FB1Bull, 0xD1310BA698DFB5ACull, 0x2FFD72DBD01ADFB7ull, 0xB8E1AFED6A267E96ull,
+    0xBA7C9045F12C7F99ull, 0x24A19947B3916CF7ull, 0x0801F2E2858EFC16ull, 0x636920D871574E69ull};
+constexpr u64 kBlakeC[16] = {
+    0x243F6A8885A308D3ull, 0x13198A2E03707344ull, 0xA4093822299F31D0ull, 0x082EFA98EC4E6C89ull,
+    0x452821E638D01377ull, 0xBE5466CF34E90C6Cull, 0xC0AC29B7C97C50DDull, 0x3F84D5B5B5470917ull,
+    0x9216D5D98979FB1Bull, 0xD1310BA698DFB5ACull, 0x2FFD72DBD01ADFB7ull, 0xB8E1AFED6A267E96ull,
+    0xBA7C9045F12C7F99ull, 0x24A19947B3916CF7ull, 0x0801F2E2858EFC16ull, 0x636920D871574E69ull};
+constexpr unsigned char kSigma[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+constexpr u64 kSha512Iv[8] = {0x6A09E667F3BCC908ull, 0xBB67AE8584CAA73Bull, 0x3C6EF372FE94F82Bull, 0xA54FF53A5F1D36F1ull,
+                              0x510E527FADE682D1ull, 0x9B05688C2B3E6C1Full, 0x1F83D9ABFB41BD6Bull, 0x5BE0CD19137E2179ull};
+
+#define BLAKE_G(a, b, c, d, x, y)                 \
+  do {                                            \
+    v[a] = v[a] + v[b] + (m[x] ^ kBlakeC[y]);     \
+    v[d] = rotr64(v[d] ^ v[a], 32);               \
+    v[c] = v[c] + v[d];                           \
+    v[b] = rotr64(v[b] ^ v[c], 25);               \
+    v[a] = v[a] + v[b] + (m[y] ^ kBlakeC[x]);     \
+    v[d] = rotr64(v[d] ^ v[a], 16);               \
+    v[c] = v[c] + v[d];                           \
+    v[b] = rotr64(v[b] ^ v[c], 11);               \
+  } while (0)
+
+__global__ __launch_bounds__(kBlock) void k_blake512_80(X11Params p, u32 base, u64* __restrict__ H, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 m[16];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) m[k] = p.m[k];
+  m[9] = p.m9_hi | bswap32(base + i);
+  m[10] = 0x8000000000000000ull;
+  m[11] = 0; m[12] = 0; m[13] = 1; m[14] = 0; m[15] = 640;
+  u64 v[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = kSha512Iv[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[8 + k] = kBlakeC[k];
+  v[12] = 640 ^ kBlakeC[4];
+  v[13] = 640 ^ kBlakeC[5];
+  v[14] = kBlakeC[6];
+  v[15] = kBlakeC[7];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const unsigned char* s = kSigma[r % 10];
+    BLAKE_G(0, 4, 8, 12, s[0], s[1]);
+    BLAKE_G(1, 5, 9, 13, s[2], s[3]);
+    BLAKE_G(2, 6, 10, 14, s[4], s[5]);
+    BLAKE_G(3, 7, 11, 15, s[6], s[7]);
+    BLAKE_G(0, 5, 10, 15, s[8], s[9]);
+    BLAKE_G(1, 6, 11, 12, s[10], s[11]);
+    BLAKE_G(2, 7, 8, 13, s[12], s[13]);
+    BLAKE_G(3, 4, 9, 14, s[14], s[15]);
+  }
+  u64 h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = bswap64(kSha512Iv[k] ^ v[k] ^ v[k + 8]);
+  store_hash(H, stride, i, h);
+}
+#undef BLAKE_G
+
+// ------------------------------------------------------------------ BMW-512
+__device__ __forceinline__ u64 bs0(u64 x) { return (x >> 1) ^ (x << 3) ^ rotl64(x, 4) ^ rotl64(x, 37); }
+__device__ __forceinline__ u64 bs1(u64 x) { return (x >> 1) ^ (x << 2) ^ rotl64(x, 13) ^ rotl64(x, 43); }
+__device__ __forceinline__ u64 bs2(u64 x) { return (x >> 2) ^ (x << 1) ^ rotl64(x, 19) ^ rotl64(x, 53); }
+__device__ __forceinline__ u64 bs3(u64 x) { return (x >> 2) ^ (x << 2) ^ rotl64(x, 28) ^ rotl64(x, 59); }
+__device__ __forceinline__ u64 bs4(u64 x) { return (x >> 1) ^ x; }
+__device__ __forceinline__ u64 bs5(u64 x) { return (x >> 2) ^ x; }
+
+__device__ __forceinline__ void bmw_compress(u64 H[16], const u64 M[16]) {
+  u64 X[16], Q[32];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) X[k] = M[k] ^ H[k];
+  Q[0] = bs0(X[5] - X[7] + X[10] + X[13] + X[14]) + H[1];
+  Q[1] = bs1(X[6] - X[8] + X[11] + X[14] - X[15]) + H[2];
+  Q[2] = bs2(X[0] + X[7] + X[9] - X[12] + X[15]) + H[3];
+  Q[3] = bs3(X[0] - X[1] + X[8] - X[10] + X[13]) + H[4];
+  Q[4] = bs4(X[1] + X[2] + X[9] - X[11] - X[14]) + H[5];
+  Q[5] = bs0(X[3] - X[2] + X[10] - X[12] + X[15]) + H[6];
+  Q[6] = bs1(X[4] - X[0] - X[3] - X[11] + X[13]) + H[7];
+  Q[7] = bs2(X[1] - X[4] - X[5] - X[12] - X[14]) + H[8];
+  Q[8] = bs3(X[2] - X[5] - X[6] + X[13] - X[15]) + H[9];
+  Q[9] = bs4(X[0] - X[3] + X[6] - X[7] + X[14]) + H[10];
+  Q[10] = bs0(X[8] - X[1] - X[4] - X[7] + X[15]) + H[11];
+  Q[11] = bs1(X[8] - X[0] - X[2] - X[5] + X[9]) + H[12];
+  Q[12] = bs2(X[1] + X[3] - X[6] - X[9] + X[10]) + H[13];
+  Q[13] = bs3(X[2] + X[4] + X[7] + X[10] + X[11]) + H[14];
+  Q[14] = bs4(X[3] - X[5] + X[8] - X[11] - X[12]) + H[15];
+  Q[15] = bs0(X[12] - X[4] - X[6] - X[9] + X[13]) + H[0];
+#pragma unroll
+  for (int j = 16; j < 32; ++j) {
+    const int jj = j - 16;
+    u64 add = rotl64(M[jj & 15], (jj & 15) + 1) + rotl64(M[(jj + 3) & 15], ((jj + 3) & 15) + 1) -
+              rotl64(M[(jj + 10) & 15], ((jj + 10) & 15) + 1) + (u64)j * 0x0555555555555555ull;
+    add ^= H[(jj + 7) & 15];
+    u64 q;
+    if (j < 18) {
+      q = bs1(Q[j - 16]) + bs2(Q[j - 15]) + bs3(Q[j - 14]) + bs0(Q[j - 13]) + bs1(Q[j - 12]) + bs2(Q[j - 11]) +
+          bs3(Q[j - 10]) + bs0(Q[j - 9]) + bs1(Q[j - 8]) + bs2(Q[j - 7]) + bs3(Q[j - 6]) + bs0(Q[j - 5]) +
+          bs1(Q[j - 4]) + bs2(Q[j - 3]) + bs3(Q[j - 2]) + bs0(Q[j - 1]);
+    } else {
+      q = Q[j - 16] + rotl64(Q[j - 15], 5) + Q[j - 14] + rotl64(Q[j - 13], 11) + Q[j - 12] + rotl64(Q[j - 11], 27) +
+          Q[j - 10] + rotl64(Q[j - 9], 32) + Q[j - 8] + rotl64(Q[j - 7], 37) + Q[j - 6] + rotl64(Q[j - 5], 43) +
+          Q[j - 4] + rotl64(Q[j - 3], 53) + bs4(Q[j - 2]) + bs5(Q[j - 1]);
+    }
+    Q[j] = q + add;
+  }
+  u64 XL = Q[16] ^ Q[17] ^ Q[18] ^ Q[19] ^ Q[20] ^ Q[21] ^ Q[22] ^ Q[23];
+  u64 XH = XL ^ Q[24] ^ Q[25] ^ Q[26] ^ Q[27] ^ Q[28] ^ Q[29] ^ Q[30] ^ Q[31];
+  H[0] = ((XH << 5) ^ (Q[16] >> 5) ^ M[0]) + (XL ^ Q[24] ^ Q[0]);
+  H[1] = ((XH >> 7) ^ (Q[17] << 8) ^ M[1]) + (XL ^ Q[25] ^ Q[1]);
+  H[2] = ((XH >> 5) ^ (Q[18] << 5) ^ M[2]) + (XL ^ Q[26] ^ Q[2]);
+  H[3] = ((XH >> 1) ^ (Q[19] << 5) ^ M[3]) + (XL ^ Q[27] ^ Q[3]);
+  H[4] = ((XH >> 3) ^ Q[20] ^ M[4]) + (XL ^ Q[28] ^ Q[4]);
+  H[5] = ((XH << 6) ^ (Q[21] >> 6) ^ M[5]) + (XL ^ Q[29] ^ Q[5]);
+  H[6] = ((XH >> 4) ^ (Q[22] << 6) ^ M[6]) + (XL ^ Q[30] ^ Q[6]);
+  H[7] = ((XH >> 11) ^ (Q[23] << 2) ^ M[7]) + (XL ^ Q[31] ^ Q[7]);
+  H[8] = rotl64(H[4], 9) + (XH ^ Q[24] ^ M[8]) + ((XL << 8) ^ Q[23] ^ Q[8]);
+  H[9] = rotl64(H[5], 10) + (XH ^ Q[25] ^ M[9]) + ((XL >> 6) ^ Q[16] ^ Q[9]);
+  H[10] = rotl64(H[6], 11) + (XH ^ Q[26] ^ M[10]) + ((XL << 6) ^ Q[17] ^ Q[10]);
+  H[11] = rotl64(H[7], 12) + (XH ^ Q[27] ^ M[11]) + ((XL << 4) ^ Q[18] ^ Q[11]);
+  H[12] = rotl64(H[0], 13) + (XH ^ Q[28] ^ M[12]) + ((XL >> 3) ^ Q[19] ^ Q[12]);
+  H[13] = rotl64(H[1], 14) + (XH ^ Q[29] ^ M[13]) + ((XL >> 4) ^ Q[20] ^ Q[13]);
+  H[14] = rotl64(H[2], 15) + (XH ^ Q[30] ^ M[14]) + ((XL >> 7) ^ Q[21] ^ Q[14]);
+  H[15] = rotl64(H[3], 16) + (XH ^ Q[31] ^ M[15]) + ((XL >> 2) ^ Q[22] ^ Q[15]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_bmw512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 M[16], H[16];
+  load_hash(Hb, stride, i, M);
+  M[8] = 0x80; M[9] = 0; M[10] = 0; M[11] = 0; M[12] = 0; M[13] = 0; M[14] = 0; M[15] = 512;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const u64 b = 0x80 + 8 * k;
+    H[k] = (b << 56) | ((b + 1) << 48) | ((b + 2) << 40) | ((b + 3) << 32) | ((b + 4) << 24) | ((b + 5) << 16) |
+           ((b + 6) << 8) | (b + 7);
+  }
+  bmw_compress(H, M);
+  u64 F[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) F[k] = 0xAAAAAAAAAAAAAAA0ull + (u64)k;
+  bmw_compress(F, H);
+  store_hash(Hb, stride, i, F + 8);
+}
+
+// ------------------------------------------------------------------ Groestl-512
+// Column j of the 8x16 byte state is one 64-bit word (row r in byte r). A round
+// is 128 T-table lookups from LDS: T[r] = rotl64(T0, 8r).
+template <bool kQ>
+__device__ __forceinline__ void groestl_perm(const u64 (*T)[256], u64 a[16]) {
+  constexpr int SP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
+  constexpr int SQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
+  for (int r = 0; r < 14; ++r) {
+    if (!kQ) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] ^= (u64)((j << 4) ^ r);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] ^= ~((u64)((j << 4) ^ r) << 56);
+    }
+    u64 t[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      u64 acc = 0;
+#pragma unroll
+      for (int row = 0; row < 8; ++row) {
+        const int src = (j + (kQ ? SQ[row] : SP[row])) & 15;
+        const u32 byte = row < 4 ? (lo32(a[src]) >> (8 * row)) & 0xff : (hi32(a[src]) >> (8 * (row - 4))) & 0xff;
+        acc ^= T[row][byte];
+      }
+      t[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = t[j];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u64 T[8][256];
+  for (int x = threadIdx.x; x < 256; x += kBlock) {
+    const u64 v = x11t::GROESTL_T0[x];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) T[r][x] = r ? rotl64(v, 8 * r) : v;
+  }
+  __syncthreads();
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 m[16], p[16], q[16];
+  load_hash(Hb, stride, i, m);
+  m[8] = 0x80;
+#pragma unroll
+  for (int k = 9; k < 15; ++k) m[k] = 0;
+  m[15] = 0x0100000000000000ull;  // one block, 64-bit big-endian count
+  const u64 iv15 = 0x0002000000000000ull;  // 512 in the last bytes of h
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { p[k] = m[k]; q[k] = m[k]; }
+  p[15] ^= iv15;
+  groestl_perm<false>(T, p);
+  groestl_perm<true>(T, q);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) p[k] ^= q[k];
+  p[15] ^= iv15;  // h' = P(h^m) ^ Q(m) ^ h
+#pragma unroll
+  for (int k = 0; k < 16; ++k) q[k] = p[k];
+  groestl_perm<false>(T, q);
+  u64 out[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = q[8 + k] ^ p[8 + k];
+  store_hash(Hb, stride, i, out);
+}
+
+// ------------------------------------------------------------------ Skein-512
+constexpr int kSkeinR[8][4] = {{46, 36, 19, 37}, {33, 27, 14, 42}, {17, 49, 36, 39}, {44, 9, 54, 56},
+                               {39, 30, 34, 24}, {13, 50, 10, 17}, {25, 29, 39, 43}, {8, 35, 56, 22}};
+
+__device__ __forceinline__ void threefish512(const u64 key[8], u64 t0, u64 t1, u64 v[8]) {
+  u64 k[9];
+  k[8] = 0x1BD11BDAA9FC1A22ull;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { k[j] = key[j]; k[8] ^= key[j]; }
+  const u64 t[3] = {t0, t1, t0 ^ t1};
+#pragma unroll
+  for (int d = 0; d < 72; ++d) {
+    if ((d & 3) == 0) {
+      const int s = d / 4;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += k[(s + j) % 9];
+      v[5] += t[s % 3];
+      v[6] += t[(s + 1) % 3];
+      v[7] += (u64)s;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] += v[2 * j + 1];
+      v[2 * j + 1] = rotl64(v[2 * j + 1], kSkeinR[d & 7][j]) ^ v[2 * j];
+    }
+    const u64 p0 = v[2], p1 = v[1], p2 = v[4], p3 = v[7], p4 = v[6], p5 = v[5], p6 = v[0], p7 = v[3];
+    v[0] = p0; v[1] = p1; v[2] = p2; v[3] = p3; v[4] = p4; v[5] = p5; v[6] = p6; v[7] = p7;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] += k[(18 + j) % 9];
+  v[5] += t[0];
+  v[6] += t[1];
+  v[7] += 18;
+}
+
+__global__ __launch_bounds__(kBlock) void k_skein512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 m[8], v[8], h[8];
+  load_hash(Hb, stride, i, m);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { v[k] = m[k]; h[k] = x11t::SKEIN_IV[k]; }
+  threefish512(h, 64, 0xF000000000000000ull, v);  // message: first|final, type 48, position 64
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { h[k] = v[k] ^ m[k]; v[k] = 0; }
+  threefish512(h, 8, 0xFF00000000000000ull, v);   // output: first|final, type 63, position 8
+  store_hash(Hb, stride, i, v);
+}
+
+// ------------------------------------------------------------------ JH-512
+// Bitsliced E8 on the state kept in memory order (x[k][w] = LE u32 word w of
+// bytes 16k..16k+15); constants re-labelled from the spec constants by
+// tools/gen_x11_tables.cpp, which checks this formulation against the spec form.
+__constant__ u32 c_jh_bc[42][8];
+
+#define JH_SS(m0, m1, m2, m3, m4, m5, m6, m7, cc0, cc1) \
+  do {                                                  \
+    u32 t0_, t1_;                                       \
+    m3 = ~m3; m7 = ~m7;                                 \
+    m0 ^= (~m2) & (cc0); m4 ^= (~m6) & (cc1);           \
+    t0_ = (cc0) ^ (m0 & m1); t1_ = (cc1) ^ (m4 & m5);   \
+    m0 ^= m2 & m3; m4 ^= m6 & m7;                       \
+    m3 ^= (~m1) & m2; m7 ^= (~m5) & m6;                 \
+    m1 ^= m0 & m2; m5 ^= m4 & m6;                       \
+    m2 ^= m0 & (~m3); m6 ^= m4 & (~m7);                 \
+    m0 ^= m1 | m3; m4 ^= m5 | m7;                       \
+    m3 ^= m1 & m2; m7 ^= m5 & m6;                       \
+    m1 ^= t0_ & m0; m5 ^= t1_ & m4;                     \
+    m2 ^= t0_; m6 ^= t1_;                               \
+  } while (0)
+#define JH_L(m0, m1, m2, m3, m4, m5, m6, m7) \
+  do {                                       \
+    m4 ^= m1; m5 ^= m2; m6 ^= m0 ^ m3; m7 ^= m0; \
+    m0 ^= m5; m1 ^= m6; m2 ^= m4 ^ m7; m3 ^= m4; \
+  } while (0)
+
+template <int K>
+__device__ __forceinline__ u32 jh_swap(u32 x) {
+  if (K == 0) return ((x & 0x55555555u) << 1) | ((x >> 1) & 0x55555555u);
+  if (K == 1) return ((x & 0x33333333u) << 2) | ((x >> 2) & 0x33333333u);
+  if (K == 2) return ((x & 0x0F0F0F0Fu) << 4) | ((x >> 4) & 0x0F0F0F0Fu);
+  if (K == 3) return __builtin_amdgcn_perm(x, x, 0x02030001u);  // swap bytes within each 16-bit half
+  return rotl32(x, 16);
+}
+
+template <int K>
+__device__ __forceinline__ void jh_round(u32 x[8][4], const u32* c) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    JH_SS(x[0][w], x[2][w], x[4][w], x[6][w], x[1][w], x[3][w], x[5][w], x[7][w], c[w], c[4 + w]);
+    JH_L(x[0][w], x[2][w], x[4][w], x[6][w], x[1][w], x[3][w], x[5][w], x[7][w]);
+  }
+#pragma unroll
+  for (int o = 1; o < 8; o += 2) {
+    if (K < 5) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) x[o][w] = jh_swap<K>(x[o][w]);
+    } else if (K == 5) {
+      u32 t = x[o][0]; x[o][0] = x[o][1]; x[o][1] = t;
+      t = x[o][2]; x[o][2] = x[o][3]; x[o][3] = t;
+    } else {
+      u32 t = x[o][0]; x[o][0] = x[o][2]; x[o][2] = t;
+      t = x[o][1]; x[o][1] = x[o][3]; x[o][3] = t;
+    }
+  }
+}
+
+__device__ __forceinline__ void jh_E8(u32 x[8][4]) {
+  for (int r = 0; r < 42; r += 7) {
+    jh_round<0>(x, c_jh_bc[r + 0]);
+    jh_round<1>(x, c_jh_bc[r + 1]);
+    jh_round<2>(x, c_jh_bc[r + 2]);
+    jh_round<3>(x, c_jh_bc[r + 3]);
+    jh_round<4>(x, c_jh_bc[r + 4]);
+    jh_round<5>(x, c_jh_bc[r + 5]);
+    jh_round<6>(x, c_jh_bc[r + 6]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_jh512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  u32 m[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { m[2 * k] = lo32(h[k]); m[2 * k + 1] = hi32(h[k]); }
+  u32 x[8][4];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) x[k / 4][k % 4] = x11t::JH_IV[k];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x[k / 4][k % 4] ^= m[k];
+  jh_E8(x);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) x[4 + k / 4][k % 4] ^= m[k];
+  // padding block: 0x80, zeros, 128-bit big-endian bit length (512)
+  x[0][0] ^= 0x80u;
+  x[3][3] ^= 0x00020000u;
+  jh_E8(x);
+  x[4][0] ^= 0x80u;
+  x[7][3] ^= 0x00020000u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = mk64(x[4 + k / 2][2 * (k % 2)], x[4 + k / 2][2 * (k % 2) + 1]);
+  store_hash(Hb, stride, i, h);
+}
+
+// ------------------------------------------------------------------ Keccak-512
+__constant__ u64 c_keccak_rc[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+constexpr int kKeccakRot[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+
+__device__ __forceinline__ u64 rotl64z(u64 x, int n) { return n == 0 ? x : rotl64(x, n); }
+
+__global__ __launch_bounds__(kBlock) void k_keccak512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 A[25];
+  load_hash(Hb, stride, i, A);
+  A[8] = 0x8000000000000001ull;  // pad 0x01 at byte 64, 0x80 at byte 71 (rate 72)
+#pragma unroll
+  for (int k = 9; k < 25; ++k) A[k] = 0;
+  for (int r = 0; r < 24; ++r) {
+    u64 C[5], D[5], B[25];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+#pragma unroll
+    for (int k = 0; k < 25; ++k) A[k] ^= D[k % 5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64z(A[x + 5 * y], kKeccakRot[x + 5 * y]);
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+      for (int y = 0; y < 5; ++y) A[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+    A[0] ^= c_keccak_rc[r];
+  }
+  store_hash(Hb, stride, i, A);
+}
+
+}  // namespace x11k
+
+static bool g_jh_ready = false;
+
+hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
+                              hipStream_t s) {
+  using namespace x11k;
+  if (!g_jh_ready) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_jh_bc), x11t::JH_BC, sizeof(x11t::JH_BC));
+    if (e != hipSuccess) return e;
+    g_jh_ready = true;
+  }
+  const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+  switch (stage) {
+    case kX11Blake: k_blake512_80<<<grid, block, 0, s>>>(p, base, H, stride, n); break;
+    case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Groestl: k_groestl512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace otedama

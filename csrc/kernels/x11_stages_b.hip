@@ -1,0 +1,614 @@
+// X11 stages 7-11 on gfx950: Luffa-512, CubeHash16/32-512, SHAvite-3-512,
+// SIMD-512, ECHO-512 (all on the 64-byte output of the previous stage), plus the
+// chain launcher and the target compare fused into the ECHO stage.
+//
+// Luffa / CubeHash / SHAvite / ECHO: one lane per nonce. The padding blocks of
+// the fixed 64-byte inputs are folded into constants (SHAvite and ECHO are a
+// single compression; their counters are the constant 512).
+// SIMD: eight lanes per nonce. Lane j owns NTT columns 2j and 2j+1, which are
+// exactly the coefficients its message words W[.][j] are built from, so the
+// 256-point NTT and the expansion need no lane exchange; the 36 Feistel steps
+// keep state column j in lane j and exchange one word per step with an xor
+// shuffle inside the 8-lane group.
+// Bit-exact oracle: csrc/cpu/x11_cpu.cpp (tests/test_x11_gpu.py compares every stage).
+#include "otedama/x11_launch.h"
+#include "x11_common.h"
+
+namespace otedama {
+namespace x11k {
+
+// ------------------------------------------------------------------ Luffa-512
+constexpr u32 kLuffaIv[5][8] = {
+    {0x6d251e69, 0x44b051e0, 0x4eaa6fb4, 0xdbf78465, 0x6e292011, 0x90152df4, 0xee058139, 0xdef610bb},
+    {0xc3b44b95, 0xd9d2f256, 0x70eee9a0, 0xde099fa3, 0x5d9b0557, 0x8fc944b3, 0xcf1ccf0e, 0x746cd581},
+    {0xf7efc89d, 0x5dba5781, 0x04016ce5, 0xad659c05, 0x0306194f, 0x666d1836, 0x24aa230a, 0x8b264ae7},
+    {0x858075d5, 0x36d79cce, 0xe571f7d7, 0x204b1f67, 0x35870c6a, 0x57e9e923, 0x14bcb808, 0x7cde72ce},
+    {0x6c68e9be, 0x5ec41e22, 0xc825b7c7, 0xaffb4363, 0xf5df3999, 0x0fc688f1, 0xb07224cc, 0x03e86cea}};
+constexpr u32 kLuffaRc0[5][8] = {
+    {0x303994a6, 0xc0e65299, 0x6cc33a12, 0xdc56983e, 0x1e00108f, 0x7800423d, 0x8f5b7882, 0x96e1db12},
+    {0xb6de10ed, 0x70f47aae, 0x0707a3d4, 0x1c1e8f51, 0x707a3d45, 0xaeb28562, 0xbaca1589, 0x40a46f3e},
+    {0xfc20d9d2, 0x34552e25, 0x7ad8818f, 0x8438764a, 0xbb6de032, 0xedb780c8, 0xd9847356, 0xa2c78434},
+    {0xb213afa5, 0xc84ebe95, 0x4e608a22, 0x56d858fe, 0x343b138f, 0xd0ec4e3d, 0x2ceb4882, 0xb3ad2208},
+    {0xf0d2e9e3, 0xac11d7fa, 0x1bcb66f2, 0x6f2d9bc9, 0x78602649, 0x8edae952, 0x3b6ba548, 0xedae9520}};
+constexpr u32 kLuffaRc4[5][8] = {
+    {0xe0337818, 0x441ba90d, 0x7f34d442, 0x9389217f, 0xe5a8bce6, 0x5274baf4, 0x26889ba7, 0x9a226e9d},
+    {0x01685f3d, 0x05a17cf4, 0xbd09caca, 0xf4272b28, 0x144ae5cc, 0xfaa7ae2b, 0x2e48f1c1, 0xb923c704},
+    {0xe25e72c1, 0xe623bb72, 0x5c58a4a4, 0x1e38e2e7, 0x78e38b9d, 0x27586719, 0x36eda57f, 0x703aace7},
+    {0xe028c9bf, 0x44756f91, 0x7e8fce32, 0x956548be, 0xfe191be2, 0x3cb226e5, 0x5944a28e, 0xa1c4c355},
+    {0x5090d577, 0x2d1925ab, 0xb46496ac, 0xd1925ab0, 0x29131ab6, 0x0fc053c3, 0x3f014f0c, 0xfc053c31}};
+
+// Multiplication by x in GF(2^32)[x]/(the Luffa polynomial) on a 256-bit word.
+__device__ __forceinline__ void luffa_m2(u32 a[8]) {
+  const u32 t = a[7];
+  a[7] = a[6]; a[6] = a[5]; a[5] = a[4];
+  a[4] = a[3] ^ t; a[3] = a[2] ^ t; a[2] = a[1];
+  a[1] = a[0] ^ t; a[0] = t;
+}
+// Bitsliced SubCrumb (4-bit S-box {13,14,0,1,5,10,7,6,11,3,9,12,15,8,2,4}, a0 = bit 0);
+// checked against the table over all 16 inputs.
+#define LUFFA_SUBCRUMB(a0, a1, a2, a3) \
+  do {                                 \
+    u32 t_ = (a0);                     \
+    (a0) |= (a1); (a2) ^= (a3);        \
+    (a1) = ~(a1); (a0) ^= (a3);        \
+    (a3) &= t_; (a1) ^= (a3);          \
+    (a3) ^= (a2); (a2) &= (a0);        \
+    (a0) = ~(a0); (a2) ^= (a1);        \
+    (a1) |= (a3); t_ ^= (a1);          \
+    (a3) ^= (a2); (a2) &= (a1);        \
+    (a1) ^= (a0); (a0) = t_;           \
+  } while (0)
+#define LUFFA_MIXWORD(u, v)          \
+  do {                               \
+    (v) ^= (u);                      \
+    (u) = rotl32((u), 2) ^ (v);      \
+    (v) = rotl32((v), 14) ^ (u);     \
+    (u) = rotl32((u), 10) ^ (v);     \
+    (v) = rotl32((v), 1);            \
+  } while (0)
+
+template <int J>
+__device__ __forceinline__ void luffa_Q(u32 a[8]) {
+#pragma unroll
+  for (int k = 4; k < 8; ++k) a[k] = rotl32(a[k], J);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    LUFFA_SUBCRUMB(a[0], a[1], a[2], a[3]);
+    LUFFA_SUBCRUMB(a[5], a[6], a[7], a[4]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) LUFFA_MIXWORD(a[k], a[k + 4]);
+    a[0] ^= kLuffaRc0[J][r];
+    a[4] ^= kLuffaRc4[J][r];
+  }
+}
+
+// Message injection MI5 followed by the five sub-permutations Q_j.
+__device__ __forceinline__ void luffa_round(u32 V[5][8], const u32 Min[8]) {
+  u32 t[8], M[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { M[k] = Min[k]; t[k] = V[0][k] ^ V[1][k] ^ V[2][k] ^ V[3][k] ^ V[4][k]; }
+  luffa_m2(t);
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[j][k] ^= t[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[k] = V[0][k];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    luffa_m2(V[j]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[j][k] ^= (j < 4 ? V[j + 1][k] : t[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[k] = V[4][k];
+#pragma unroll
+  for (int j = 4; j >= 0; --j) {
+    luffa_m2(V[j]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[j][k] ^= (j > 0 ? V[j - 1][k] : t[k]);
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[j][k] ^= M[k];
+    if (j < 4) luffa_m2(M);
+  }
+  luffa_Q<0>(V[0]);
+  luffa_Q<1>(V[1]);
+  luffa_Q<2>(V[2]);
+  luffa_Q<3>(V[3]);
+  luffa_Q<4>(V[4]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_luffa512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  u32 V[5][8];
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) V[j][k] = kLuffaIv[j][k];
+  // Five rounds: two message blocks (big-endian words), the padding block, two blank
+  // output rounds. Rolled: each round is ~3k instructions.
+#pragma unroll 1
+  for (int b = 0; b < 5; ++b) {
+    u32 M[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u64 w = b == 0 ? h[k] : h[4 + k];
+      M[2 * k] = b < 2 ? bswap32(lo32(w)) : 0u;
+      M[2 * k + 1] = b < 2 ? bswap32(hi32(w)) : 0u;
+    }
+    if (b == 2) M[0] = 0x80000000u;
+    luffa_round(V, M);
+    if (b >= 3) {
+      u32 o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = bswap32(V[0][k] ^ V[1][k] ^ V[2][k] ^ V[3][k] ^ V[4][k]);
+      if (b == 3) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = mk64(o[2 * k], o[2 * k + 1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[4 + k] = mk64(o[2 * k], o[2 * k + 1]);
+      }
+    }
+  }
+  store_hash(Hb, stride, i, h);
+}
+#undef LUFFA_SUBCRUMB
+#undef LUFFA_MIXWORD
+
+// ------------------------------------------------------------------ CubeHash-512
+// One round; the word swaps are register renames once two rounds are unrolled
+// (the round's permutation is an involution).
+__device__ __forceinline__ void cube_round(u32 x[32]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i + 16] += x[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = rotl32(x[i], 7);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { const u32 t = x[i]; x[i] = x[i + 8]; x[i + 8] = t; }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] ^= x[i + 16];
+#pragma unroll
+  for (int i = 16; i < 32; ++i)
+    if (!(i & 2)) { const u32 t = x[i]; x[i] = x[i + 2]; x[i + 2] = t; }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i + 16] += x[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = rotl32(x[i], 11);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (!(i & 4)) { const u32 t = x[i]; x[i] = x[i + 4]; x[i + 4] = t; }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] ^= x[i + 16];
+#pragma unroll
+  for (int i = 16; i < 32; ++i)
+    if (!(i & 1)) { const u32 t = x[i]; x[i] = x[i + 1]; x[i + 1] = t; }
+}
+__device__ __forceinline__ void cube_rounds(u32 x[32], int n) {
+#pragma unroll 1
+  for (int r = 0; r < n; r += 2) {
+    cube_round(x);
+    cube_round(x);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cubehash512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  u32 x[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) x[k] = x11t::CUBE_IV[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { x[2 * k] ^= lo32(h[k]); x[2 * k + 1] ^= hi32(h[k]); }
+  cube_rounds(x, 16);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { x[2 * k] ^= lo32(h[4 + k]); x[2 * k + 1] ^= hi32(h[4 + k]); }
+  cube_rounds(x, 16);
+  x[0] ^= 0x80u;  // padding block
+  cube_rounds(x, 16);
+  x[31] ^= 1u;    // finalization
+  cube_rounds(x, 160);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = mk64(x[2 * k], x[2 * k + 1]);
+  store_hash(Hb, stride, i, h);
+}
+
+// ------------------------------------------------------------------ SHAvite-3-512
+constexpr u32 kShaviteIv[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 0xD1901A06, 0x430AE307,
+                                0xB29F5CD1, 0xDF07FBFC, 0x8E45D73D, 0x681AB538, 0xBDE86578, 0xDD577E47,
+                                0xE275EADE, 0x502D9FCD, 0xB9357178, 0x022A4B9A};
+
+// F: four keyed AES rounds (key added before each keyless round).
+__device__ __forceinline__ void shavite_F(const u32 (*T)[256], u32 x[4], const u32* k) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    x[0] ^= k[4 * r]; x[1] ^= k[4 * r + 1]; x[2] ^= k[4 * r + 2]; x[3] ^= k[4 * r + 3];
+    aes_round(T, x[0], x[1], x[2], x[3]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u32 T[4][256];
+  aes_tables_to_lds(T);
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
+  u32 rk[32];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { rk[2 * k] = lo32(h[k]); rk[2 * k + 1] = hi32(h[k]); }
+  rk[16] = 0x80u;
+#pragma unroll
+  for (int k = 17; k < 32; ++k) rk[k] = 0;
+  rk[27] = 0x02000000u;  // 512-bit length at bytes 110..113
+  rk[31] = 0x02000000u;  // digest size 512 at bytes 126..127
+  u32 A[4], B[4], C[4], D[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[k] = kShaviteIv[k]; B[k] = kShaviteIv[4 + k]; C[k] = kShaviteIv[8 + k]; D[k] = kShaviteIv[12 + k];
+  }
+  // counter = {512, 0, 0, 0}
+#pragma unroll 1
+  for (int r = 0; r < 14; ++r) {
+    if (r & 1) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        u32 t0 = rk[4 * g + 1], t1 = rk[4 * g + 2], t2 = rk[4 * g + 3], t3 = rk[4 * g];
+        aes_round(T, t0, t1, t2, t3);
+        const int p = g ? 4 * g - 4 : 28;
+        rk[4 * g] = t0 ^ rk[p];
+        rk[4 * g + 1] = t1 ^ rk[p + 1];
+        rk[4 * g + 2] = t2 ^ rk[p + 2];
+        rk[4 * g + 3] = t3 ^ rk[p + 3];
+        if (g == 0 && r == 1) { rk[0] ^= 512u; rk[3] = ~rk[3]; }
+        if (g == 1 && r == 5) { rk[7] ^= ~512u; }
+        if (g == 7 && r == 9) { rk[30] ^= 512u; rk[31] = ~rk[31]; }
+        if (g == 6 && r == 13) { rk[25] ^= 512u; rk[27] = ~rk[27]; }
+      }
+    } else if (r) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) rk[k] ^= k >= 7 ? rk[k - 7] : rk[k + 25];
+    }
+    u32 x[4] = {B[0], B[1], B[2], B[3]};
+    shavite_F(T, x, rk);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) A[k] ^= x[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = D[k];
+    shavite_F(T, x, rk + 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      C[k] ^= x[k];
+      const u32 t = D[k];
+      D[k] = C[k]; C[k] = B[k]; B[k] = A[k]; A[k] = t;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    h[k] = mk64(kShaviteIv[2 * k] ^ A[2 * k], kShaviteIv[2 * k + 1] ^ A[2 * k + 1]);
+    h[2 + k] = mk64(kShaviteIv[4 + 2 * k] ^ B[2 * k], kShaviteIv[5 + 2 * k] ^ B[2 * k + 1]);
+    h[4 + k] = mk64(kShaviteIv[8 + 2 * k] ^ C[2 * k], kShaviteIv[9 + 2 * k] ^ C[2 * k + 1]);
+    h[6 + k] = mk64(kShaviteIv[12 + 2 * k] ^ D[2 * k], kShaviteIv[13 + 2 * k] ^ D[2 * k + 1]);
+  }
+  store_hash(Hb, stride, i, h);
+}
+
+// ------------------------------------------------------------------ SIMD-512
+constexpr u32 kSimdIv[32] = {
+    0x0BA16B95, 0x72F999AD, 0x9FECC2AE, 0xBA3264FC, 0x5E894929, 0x8E9F30E5, 0x2F1DAA37, 0xF0F2C558,
+    0xAC506643, 0xA90635A5, 0xE25B878B, 0xAAB7878F, 0x88817F7A, 0x0A02892B, 0x559A7550, 0x598F657E,
+    0x7EEF60A1, 0x6B70E3E8, 0x9C1714D1, 0xB958E2A8, 0xAB02675E, 0xED1C014F, 0xCD8D65BB, 0xFDB7A257,
+    0x09254899, 0xD699C7BC, 0x9019B6DC, 0x2B9022E4, 0x8FA14956, 0x21BF9BD3, 0xB94D0943, 0x6FFDDC22};
+constexpr int kSimdPP[7] = {1, 6, 2, 3, 5, 7, 4};
+constexpr int kSimdRS[4][4] = {{3, 23, 17, 27}, {28, 19, 22, 7}, {29, 9, 15, 5}, {4, 13, 10, 25}};
+constexpr int kSimdSB[32] = {4, 6, 0, 2, 7, 5, 3, 1, 15, 11, 12, 8, 9, 13, 10, 14,
+                             17, 18, 23, 20, 22, 21, 16, 19, 30, 24, 25, 31, 27, 29, 28, 26};
+
+constexpr u32 pow257(u32 b, u32 e) {
+  u32 r = 1;
+  for (u32 k = 0; k < e; ++k) r = r * b % 257u;
+  return r;
+}
+// alpha^b and alpha^-b (alpha = 41, a 256th root of unity mod 257, alpha^16 = 2) for NTT column b.
+__constant__ u32 c_simd_alpha[16] = {
+    pow257(41, 0), pow257(41, 1), pow257(41, 2), pow257(41, 3), pow257(41, 4), pow257(41, 5), pow257(41, 6),
+    pow257(41, 7), pow257(41, 8), pow257(41, 9), pow257(41, 10), pow257(41, 11), pow257(41, 12), pow257(41, 13),
+    pow257(41, 14), pow257(41, 15)};
+__constant__ u32 c_simd_beta[16] = {
+    pow257(41, 0), pow257(41, 255), pow257(41, 254), pow257(41, 253), pow257(41, 252), pow257(41, 251),
+    pow257(41, 250), pow257(41, 249), pow257(41, 248), pow257(41, 247), pow257(41, 246), pow257(41, 245),
+    pow257(41, 244), pow257(41, 243), pow257(41, 242), pow257(41, 241)};
+
+
+// Reduce |x| < 2^26 to [0, 256] (256 = -1 mod 257: x = 256q + r == r - q).
+__device__ __forceinline__ int red257(int x) {
+  x = (x & 255) - (x >> 8);
+  x = (x & 255) - (x >> 8);
+  x = (x & 255) - (x >> 8);
+  return x < 0 ? x + 257 : x;
+}
+// x * 2^E mod 257 up to reduction: 2^8 = -1, so 2^E = (-1)^((E >> 3) & 1) 2^(E & 7).
+template <int E>
+__device__ __forceinline__ int mul2pow(int x) {
+  constexpr int e = ((E % 16) + 16) % 16;
+  return e < 8 ? (x << e) : -(x << (e - 8));
+}
+// 2^e mod 257 for a lane-varying e.
+__device__ __forceinline__ int pow2_257(u32 e) {
+  const int v = 1 << (e & 7);
+  return (e & 8) ? 257 - v : v;
+}
+
+// The 16 NTT outputs q[16a + b], a = 0..15, of column b of the first (message) block:
+// y = sum_{j<64} x_j alpha^((16a+b) j) plus the first-block twiddle alpha^-(16a+b),
+// centred to [-128, 128]. With j = 16c + d and alpha^16 = 2:
+// y = sum_d 2^(ad) u_d,  u_d = sum_c x_{16c+d} alpha^(b(16c+d)).
+__device__ __forceinline__ void simd_ntt_column(const u32 xw[16], u32 b, int q[16]) {
+  const int g1 = pow2_257(b), g2 = pow2_257(2 * b), g3 = pow2_257(3 * b);
+  const int ab = (int)c_simd_alpha[b];
+  int u[16];
+  int f = 1;  // alpha^(b d)
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const int sh = 8 * (d & 3);
+    const int x0 = (xw[(d >> 2)] >> sh) & 0xff;
+    const int x1 = (xw[4 + (d >> 2)] >> sh) & 0xff;
+    const int x2 = (xw[8 + (d >> 2)] >> sh) & 0xff;
+    const int x3 = (xw[12 + (d >> 2)] >> sh) & 0xff;
+    const int s = x0 + x1 * g1 + x2 * g2 + x3 * g3;  // < 2^18
+    u[d] = red257(red257(s) * f);
+    if (d < 15) f = red257(f * ab);
+  }
+  const int beta = (int)c_simd_beta[b];
+#pragma unroll
+  for (int a = 0; a < 16; ++a) {
+    int y = 0;
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+      const int e = (a * d) & 15;
+      y += e < 8 ? (u[d] << e) : -(u[d] << (e - 8));
+    }
+    const int e = (16 - a) & 15;  // twiddle alpha^-(16a+b) = 2^-a beta_b
+    y += e < 8 ? (beta << e) : -(beta << (e - 8));
+    const int v = red257(y);
+    q[a] = v <= 128 ? v : v - 257;
+  }
+}
+
+__device__ __forceinline__ u32 simd_if(u32 x, u32 y, u32 z) { return ((y ^ z) & x) ^ z; }
+__device__ __forceinline__ u32 simd_maj(u32 x, u32 y, u32 z) { return (x & y) | ((x | y) & z); }
+
+// One Feistel step on state column j (this lane); tA of lane j ^ PP comes over the 8-lane group.
+template <bool kMaj, int R, int S, int PP>
+__device__ __forceinline__ void simd_step(u32& s0, u32& s1, u32& s2, u32& s3, u32 w) {
+  const u32 tA = rotl32(s0, R);
+  const u32 f = kMaj ? simd_maj(s0, s1, s2) : simd_if(s0, s1, s2);
+  const u32 tt = s3 + w + f;
+  const u32 other = (u32)__shfl_xor((int)tA, PP, 8);
+  s0 = rotl32(tt, S) + other;
+  s3 = s2;
+  s2 = s1;
+  s1 = tA;
+}
+
+template <int RD>
+__device__ __forceinline__ void simd_round(u32& s0, u32& s1, u32& s2, u32& s3, const u32 w[8]) {
+  constexpr int r0 = kSimdRS[RD][0], r1 = kSimdRS[RD][1], r2 = kSimdRS[RD][2], r3 = kSimdRS[RD][3];
+  simd_step<false, r0, r1, kSimdPP[(0 + RD) % 7]>(s0, s1, s2, s3, w[0]);
+  simd_step<false, r1, r2, kSimdPP[(1 + RD) % 7]>(s0, s1, s2, s3, w[1]);
+  simd_step<false, r2, r3, kSimdPP[(2 + RD) % 7]>(s0, s1, s2, s3, w[2]);
+  simd_step<false, r3, r0, kSimdPP[(3 + RD) % 7]>(s0, s1, s2, s3, w[3]);
+  simd_step<true, r0, r1, kSimdPP[(4 + RD) % 7]>(s0, s1, s2, s3, w[4]);
+  simd_step<true, r1, r2, kSimdPP[(5 + RD) % 7]>(s0, s1, s2, s3, w[5]);
+  simd_step<true, r2, r3, kSimdPP[(6 + RD) % 7]>(s0, s1, s2, s3, w[6]);
+  simd_step<true, r3, r0, kSimdPP[(7 + RD) % 7]>(s0, s1, s2, s3, w[7]);
+}
+
+// 32 message steps + 4 feed-forward steps; h0..h3 = chaining column, s0..s3 = h ^ block.
+__device__ __forceinline__ void simd_compress(u32& s0, u32& s1, u32& s2, u32& s3, u32 h0, u32 h1, u32 h2, u32 h3,
+                                              const u32 W[32]) {
+  simd_round<0>(s0, s1, s2, s3, W);
+  simd_round<1>(s0, s1, s2, s3, W + 8);
+  simd_round<2>(s0, s1, s2, s3, W + 16);
+  simd_round<3>(s0, s1, s2, s3, W + 24);
+  simd_step<false, 4, 13, kSimdPP[4]>(s0, s1, s2, s3, h0);
+  simd_step<false, 13, 10, kSimdPP[5]>(s0, s1, s2, s3, h1);
+  simd_step<false, 10, 25, kSimdPP[6]>(s0, s1, s2, s3, h2);
+  simd_step<false, 25, 4, kSimdPP[0]>(s0, s1, s2, s3, h3);
+}
+
+__device__ __forceinline__ u32 simd_inner(int l, int h, int mm) {
+  return ((u32)(l * mm) & 0xFFFFu) + ((u32)(h * mm) << 16);
+}
+
+// Eight lanes per hash: launch with 8 * n threads.
+__global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 t = blockIdx.x * kBlock + threadIdx.x;
+  const u32 i = t >> 3, j = t & 7;
+  if (i >= n) return;  // whole 8-lane groups exit together
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  u32 xw[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { xw[2 * k] = lo32(h[k]); xw[2 * k + 1] = hi32(h[k]); }
+  int qa[16], qb[16];
+  simd_ntt_column(xw, 2 * j, qa);
+  simd_ntt_column(xw, 2 * j + 1, qb);
+  u32 W[32];
+#pragma unroll
+  for (int st = 0; st < 32; ++st) {
+    const int sb = kSimdSB[st];
+    if (st < 16) W[st] = simd_inner(qa[sb], qb[sb], 185);
+    else if (st < 24) W[st] = simd_inner(qa[sb - 16], qa[sb - 8], 233);
+    else W[st] = simd_inner(qb[sb - 24], qb[sb - 16], 233);
+  }
+  // Column j of the chaining value and of the block (message words j and 8 + j).
+  u32 m0 = 0, m1 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (j == (u32)k) { m0 = xw[k]; m1 = xw[8 + k]; }
+  }
+  u32 iv0 = 0, iv1 = 0, iv2 = 0, iv3 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (j == (u32)k) { iv0 = kSimdIv[k]; iv1 = kSimdIv[8 + k]; iv2 = kSimdIv[16 + k]; iv3 = kSimdIv[24 + k]; }
+  }
+  u32 s0 = iv0 ^ m0, s1 = iv1 ^ m1, s2 = iv2, s3 = iv3;
+  simd_compress(s0, s1, s2, s3, iv0, iv1, iv2, iv3, W);
+  // Final block: the 512-bit length (word 0), expanded with the final tweak (constant).
+#pragma unroll
+  for (int st = 0; st < 32; ++st) {
+    u32 v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v = (j == (u32)k) ? x11t::SIMD_WF[st][k] : v;
+    W[st] = v;
+  }
+  const u32 c0 = s0, c1 = s1, c2 = s2, c3 = s3;
+  if (j == 0) s0 ^= 512u;
+  simd_compress(s0, s1, s2, s3, c0, c1, c2, c3, W);
+  // Output words j (s0) and 8 + j (s1); even lanes pair with their odd neighbour.
+  const u32 n0 = (u32)__shfl_down((int)s0, 1, 8);
+  const u32 n1 = (u32)__shfl_down((int)s1, 1, 8);
+  if ((j & 1) == 0) {
+    __builtin_nontemporal_store(mk64(s0, n0), Hb + (size_t)(j >> 1) * stride + i);
+    __builtin_nontemporal_store(mk64(s1, n1), Hb + (size_t)(4 + (j >> 1)) * stride + i);
+  }
+}
+
+// ------------------------------------------------------------------ ECHO-512
+__device__ __forceinline__ u32 xt4(u32 x) { return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1bu); }
+
+// One ECHO round: BIG.SubWords (two AES rounds per 128-bit word, the first keyed by the
+// running counter), BIG.ShiftRows (a renaming), BIG.MixColumns (bytewise, 4 bytes per u32).
+__device__ __forceinline__ void echo_round(const u32 (*T)[256], u32 W[16][4], u32 k) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    aes_round(T, W[i][0], W[i][1], W[i][2], W[i][3]);
+    W[i][0] ^= k + (u32)i;
+    aes_round(T, W[i][0], W[i][1], W[i][2], W[i][3]);
+  }
+  u32 N[16][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      // column c of the row-shifted state: rows rr come from column (c + rr) & 3
+      const u32 a0 = W[4 * c][w], a1 = W[4 * ((c + 1) & 3) + 1][w], a2 = W[4 * ((c + 2) & 3) + 2][w],
+                a3 = W[4 * ((c + 3) & 3) + 3][w];
+      const u32 ab = a0 ^ a1, bc = a1 ^ a2, cd = a2 ^ a3, da = a3 ^ a0;
+      N[4 * c + 0][w] = xt4(ab) ^ a1 ^ cd;
+      N[4 * c + 1][w] = xt4(bc) ^ a0 ^ cd;
+      N[4 * c + 2][w] = xt4(cd) ^ ab ^ a3;
+      N[4 * c + 3][w] = xt4(da) ^ a0 ^ bc;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) W[i][w] = N[i][w];
+}
+
+// kSearch: compare the top 64 bits of the X11 digest (ECHO output bytes 24..31) with
+// the target and append hits to out[1..cap] (out[0] counts); otherwise write H.
+template <bool kSearch>
+__global__ __launch_bounds__(kBlock) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
+                                                       u64 target_hi, u32* __restrict__ out, u32 cap) {
+  __shared__ u32 T[4][256];
+  aes_tables_to_lds(T);
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  u32 W[16][4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { W[k][0] = 512u; W[k][1] = 0; W[k][2] = 0; W[k][3] = 0; }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    W[8 + k][0] = lo32(h[2 * k]); W[8 + k][1] = hi32(h[2 * k]);
+    W[8 + k][2] = lo32(h[2 * k + 1]); W[8 + k][3] = hi32(h[2 * k + 1]);
+  }
+  // padding: 0x80 at byte 64, digest size 512 at bytes 110..111, bit count 512 at 112..127
+#pragma unroll
+  for (int k = 12; k < 16; ++k) { W[k][0] = 0; W[k][1] = 0; W[k][2] = 0; W[k][3] = 0; }
+  W[12][0] = 0x80u;
+  W[14][3] = 0x02000000u;
+  W[15][0] = 512u;
+#pragma unroll 1
+  for (int r = 0; r < 10; ++r) echo_round(T, W, 512u + 16u * (u32)r);
+  // V' = V ^ M ^ W[0..7] ^ W[8..15]; the digest is V'[0..3], V = {512, 0, 0, 0}.
+  if (kSearch) {
+    const u64 top = mk64(lo32(h[3]) ^ W[1][2] ^ W[9][2], hi32(h[3]) ^ W[1][3] ^ W[9][3]);
+    if (top <= target_hi) {
+      const u32 s = atomicAdd(out, 1u);
+      if (s < cap) out[1 + s] = base + i;
+    }
+  } else {
+    u64 o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[2 * k] = mk64(lo32(h[2 * k]) ^ W[k][0] ^ W[8 + k][0] ^ 512u,
+                      hi32(h[2 * k]) ^ W[k][1] ^ W[8 + k][1]);
+      o[2 * k + 1] = mk64(lo32(h[2 * k + 1]) ^ W[k][2] ^ W[8 + k][2], hi32(h[2 * k + 1]) ^ W[k][3] ^ W[8 + k][3]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[4 + k] = 0;
+    store_hash(Hb, stride, i, o);
+  }
+}
+
+}  // namespace x11k
+
+hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
+                              uint32_t* out, uint32_t cap, hipStream_t s) {
+  using namespace x11k;
+  const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+  switch (stage) {
+    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Shavite: k_shavite512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Simd: {
+      const dim3 g8((8ull * n + kBlock - 1) / kBlock);
+      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n);
+      break;
+    }
+    case kX11Echo:
+      if (out) k_echo512_64<true><<<grid, block, 0, s>>>(H, stride, n, base, p.target_hi, out, cap);
+      else k_echo512_64<false><<<grid, block, 0, s>>>(H, stride, n, base, p.target_hi, nullptr, 0);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t x11_launch_stage(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
+                            uint32_t* out, uint32_t cap, hipStream_t s) {
+  if (stage < 0 || stage >= kX11Stages || n == 0 || stride < n || !H) return hipErrorInvalidValue;
+  if (stage <= kX11Keccak) return x11_launch_stage_a(stage, p, base, H, stride, n, s);
+  return x11_launch_stage_b(stage, p, base, H, stride, n, out, cap, s);
+}
+
+// The whole chain over nonces base .. base + n - 1. H: 8 * stride u64 (stride >= n).
+// out != null: search mode (ECHO compares, H keeps the SIMD output); else H = digests.
+hipError_t x11_launch_chain(const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
+                            uint32_t* out, uint32_t cap, hipStream_t s) {
+  for (int st = kX11Blake; st <= kX11Keccak; ++st) {
+    const hipError_t e = x11_launch_stage_a(st, p, base, H, stride, n, s);
+    if (e != hipSuccess) return e;
+  }
+  for (int st = kX11Luffa; st <= kX11Echo; ++st) {
+    const hipError_t e = x11_launch_stage_b(st, p, base, H, stride, n, out, cap, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace otedama

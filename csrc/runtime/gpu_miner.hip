@@ -18,6 +18,7 @@
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
 #include "otedama/trace.h"
+#include "otedama/x11_launch.h"
 
 namespace otedama {
 
@@ -92,6 +93,8 @@ void GpuMiner::loop() {
   // scrypt scratch (allocated lazily on the first scrypt job)
   void* scratch = nullptr;
   void* xbuf = nullptr;
+  // X11 intermediate digests (8 u64 planes x batch), allocated on the first x11 job
+  uint64_t* x11_h = nullptr;
   // Released on every exit, including a HIP error thrown mid-loop (device fault): in-flight
   // batches are drained first so nothing is freed under a running kernel or copy.
   struct Release {
@@ -107,6 +110,7 @@ void GpuMiner::loop() {
     }
     if (scratch) (void)hipFree(scratch);
     if (xbuf) (void)hipFree(xbuf);
+    if (x11_h) (void)hipFree(x11_h);
     if (stream) (void)hipStreamDestroy(stream);
   }};
   OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -121,6 +125,8 @@ void GpuMiner::loop() {
   const int scrypt_gap = kScryptCoop;
   const int scrypt_grid = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
+  // X11: eleven stage kernels per batch over a 64 B/nonce digest buffer (512 MiB at 2^23).
+  const uint32_t x11_batch = 1u << 23;
 
   uint64_t cur_gen = ~0ull;
   uint64_t k = 0;       // variant-stripe position
@@ -182,7 +188,9 @@ void GpuMiner::loop() {
     s.gen = gen;
     s.variant = v;
     job->variant_header(v, s.header, &s.version, &s.ntime, &s.en2);
-    s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch" : "otd.sha256d.batch");
+    s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch"
+                          : job->algo == Algo::kX11  ? "otd.x11.batch"
+                                                     : "otd.sha256d.batch");
     OTD_HIP(hipMemsetAsync(s.d_out, 0, sizeof(uint32_t), stream));
     OTD_HIP(hipEventRecord(s.start, stream));
     if (job->algo == Algo::kScrypt) {
@@ -196,6 +204,13 @@ void GpuMiner::loop() {
       s.count = remaining < scrypt_batch ? remaining : scrypt_batch;
       OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, s.d_out,
                                    kHitCap, scrypt_grid, stream));
+    } else if (job->algo == Algo::kX11) {
+      if (!x11_h) OTD_HIP(hipMalloc(&x11_h, uint64_t(x11_batch) * 64));
+      X11Params p;
+      x11_prepare(s.header, job->target, &p);
+      const uint64_t remaining = (1ull << 32) - nonce_off;
+      s.count = remaining < x11_batch ? remaining : x11_batch;
+      OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), s.d_out, kHitCap, stream));
     } else {
       Sha256dParams p;
       sha256d_prepare(s.header, job->target, &p);
@@ -228,6 +243,18 @@ void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uint
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
   OTD_HIP(launch_scrypt_search(p, base, count, reinterpret_cast<void*>(xbuf), reinterpret_cast<void*>(scratch), gap,
                                reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream)));
+}
+
+void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
+                         uintptr_t out, uint32_t cap, uintptr_t stream) {
+  OTD_HIP(x11_launch_stage(stage, p, base, reinterpret_cast<uint64_t*>(H), stride, n, reinterpret_cast<uint32_t*>(out),
+                           cap, reinterpret_cast<hipStream_t>(stream)));
+}
+
+void py_launch_x11(const X11Params& p, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n, uintptr_t out,
+                   uint32_t cap, uintptr_t stream) {
+  OTD_HIP(x11_launch_chain(p, base, reinterpret_cast<uint64_t*>(H), stride, n, reinterpret_cast<uint32_t*>(out), cap,
+                           reinterpret_cast<hipStream_t>(stream)));
 }
 
 int gpu_device_count() {

@@ -8,6 +8,7 @@
 #include "otedama/job.h"
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
+#include "otedama/x11.h"
 
 namespace otedama {
 
@@ -152,6 +153,7 @@ void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]) {
 
 bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32], uint8_t hash_out[32]) {
   if (algo == Algo::kScrypt) scrypt_1024_1_1(header80, hash_out);
+  else if (algo == Algo::kX11) x11::x11(header80, 80, hash_out, nullptr);
   else sha256d(header80, 80, hash_out);
   return le256_leq(hash_out, target);
 }

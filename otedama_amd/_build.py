@@ -26,12 +26,15 @@ ARCH = os.environ.get("OTEDAMA_OFFLOAD_ARCH", "gfx950")
 HIP_SOURCES = [
     "kernels/sha256d_search.hip",
     "kernels/scrypt_search.hip",
+    "kernels/x11_stages_a.hip",
+    "kernels/x11_stages_b.hip",
     "runtime/gpu_miner.hip",
 ]
 CXX_SOURCES = [
     "cpu/sha256_cpu.cpp",
     "cpu/job_prepare.cpp",
     "cpu/aead.cpp",
+    "cpu/x11_cpu.cpp",
     "runtime/miner_common.cpp",
     "bindings.cpp",
 ]

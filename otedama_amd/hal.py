@@ -12,7 +12,7 @@ Parity: internal/hal/{device,registry,gpu_linux}.go
 MI355X-native difference: the reference hard-codes ``SHA256d = False`` for
 every GPU (gpu_linux.go:131) because it has no GPU compute. Here the HIP driver
 enumerates devices through the native runtime and reports the kernels that
-exist for the device's ISA: gfx950 -> sha256d and scrypt. The DRM
+exist for the device's ISA: gfx950 -> sha256d, scrypt and x11. The DRM
 driver is kept for non-HIP render nodes (presence only, no hashing), and
 render nodes that the HIP driver already owns are not reported twice.
 """
@@ -115,7 +115,7 @@ class CPUDriver:
 
 
 # ISA -> kernels compiled into the native extension (csrc/kernels)
-KERNEL_ISAS = {"gfx950": Capabilities(sha256d=True, general_compute=True, scrypt=True)}
+KERNEL_ISAS = {"gfx950": Capabilities(sha256d=True, general_compute=True, scrypt=True, x11=True)}
 
 
 class HIPDriver:

@@ -6,7 +6,8 @@ the gfx950 search op that mines it.
 
   sha256d  Bitcoin double SHA-256      reference: internal/miner/sha256d.go:107-117
   scrypt   Litecoin scrypt(1024,1,1)   [NO REFERENCE CODE] (removed in v3, CHANGELOG.md:6623)
-  x11      Dash 11-hash chain          not offered (no validatable known-answer source; see ALGORITHMS)
+  x11      Dash 11-hash chain          [NO REFERENCE CODE] (never implemented upstream); CPU oracle
+                                       csrc/cpu/x11_cpu.cpp, pinned by the Dash genesis block
 """
 from __future__ import annotations
 
@@ -15,6 +16,13 @@ from dataclasses import dataclass
 from typing import Callable
 
 from otedama_amd.models.header import DIFF1_TARGET_INT, sha256d
+
+
+def x11_hash(header80: bytes) -> bytes:
+    """X11 = first 32 bytes of ECHO(SIMD(...BLAKE-512(header))) via the native CPU chain."""
+    from otedama_amd.ops.native import require_native
+
+    return require_native().x11(bytes(header80))
 
 
 def scrypt_hash(header80: bytes) -> bytes:
@@ -35,8 +43,9 @@ ALGORITHMS: dict[str, PowAlgorithm] = {
     "sha256d": PowAlgorithm("sha256d", DIFF1_TARGET_INT, sha256d, True, "Bitcoin SHA-256d"),
     # Litecoin-family pools define share difficulty 1 as 2^16 easier than Bitcoin's.
     "scrypt": PowAlgorithm("scrypt", 0xFFFF << 224, scrypt_hash, True, "Litecoin scrypt N=1024 r=1 p=1"),
-    # X11 (Dash) is not offered: its eleven 512-bit hashes have no offline known-answer source here, so a
-    # kernel could not be validated. Asking for it fails in get() with a clear error.
+    # Dash (X11) pools use the Bitcoin difficulty-1 target. The CPU chain reproduces the Dash genesis
+    # block hash (tests/test_x11_kat.py); the gfx950 kernels are checked stage by stage against it.
+    "x11": PowAlgorithm("x11", DIFF1_TARGET_INT, x11_hash, True, "Dash X11 (11 chained 512-bit hashes)"),
 }
 
 

@@ -8,6 +8,7 @@ read back with :meth:`SearchResult.nonces` after a synchronize.
 Kernels (csrc/kernels):
   * ``otd_sha256d_search``   — SHA-256d nonce search (K1)
   * ``otd_scrypt_*``         — scrypt N=1024,r=1,p=1 three-stage search (K5)
+  * ``x11k::k_*512_*``       — X11 eleven-stage chain, one kernel per stage (K6)
 """
 from __future__ import annotations
 
@@ -126,3 +127,57 @@ class ScryptSearch:
         r = self.launch(self.prepare(header80, target32), base, count)
         torch.cuda.synchronize(self.device)
         return r.nonces()
+
+
+X11_BATCH = 1 << 23  # nonces per chain launch: 512 MiB of 64-byte digests, ~20-40 ms of work
+
+
+class X11Search:
+    """X11 search: eleven stage kernels over a 64 B/nonce digest buffer (8 u64 planes),
+    the target compare fused into the ECHO stage. ``trace`` runs the chain stage by
+    stage and returns every intermediate digest (for the per-stage numerics tests)."""
+
+    def __init__(self, device="cuda:0", cap: int = 1024, batch: int = X11_BATCH):
+        self.native = require_native()
+        self.device = torch.device(device)
+        self.cap = cap
+        self.batch = int(batch)
+        if not 0 < self.batch <= 1 << 26:
+            raise ValueError("batch must be in [1, 2^26]")
+        self.H = torch.empty(8 * self.batch, dtype=torch.int64, device=self.device)
+        self.out = torch.zeros(1 + cap, dtype=torch.int32, device=self.device)
+
+    def prepare(self, header80: bytes, target32: bytes) -> bytes:
+        return self.native.x11_prepare(header80, target32)
+
+    def launch(self, params: bytes, base: int = 0, count: int | None = None,
+               stream: torch.cuda.Stream | None = None) -> SearchResult:
+        count = self.batch if count is None else count
+        if not 0 < count <= self.batch:
+            raise ValueError(f"count must be in [1, {self.batch}]")
+        stream = stream or torch.cuda.current_stream(self.device)
+        self.out[:1].zero_()
+        self.native.launch_x11(params, base & 0xFFFFFFFF, self.H.data_ptr(), self.batch, int(count),
+                               self.out.data_ptr(), self.cap, stream.cuda_stream)
+        return SearchResult(self.out, self.cap)
+
+    def search(self, header80: bytes, target32: bytes, base: int = 0, count: int | None = None) -> list[int]:
+        r = self.launch(self.prepare(header80, target32), base, count)
+        torch.cuda.synchronize(self.device)
+        return r.nonces()
+
+    def trace(self, header80: bytes, base: int, count: int) -> list[torch.Tensor]:
+        """Digests after each of the 11 stages: list of uint8 [count, 64] CPU tensors."""
+        if not 0 < count <= self.batch:
+            raise ValueError(f"count must be in [1, {self.batch}]")
+        params = self.prepare(header80, bytes(32))
+        stream = torch.cuda.current_stream(self.device)
+        planes = self.H.view(8, self.batch)
+        out = []
+        for st in range(self.native.X11_STAGES):
+            self.native.launch_x11_stage(params, st, base & 0xFFFFFFFF, self.H.data_ptr(), self.batch, int(count),
+                                         0, 0, stream.cuda_stream)
+            torch.cuda.synchronize(self.device)
+            words = planes[:, :count].t().contiguous().cpu()          # [count, 8] int64 (LE words)
+            out.append(words.view(torch.uint8).reshape(count, 64))
+        return out

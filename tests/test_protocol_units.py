@@ -256,7 +256,7 @@ def test_hal_capabilities_match_kernels():
     cpu = hal.CPUDriver(2).enumerate()[0]
     assert cpu.capabilities().sha256d and not cpu.capabilities().scrypt  # CpuMiner is SHA-256d only
     gfx950 = hal.KERNEL_ISAS["gfx950"]
-    assert gfx950.sha256d and gfx950.scrypt and not gfx950.x11
-    assert set(algorithms.ALGORITHMS) == {"sha256d", "scrypt"}
+    assert gfx950.sha256d and gfx950.scrypt and gfx950.x11
+    assert set(algorithms.ALGORITHMS) == {"sha256d", "scrypt", "x11"}
     with pytest.raises(ValueError, match="unknown algorithm"):
-        algorithms.get("x11")
+        algorithms.get("x17")

@@ -1,0 +1,106 @@
+"""gfx950 X11 kernels (K6) vs the CPU chain (csrc/cpu/x11_cpu.cpp), run on a real MI355X via gpurun.
+
+Integer hashes are exact: every intermediate 64-byte digest of every stage kernel must equal the CPU
+oracle's for the same nonce, and a search must report exactly the nonces the CPU finds. The CPU chain
+itself is pinned by the Dash genesis block (tests/test_x11_kat.py).
+"""
+import json
+import random
+import struct
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KAT = json.loads((Path(__file__).parent / "fixtures" / "x11_dash_genesis.json").read_text())
+STAGES = ["blake", "bmw", "groestl", "skein", "jh", "keccak", "luffa", "cubehash", "shavite", "simd", "echo"]
+
+
+def _native():
+    from otedama_amd.ops.native import require_native
+
+    return require_native()
+
+
+def _hdr(prefix76: bytes, nonce: int) -> bytes:
+    return prefix76 + struct.pack("<I", nonce & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_x11_every_stage_matches_cpu(seed):
+    from otedama_amd.ops.search import X11Search
+
+    N = _native()
+    rng = random.Random(seed)
+    prefix = bytes(rng.getrandbits(8) for _ in range(76))
+    base = rng.getrandbits(32)
+    count = 1000  # not a multiple of the block size: tail lanes / 8-lane SIMD groups
+    s = X11Search("cuda:0", batch=1024)
+    trace = s.trace(prefix + bytes(4), base, count)
+    picks = sorted({0, count - 1, *rng.sample(range(count), 30)})
+    for k in picks:
+        ref = N.x11_trace(_hdr(prefix, base + k))
+        for st in range(11):
+            got = bytes(trace[st][k].tolist())
+            want = ref[64 * st : 64 * st + 64]
+            if st == 10:  # the chain digest is the first half of ECHO-512
+                got, want = got[:32], want[:32]
+            assert got == want, f"stage {st} ({STAGES[st]}) nonce {base + k:#x}: {got.hex()} != {want.hex()}"
+
+
+def test_x11_finds_dash_genesis_nonce():
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import X11Search
+
+    hdr = bytes.fromhex(KAT["header_hex"])
+    nonce = KAT["nonce"]
+    bits = int(KAT["bits"], 16)
+    target = (bits & 0xFFFFFF) << (8 * ((bits >> 24) - 3))
+    s = X11Search("cuda:0", batch=1 << 16)
+    assert s.search(hdr, int_to_hash(target), nonce - 40000, 1 << 16) == [nonce]
+
+
+def test_x11_search_matches_cpu_easy_target():
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import X11Search
+
+    N = _native()
+    rng = random.Random(7)
+    prefix = bytes(rng.getrandbits(8) for _ in range(76))
+    base = 0xFFFFFFFF - 1500  # wraps past 2^32 - 1 inside the window
+    count = 3000
+    target_int = (1 << 250) - 1  # ~1/64 hit rate
+    s = X11Search("cuda:0", cap=4096, batch=4096)
+    got = sorted(s.search(prefix + bytes(4), int_to_hash(target_int), base, count))
+    # the kernel pre-filters on the top 64 bits: re-verify the full 256-bit compare on the host
+    got_full = [n for n in got if int.from_bytes(N.x11(_hdr(prefix, n)), "little") <= target_int]
+    ref = sorted((base + k) & 0xFFFFFFFF for k in range(count)
+                 if int.from_bytes(N.x11(_hdr(prefix, base + k)), "little") <= target_int)
+    assert got_full == ref and len(ref) > 10
+
+
+def test_x11_native_miner_submits_valid_shares():
+    import time
+
+    from otedama_amd.models.header import int_to_hash
+
+    N = _native()
+    rng = random.Random(11)
+    hdr = bytes(rng.getrandbits(8) for _ in range(80))
+    target = int_to_hash((1 << 244) - 1)  # ~1 share per 4096 nonces
+    m = N.GpuMiner(0, "gpu-x11-test", 1 << 22, 256 * 6)
+    m.set_job({"header": hdr, "target": target, "algo": "x11", "epoch": 1, "job_id": "x"})
+    m.start()
+    shares = []
+    t0 = time.time()
+    while len(shares) < 20 and time.time() - t0 < 30:
+        shares += m.poll(256)
+        time.sleep(0.05)
+    m.stop()
+    st = m.stats()
+    assert not st["faulted"], st["error"]
+    assert len(shares) >= 20 and st["rejected_candidates"] == 0
+    for sh in shares[:20]:
+        h = N.x11(hdr[:76] + struct.pack("<I", sh["nonce"]))
+        assert h == sh["hash"] and int.from_bytes(h, "little") <= int.from_bytes(target, "little")
