@@ -15,7 +15,8 @@ Data: synthetic 80-byte block headers (random prev-hash / merkle root), share
 target = difficulty 1. Every hit found in the timed region is re-verified on
 the CPU after timing. Weak scaling: per-GPU work is fixed as N grows.
 
-Then scrypt(1024,1,1) is timed the same way (HBM-resident scratchpads), and
+Then scrypt(1024,1,1) is timed the same way (HBM-resident scratchpads), then
+X11 (eleven chained 512-bit hashes, nonce ranges partitioned across ranks), and
 p50 share latency is measured end-to-end (GPU hit -> SV2 SubmitSharesStandard
 -> pool validation -> SubmitSharesSuccess) against the in-process local pool.
 
@@ -62,6 +63,7 @@ def main() -> int:
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
+    ap.add_argument("--x11-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--no-latency", action="store_true")
     args = ap.parse_args()
 
@@ -168,6 +170,49 @@ def main() -> int:
         del sc
         torch.cuda.empty_cache()
 
+    # ------------------------------------------------------------------ X11
+    # BASELINE config 4: X11 with the nonce range partitioned across ranks (rank r takes batches
+    # r, r + N, r + 2N, ...). Target 2^-20 so every step yields hits that are re-verified on the CPU.
+    x11_hps = None
+    x11_info = {}
+    xsteps = args.steps if args.x11_steps < 0 else args.x11_steps
+    if xsteps > 0:
+        from otedama_amd.models.header import int_to_hash
+        from otedama_amd.ops.search import X11Search
+
+        xs = X11Search(dev, cap=4096)
+        xtarget_int = (1 << 236) - 1
+        hdr, _, _, _ = N.variant_header(job, stripe.start)
+        xparams = N.x11_prepare(hdr, int_to_hash(xtarget_int))
+        xs.launch(xparams, 0)
+        torch.cuda.synchronize(dev)
+        barrier(info)
+        torch.cuda.synchronize(dev)
+        xhits: list[list[int]] = []
+        t0 = time.perf_counter()
+        for i in range(xsteps):
+            base = ((i * world + info.rank) * xs.batch) & 0xFFFFFFFF
+            r = xs.launch(xparams, base)
+            xhits.append(r.buf.clone())
+        torch.cuda.synchronize(dev)
+        barrier(info)
+        torch.cuda.synchronize(dev)
+        xelapsed = comm.allreduce_max(time.perf_counter() - t0)
+        xtotal = comm.allreduce_counters(xsteps * xs.batch)[0] if world > 1 else xsteps * xs.batch
+        x11_hps = xtotal / xelapsed
+        xfound = xver = 0
+        for buf in xhits:
+            host = buf.cpu().tolist()
+            for nonce in host[1 : 1 + min(host[0] & 0xFFFFFFFF, xs.cap)]:
+                xfound += 1
+                h = N.x11(hdr[:76] + (nonce & 0xFFFFFFFF).to_bytes(4, "little"))
+                xver += int.from_bytes(h, "little") <= xtarget_int
+        xfound, xver, _, _ = comm.allreduce_counters(xfound, xver)
+        x11_info = {"batch_per_launch": xs.batch, "kernels": "11 stage kernels per batch (tools/bench_x11.py)",
+                    "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20"}
+        del xs
+        torch.cuda.empty_cache()
+
     # ---------------------------------------------------------- share latency
     latency = None
     if not args.no_latency and info.is_primary:
@@ -206,6 +251,8 @@ def main() -> int:
             "hits_verified": verified,
             "scrypt_hashes_per_sec": scrypt_hps,
             "scrypt": scrypt_info,
+            "x11_hashes_per_sec": x11_hps,
+            "x11": x11_info,
             "p50_share_latency_ms": (latency or {}).get("p50_ms") if isinstance(latency, dict) else None,
             "share_latency": latency,
         }

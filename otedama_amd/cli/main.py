@@ -81,7 +81,7 @@ def run_flagset(name: str, out: TextIO) -> FlagSet:
                              "(default/file/env/flag).")
     fs.bool("json", False, "(config show only) Emit the resolved configuration as a JSON object instead of text.")
     # MI355X additions
-    fs.string("algorithm", "", "(run only) Proof-of-work algorithm: sha256d | scrypt.")
+    fs.string("algorithm", "", "(run only) Proof-of-work algorithm: sha256d | scrypt | x11.")
     fs.string("gpus", "", "(run only) GPUs to mine on: all | none | comma-separated HIP ordinals.")
     fs.int("cpu-threads", -1, "(run only) CPU miner threads (0 = only when no GPU; -1 = config).")
     fs.bool("enable-ai-provider", False, "(run only) Enable the simulated AI-inference yield provider in "

@@ -26,7 +26,7 @@ def _bump(addr: str, k: int) -> str:
 
 def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs = FlagSet("pool", stderr)
-    fs.string("algorithms", "sha256d", "Comma-separated algorithms to serve (sha256d, scrypt).")
+    fs.string("algorithms", "sha256d", "Comma-separated algorithms to serve (sha256d, scrypt, x11).")
     fs.string("listen-sv2", "127.0.0.1:3336", "Stratum V2 listen address (port +1 per extra algorithm).")
     fs.string("listen-v1", "127.0.0.1:3333", "Stratum V1 listen address (port +1 per extra algorithm).")
     fs.string("payout-address", "", "Operator address paid by the coinbase (empty = OP_RETURN).")
@@ -45,8 +45,8 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         return rc
     algos = [a.strip() for a in fs["algorithms"].split(",") if a.strip()]
     for a in algos:
-        if a not in ("sha256d", "scrypt"):
-            stderr.write(f"pool: unsupported algorithm {a!r} (sha256d, scrypt)\n")
+        if a not in ("sha256d", "scrypt", "x11"):
+            stderr.write(f"pool: unsupported algorithm {a!r} (sha256d, scrypt, x11)\n")
             return EXIT_CONFIG
     if fs["payout-address"]:
         from otedama_amd.config import validate_bitcoin_address

@@ -54,7 +54,7 @@ class WorkerConfig:
 
 @dataclass
 class MiningConfig:
-    algorithm: str = "sha256d"          # sha256d | scrypt
+    algorithm: str = "sha256d"          # sha256d | scrypt | x11
     gpus: str = "all"                   # "all", "none", or comma list of device indices
     cpu_threads: int = 0                # 0 = CPU miner only when no GPU is present
     batch_nonces: int = 1 << 29         # per-launch nonce batch (share latency vs launch overhead)
@@ -132,8 +132,8 @@ class Config:
             v = getattr(self, name)
             if v < 0:
                 issues.append(f"{name} {v:{fmt_}} must be >= 0 (0 = disabled)")
-        if self.mining.algorithm not in ("sha256d", "scrypt"):
-            issues.append(f"mining.algorithm {self.mining.algorithm!r} is not one of sha256d, scrypt")
+        if self.mining.algorithm not in ("sha256d", "scrypt", "x11"):
+            issues.append(f"mining.algorithm {self.mining.algorithm!r} is not one of sha256d, scrypt, x11")
         if self.mining.cpu_threads < 0:
             issues.append("mining.cpu_threads must be >= 0")
         if not 1 << 16 <= self.mining.batch_nonces <= 1 << 32:

@@ -27,7 +27,7 @@ async def _probe(device_index: int, seconds: float, algorithm: str, shares_per_s
     devs = [d for d in hal.HIPDriver().enumerate() if d.index == device_index]
     if not devs:
         raise RuntimeError(f"no HIP device {device_index}")
-    hashes_per_diff1 = 2.0 ** 32 if algorithm == "sha256d" else 2.0 ** 16
+    hashes_per_diff1 = 2.0 ** 16 if algorithm == "scrypt" else 2.0 ** 32  # scrypt pools: diff1 = 0xFFFF << 224
     diff = expected_hashrate / (shares_per_sec * hashes_per_diff1)
     pool = PoolServer(PoolOptions(algorithm=algorithm, initial_difficulty=diff, retarget_seconds=3600,
                                   payout_address=PROBE_ADDR, listen_v1=""))

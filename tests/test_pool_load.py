@@ -1,4 +1,4 @@
-"""Pool under load (BASELINE config 5 shape, tools/bench_pool.py): SHA-256d and scrypt pools each take a
+"""Pool under load (BASELINE config 5 shape, tools/bench_pool.py): SHA-256d, scrypt and X11 pools each take a
 flood of SV2 submits from several miners. scrypt shares are hashed on the pool's native thread pool,
 off the event loop. Every share is valid at the clamped minimum difficulty, so any rejection is a bug."""
 import asyncio
@@ -20,7 +20,8 @@ def test_mixed_pool_load():
 
     async def both():
         return await asyncio.wait_for(asyncio.gather(mod._run_pool("sha256d", 2, 1.0, 2),
-                                                     mod._run_pool("scrypt", 2, 1.0, 2)), 60)
+                                                     mod._run_pool("scrypt", 2, 1.0, 2),
+                                                     mod._run_pool("x11", 2, 1.0, 2)), 60)
 
     res = asyncio.run(both())
     for r in res:

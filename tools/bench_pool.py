@@ -9,7 +9,7 @@ Difficulty is pinned at the minimum, so every nonce is a valid share. The pool s
 inline, scrypt on its native thread pool), journals the share and runs vardiff.
 
 Output: one JSON line per pool with validated shares/s and submit->ack latency quantiles.
-Usage: python tools/bench_pool.py [--algo sha256d|scrypt|mixed] [--miners 16] [--seconds 10]
+Usage: python tools/bench_pool.py [--algo sha256d|scrypt|x11|mixed] [--miners 16] [--seconds 10]
 """
 from __future__ import annotations
 
@@ -73,14 +73,14 @@ async def _run_pool(algo: str, miners: int, seconds: float, inflight: int) -> di
 
 
 async def main_async(args) -> list[dict]:
-    algos = ["sha256d", "scrypt"] if args.algo == "mixed" else [args.algo]
+    algos = ["sha256d", "scrypt", "x11"] if args.algo == "mixed" else [args.algo]
     per = max(1, args.miners // len(algos))
     return list(await asyncio.gather(*(_run_pool(a, per, args.seconds, args.inflight) for a in algos)))
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--algo", choices=("sha256d", "scrypt", "mixed"), default="mixed")
+    ap.add_argument("--algo", choices=("sha256d", "scrypt", "x11", "mixed"), default="mixed")
     ap.add_argument("--miners", type=int, default=16)
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--inflight", type=int, default=8)

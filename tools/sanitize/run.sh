@@ -7,7 +7,7 @@ ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
 OUT="${OTEDAMA_SANITIZE_OUT:-$ROOT/build/sanitize}"
 SECS="${1:-4}"
 mkdir -p "$OUT"
-SRCS=("$ROOT/csrc/cpu/sha256_cpu.cpp" "$ROOT/csrc/cpu/job_prepare.cpp" "$ROOT/csrc/cpu/aead.cpp"
+SRCS=("$ROOT/csrc/cpu/sha256_cpu.cpp" "$ROOT/csrc/cpu/job_prepare.cpp" "$ROOT/csrc/cpu/aead.cpp" "$ROOT/csrc/cpu/x11_cpu.cpp"
       "$ROOT/csrc/runtime/miner_common.cpp" "$ROOT/tools/sanitize/stress_runtime.cpp")
 # ROCm clang: its compiler-rt TSan intercepts pthread_cond_clockwait (libstdc++ wait_for);
 # GCC 11's libtsan does not and reports a false "double lock" on the pause path.

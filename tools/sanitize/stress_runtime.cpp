@@ -227,6 +227,14 @@ static void test_crypto_memory() {
   std::thread t([&] { scrypt_1024_1_1(hdr, out2); });  // per-thread scratch pad
   t.join();
   CHECK(std::memcmp(out, out2, 32) == 0, "scrypt differs across threads");
+  // X11: first use races the one-time S-box / JH constant init across verifier threads.
+  {
+    uint8_t x[4][32];
+    std::vector<std::thread> vs;
+    for (int i = 0; i < 4; ++i) vs.emplace_back([&, i] { verify_share(Algo::kX11, hdr, hdr, x[i]); });
+    for (auto& v : vs) v.join();
+    for (int i = 1; i < 4; ++i) CHECK(std::memcmp(x[0], x[i], 32) == 0, "x11 differs across threads");
+  }
   for (size_t kl : {0ul, 1ul, 64ul, 65ul, 200ul}) {
     std::vector<uint8_t> k(kl, 0x5a), msg(kl * 3 + 1, 0x33), dk(77);
     hmac_sha256(k.data(), k.size(), msg.data(), msg.size(), out);
