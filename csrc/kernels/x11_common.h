@@ -6,13 +6,14 @@
 // coalesced 512-byte wave access; at 64 B per hash per stage the traffic is
 // ~1% of the HBM roofline at the stages' ALU-bound rates. Splitting the chain
 // lets every stage run at its own register budget / occupancy and keep its own
-// LDS tables (Groestl 16 KiB, AES 4 KiB) instead of the union of all eleven.
+// LDS tables (bank-private 64 KiB Groestl / AES tables) instead of the union of all eleven.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "otedama/job.h"
+#include "cdna_bitops.h"
 #include "x11_tables.h"
 
 namespace otedama {
@@ -23,9 +24,18 @@ typedef uint64_t u64;
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ u64 rotl64(u64 x, int n) { return (x << n) | (x >> (64 - n)); }
-__device__ __forceinline__ u64 rotr64(u64 x, int n) { return (x >> n) | (x << (64 - n)); }
-__device__ __forceinline__ u32 rotl32(u32 x, int n) { return (x << n) | (x >> (32 - n)); }
+// 64-bit rotates as two v_alignbit_b32 (hipcc otherwise emits a 64-bit shift pair + two ors).
+// n is a compile-time constant once the round loops unroll, so the branches fold.
+__device__ __forceinline__ u64 rotl64(u64 x, int n) {
+  const u32 lo = (u32)x, hi = (u32)(x >> 32);
+  if ((n & 63) == 0) return x;
+  if (n == 32) return (u64)hi | ((u64)lo << 32);
+  if (n < 32)
+    return (u64)__builtin_amdgcn_alignbit(lo, hi, 32 - n) | ((u64)__builtin_amdgcn_alignbit(hi, lo, 32 - n) << 32);
+  return (u64)__builtin_amdgcn_alignbit(hi, lo, 64 - n) | ((u64)__builtin_amdgcn_alignbit(lo, hi, 64 - n) << 32);
+}
+__device__ __forceinline__ u64 rotr64(u64 x, int n) { return rotl64(x, (64 - n) & 63); }
+__device__ __forceinline__ u32 rotl32(u32 x, int n) { return __builtin_amdgcn_alignbit(x, x, (32 - n) & 31); }
 __device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ u64 bswap64(u64 x) { return __builtin_bswap64(x); }
 __device__ __forceinline__ u32 lo32(u64 x) { return (u32)x; }
@@ -41,25 +51,95 @@ __device__ __forceinline__ void store_hash(u64* __restrict__ H, u32 stride, u32 
   for (int w = 0; w < 8; ++w) __builtin_nontemporal_store(h[w], H + (size_t)w * stride + i);
 }
 
-// AES T-tables in LDS: T[r][x] = rotl32(AES_T0[x], 8r).
-__device__ __forceinline__ void aes_tables_to_lds(u32 (*T)[256]) {
-  for (int x = threadIdx.x; x < 256; x += blockDim.x) {
-    const u32 v = x11t::AES_T0[x];
-    T[0][x] = v;
-    T[1][x] = rotl32(v, 8);
-    T[2][x] = rotl32(v, 16);
-    T[3][x] = rotl32(v, 24);
+// Any 3-input boolean function / xor3 in one v_bitop3_b32 (hipcc rarely forms it itself).
+using otedama_dev::xor3;
+template <unsigned TT>
+__device__ __forceinline__ u32 bop3(u32 a, u32 b, u32 c) {
+  u32 r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
+  return r;
+}
+__device__ __forceinline__ u64 xor3_64(u64 a, u64 b, u64 c) { return mk64(xor3(lo32(a), lo32(b), lo32(c)), xor3(hi32(a), hi32(b), hi32(c))); }
+
+// ---------------------------------------------------------------- bank-private tables
+// Random 8-bit table lookups from a shared table cost ~3.1x their conflict-free LDS time on
+// gfx950 (measured: SQ_LDS_BANK_CONFLICT = 67% of SQ_LDS_IDX_ACTIVE for Groestl/ECHO/SHAvite,
+// profiles/r1/x11/pmc_baseline.csv). Here every lane reads its own copy of the table, placed so
+// that lane l only ever touches bank(s) owned by l inside its 32-lane half-wave: conflict-free.
+// The address of entry x is (x << 8) | lane_offset, built with one v_perm_b32 straight from the
+// state word (byte k of w -> address byte 1, lane offset -> byte 0).
+__device__ __forceinline__ u32 lds_addr(u32 w, int k, u32 laneoff) {
+  return __builtin_amdgcn_perm(w, laneoff, 0x0c0c0000u | ((4u + (u32)k) << 8));
+}
+
+// AES: T0 only (T1..T3 are byte rotations), 64 copies, dword 64x + l = T0[x] (ds_read_b32 banks
+// are (a/4) mod 32 per 32-lane half: lane l -> bank l mod 32). 64 KiB.
+constexpr u32 kAesPrivWords = 256 * 64;
+__device__ __forceinline__ void aes_priv_fill(u32* T) {
+  for (u32 c = threadIdx.x; c < kAesPrivWords / 4; c += blockDim.x) {
+    const u32 v = x11t::AES_T0[c >> 4];
+    reinterpret_cast<uint4*>(T)[c] = make_uint4(v, v, v, v);
   }
   __syncthreads();
 }
-// Keyless AES round (SubBytes, ShiftRows, MixColumns) on four LE column words.
-__device__ __forceinline__ void aes_round(const u32 (*T)[256], u32& x0, u32& x1, u32& x2, u32& x3) {
-  const u32 y0 = T[0][x0 & 0xff] ^ T[1][(x1 >> 8) & 0xff] ^ T[2][(x2 >> 16) & 0xff] ^ T[3][x3 >> 24];
-  const u32 y1 = T[0][x1 & 0xff] ^ T[1][(x2 >> 8) & 0xff] ^ T[2][(x3 >> 16) & 0xff] ^ T[3][x0 >> 24];
-  const u32 y2 = T[0][x2 & 0xff] ^ T[1][(x3 >> 8) & 0xff] ^ T[2][(x0 >> 16) & 0xff] ^ T[3][x1 >> 24];
-  const u32 y3 = T[0][x3 & 0xff] ^ T[1][(x0 >> 8) & 0xff] ^ T[2][(x1 >> 16) & 0xff] ^ T[3][x2 >> 24];
-  x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+__device__ __forceinline__ u32 aes_laneoff() { return (threadIdx.x & 63u) << 2; }
+__device__ __forceinline__ u32 aes_lk(const u32* T, u32 lo, u32 w, int k) {
+  return *reinterpret_cast<const u32*>(reinterpret_cast<const char*>(T) + lds_addr(w, k, lo));
 }
+// AES round (SubBytes, ShiftRows, MixColumns) on four LE column words, then AddRoundKey:
+// the key words ride in the second xor3 of each column, so a keyed round costs no more than
+// a keyless one.
+#define AES_COLS_(T, lo, x0, x1, x2, x3)                                                                   \
+  const u32 a0 = aes_lk(T, lo, x0, 0), a1 = aes_lk(T, lo, x1, 1), a2 = aes_lk(T, lo, x2, 2),          \
+            a3 = aes_lk(T, lo, x3, 3);                                                                \
+  const u32 b0 = aes_lk(T, lo, x1, 0), b1 = aes_lk(T, lo, x2, 1), b2 = aes_lk(T, lo, x3, 2),          \
+            b3 = aes_lk(T, lo, x0, 3);                                                                \
+  const u32 c0 = aes_lk(T, lo, x2, 0), c1 = aes_lk(T, lo, x3, 1), c2 = aes_lk(T, lo, x0, 2),          \
+            c3 = aes_lk(T, lo, x1, 3);                                                                \
+  const u32 d0 = aes_lk(T, lo, x3, 0), d1 = aes_lk(T, lo, x0, 1), d2 = aes_lk(T, lo, x1, 2),          \
+            d3 = aes_lk(T, lo, x2, 3)
+__device__ __forceinline__ void aes_round_k(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3, u32 k0, u32 k1,
+                                            u32 k2, u32 k3) {
+  AES_COLS_(T, lo, x0, x1, x2, x3);
+  x0 = xor3(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);
+  x1 = xor3(xor3(b0, rotl32(b1, 8), rotl32(b2, 16)), rotl32(b3, 24), k1);
+  x2 = xor3(xor3(c0, rotl32(c1, 8), rotl32(c2, 16)), rotl32(c3, 24), k2);
+  x3 = xor3(xor3(d0, rotl32(d1, 8), rotl32(d2, 16)), rotl32(d3, 24), k3);
+}
+__device__ __forceinline__ void aes_round_key0(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3, u32 k0) {
+  AES_COLS_(T, lo, x0, x1, x2, x3);
+  x0 = xor3(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);
+  x1 = xor3(b0, rotl32(b1, 8), rotl32(b2, 16)) ^ rotl32(b3, 24);
+  x2 = xor3(c0, rotl32(c1, 8), rotl32(c2, 16)) ^ rotl32(c3, 24);
+  x3 = xor3(d0, rotl32(d1, 8), rotl32(d2, 16)) ^ rotl32(d3, 24);
+}
+__device__ __forceinline__ void aes_round(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3) {
+  AES_COLS_(T, lo, x0, x1, x2, x3);
+  x0 = xor3(a0, rotl32(a1, 8), rotl32(a2, 16)) ^ rotl32(a3, 24);
+  x1 = xor3(b0, rotl32(b1, 8), rotl32(b2, 16)) ^ rotl32(b3, 24);
+  x2 = xor3(c0, rotl32(c1, 8), rotl32(c2, 16)) ^ rotl32(c3, 24);
+  x3 = xor3(d0, rotl32(d1, 8), rotl32(d2, 16)) ^ rotl32(d3, 24);
+}
+#undef AES_COLS_
+
+// Groestl: T0 only (row r is rotl64(T0, 8r); rows r and r+4 differ by a half swap, which is free),
+// 32 copies, qword 32x + (l mod 32) = T0[x] (ds_read_b64 banks are (a/4) mod 64 per 32-lane half:
+// lane l -> banks 2l, 2l+1). 64 KiB.
+constexpr u32 kGroestlPrivQwords = 256 * 32;
+__device__ __forceinline__ void groestl_priv_fill(u64* T) {
+  for (u32 c = threadIdx.x; c < kGroestlPrivQwords / 2; c += blockDim.x) {
+    const u64 v = x11t::GROESTL_T0[c >> 4];
+    reinterpret_cast<uint4*>(T)[c] = make_uint4(lo32(v), hi32(v), lo32(v), hi32(v));
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ u32 groestl_laneoff() { return (threadIdx.x & 31u) << 3; }
+__device__ __forceinline__ u64 groestl_lk(const u64* T, u32 lo, u32 w, int k) {
+  return *reinterpret_cast<const u64*>(reinterpret_cast<const char*>(T) + lds_addr(w, k, lo));
+}
+
+// Grid for a grid-stride kernel: enough resident blocks to fill every CU `per_cu` times over.
+int x11_device_cus();
 
 }  // namespace x11k
 

@@ -163,69 +163,74 @@ __global__ __launch_bounds__(kBlock) void k_bmw512_64(u64* __restrict__ Hb, u32 
 }
 
 // ------------------------------------------------------------------ Groestl-512
-// Column j of the 8x16 byte state is one 64-bit word (row r in byte r). A round
-// is 128 T-table lookups from LDS: T[r] = rotl64(T0, 8r).
+// Column j of the 8x16 byte state is one 64-bit word (row r in byte r). Output column j is
+// XOR_r T_r[row r byte of column (j + shift_r) mod 16] with T_r = rotl64(T0, 8r). Rows r and r+4
+// differ by a half swap (free), so with L_r = T0[b_r] ^ swap(T0[b_(r+4)]) the column is
+// L0 ^ rotl8(L1 ^ rotl8(L2 ^ rotl8(L3))): 8 conflict-free lookups from the lane's private T0
+// copy, 3 64-bit rotates, 4 64-bit (x)xor3s.
+constexpr int kGroestlBlock = 512;
+__device__ __forceinline__ u64 swap64(u64 x) { return mk64(hi32(x), lo32(x)); }
+
 template <bool kQ>
-__device__ __forceinline__ void groestl_perm(const u64 (*T)[256], u64 a[16]) {
+__device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
   constexpr int SP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
   constexpr int SQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
-  for (int r = 0; r < 14; ++r) {
+#pragma unroll 1
+  for (u32 r = 0; r < 14; ++r) {
     if (!kQ) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] ^= (u64)((j << 4) ^ r);
+      for (int j = 0; j < 16; ++j) a[j] ^= (u64)(((u32)j << 4) ^ r);
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] ^= ~((u64)((j << 4) ^ r) << 56);
+      for (int j = 0; j < 16; ++j) a[j] = mk64(~lo32(a[j]), hi32(a[j]) ^ ~((((u32)j << 4) ^ r) << 24));
     }
     u64 t[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      u64 acc = 0;
+      u32 w[8];
 #pragma unroll
       for (int row = 0; row < 8; ++row) {
-        const int src = (j + (kQ ? SQ[row] : SP[row])) & 15;
-        const u32 byte = row < 4 ? (lo32(a[src]) >> (8 * row)) & 0xff : (hi32(a[src]) >> (8 * (row - 4))) & 0xff;
-        acc ^= T[row][byte];
+        const u64 src = a[(j + (kQ ? SQ[row] : SP[row])) & 15];
+        w[row] = row < 4 ? lo32(src) : hi32(src);
       }
-      t[j] = acc;
+      const u64 L3 = groestl_lk(T, lo, w[3], 3) ^ swap64(groestl_lk(T, lo, w[7], 3));
+      const u64 L2 = xor3_64(groestl_lk(T, lo, w[2], 2), swap64(groestl_lk(T, lo, w[6], 2)), rotl64(L3, 8));
+      const u64 L1 = xor3_64(groestl_lk(T, lo, w[1], 1), swap64(groestl_lk(T, lo, w[5], 1)), rotl64(L2, 8));
+      t[j] = xor3_64(groestl_lk(T, lo, w[0], 0), swap64(groestl_lk(T, lo, w[4], 0)), rotl64(L1, 8));
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = t[j];
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  __shared__ u64 T[8][256];
-  for (int x = threadIdx.x; x < 256; x += kBlock) {
-    const u64 v = x11t::GROESTL_T0[x];
+__global__ __launch_bounds__(kGroestlBlock) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u64 T[kGroestlPrivQwords];
+  groestl_priv_fill(T);
+  const u32 lo = groestl_laneoff();
+  for (u32 i = blockIdx.x * kGroestlBlock + threadIdx.x; i < n; i += gridDim.x * kGroestlBlock) {
+    u64 m[16], p[16], q[16];
+    load_hash(Hb, stride, i, m);
+    m[8] = 0x80;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) T[r][x] = r ? rotl64(v, 8 * r) : v;
+    for (int k = 9; k < 15; ++k) m[k] = 0;
+    m[15] = 0x0100000000000000ull;  // one block, 64-bit big-endian count
+    const u64 iv15 = 0x0002000000000000ull;  // 512 in the last bytes of h
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { p[k] = m[k]; q[k] = m[k]; }
+    p[15] ^= iv15;
+    groestl_perm<false>(T, lo, p);
+    groestl_perm<true>(T, lo, q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] ^= q[k];
+    p[15] ^= iv15;  // h' = P(h^m) ^ Q(m) ^ h
+#pragma unroll
+    for (int k = 0; k < 16; ++k) q[k] = p[k];
+    groestl_perm<false>(T, lo, q);
+    u64 out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = q[8 + k] ^ p[8 + k];
+    store_hash(Hb, stride, i, out);
   }
-  __syncthreads();
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  u64 m[16], p[16], q[16];
-  load_hash(Hb, stride, i, m);
-  m[8] = 0x80;
-#pragma unroll
-  for (int k = 9; k < 15; ++k) m[k] = 0;
-  m[15] = 0x0100000000000000ull;  // one block, 64-bit big-endian count
-  const u64 iv15 = 0x0002000000000000ull;  // 512 in the last bytes of h
-#pragma unroll
-  for (int k = 0; k < 16; ++k) { p[k] = m[k]; q[k] = m[k]; }
-  p[15] ^= iv15;
-  groestl_perm<false>(T, p);
-  groestl_perm<true>(T, q);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) p[k] ^= q[k];
-  p[15] ^= iv15;  // h' = P(h^m) ^ Q(m) ^ h
-#pragma unroll
-  for (int k = 0; k < 16; ++k) q[k] = p[k];
-  groestl_perm<false>(T, q);
-  u64 out[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) out[k] = q[8 + k] ^ p[8 + k];
-  store_hash(Hb, stride, i, out);
 }
 
 // ------------------------------------------------------------------ Skein-512
@@ -431,7 +436,11 @@ hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint
   switch (stage) {
     case kX11Blake: k_blake512_80<<<grid, block, 0, s>>>(p, base, H, stride, n); break;
     case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Groestl: k_groestl512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Groestl: {
+      const u32 want = (n + kGroestlBlock - 1) / kGroestlBlock, cap = (u32)x11_device_cus() * 2 * 4;
+      k_groestl512_64<<<dim3(want < cap ? want : cap), dim3(kGroestlBlock), 0, s>>>(H, stride, n);
+      break;
+    }
     case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n); break;

@@ -226,20 +226,22 @@ constexpr u32 kShaviteIv[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 
                                 0xB29F5CD1, 0xDF07FBFC, 0x8E45D73D, 0x681AB538, 0xBDE86578, 0xDD577E47,
                                 0xE275EADE, 0x502D9FCD, 0xB9357178, 0x022A4B9A};
 
-// F: four keyed AES rounds (key added before each keyless round).
-__device__ __forceinline__ void shavite_F(const u32 (*T)[256], u32 x[4], const u32* k) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    x[0] ^= k[4 * r]; x[1] ^= k[4 * r + 1]; x[2] ^= k[4 * r + 2]; x[3] ^= k[4 * r + 3];
-    aes_round(T, x[0], x[1], x[2], x[3]);
-  }
+// F: four AES rounds, round key i added before round i; keys 1..3 ride in the previous round's
+// output xor3.
+constexpr int kAesBlock = 512;
+__device__ __forceinline__ void shavite_F(const u32* T, u32 lo, u32 x[4], const u32* k) {
+  x[0] ^= k[0]; x[1] ^= k[1]; x[2] ^= k[2]; x[3] ^= k[3];
+  aes_round_k(T, lo, x[0], x[1], x[2], x[3], k[4], k[5], k[6], k[7]);
+  aes_round_k(T, lo, x[0], x[1], x[2], x[3], k[8], k[9], k[10], k[11]);
+  aes_round_k(T, lo, x[0], x[1], x[2], x[3], k[12], k[13], k[14], k[15]);
+  aes_round(T, lo, x[0], x[1], x[2], x[3]);
 }
 
-__global__ __launch_bounds__(kBlock) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  __shared__ u32 T[4][256];
-  aes_tables_to_lds(T);
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+__global__ __launch_bounds__(kAesBlock) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u32 T[kAesPrivWords];
+  aes_priv_fill(T);
+  const u32 lo = aes_laneoff();
+  for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
   u64 h[8];
   load_hash(Hb, stride, i, h);
   // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void k_shavite512_64(u64* __restrict__ Hb, 
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         u32 t0 = rk[4 * g + 1], t1 = rk[4 * g + 2], t2 = rk[4 * g + 3], t3 = rk[4 * g];
-        aes_round(T, t0, t1, t2, t3);
+        aes_round(T, lo, t0, t1, t2, t3);
         const int p = g ? 4 * g - 4 : 28;
         rk[4 * g] = t0 ^ rk[p];
         rk[4 * g + 1] = t1 ^ rk[p + 1];
@@ -279,12 +281,12 @@ __global__ __launch_bounds__(kBlock) void k_shavite512_64(u64* __restrict__ Hb, 
       for (int k = 0; k < 32; ++k) rk[k] ^= k >= 7 ? rk[k - 7] : rk[k + 25];
     }
     u32 x[4] = {B[0], B[1], B[2], B[3]};
-    shavite_F(T, x, rk);
+    shavite_F(T, lo, x, rk);
 #pragma unroll
     for (int k = 0; k < 4; ++k) A[k] ^= x[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = D[k];
-    shavite_F(T, x, rk + 16);
+    shavite_F(T, lo, x, rk + 16);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       C[k] ^= x[k];
@@ -300,6 +302,7 @@ __global__ __launch_bounds__(kBlock) void k_shavite512_64(u64* __restrict__ Hb, 
     h[6 + k] = mk64(kShaviteIv[12 + 2 * k] ^ D[2 * k], kShaviteIv[13 + 2 * k] ^ D[2 * k + 1]);
   }
   store_hash(Hb, stride, i, h);
+  }
 }
 
 // ------------------------------------------------------------------ SIMD-512
@@ -485,16 +488,21 @@ __global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32
 }
 
 // ------------------------------------------------------------------ ECHO-512
-__device__ __forceinline__ u32 xt4(u32 x) { return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1bu); }
+// GF(2^8) doubling of 4 packed bytes: the 0x1b reduction as one packed 16-bit multiply (full rate;
+// a 32-bit v_mul_lo_u32 is quarter rate) and the masked shift + xor as one v_bitop3 ((a & c) ^ b).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32 xt4(u32 x) {
+  const u16x2 m = __builtin_bit_cast(u16x2, (x >> 7) & 0x01010101u) * (u16x2)(0x1b);
+  return bop3<0x6C>(x << 1, __builtin_bit_cast(u32, m), 0xfefefefeu);
+}
 
 // One ECHO round: BIG.SubWords (two AES rounds per 128-bit word, the first keyed by the
 // running counter), BIG.ShiftRows (a renaming), BIG.MixColumns (bytewise, 4 bytes per u32).
-__device__ __forceinline__ void echo_round(const u32 (*T)[256], u32 W[16][4], u32 k) {
+__device__ __forceinline__ void echo_round(const u32* T, u32 lo, u32 W[16][4], u32 k) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    aes_round(T, W[i][0], W[i][1], W[i][2], W[i][3]);
-    W[i][0] ^= k + (u32)i;
-    aes_round(T, W[i][0], W[i][1], W[i][2], W[i][3]);
+    aes_round_key0(T, lo, W[i][0], W[i][1], W[i][2], W[i][3], k + (u32)i);
+    aes_round(T, lo, W[i][0], W[i][1], W[i][2], W[i][3]);
   }
   u32 N[16][4];
 #pragma unroll
@@ -505,10 +513,10 @@ __device__ __forceinline__ void echo_round(const u32 (*T)[256], u32 W[16][4], u3
       const u32 a0 = W[4 * c][w], a1 = W[4 * ((c + 1) & 3) + 1][w], a2 = W[4 * ((c + 2) & 3) + 2][w],
                 a3 = W[4 * ((c + 3) & 3) + 3][w];
       const u32 ab = a0 ^ a1, bc = a1 ^ a2, cd = a2 ^ a3, da = a3 ^ a0;
-      N[4 * c + 0][w] = xt4(ab) ^ a1 ^ cd;
-      N[4 * c + 1][w] = xt4(bc) ^ a0 ^ cd;
-      N[4 * c + 2][w] = xt4(cd) ^ ab ^ a3;
-      N[4 * c + 3][w] = xt4(da) ^ a0 ^ bc;
+      N[4 * c + 0][w] = xor3(xt4(ab), a1, cd);
+      N[4 * c + 1][w] = xor3(xt4(bc), a0, cd);
+      N[4 * c + 2][w] = xor3(xt4(cd), ab, a3);
+      N[4 * c + 3][w] = xor3(xt4(da), a0, bc);
     }
   }
 #pragma unroll
@@ -520,12 +528,12 @@ __device__ __forceinline__ void echo_round(const u32 (*T)[256], u32 W[16][4], u3
 // kSearch: compare the top 64 bits of the X11 digest (ECHO output bytes 24..31) with
 // the target and append hits to out[1..cap] (out[0] counts); otherwise write H.
 template <bool kSearch>
-__global__ __launch_bounds__(kBlock) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
-                                                       u64 target_hi, u32* __restrict__ out, u32 cap) {
-  __shared__ u32 T[4][256];
-  aes_tables_to_lds(T);
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+__global__ __launch_bounds__(kAesBlock) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
+                                                          u64 target_hi, u32* __restrict__ out, u32 cap) {
+  __shared__ u32 T[kAesPrivWords];
+  aes_priv_fill(T);
+  const u32 lo = aes_laneoff();
+  for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
   u64 h[8];
   load_hash(Hb, stride, i, h);
   u32 W[16][4];
@@ -543,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_echo512_64(u64* __restrict__ Hb, u32
   W[14][3] = 0x02000000u;
   W[15][0] = 512u;
 #pragma unroll 1
-  for (int r = 0; r < 10; ++r) echo_round(T, W, 512u + 16u * (u32)r);
+  for (int r = 0; r < 10; ++r) echo_round(T, lo, W, 512u + 16u * (u32)r);
   // V' = V ^ M ^ W[0..7] ^ W[8..15]; the digest is V'[0..3], V = {512, 0, 0, 0}.
   if (kSearch) {
     const u64 top = mk64(lo32(h[3]) ^ W[1][2] ^ W[9][2], hi32(h[3]) ^ W[1][3] ^ W[9][3]);
@@ -563,26 +571,44 @@ __global__ __launch_bounds__(kBlock) void k_echo512_64(u64* __restrict__ Hb, u32
     for (int k = 0; k < 4; ++k) o[4 + k] = 0;
     store_hash(Hb, stride, i, o);
   }
+  }
 }
 
+}  // namespace x11k
+
+namespace x11k {
+int x11_device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
 }  // namespace x11k
 
 hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
                               uint32_t* out, uint32_t cap, hipStream_t s) {
   using namespace x11k;
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+  // bank-private AES table (64 KiB): 2 resident blocks of 512 per CU, grid-stride over the batch
+  const u32 aes_want = (n + kAesBlock - 1) / kAesBlock, aes_cap = (u32)x11_device_cus() * 2 * 4;
+  const dim3 aes_grid(aes_want < aes_cap ? aes_want : aes_cap), aes_block(kAesBlock);
   switch (stage) {
     case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Shavite: k_shavite512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n); break;
     case kX11Simd: {
       const dim3 g8((8ull * n + kBlock - 1) / kBlock);
       k_simd512_64<<<g8, block, 0, s>>>(H, stride, n);
       break;
     }
     case kX11Echo:
-      if (out) k_echo512_64<true><<<grid, block, 0, s>>>(H, stride, n, base, p.target_hi, out, cap);
-      else k_echo512_64<false><<<grid, block, 0, s>>>(H, stride, n, base, p.target_hi, nullptr, 0);
+      if (out) k_echo512_64<true><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, out, cap);
+      else k_echo512_64<false><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, nullptr, 0);
       break;
     default: return hipErrorInvalidValue;
   }
