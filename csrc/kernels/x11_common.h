@@ -21,6 +21,7 @@ namespace x11k {
 
 typedef uint32_t u32;
 typedef uint64_t u64;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // packed 16-bit VALU ops (v_pk_*)
 
 constexpr int kBlock = 256;
 

@@ -316,88 +316,70 @@ constexpr int kSimdRS[4][4] = {{3, 23, 17, 27}, {28, 19, 22, 7}, {29, 9, 15, 5},
 constexpr int kSimdSB[32] = {4, 6, 0, 2, 7, 5, 3, 1, 15, 11, 12, 8, 9, 13, 10, 14,
                              17, 18, 23, 20, 22, 21, 16, 19, 30, 24, 25, 31, 27, 29, 28, 26};
 
-constexpr u32 pow257(u32 b, u32 e) {
-  u32 r = 1;
-  for (u32 k = 0; k < e; ++k) r = r * b % 257u;
-  return r;
+// Column b of the first-block NTT (see tools/gen_x11_tables.cpp, which checks this exact integer
+// form against the direct transform): u_d = dot4(X_d, PT[b][d]) + S_d with X_d = bytes x[16c+d]
+// (c = 0..3) and PT[b][d] byte c = alpha^(b(16c+d)) - 1, so one v_dot4_u32_u8 per coefficient;
+// then the 16-point DFT with root 2 as 4 x 4 with root 16 (shifts and adds only), the first-block
+// twiddle beta_b 2^-a, and a centred reduction mod 257.
+__device__ __forceinline__ int fold257(int x) { return (x & 255) - (x >> 8); }
+__device__ __forceinline__ int centre257(int x) {
+  x = fold257(fold257(fold257(x)));  // |x| < 2^27 -> [-8, 264]
+  return x > 128 ? x - 257 : x;
 }
-// alpha^b and alpha^-b (alpha = 41, a 256th root of unity mod 257, alpha^16 = 2) for NTT column b.
-__constant__ u32 c_simd_alpha[16] = {
-    pow257(41, 0), pow257(41, 1), pow257(41, 2), pow257(41, 3), pow257(41, 4), pow257(41, 5), pow257(41, 6),
-    pow257(41, 7), pow257(41, 8), pow257(41, 9), pow257(41, 10), pow257(41, 11), pow257(41, 12), pow257(41, 13),
-    pow257(41, 14), pow257(41, 15)};
-__constant__ u32 c_simd_beta[16] = {
-    pow257(41, 0), pow257(41, 255), pow257(41, 254), pow257(41, 253), pow257(41, 252), pow257(41, 251),
-    pow257(41, 250), pow257(41, 249), pow257(41, 248), pow257(41, 247), pow257(41, 246), pow257(41, 245),
-    pow257(41, 244), pow257(41, 243), pow257(41, 242), pow257(41, 241)};
-
-
-// Reduce |x| < 2^26 to [0, 256] (256 = -1 mod 257: x = 256q + r == r - q).
-__device__ __forceinline__ int red257(int x) {
-  x = (x & 255) - (x >> 8);
-  x = (x & 255) - (x >> 8);
-  x = (x & 255) - (x >> 8);
-  return x < 0 ? x + 257 : x;
-}
-// x * 2^E mod 257 up to reduction: 2^8 = -1, so 2^E = (-1)^((E >> 3) & 1) 2^(E & 7).
 template <int E>
 __device__ __forceinline__ int mul2pow(int x) {
   constexpr int e = ((E % 16) + 16) % 16;
-  return e < 8 ? (x << e) : -(x << (e - 8));
+  if constexpr (e < 8) return x << e;
+  else return -(x << (e - 8));
 }
-// 2^e mod 257 for a lane-varying e.
-__device__ __forceinline__ int pow2_257(u32 e) {
-  const int v = 1 << (e & 7);
-  return (e & 8) ? 257 - v : v;
+__device__ __forceinline__ void dft4_16(int i0, int i1, int i2, int i3, int& o0, int& o1, int& o2, int& o3) {
+  const int e0 = i0 + i2, e1 = i0 - i2, p0 = i1 + i3, p1 = i1 - i3;
+  o0 = e0 + p0; o2 = e0 - p0; o1 = e1 + (p1 << 4); o3 = e1 - (p1 << 4);
 }
-
-// The 16 NTT outputs q[16a + b], a = 0..15, of column b of the first (message) block:
-// y = sum_{j<64} x_j alpha^((16a+b) j) plus the first-block twiddle alpha^-(16a+b),
-// centred to [-128, 128]. With j = 16c + d and alpha^16 = 2:
-// y = sum_d 2^(ad) u_d,  u_d = sum_c x_{16c+d} alpha^(b(16c+d)).
-__device__ __forceinline__ void simd_ntt_column(const u32 xw[16], u32 b, int q[16]) {
-  const int g1 = pow2_257(b), g2 = pow2_257(2 * b), g3 = pow2_257(3 * b);
-  const int ab = (int)c_simd_alpha[b];
+__device__ __forceinline__ void simd_ntt_column(const u32 X[16], const u32 S[16], const u32* PT, int beta, int q[16]) {
   int u[16];
-  int f = 1;  // alpha^(b d)
 #pragma unroll
-  for (int d = 0; d < 16; ++d) {
-    const int sh = 8 * (d & 3);
-    const int x0 = (xw[(d >> 2)] >> sh) & 0xff;
-    const int x1 = (xw[4 + (d >> 2)] >> sh) & 0xff;
-    const int x2 = (xw[8 + (d >> 2)] >> sh) & 0xff;
-    const int x3 = (xw[12 + (d >> 2)] >> sh) & 0xff;
-    const int s = x0 + x1 * g1 + x2 * g2 + x3 * g3;  // < 2^18
-    u[d] = red257(red257(s) * f);
-    if (d < 15) f = red257(f * ab);
+  for (int d = 0; d < 16; ++d) u[d] = fold257((int)__builtin_amdgcn_udot4(X[d], PT[d], S[d], false));
+  int W[4][4];
+#pragma unroll
+  for (int d1 = 0; d1 < 4; ++d1) {
+    int v0, v1, v2, v3;
+    dft4_16(u[d1], u[4 + d1], u[8 + d1], u[12 + d1], v0, v1, v2, v3);
+    W[d1][0] = v0;
+    W[d1][1] = d1 == 0 ? v1 : d1 == 1 ? mul2pow<1>(v1) : d1 == 2 ? mul2pow<2>(v1) : mul2pow<3>(v1);
+    W[d1][2] = d1 == 0 ? v2 : d1 == 1 ? mul2pow<2>(v2) : d1 == 2 ? mul2pow<4>(v2) : mul2pow<6>(v2);
+    W[d1][3] = d1 == 0 ? v3 : d1 == 1 ? mul2pow<3>(v3) : d1 == 2 ? mul2pow<6>(v3) : mul2pow<9>(v3);
   }
-  const int beta = (int)c_simd_beta[b];
 #pragma unroll
-  for (int a = 0; a < 16; ++a) {
-    int y = 0;
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-      const int e = (a * d) & 15;
-      y += e < 8 ? (u[d] << e) : -(u[d] << (e - 8));
-    }
-    const int e = (16 - a) & 15;  // twiddle alpha^-(16a+b) = 2^-a beta_b
-    y += e < 8 ? (beta << e) : -(beta << (e - 8));
-    const int v = red257(y);
-    q[a] = v <= 128 ? v : v - 257;
+  for (int a1 = 0; a1 < 4; ++a1) {
+    int y0, y1, y2, y3;
+    dft4_16(W[0][a1], W[1][a1], W[2][a1], W[3][a1], y0, y1, y2, y3);
+    q[a1] = centre257(y0 + (a1 == 0 ? beta : a1 == 1 ? mul2pow<15>(beta) : a1 == 2 ? mul2pow<14>(beta) : mul2pow<13>(beta)));
+    q[a1 + 4] = centre257(y1 + (a1 == 0 ? mul2pow<12>(beta) : a1 == 1 ? mul2pow<11>(beta) : a1 == 2 ? mul2pow<10>(beta) : mul2pow<9>(beta)));
+    q[a1 + 8] = centre257(y2 + (a1 == 0 ? mul2pow<8>(beta) : a1 == 1 ? mul2pow<7>(beta) : a1 == 2 ? mul2pow<6>(beta) : mul2pow<5>(beta)));
+    q[a1 + 12] = centre257(y3 + (a1 == 0 ? mul2pow<4>(beta) : a1 == 1 ? mul2pow<3>(beta) : a1 == 2 ? mul2pow<2>(beta) : mul2pow<1>(beta)));
   }
 }
 
-__device__ __forceinline__ u32 simd_if(u32 x, u32 y, u32 z) { return ((y ^ z) & x) ^ z; }
-__device__ __forceinline__ u32 simd_maj(u32 x, u32 y, u32 z) { return (x & y) | ((x | y) & z); }
+// tA of lane j ^ PP inside the 8-lane group, by DPP (quad_perm for xor 1/2/3, row_half_mirror for
+// xor 7; xor 4/5/6 = xor 7 then xor 3/2/1). The compiler fuses the DPP mov into the consuming add.
+template <int PP>
+__device__ __forceinline__ u32 simd_xlane(u32 v) {
+  constexpr int q = PP == 1 || PP == 6 ? 0xB1 : PP == 2 || PP == 5 ? 0x4E : 0x1B;  // xor 1 / 2 / 3
+  if (PP >= 4) {
+    v = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // xor 7
+    if (PP == 7) return v;
+  }
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);
+}
 
-// One Feistel step on state column j (this lane); tA of lane j ^ PP comes over the 8-lane group.
+// One Feistel step on state column j (this lane).
 template <bool kMaj, int R, int S, int PP>
 __device__ __forceinline__ void simd_step(u32& s0, u32& s1, u32& s2, u32& s3, u32 w) {
   const u32 tA = rotl32(s0, R);
-  const u32 f = kMaj ? simd_maj(s0, s1, s2) : simd_if(s0, s1, s2);
+  const u32 f = kMaj ? bop3<0xE8>(s0, s1, s2) : bop3<0xCA>(s0, s1, s2);  // MAJ / IF
   const u32 tt = s3 + w + f;
-  const u32 other = (u32)__shfl_xor((int)tA, PP, 8);
-  s0 = rotl32(tt, S) + other;
+  s0 = rotl32(tt, S) + simd_xlane<PP>(tA);
   s3 = s2;
   s2 = s1;
   s1 = tA;
@@ -429,13 +411,39 @@ __device__ __forceinline__ void simd_compress(u32& s0, u32& s1, u32& s2, u32& s3
   simd_step<false, 25, 4, kSimdPP[0]>(s0, s1, s2, s3, h3);
 }
 
-__device__ __forceinline__ u32 simd_inner(int l, int h, int mm) {
-  return ((u32)(l * mm) & 0xFFFFu) + ((u32)(h * mm) << 16);
+// W = (l * mm mod 2^16) | (h * mm mod 2^16) << 16: pack (l, h) as u16 halves (one v_perm), then one
+// packed 16-bit multiply.
+__device__ __forceinline__ u32 simd_inner(int l, int h, unsigned short mm) {
+  const u32 lh = __builtin_amdgcn_perm((u32)h, (u32)l, 0x05040100u);
+  return __builtin_bit_cast(u32, __builtin_bit_cast(u16x2, lh) * (u16x2)(mm));
 }
 
+// Per-block LDS tables (dwords): for lane column pair j, PT[2j][0..15] PT[2j+1][0..15] at 36j (row
+// stride 36 keeps the 8 distinct rows of a ds_read_b128 lane group on distinct banks); final-block
+// words W_F[st][j] at 288 + 36j; SIMD IV at 576; beta_b at 608.
+constexpr int kSimdBlock = 256;
+constexpr u32 kSimdLds = 624;
+
 // Eight lanes per hash: launch with 8 * n threads.
-__global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  const u32 t = blockIdx.x * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ __attribute__((aligned(16))) u32 L[kSimdLds];
+  for (u32 t = threadIdx.x; t < kSimdLds; t += kSimdBlock) {
+    u32 v = 0;
+    if (t < 288) {
+      const u32 jj = t / 36, k = t % 36;
+      v = k < 16 ? x11t::SIMD_PT[2 * jj][k] : k < 32 ? x11t::SIMD_PT[2 * jj + 1][k - 16] : 0u;
+    } else if (t < 576) {
+      const u32 jj = (t - 288) / 36, k = (t - 288) % 36;
+      v = k < 32 ? x11t::SIMD_WF[k][jj] : 0u;
+    } else if (t < 608) {
+      v = kSimdIv[t - 576];
+    } else {
+      v = x11t::SIMD_BETA[t - 608];
+    }
+    L[t] = v;
+  }
+  __syncthreads();
+  const u32 t = blockIdx.x * kSimdBlock + threadIdx.x;
   const u32 i = t >> 3, j = t & 7;
   if (i >= n) return;  // whole 8-lane groups exit together
   u64 h[8];
@@ -443,9 +451,25 @@ __global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32
   u32 xw[16];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { xw[2 * k] = lo32(h[k]); xw[2 * k + 1] = hi32(h[k]); }
+  // X_d = (x[d], x[16 + d], x[32 + d], x[48 + d]): 4x4 byte transposes of (xw[g], xw[4+g], xw[8+g], xw[12+g])
+  u32 X[16], S[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const u32 p01l = __builtin_amdgcn_perm(xw[4 + g], xw[g], 0x05010400u);
+    const u32 p01h = __builtin_amdgcn_perm(xw[4 + g], xw[g], 0x07030602u);
+    const u32 p23l = __builtin_amdgcn_perm(xw[12 + g], xw[8 + g], 0x05010400u);
+    const u32 p23h = __builtin_amdgcn_perm(xw[12 + g], xw[8 + g], 0x07030602u);
+    X[4 * g + 0] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+    X[4 * g + 1] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+    X[4 * g + 2] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+    X[4 * g + 3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
+  }
+#pragma unroll
+  for (int d = 0; d < 16; ++d) S[d] = __builtin_amdgcn_udot4(X[d], 0x01010101u, 0u, false);
+  const u32* row = L + 36 * j;
   int qa[16], qb[16];
-  simd_ntt_column(xw, 2 * j, qa);
-  simd_ntt_column(xw, 2 * j + 1, qb);
+  simd_ntt_column(X, S, row, (int)L[608 + 2 * j], qa);
+  simd_ntt_column(X, S, row + 16, (int)L[609 + 2 * j], qb);
   u32 W[32];
 #pragma unroll
   for (int st = 0; st < 32; ++st) {
@@ -454,33 +478,22 @@ __global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32
     else if (st < 24) W[st] = simd_inner(qa[sb - 16], qa[sb - 8], 233);
     else W[st] = simd_inner(qb[sb - 24], qb[sb - 16], 233);
   }
-  // Column j of the chaining value and of the block (message words j and 8 + j).
-  u32 m0 = 0, m1 = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (j == (u32)k) { m0 = xw[k]; m1 = xw[8 + k]; }
-  }
-  u32 iv0 = 0, iv1 = 0, iv2 = 0, iv3 = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (j == (u32)k) { iv0 = kSimdIv[k]; iv1 = kSimdIv[8 + k]; iv2 = kSimdIv[16 + k]; iv3 = kSimdIv[24 + k]; }
-  }
+  // Column j of the chaining value (IV) and of the block (message words j and 8 + j).
+  const u32 iv0 = L[576 + j], iv1 = L[584 + j], iv2 = L[592 + j], iv3 = L[600 + j];
+  const u32* Hw = reinterpret_cast<const u32*>(Hb);  // message words j and 8 + j (L2-resident re-read)
+  const u32 m0 = Hw[((size_t)(j >> 1) * stride + i) * 2 + (j & 1)];
+  const u32 m1 = Hw[((size_t)(4 + (j >> 1)) * stride + i) * 2 + (j & 1)];
   u32 s0 = iv0 ^ m0, s1 = iv1 ^ m1, s2 = iv2, s3 = iv3;
   simd_compress(s0, s1, s2, s3, iv0, iv1, iv2, iv3, W);
-  // Final block: the 512-bit length (word 0), expanded with the final tweak (constant).
+  // Final block: the 512-bit length (word 0), expanded with the final tweak (constant W_F).
+  const u32* wf = L + 288 + 36 * j;
 #pragma unroll
-  for (int st = 0; st < 32; ++st) {
-    u32 v = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v = (j == (u32)k) ? x11t::SIMD_WF[st][k] : v;
-    W[st] = v;
-  }
+  for (int st = 0; st < 32; ++st) W[st] = wf[st];
   const u32 c0 = s0, c1 = s1, c2 = s2, c3 = s3;
   if (j == 0) s0 ^= 512u;
   simd_compress(s0, s1, s2, s3, c0, c1, c2, c3, W);
-  // Output words j (s0) and 8 + j (s1); even lanes pair with their odd neighbour.
-  const u32 n0 = (u32)__shfl_down((int)s0, 1, 8);
-  const u32 n1 = (u32)__shfl_down((int)s1, 1, 8);
+  // Output words j (s0) and 8 + j (s1); even lanes pair with their odd neighbour (DPP xor 1).
+  const u32 n0 = simd_xlane<1>(s0), n1 = simd_xlane<1>(s1);
   if ((j & 1) == 0) {
     __builtin_nontemporal_store(mk64(s0, n0), Hb + (size_t)(j >> 1) * stride + i);
     __builtin_nontemporal_store(mk64(s1, n1), Hb + (size_t)(4 + (j >> 1)) * stride + i);
@@ -490,7 +503,6 @@ __global__ __launch_bounds__(kBlock) void k_simd512_64(u64* __restrict__ Hb, u32
 // ------------------------------------------------------------------ ECHO-512
 // GF(2^8) doubling of 4 packed bytes: the 0x1b reduction as one packed 16-bit multiply (full rate;
 // a 32-bit v_mul_lo_u32 is quarter rate) and the masked shift + xor as one v_bitop3 ((a & c) ^ b).
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32 xt4(u32 x) {
   const u16x2 m = __builtin_bit_cast(u16x2, (x >> 7) & 0x01010101u) * (u16x2)(0x1b);
   return bop3<0x6C>(x << 1, __builtin_bit_cast(u32, m), 0xfefefefeu);

@@ -9,7 +9,7 @@
 //     direct transform;
 //   * AES T-table round vs the byte-wise round.
 //
-// Build + run: g++ -O2 -std=c++17 tools/gen_x11_tables.cpp csrc/cpu/x11_cpu.cpp -o /tmp/gen && /tmp/gen > csrc/kernels/x11_tables.h
+// Build + run: g++ -O2 -std=c++17 -Icsrc/include tools/gen_x11_tables.cpp csrc/cpu/x11_cpu.cpp -o /tmp/gen && /tmp/gen > csrc/kernels/x11_tables.h
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -166,6 +166,68 @@ static void ntt_split(const u8 x[64], int y[256]) {
     }
 }
 
+// ----------------------------------------------------------------- SIMD GPU form
+// The gfx950 kernel computes column b of the first-block NTT as
+//   u_d = dot4(X_d, P'_b[d]) + S_d            (X_d byte c = x[16c+d], P'_b[d] byte c = alpha^(b(16c+d)) - 1,
+//                                               S_d = sum of X_d's bytes)
+//   y_a = sum_d 2^(ad) u_d                     (16-point DFT with root 2 as 4 x 4 with root 16)
+//   q   = centre(y_a + beta_b 2^-a),  beta_b = alpha^-b
+// Model it here with the same integer steps and compare with the direct transform.
+static u32 SIMD_PT[16][16];  // [b][d] packed bytes
+static u32 SIMD_BETA[16];
+static int fold(int x) { return (x & 255) - (x >> 8); }
+static int centre(int x) { x = fold(fold(fold(x))); return x > 128 ? x - 257 : x; }
+static int m2(int x, int e) { e &= 15; return e < 8 ? (x << e) : -(x << (e - 8)); }
+static void dft4(int i0, int i1, int i2, int i3, int o[4]) {
+    int e0 = i0 + i2, e1 = i0 - i2, p0 = i1 + i3, p1 = i1 - i3;
+    o[0] = e0 + p0; o[2] = e0 - p0; o[1] = e1 + (p1 << 4); o[3] = e1 - (p1 << 4);
+}
+static void simd_gpu_column(const u8 x[64], int b, int q[16]) {
+    int u[16];
+    for (int d = 0; d < 16; ++d) {
+        int acc = 0;
+        for (int c = 0; c < 4; ++c) acc += x[16 * c + d] * (int)((SIMD_PT[b][d] >> (8 * c)) & 0xff) + x[16 * c + d];
+        u[d] = fold(acc);
+    }
+    int V[4][4], W[4][4];
+    for (int d1 = 0; d1 < 4; ++d1) dft4(u[d1], u[4 + d1], u[8 + d1], u[12 + d1], V[d1]);
+    for (int d1 = 0; d1 < 4; ++d1)
+        for (int a1 = 0; a1 < 4; ++a1) W[d1][a1] = m2(V[d1][a1], a1 * d1);
+    for (int a1 = 0; a1 < 4; ++a1) {
+        int y[4];
+        dft4(W[0][a1], W[1][a1], W[2][a1], W[3][a1], y);
+        for (int a2 = 0; a2 < 4; ++a2) {
+            int a = a1 + 4 * a2;
+            q[a] = centre(y[a2] + m2((int)SIMD_BETA[b], 16 - a));
+        }
+    }
+}
+static void simd_gpu_check(std::mt19937_64& rng) {
+    for (int b = 0; b < 16; ++b) {
+        SIMD_BETA[b] = (u32)pw(41, (256 - b) % 256);
+        for (int d = 0; d < 16; ++d) {
+            u32 v = 0;
+            for (int c = 0; c < 4; ++c) v |= (u32)(pw(41, b * (16 * c + d)) - 1) << (8 * c);
+            SIMD_PT[b][d] = v;
+        }
+    }
+    for (int t = 0; t < 64; ++t) {
+        u8 x[64];
+        for (auto& v : x) v = (u8)rng();
+        if (t == 0) memset(x, 0xff, 64);  // magnitude corner
+        for (int b = 0; b < 16; ++b) {
+            int q[16];
+            simd_gpu_column(x, b, q);
+            for (int a = 0; a < 16; ++a) {
+                int i = 16 * a + b, acc = 0;
+                for (int j = 0; j < 64; ++j) acc = (acc + x[j] * pw(41, i * j)) % 257;
+                int v = md(acc + pw(41, (255 * i) % 256));
+                CHECK(q[a] == (v <= 128 ? v : v - 257), "simd gpu column form == direct NTT");
+            }
+        }
+    }
+}
+
 int main() {
     const u8* S = aes_sbox();
     // AES T0: contribution of a row-0 input byte to one MixColumns output column (LE word).
@@ -223,6 +285,7 @@ int main() {
             WF[st][j] = ((u32)(l * mm) & 0xFFFFu) + ((u32)(h * mm) << 16);
         }
     }
+    simd_gpu_check(rng);
     if (fail) return 1;
 
     printf("// Generated by tools/gen_x11_tables.cpp from csrc/cpu/x11_cpu.cpp -- do not edit.\n");
@@ -257,7 +320,16 @@ int main() {
         for (int j = 0; j < 8; ++j) printf("%s0x%08xu", j ? ", " : "", WF[st][j]);
         printf("},");
     }
+    printf("};\n\n// SIMD-512 first-block NTT column tables: [b][d] byte c = alpha^(b(16c+d)) - 1 (alpha = 41).\n");
+    printf("static constexpr uint32_t SIMD_PT[16][16] = {");
+    for (int b = 0; b < 16; ++b) {
+        printf("\n    {");
+        for (int d = 0; d < 16; ++d) printf("%s0x%08xu", d ? ", " : "", SIMD_PT[b][d]);
+        printf("},");
+    }
+    printf("};\n\n// alpha^-b for NTT column b.\nstatic constexpr uint32_t SIMD_BETA[16] = {");
+    for (int b = 0; b < 16; ++b) printf("%s%uu", b ? ", " : "", SIMD_BETA[b]);
     printf("};\n\n}  // namespace x11t\n}  // namespace otedama\n");
-    fprintf(stderr, "x11 tables generated; JH bitslice, SIMD split NTT checks passed\n");
+    fprintf(stderr, "x11 tables generated; JH bitslice, SIMD split NTT, SIMD GPU column form checks passed\n");
     return 0;
 }
