@@ -203,7 +203,7 @@ __device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
   }
 }
 
-__global__ __launch_bounds__(kGroestlBlock) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ u64 T[kGroestlPrivQwords];
   groestl_priv_fill(T);
   const u32 lo = groestl_laneoff();
@@ -288,25 +288,32 @@ __global__ __launch_bounds__(kBlock) void k_skein512_64(u64* __restrict__ Hb, u3
 // tools/gen_x11_tables.cpp, which checks this formulation against the spec form.
 __constant__ u32 c_jh_bc[42][8];
 
+// The JH authors' bitsliced S-box layer (constant bit cc selects S0/S1) with every and/or/not + xor
+// pair as one v_bitop3 (truth tables for a = 0xF0, b = 0xCC, c = 0xAA); the complement of m3 is
+// folded into its three uses. 10 VALU per 4 planes (hipcc alone: ~20).
+#define JH_SB4(m0, m1, m2, m3, cc)                 \
+  do {                                              \
+    u32 t_;                                         \
+    m0 = bop3<0xD2>(m0, m2, cc);   /* m0 ^= ~m2 & cc */        \
+    t_ = bop3<0x78>(cc, m0, m1);   /* t = cc ^ (m0 & m1) */    \
+    m0 = bop3<0xB4>(m0, m2, m3);   /* m0 ^= m2 & ~M3 */        \
+    m3 = bop3<0x2D>(m3, m1, m2);   /* m3 = ~M3 ^ (~m1 & m2) */ \
+    m1 = bop3<0x78>(m1, m0, m2);   /* m1 ^= m0 & m2 */         \
+    m2 = bop3<0xB4>(m2, m0, m3);   /* m2 ^= m0 & ~m3 */        \
+    m0 = bop3<0x1E>(m0, m1, m3);   /* m0 ^= m1 | m3 */         \
+    m3 = bop3<0x78>(m3, m1, m2);   /* m3 ^= m1 & m2 */         \
+    m1 = bop3<0x78>(m1, t_, m0);   /* m1 ^= t & m0 */          \
+    m2 ^= t_;                                       \
+  } while (0)
 #define JH_SS(m0, m1, m2, m3, m4, m5, m6, m7, cc0, cc1) \
   do {                                                  \
-    u32 t0_, t1_;                                       \
-    m3 = ~m3; m7 = ~m7;                                 \
-    m0 ^= (~m2) & (cc0); m4 ^= (~m6) & (cc1);           \
-    t0_ = (cc0) ^ (m0 & m1); t1_ = (cc1) ^ (m4 & m5);   \
-    m0 ^= m2 & m3; m4 ^= m6 & m7;                       \
-    m3 ^= (~m1) & m2; m7 ^= (~m5) & m6;                 \
-    m1 ^= m0 & m2; m5 ^= m4 & m6;                       \
-    m2 ^= m0 & (~m3); m6 ^= m4 & (~m7);                 \
-    m0 ^= m1 | m3; m4 ^= m5 | m7;                       \
-    m3 ^= m1 & m2; m7 ^= m5 & m6;                       \
-    m1 ^= t0_ & m0; m5 ^= t1_ & m4;                     \
-    m2 ^= t0_; m6 ^= t1_;                               \
+    JH_SB4(m0, m1, m2, m3, cc0);                        \
+    JH_SB4(m4, m5, m6, m7, cc1);                        \
   } while (0)
 #define JH_L(m0, m1, m2, m3, m4, m5, m6, m7) \
   do {                                       \
-    m4 ^= m1; m5 ^= m2; m6 ^= m0 ^ m3; m7 ^= m0; \
-    m0 ^= m5; m1 ^= m6; m2 ^= m4 ^ m7; m3 ^= m4; \
+    m4 ^= m1; m5 ^= m2; m6 = xor3(m6, m0, m3); m7 ^= m0; \
+    m0 ^= m5; m1 ^= m6; m2 = xor3(m2, m4, m7); m3 ^= m4; \
   } while (0)
 
 template <int K>
@@ -391,6 +398,12 @@ constexpr int kKeccakRot[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 
 
 __device__ __forceinline__ u64 rotl64z(u64 x, int n) { return n == 0 ? x : rotl64(x, n); }
 
+// chi: a ^ (~b & c) in one v_bitop3 per 32-bit half.
+__device__ __forceinline__ u64 keccak_chi(u64 a, u64 b, u64 c) {
+  return mk64(bop3<0xD2>(lo32(a), lo32(b), lo32(c)), bop3<0xD2>(hi32(a), hi32(b), hi32(c)));
+}
+__device__ __forceinline__ u64 xor5_64(u64 a, u64 b, u64 c, u64 d, u64 e) { return xor3_64(xor3_64(a, b, c), d, e); }
+
 __global__ __launch_bounds__(kBlock) void k_keccak512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   const u32 i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
@@ -399,22 +412,21 @@ __global__ __launch_bounds__(kBlock) void k_keccak512_64(u64* __restrict__ Hb, u
   A[8] = 0x8000000000000001ull;  // pad 0x01 at byte 64, 0x80 at byte 71 (rate 72)
 #pragma unroll
   for (int k = 9; k < 25; ++k) A[k] = 0;
+#pragma unroll 1
   for (int r = 0; r < 24; ++r) {
     u64 C[5], D[5], B[25];
 #pragma unroll
-    for (int x = 0; x < 5; ++x) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+    for (int x = 0; x < 5; ++x) C[x] = xor5_64(A[x], A[x + 5], A[x + 10], A[x + 15], A[x + 20]);
 #pragma unroll
     for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
 #pragma unroll
-    for (int k = 0; k < 25; ++k) A[k] ^= D[k % 5];
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(A[x + 5 * y] ^ D[x], kKeccakRot[x + 5 * y]);
 #pragma unroll
     for (int x = 0; x < 5; ++x)
 #pragma unroll
-      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64z(A[x + 5 * y], kKeccakRot[x + 5 * y]);
-#pragma unroll
-    for (int x = 0; x < 5; ++x)
-#pragma unroll
-      for (int y = 0; y < 5; ++y) A[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+      for (int y = 0; y < 5; ++y) A[x + 5 * y] = keccak_chi(B[x + 5 * y], B[(x + 1) % 5 + 5 * y], B[(x + 2) % 5 + 5 * y]);
     A[0] ^= c_keccak_rc[r];
   }
   store_hash(Hb, stride, i, A);

@@ -44,19 +44,16 @@ __device__ __forceinline__ void luffa_m2(u32 a[8]) {
   a[4] = a[3] ^ t; a[3] = a[2] ^ t; a[2] = a[1];
   a[1] = a[0] ^ t; a[0] = t;
 }
-// Bitsliced SubCrumb (4-bit S-box {13,14,0,1,5,10,7,6,11,3,9,12,15,8,2,4}, a0 = bit 0);
-// checked against the table over all 16 inputs.
-#define LUFFA_SUBCRUMB(a0, a1, a2, a3) \
-  do {                                 \
-    u32 t_ = (a0);                     \
-    (a0) |= (a1); (a2) ^= (a3);        \
-    (a1) = ~(a1); (a0) ^= (a3);        \
-    (a3) &= t_; (a1) ^= (a3);          \
-    (a3) ^= (a2); (a2) &= (a0);        \
-    (a0) = ~(a0); (a2) ^= (a1);        \
-    (a1) |= (a3); t_ ^= (a1);          \
-    (a3) ^= (a2); (a2) &= (a1);        \
-    (a1) ^= (a0); (a0) = t_;           \
+// Bitsliced SubCrumb (4-bit S-box {13,14,0,1,5,10,7,6,11,3,9,12,15,8,2,4}, a0 = bit 0) as four
+// Shannon splits on a3: y_k = a3 ? g1_k(a0,a1,a2) : g0_k(a0,a1,a2), each cofactor and the select one
+// v_bitop3: 12 VALU (the and/or/xor network is 16).
+#define LUFFA_SUBCRUMB(a0, a1, a2, a3)                                                   \
+  do {                                                                                   \
+    const u32 y0_ = bop3<0xCA>(a3, bop3<0x17>(a0, a1, a2), bop3<0x4B>(a0, a1, a2));      \
+    const u32 y1_ = bop3<0xCA>(a3, bop3<0x1B>(a0, a1, a2), bop3<0xB8>(a0, a1, a2));      \
+    const u32 y2_ = bop3<0xCA>(a3, bop3<0xC2>(a0, a1, a2), bop3<0x9B>(a0, a1, a2));      \
+    const u32 y3_ = bop3<0xCA>(a3, bop3<0x67>(a0, a1, a2), bop3<0x31>(a0, a1, a2));      \
+    (a0) = y0_; (a1) = y1_; (a2) = y2_; (a3) = y3_;                                       \
   } while (0)
 #define LUFFA_MIXWORD(u, v)          \
   do {                               \
@@ -237,7 +234,7 @@ __device__ __forceinline__ void shavite_F(const u32* T, u32 lo, u32 x[4], const 
   aes_round(T, lo, x[0], x[1], x[2], x[3]);
 }
 
-__global__ __launch_bounds__(kAesBlock) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
@@ -510,18 +507,14 @@ __device__ __forceinline__ u32 xt4(u32 x) {
 
 // One ECHO round: BIG.SubWords (two AES rounds per 128-bit word, the first keyed by the
 // running counter), BIG.ShiftRows (a renaming), BIG.MixColumns (bytewise, 4 bytes per u32).
-__device__ __forceinline__ void echo_round(const u32* T, u32 lo, u32 W[16][4], u32 k) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    aes_round_key0(T, lo, W[i][0], W[i][1], W[i][2], W[i][3], k + (u32)i);
-    aes_round(T, lo, W[i][0], W[i][1], W[i][2], W[i][3]);
-  }
+// BIG.ShiftRows + BIG.MixColumns: column c of the row-shifted state takes row rr from column
+// (c + rr) & 3; the mix is bytewise over the four 128-bit rows.
+__device__ __forceinline__ void echo_mix(u32 W[16][4]) {
   u32 N[16][4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      // column c of the row-shifted state: rows rr come from column (c + rr) & 3
       const u32 a0 = W[4 * c][w], a1 = W[4 * ((c + 1) & 3) + 1][w], a2 = W[4 * ((c + 2) & 3) + 2][w],
                 a3 = W[4 * ((c + 3) & 3) + 3][w];
       const u32 ab = a0 ^ a1, bc = a1 ^ a2, cd = a2 ^ a3, da = a3 ^ a0;
@@ -536,53 +529,76 @@ __device__ __forceinline__ void echo_round(const u32* T, u32 lo, u32 W[16][4], u
 #pragma unroll
     for (int w = 0; w < 4; ++w) W[i][w] = N[i][w];
 }
+// BIG.SubWords of word i: two AES rounds, the first keyed by the running counter k.
+__device__ __forceinline__ void echo_sub(const u32* T, u32 lo, u32 x[4], u32 k) {
+  aes_round_key0(T, lo, x[0], x[1], x[2], x[3], k);
+  aes_round(T, lo, x[0], x[1], x[2], x[3]);
+}
+__device__ __forceinline__ void echo_round(const u32* T, u32 lo, u32 W[16][4], u32 k) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) echo_sub(T, lo, W[i], k + (u32)i);
+  echo_mix(W);
+}
 
 // kSearch: compare the top 64 bits of the X11 digest (ECHO output bytes 24..31) with
 // the target and append hits to out[1..cap] (out[0] counts); otherwise write H.
+// Round 0 only transforms the four message words (the other twelve are nonce-independent:
+// x11t::ECHO_R0); in search mode round 9 only computes the two output rows the compare needs.
 template <bool kSearch>
-__global__ __launch_bounds__(kAesBlock) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
                                                           u64 target_hi, u32* __restrict__ out, u32 cap) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
-  u64 h[8];
-  load_hash(Hb, stride, i, h);
-  u32 W[16][4];
+    u64 h[8];
+    load_hash(Hb, stride, i, h);
+    u32 W[16][4];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { W[k][0] = 512u; W[k][1] = 0; W[k][2] = 0; W[k][3] = 0; }
+    for (int k = 0; k < 16; ++k)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    W[8 + k][0] = lo32(h[2 * k]); W[8 + k][1] = hi32(h[2 * k]);
-    W[8 + k][2] = lo32(h[2 * k + 1]); W[8 + k][3] = hi32(h[2 * k + 1]);
-  }
-  // padding: 0x80 at byte 64, digest size 512 at bytes 110..111, bit count 512 at 112..127
-#pragma unroll
-  for (int k = 12; k < 16; ++k) { W[k][0] = 0; W[k][1] = 0; W[k][2] = 0; W[k][3] = 0; }
-  W[12][0] = 0x80u;
-  W[14][3] = 0x02000000u;
-  W[15][0] = 512u;
-#pragma unroll 1
-  for (int r = 0; r < 10; ++r) echo_round(T, lo, W, 512u + 16u * (u32)r);
-  // V' = V ^ M ^ W[0..7] ^ W[8..15]; the digest is V'[0..3], V = {512, 0, 0, 0}.
-  if (kSearch) {
-    const u64 top = mk64(lo32(h[3]) ^ W[1][2] ^ W[9][2], hi32(h[3]) ^ W[1][3] ^ W[9][3]);
-    if (top <= target_hi) {
-      const u32 s = atomicAdd(out, 1u);
-      if (s < cap) out[1 + s] = base + i;
-    }
-  } else {
-    u64 o[8];
+      for (int w = 0; w < 4; ++w) W[k][w] = x11t::ECHO_R0[k][w];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      o[2 * k] = mk64(lo32(h[2 * k]) ^ W[k][0] ^ W[8 + k][0] ^ 512u,
-                      hi32(h[2 * k]) ^ W[k][1] ^ W[8 + k][1]);
-      o[2 * k + 1] = mk64(lo32(h[2 * k + 1]) ^ W[k][2] ^ W[8 + k][2], hi32(h[2 * k + 1]) ^ W[k][3] ^ W[8 + k][3]);
+      W[8 + k][0] = lo32(h[2 * k]); W[8 + k][1] = hi32(h[2 * k]);
+      W[8 + k][2] = lo32(h[2 * k + 1]); W[8 + k][3] = hi32(h[2 * k + 1]);
+      echo_sub(T, lo, W[8 + k], 512u + 8u + (u32)k);
     }
+    echo_mix(W);
+#pragma unroll 1
+    for (int r = 1; r < 9; ++r) echo_round(T, lo, W, 512u + 16u * (u32)r);
+    // V' = V ^ M ^ W[0..7] ^ W[8..15]; the digest is V'[0..3], V = {512, 0, 0, 0}.
+    if (kSearch) {
+      // rows W'[1] (column 0: words 0, 5, 10, 15) and W'[9] (column 2: words 8, 13, 2, 7), halves 2..3
+      constexpr u32 k9 = 512u + 16u * 9u;
+      echo_sub(T, lo, W[0], k9 + 0); echo_sub(T, lo, W[5], k9 + 5);
+      echo_sub(T, lo, W[10], k9 + 10); echo_sub(T, lo, W[15], k9 + 15);
+      echo_sub(T, lo, W[8], k9 + 8); echo_sub(T, lo, W[13], k9 + 13);
+      echo_sub(T, lo, W[2], k9 + 2); echo_sub(T, lo, W[7], k9 + 7);
+      u32 t[2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[4 + k] = 0;
-    store_hash(Hb, stride, i, o);
-  }
+      for (int w = 2; w < 4; ++w) {
+        const u32 r1 = xor3(xt4(W[5][w] ^ W[10][w]), W[0][w], W[10][w] ^ W[15][w]);   // column 0, row 1
+        const u32 r9 = xor3(xt4(W[13][w] ^ W[2][w]), W[8][w], W[2][w] ^ W[7][w]);     // column 2, row 1
+        t[w - 2] = xor3(r1, r9, w == 2 ? lo32(h[3]) : hi32(h[3]));
+      }
+      const u64 top = mk64(t[0], t[1]);
+      if (top <= target_hi) {
+        const u32 s = atomicAdd(out, 1u);
+        if (s < cap) out[1 + s] = base + i;
+      }
+    } else {
+      echo_round(T, lo, W, 512u + 16u * 9u);
+      u64 o[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[2 * k] = mk64(lo32(h[2 * k]) ^ W[k][0] ^ W[8 + k][0] ^ 512u, hi32(h[2 * k]) ^ W[k][1] ^ W[8 + k][1]);
+        o[2 * k + 1] = mk64(lo32(h[2 * k + 1]) ^ W[k][2] ^ W[8 + k][2], hi32(h[2 * k + 1]) ^ W[k][3] ^ W[8 + k][3]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[4 + k] = 0;
+      store_hash(Hb, stride, i, o);
+    }
   }
 }
 
