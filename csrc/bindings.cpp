@@ -179,6 +179,7 @@ PYBIND11_MODULE(_native, m) {
     x11::stage(i, reinterpret_cast<const uint8_t*>(s.data()), s.size(), o);
     return to_bytes(o, 64);
   }, py::arg("stage"), py::arg("msg"));
+  m.def("x11_luffa_sbox_selfcheck", &x11::luffa_sbox_selfcheck);
   m.def("cpu_scan_sha256d", [](const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     std::vector<uint32_t> hits;

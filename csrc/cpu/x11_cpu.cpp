@@ -39,6 +39,7 @@ static inline void st32be(u8* p, u32 v) { for (int i = 3; i >= 0; --i) { p[i] = 
 static u8 SBOX[256];
 static bool sbox_ready = false;
 static inline u8 rotl8(u8 x, int n) { return (u8)((x << n) | (x >> (8 - n))); }
+static void init_gmul();
 static void init_sbox_impl() {
     if (sbox_ready) return;
     u8 p = 1, q = 1;
@@ -49,6 +50,7 @@ static void init_sbox_impl() {
         SBOX[p] = (u8)(q ^ rotl8(q, 1) ^ rotl8(q, 2) ^ rotl8(q, 3) ^ rotl8(q, 4) ^ 0x63);
     } while (p != 1);
     SBOX[0] = 0x63;
+    init_gmul();
     sbox_ready = true;
 }
 // Thread-safe one-time init (miner threads verify shares concurrently).
@@ -59,6 +61,11 @@ static inline u8 gmul(u8 a, u8 b) {
     u8 r = 0;
     while (b) { if (b & 1) r ^= a; a = xt(a); b >>= 1; }
     return r;
+}
+static u8 GMUL[8][256];  // GMUL[c][x] = c * x in GF(2^8), c < 8 (filled with the S-box)
+static void init_gmul() {
+    for (int c = 0; c < 8; ++c)
+        for (int x = 0; x < 256; ++x) GMUL[c][x] = gmul((u8)x, (u8)c);
 }
 // One AES round on a 16-byte column-major state, round key k (null = 0).
 static void aes_round(u8 s[16], const u8* k) {
@@ -312,7 +319,7 @@ static void groestl_perm(u8 a[128], bool q) {
         for (int j = 0; j < 16; ++j)
             for (int i = 0; i < 8; ++i) {
                 u8 s = 0;
-                for (int k = 0; k < 8; ++k) s ^= gmul(t[j * 8 + k], MB[(k - i + 8) & 7]);
+                for (int k = 0; k < 8; ++k) s ^= GMUL[MB[(k - i + 8) & 7]][t[j * 8 + k]];
                 a[j * 8 + i] = s;
             }
     }
@@ -443,18 +450,23 @@ int jh_perm_dest(int k, int dim) {
     return k;
 }
 // Round R_d on 2^d elements with constant bits cb[2^d].
+static u8 JH_P8[256];  // jh_perm_dest(i, 8), tabulated with the round constants
 static void jh_round(u8* e, int dim, const u8* cb) {
     int n = 1 << dim;
     for (int i = 0; i < n; ++i) e[i] = JH_S[cb[i]][e[i]];
     for (int i = 0; i < n; i += 2) jh_L(e[i], e[i + 1]);
     u8 t[256];
-    for (int i = 0; i < n; ++i) t[jh_perm_dest(i, dim)] = e[i];
+    if (dim == 8)
+        for (int i = 0; i < n; ++i) t[JH_P8[i]] = e[i];
+    else
+        for (int i = 0; i < n; ++i) t[jh_perm_dest(i, dim)] = e[i];
     memcpy(e, t, n);
 }
 static u8 JH_C[42][256];  // round-constant bits, one per element
 static bool jh_ready = false;
 static void jh_init_constants_impl() {
     if (jh_ready) return;
+    for (int i = 0; i < 256; ++i) JH_P8[i] = (u8)jh_perm_dest(i, 8);
     // C0 = first 256 bits of the fractional part of sqrt(2)
     static const u8 C0[32] = {0x6a, 0x09, 0xe6, 0x67, 0xf3, 0xbc, 0xc9, 0x08, 0xb2, 0xfb, 0x13, 0x66, 0xea, 0x95, 0x7d, 0x3e,
                               0x3a, 0xde, 0xc1, 0x75, 0x12, 0x77, 0x50, 0x99, 0xda, 0x2f, 0x59, 0x0b, 0x06, 0x67, 0x32, 0x2a};
@@ -589,7 +601,8 @@ static inline void luffa_m2(u32 a[8]) {
 }
 static const u8 LUFFA_SBOX[16] = {13, 14, 0, 1, 5, 10, 7, 6, 11, 3, 9, 12, 15, 8, 2, 4};
 // SubCrumb on four words (x0 = least significant bit of each crumb).
-static void luffa_subcrumb(u32& x0, u32& x1, u32& x2, u32& x3) {
+// Table form (the definition) and the Luffa authors' bitsliced form; luffa_sbox_selfcheck() ties them.
+static void luffa_subcrumb_table(u32& x0, u32& x1, u32& x2, u32& x3) {
     u32 y0 = 0, y1 = 0, y2 = 0, y3 = 0;
     for (int l = 0; l < 32; ++l) {
         int v = (int)(((x3 >> l) & 1) << 3 | ((x2 >> l) & 1) << 2 | ((x1 >> l) & 1) << 1 | ((x0 >> l) & 1));
@@ -598,6 +611,25 @@ static void luffa_subcrumb(u32& x0, u32& x1, u32& x2, u32& x3) {
         y2 |= (u32)((s >> 2) & 1) << l; y3 |= (u32)((s >> 3) & 1) << l;
     }
     x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+}
+static inline void luffa_subcrumb(u32& a0, u32& a1, u32& a2, u32& a3) {
+    u32 t = a0;
+    a0 |= a1; a2 ^= a3; a1 = ~a1; a0 ^= a3; a3 &= t; a1 ^= a3; a3 ^= a2; a2 &= a0;
+    a0 = ~a0; a2 ^= a1; a1 |= a3; t ^= a1; a3 ^= a2; a2 &= a1; a1 ^= a0; a0 = t;
+}
+bool luffa_sbox_selfcheck() {
+    u32 seed = 0x12345678u;
+    for (int t = 0; t < 80; ++t) {  // t < 16: input t in every bit lane; then pseudo-random words
+        u32 a[4], b[4];
+        for (int k = 0; k < 4; ++k) {
+            seed = seed * 1664525u + 1013904223u;
+            a[k] = b[k] = t < 16 ? (((t >> k) & 1) ? 0xFFFFFFFFu : 0u) : seed;
+        }
+        luffa_subcrumb_table(a[0], a[1], a[2], a[3]);
+        luffa_subcrumb(b[0], b[1], b[2], b[3]);
+        for (int k = 0; k < 4; ++k) if (a[k] != b[k]) return false;
+    }
+    return true;
 }
 static inline void luffa_mixword(u32& u, u32& v) {
     v ^= u;
@@ -809,11 +841,16 @@ static int simd_pow(int b, int e) {
 }
 int simd_root = 41;  // evaluation root of the message NTT (self-test knob)
 static void simd_expand(const u8 blk[128], bool final, int q[256]) {
+    // y_i = sum_j blk_j root^(ij); root^256 = 1 (Fermat), so the exponent is taken mod 256.
+    int pr[256], p41[256];
+    pr[0] = p41[0] = 1;
+    for (int k = 1; k < 256; ++k) { pr[k] = pr[k - 1] * mod257(simd_root) % 257; p41[k] = p41[k - 1] * 41 % 257; }
     for (int i = 0; i < 256; ++i) {
-        int a = simd_pow(simd_root, i), acc = 0, p = 1;
-        for (int j = 0; j < 128; ++j) { acc = (acc + blk[j] * p) % 257; p = p * a % 257; }
-        int tw = simd_pow(41, (255 * i) % 256);
-        if (final) tw += simd_pow(41, (253 * i) % 256);
+        int acc = 0;  // < 128 * 255 * 256
+        for (int j = 0; j < 128; ++j)
+            if (blk[j]) acc += blk[j] * pr[(i * j) & 255];
+        int tw = p41[(255 * i) % 256];
+        if (final) tw += p41[(253 * i) % 256];
         int v = mod257(acc + tw);
         q[i] = v <= 128 ? v : v - 257;
     }

@@ -12,6 +12,8 @@ namespace x11 {
 void x11(const uint8_t* msg, size_t len, uint8_t out[32], uint8_t* trace);
 // Stage i (0 = BLAKE-512 ... 10 = ECHO-512) of the chain on an arbitrary message.
 void stage(int i, const uint8_t* msg, size_t len, uint8_t out[64]);
+// The bitsliced Luffa SubCrumb used by the chain equals the S-box table (all inputs, every bit lane).
+bool luffa_sbox_selfcheck();
 }  // namespace x11
 
 constexpr int kX11StageCount = 11;

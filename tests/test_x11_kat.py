@@ -49,3 +49,41 @@ def test_x11_not_offered_without_a_passing_kat():
         pytest.skip("x11 not implemented (docs/PARITY.md K6)")
     digest = algo.hash(bytes.fromhex(KAT["header_hex"]))
     assert digest[::-1].hex() == KAT["x11_hash_display"]
+
+
+def test_x11_cpu_chain_trace_regression_pins():
+    """Every intermediate digest of the CPU chain on the genesis header (regression pins; only the final digest
+    is independently known, so a change here must come with the genesis test still passing)."""
+    from otedama_amd.ops.native import load
+
+    n = load(build_if_missing=False)
+    if n is None:
+        pytest.skip("native extension not built")
+    pins = json.loads((Path(__file__).parent / "fixtures" / "x11_genesis_trace.json").read_text())
+    trace = n.x11_trace(bytes.fromhex(pins["header_hex"]))
+    for i, (name, want) in enumerate(pins["stages"].items()):
+        assert trace[64 * i : 64 * i + 64].hex() == want, name
+    assert trace[640:672][::-1].hex() == KAT["x11_hash_display"]
+
+
+def test_x11_stage_functions_accept_any_length():
+    """Each stage is a full hash (padding for any length), not only the 64-byte chain step."""
+    from otedama_amd.ops.native import load
+
+    n = load(build_if_missing=False)
+    if n is None:
+        pytest.skip("native extension not built")
+    for st in range(11):
+        outs = {n.x11_stage(st, bytes(range(256))[:L]) for L in (0, 1, 63, 64, 65, 127, 128, 129, 200)}
+        assert len(outs) == 9 and all(len(o) == 64 for o in outs)
+    with pytest.raises(ValueError):
+        n.x11_stage(11, b"")
+
+
+def test_x11_cpu_luffa_bitsliced_sbox_matches_table():
+    from otedama_amd.ops.native import load
+
+    n = load(build_if_missing=False)
+    if n is None:
+        pytest.skip("native extension not built")
+    assert n.x11_luffa_sbox_selfcheck()
