@@ -60,6 +60,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
+    ap.add_argument("--sha-variants", type=int, default=4,
+                    help="BIP320 version variants per SHA-256d launch sharing the block-2 schedule (1 = single midstate)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
@@ -68,7 +70,7 @@ def main() -> int:
     args = ap.parse_args()
 
     from otedama_amd.ops import native
-    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch
+    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, Sha256dSearchK
     from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
     from otedama_amd.utils.trace import span
 
@@ -83,17 +85,21 @@ def main() -> int:
 
     job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1
     stripe = stripe_for(info.rank, info.world_size)
-    search = Sha256dSearch(dev, grid=args.grid or None)
+    K = max(1, min(args.sha_variants, N.SHA256D_MAX_K))
+    search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
     world = info.world_size
-    gathered = torch.zeros(world, 1 + search.cap, dtype=torch.int32, device=dev)
+    slot_words = 1 + (2 if K > 1 else 1) * search.cap
+    gathered = torch.zeros(world, slot_words, dtype=torch.int32, device=dev)
     counters_hashes = 0
 
-    def variant_params(step: int) -> tuple[bytes, bytes]:
-        v = stripe.start + step * stripe.stride
-        hdr, _ver, _nt, _en2 = N.variant_header(job, v)
-        return hdr, N.sha256d_prepare(hdr, job["target"])
+    def variant_params(step: int) -> tuple[list[bytes], bytes]:
+        # step i of this rank: stripe positions K*i .. K*i + K-1 (version-rolled headers, identical block 2)
+        hdrs = [N.variant_header(job, stripe.start + (step * K + j) * stripe.stride)[0] for j in range(K)]
+        if K > 1:
+            return hdrs, N.sha256d_prepare_k(hdrs, job["target"])
+        return hdrs, N.sha256d_prepare(hdrs[0], job["target"])
 
-    hits_log: list[tuple[bytes, torch.Tensor]] = []
+    hits_log: list[tuple[list[bytes], torch.Tensor]] = []
 
     def step(i: int, record: bool) -> None:
         with span("otd.bench.sha256d_step"):
@@ -109,7 +115,7 @@ def main() -> int:
             comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered.view(-1), r.buf.view(-1)))
         else:
             gathered[0].copy_(r.buf)
-        counters_hashes += 1 << 32
+        counters_hashes += K << 32
         if record:
             hits_log.append((hdr, gathered[info.rank].clone()))
 
@@ -121,7 +127,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, True)
-    total = comm.allreduce_counters(args.steps << 32)[0] if world > 1 else args.steps << 32  # R3
+    total = comm.allreduce_counters((args.steps * K) << 32)[0] if world > 1 else (args.steps * K) << 32  # R3
     torch.cuda.synchronize(dev)
     barrier(info)
     torch.cuda.synchronize(dev)
@@ -130,12 +136,16 @@ def main() -> int:
 
     # Re-verify every hit of the timed region on the CPU (full 256-bit compare).
     found = verified = 0
-    for hdr, buf in hits_log:
+    for hdrs, buf in hits_log:
         host = buf.cpu().tolist()
         n = min(host[0] & 0xFFFFFFFF, search.cap)
-        for nonce in host[1 : 1 + n]:
+        pairs = [(host[1 + 2 * i], host[2 + 2 * i]) for i in range(n)] if K > 1 else [(x, 0) for x in host[1 : 1 + n]]
+        for nonce, vi in pairs:
             nonce &= 0xFFFFFFFF
             found += 1
+            if not 0 <= vi < K:
+                continue
+            hdr = hdrs[vi]
             h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
             if int.from_bytes(h, "little") <= int.from_bytes(job["target"], "little"):
                 verified += 1
@@ -239,10 +249,12 @@ def main() -> int:
             "data": "synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1",
             "config": {
                 "model": "sha256d",
-                "global_batch": (1 << 32) * world,
+                "global_batch": (K << 32) * world,
                 "seq_len": 80,
-                "parallelism": f"dp{world} (nonce-space: per-rank variant stripe, full 2^32 nonces per step)",
-                "algorithm": "SHA-256d nonce search, fixed midstate per variant",
+                "parallelism": f"dp{world} (nonce-space: per-rank variant stripe, full 2^32 nonces per variant per step)",
+                "algorithm": ("SHA-256d nonce search, fixed midstate per variant; "
+                              f"{K} BIP320 version variants per launch share the block-2 message schedule"),
+                "variants_per_step": K,
                 "grid": search.grid,
             },
             "sha256d_hashes_per_sec": sha_hps,

@@ -22,6 +22,8 @@ using namespace otedama;
 namespace otedama {
 void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                        uintptr_t stream);
+void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
+                         uintptr_t stream);
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
 void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
@@ -210,6 +212,18 @@ PYBIND11_MODULE(_native, m) {
     sha256d_prepare(reinterpret_cast<const uint8_t*>(hs.data()), reinterpret_cast<const uint8_t*>(ts.data()), &p);
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   });
+  m.attr("SHA256D_MAX_K") = kSha256dMaxK;
+  m.def("sha256d_prepare_k", [](const py::list& headers, const py::bytes& t) {
+    std::string ts = need(t, 32, "target");
+    std::vector<std::string> hs;
+    for (auto& h : headers) hs.push_back(need(h.cast<py::bytes>(), 80, "header"));
+    std::vector<const uint8_t*> ptrs;
+    for (auto& h : hs) ptrs.push_back(reinterpret_cast<const uint8_t*>(h.data()));
+    Sha256dParamsK p;
+    if (!sha256d_prepare_k(ptrs.data(), (int)ptrs.size(), reinterpret_cast<const uint8_t*>(ts.data()), &p))
+      throw std::invalid_argument("need 2..SHA256D_MAX_K headers with identical bytes 64..75");
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
+  }, py::arg("headers"), py::arg("target"));
   m.def("scrypt_prepare", [](const py::bytes& h, const py::bytes& t) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     ScryptParams p;
@@ -239,6 +253,16 @@ PYBIND11_MODULE(_native, m) {
     if (count == 0 || count > (1ull << 32)) throw std::invalid_argument("count must be in [1, 2^32]");
     if (grid <= 0 || out == 0) throw std::invalid_argument("bad grid / out");
     py_launch_sha256d(p, base, count, out, cap, grid, stream);
+  }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
+     py::arg("stream"));
+  m.def("launch_sha256d_k", [](const py::bytes& params, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap,
+                               int grid, uintptr_t stream) {
+    std::string ps = need(params, sizeof(Sha256dParamsK), "params");
+    Sha256dParamsK p; std::memcpy(&p, ps.data(), sizeof p);
+    if (p.k < 2 || p.k > kSha256dMaxK) throw std::invalid_argument("bad K");
+    if (count == 0 || count > (1ull << 32)) throw std::invalid_argument("count must be in [1, 2^32]");
+    if (grid <= 0 || out == 0) throw std::invalid_argument("bad grid / out");
+    py_launch_sha256d_k(p, base, count, out, cap, grid, stream);
   }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
      py::arg("stream"));
   m.def("launch_scrypt", [](const py::bytes& params, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch,
@@ -288,8 +312,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("device_id", &MinerBase::device_id);
 
   py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")
-      .def(py::init<int, std::string, uint64_t, int, size_t>(), py::arg("device"), py::arg("device_id"),
-           py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024);
+      .def(py::init<int, std::string, uint64_t, int, size_t, int>(), py::arg("device"), py::arg("device_id"),
+           py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024,
+           py::arg("sha_variants") = 4);
   py::class_<CpuMiner, MinerBase, std::shared_ptr<CpuMiner>>(m, "CpuMiner")
       .def(py::init<int, std::string, size_t>(), py::arg("threads"), py::arg("device_id") = "cpu-0",
            py::arg("queue_cap") = 1024);

@@ -52,6 +52,27 @@ void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], Scry
 
 namespace otedama {
 
+bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t target32[32], Sha256dParamsK* out) {
+  if (k < 2 || k > kSha256dMaxK) return false;
+  for (int v = 1; v < k; ++v)
+    for (int i = 64; i < 76; ++i)
+      if (headers80[v][i] != headers80[0][i]) return false;
+  for (int v = 0; v < k; ++v) {
+    Sha256dParams p;
+    sha256d_prepare(headers80[v], target32, &p);
+    if (v == 0) {
+      out->w0 = p.w0; out->w1 = p.w1; out->w2 = p.w2; out->w16 = p.w16; out->w17 = p.w17;
+      out->target_hi = p.target_hi;
+    }
+    for (int i = 0; i < 8; ++i) { out->var[v].mid[i] = p.mid[i]; out->var[v].st3[i] = p.st3[i]; }
+    out->var[v].pre3 = p.pre3;
+    out->var[v].t2_3 = p.t2_3;
+  }
+  for (int v = k; v < kSha256dMaxK; ++v) out->var[v] = out->var[0];
+  out->k = k;
+  return true;
+}
+
 void x11_prepare(const uint8_t header80[80], const uint8_t target32[32], X11Params* p) {
   for (int k = 0; k < 9; ++k) p->m[k] = (uint64_t(load_be32(header80 + 8 * k)) << 32) | load_be32(header80 + 8 * k + 4);
   p->m9_hi = uint64_t(load_be32(header80 + 72)) << 32;

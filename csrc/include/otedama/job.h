@@ -25,6 +25,25 @@ struct Sha256dParams {
 // and a 32-byte little-endian target.
 void sha256d_prepare(const uint8_t header80[80], const uint8_t target32[32], Sha256dParams* out);
 
+// K (2..4) header variants with identical bytes 64..79 (block 2 of the first hash: merkle tail,
+// ntime, nbits, nonce) and different block 1 (BIP320 version rolling): one shared block-2 message
+// schedule per nonce, K midstates (sha256d_search_k).
+constexpr int kSha256dMaxK = 4;
+struct Sha256dVariant {
+  uint32_t mid[8];
+  uint32_t st3[8];
+  uint32_t pre3, t2_3;
+};
+struct Sha256dParamsK {
+  uint32_t w0, w1, w2, w16, w17;
+  uint32_t target_hi;
+  int32_t k;
+  Sha256dVariant var[kSha256dMaxK];
+};
+// Returns false (and leaves *out undefined) unless 2 <= k <= kSha256dMaxK and every header has the
+// same bytes 64..75.
+bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t target32[32], Sha256dParamsK* out);
+
 // Scrypt (N, r=1, p=1) job parameters: the 76-byte header prefix; the nonce is
 // appended per lane as bytes 76..79.
 // The HMAC key is the whole 80-byte header (> 64 B, so K' = SHA-256(header)),

@@ -125,7 +125,8 @@ class MinerBase {
 // One host thread per GPU: double-buffered batches on a private HIP stream.
 class GpuMiner : public MinerBase {
  public:
-  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap);
+  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling), 1..4.
+  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 4);
   ~GpuMiner() override;
   void start() override;
   void stop() override;
@@ -134,6 +135,8 @@ class GpuMiner : public MinerBase {
   int device_;
   uint64_t batch_;
   int grid_;
+  int sha_k_;
+  int grid_k_ = 0;
   std::thread th_;
 };
 

@@ -24,6 +24,8 @@ namespace otedama {
 
 hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, uint32_t* out,
                                  uint32_t cap, int grid, hipStream_t stream);
+hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
+                                   int grid, hipStream_t stream);
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
                                 int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
 uint64_t scrypt_scratch_bytes(int grid, int gap);
@@ -46,17 +48,18 @@ struct Slot {
   bool busy = false;
   std::shared_ptr<const JobTemplate> job;
   uint64_t gen = 0;
-  uint64_t variant = 0;
-  uint64_t count = 0;
-  uint8_t header[80];
-  uint32_t version = 0, ntime = 0;
-  uint64_t en2 = 0;
+  uint64_t count = 0;  // nonces per variant
+  int nvar = 1;        // > 1: K-variant SHA-256d launch, hits carry the variant index
+  uint8_t header[kSha256dMaxK][80];
+  uint32_t version[kSha256dMaxK] = {0}, ntime[kSha256dMaxK] = {0};
+  uint64_t en2[kSha256dMaxK] = {0};
   TraceId range = 0;  // roctx: enqueue -> host verification of this batch
 };
 }  // namespace
 
-GpuMiner::GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap)
-    : MinerBase(std::move(device_id), queue_cap), device_(device), batch_(batch_nonces), grid_(grid) {
+GpuMiner::GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants)
+    : MinerBase(std::move(device_id), queue_cap), device_(device), batch_(batch_nonces), grid_(grid),
+      sha_k_(sha_variants < 1 ? 1 : sha_variants > kSha256dMaxK ? kSha256dMaxK : sha_variants) {
   if (batch_ == 0 || batch_ > (1ull << 32)) batch_ = 1ull << 30;
   // Batches must tile the 2^32 nonce range exactly.
   while ((1ull << 32) % batch_) --batch_;
@@ -127,6 +130,9 @@ void GpuMiner::loop() {
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
   // X11: eleven stage kernels per batch over a 64 B/nonce digest buffer (512 MiB at 2^23).
   const uint32_t x11_batch = 1u << 23;
+  // K-variant SHA-256d kernel: 4 waves/SIMD (K states per lane), best at 8 blocks of 256 per CU
+  // (tools/bench_sha_k.py: K=4 18.3 GH/s vs 16.3 single-midstate).
+  grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 8;
 
   uint64_t cur_gen = ~0ull;
   uint64_t k = 0;       // variant-stripe position
@@ -142,23 +148,25 @@ void GpuMiner::loop() {
     const uint32_t n = s.h_out[0] < kHitCap ? s.h_out[0] : kHitCap;
     TraceScope verify_scope("otd.verify_candidates");
     uint64_t good = 0, bad = 0;
-    const bool multi = false;
+    const bool multi = s.nvar > 1;
     for (uint32_t i = 0; i < n; ++i) {
       const uint32_t nonce = multi ? s.h_out[1 + 2 * i] : s.h_out[1 + i];
+      const uint32_t vi = multi ? s.h_out[2 + 2 * i] : 0u;
+      if (vi >= (uint32_t)s.nvar) { ++bad; continue; }
       uint8_t hdr[80];
-      std::memcpy(hdr, s.header, 80);
+      std::memcpy(hdr, s.header[vi], 80);
       store_le32(hdr + 76, nonce);
       ShareRecord r{};
       if (!verify_share(s.job->algo, hdr, s.job->target, r.hash)) { ++bad; continue; }
       r.epoch = s.job->epoch; r.job_id = s.job->job_id; r.channel_id = s.job->channel_id;
-      r.nonce = nonce; r.ntime = s.ntime; r.version = s.version; r.extranonce2 = s.en2;
+      r.nonce = nonce; r.ntime = s.ntime[vi]; r.version = s.version[vi]; r.extranonce2 = s.en2[vi];
       r.extranonce2_size = s.job->extranonce2_size; r.device_id = device_id_;
       r.found_at = monotonic_seconds();
       queue_.push(std::move(r));
       ++good;
     }
     std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.hashes += s.count;
+    stats_.hashes += s.count * (uint64_t)s.nvar;
     stats_.candidates += s.h_out[0];
     stats_.shares += good;
     stats_.rejected_candidates += bad;
@@ -186,8 +194,21 @@ void GpuMiner::loop() {
     finish(s);  // slot reuse: make sure its previous batch is consumed
     s.job = job;
     s.gen = gen;
-    s.variant = v;
-    job->variant_header(v, s.header, &s.version, &s.ntime, &s.en2);
+    s.nvar = 1;
+    job->variant_header(v, s.header[0], &s.version[0], &s.ntime[0], &s.en2[0]);
+    if (job->algo == Algo::kSha256d && sha_k_ > 1) {
+      // Group the next stripe positions whose headers differ only in block 1 (version rolling): they share
+      // the block-2 message schedule in sha256d_search_k. Stops at the first one that differs in 64..75.
+      int kv = 1;
+      while (kv < sha_k_) {
+        const uint64_t vk = job->variant_start + (k + kv) * job->variant_stride;
+        if (vk >= job->variant_space()) break;
+        job->variant_header(vk, s.header[kv], &s.version[kv], &s.ntime[kv], &s.en2[kv]);
+        if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
+        ++kv;
+      }
+      s.nvar = kv;
+    }
     s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch"
                           : job->algo == Algo::kX11  ? "otd.x11.batch"
                                                      : "otd.sha256d.batch");
@@ -199,7 +220,7 @@ void GpuMiner::loop() {
         OTD_HIP(hipMalloc(&xbuf, uint64_t(scrypt_batch) * 128));
       }
       ScryptParams p;
-      scrypt_prepare(s.header, job->target, &p);
+      scrypt_prepare(s.header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = remaining < scrypt_batch ? remaining : scrypt_batch;
       OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, s.d_out,
@@ -207,21 +228,29 @@ void GpuMiner::loop() {
     } else if (job->algo == Algo::kX11) {
       if (!x11_h) OTD_HIP(hipMalloc(&x11_h, uint64_t(x11_batch) * 64));
       X11Params p;
-      x11_prepare(s.header, job->target, &p);
+      x11_prepare(s.header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = remaining < x11_batch ? remaining : x11_batch;
       OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), s.d_out, kHitCap, stream));
+    } else if (s.nvar > 1) {
+      Sha256dParamsK p;
+      const uint8_t* hs[kSha256dMaxK];
+      for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
+      if (!sha256d_prepare_k(hs, s.nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
+      s.count = batch_;
+      OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_k_, stream));
     } else {
       Sha256dParams p;
-      sha256d_prepare(s.header, job->target, &p);
+      sha256d_prepare(s.header[0], job->target, &p);
       s.count = batch_;
       OTD_HIP(launch_sha256d_search(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_, stream));
     }
-    OTD_HIP(hipMemcpyAsync(s.h_out, s.d_out, (1 + kHitCap) * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    OTD_HIP(hipMemcpyAsync(s.h_out, s.d_out, (1 + (s.nvar > 1 ? 2 : 1) * kHitCap) * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, stream));
     OTD_HIP(hipEventRecord(s.done, stream));
     s.busy = true;
     nonce_off += s.count;
-    if (nonce_off >= (1ull << 32)) { nonce_off = 0; ++k; }
+    if (nonce_off >= (1ull << 32)) { nonce_off = 0; k += (uint64_t)s.nvar; }
     which ^= 1;
     finish(slots[which]);  // consume the previous batch while this one runs
   }
@@ -237,6 +266,12 @@ void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, ui
                        uintptr_t stream) {
   OTD_HIP(launch_sha256d_search(p, base, count, reinterpret_cast<uint32_t*>(out), cap, grid,
                                 reinterpret_cast<hipStream_t>(stream)));
+}
+
+void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
+                         uintptr_t stream) {
+  OTD_HIP(launch_sha256d_search_k(p, base, count, reinterpret_cast<uint32_t*>(out), cap, grid,
+                                  reinterpret_cast<hipStream_t>(stream)));
 }
 
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,

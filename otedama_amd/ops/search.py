@@ -21,6 +21,7 @@ from otedama_amd.ops.native import require_native
 # Blocks of 256 lanes per CU that stay resident for the SHA-256d kernel
 # (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
 SHA256D_BLOCKS_PER_CU = 6
+SHA256D_K_BLOCKS_PER_CU = 8  # K-variant kernel: 99-121 VGPRs (4 waves/SIMD); grid sweep 4/6/8 per CU: 18.0/18.2/18.3 GH/s
 SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
 
 
@@ -77,6 +78,56 @@ class Sha256dSearch:
         r = self.launch(self.prepare(header80, target32), base, count)
         torch.cuda.synchronize(self.device)
         return r.nonces()
+
+
+@dataclass
+class SearchResultK:
+    buf: torch.Tensor  # int32 [1 + 2*cap]: count, (nonce, variant) pairs
+    cap: int
+
+    def count(self) -> int:
+        return int(self.buf[0].item()) & 0xFFFFFFFF
+
+    def hits(self) -> list[tuple[int, int]]:
+        host = self.buf.cpu().tolist()
+        n = min(host[0] & 0xFFFFFFFF, self.cap)
+        return [(host[1 + 2 * i] & 0xFFFFFFFF, host[2 + 2 * i]) for i in range(n)]
+
+
+class Sha256dSearchK:
+    """SHA-256d over K header variants at once (BIP320 version rolling): the variants share block 2 of the
+    first hash (bytes 64..79), so each lane computes that message schedule once for K midstates."""
+
+    def __init__(self, device="cuda:0", k: int = 4, cap: int = 1024, grid: int | None = None):
+        self.native = require_native()
+        if not 2 <= k <= self.native.SHA256D_MAX_K:
+            raise ValueError(f"k must be in [2, {self.native.SHA256D_MAX_K}]")
+        self.k = k
+        self.device = torch.device(device)
+        self.cap = cap
+        self.grid = grid or default_grid(self.device, SHA256D_K_BLOCKS_PER_CU)
+        self.out = torch.zeros(1 + 2 * cap, dtype=torch.int32, device=self.device)
+
+    def prepare(self, headers: list[bytes], target32: bytes) -> bytes:
+        if len(headers) != self.k:
+            raise ValueError(f"need exactly {self.k} headers")
+        return self.native.sha256d_prepare_k(list(headers), target32)
+
+    def launch(self, params: bytes, base: int = 0, count: int = 1 << 32, out: torch.Tensor | None = None,
+               stream: torch.cuda.Stream | None = None) -> SearchResultK:
+        out = self.out if out is None else out
+        if out.numel() < 1 + 2 * self.cap or out.dtype != torch.int32 or out.device != self.device:
+            raise ValueError("out must be an int32 tensor of >= 1+2*cap elements on the search device")
+        stream = stream or torch.cuda.current_stream(self.device)
+        out[:1].zero_()
+        self.native.launch_sha256d_k(params, base & 0xFFFFFFFF, int(count), out.data_ptr(), self.cap, self.grid,
+                                     stream.cuda_stream)
+        return SearchResultK(out, self.cap)
+
+    def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:
+        r = self.launch(self.prepare(headers, target32), base, count)
+        torch.cuda.synchronize(self.device)
+        return r.hits()
 
 
 class ScryptSearch:

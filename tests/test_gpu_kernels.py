@@ -233,3 +233,24 @@ def test_gpu_fault_retires_device_and_survivor_takes_the_stripe():
         assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
     assert not ms.device_stats()["gpu-0"]["faulted"]
     assert any("re-split" in m for m in logs)
+
+
+@pytest.mark.parametrize("k", [2, 3, 4])
+def test_sha256d_k_variants_match_cpu(k):
+    """K BIP320 version variants sharing block 2: every variant's hits equal the CPU scan of its own header."""
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import Sha256dSearchK
+
+    rng = __import__("random").Random(100 + k)
+    tail = bytes(rng.getrandbits(8) for _ in range(76))
+    headers = [struct.pack("<I", 0x20000000 | (v << 13)) + tail[4:] + bytes(4) for v in range(k)]
+    target_int = (1 << 248) - 1
+    s = Sha256dSearchK("cuda:0", k=k, cap=4096)
+    base = rng.getrandbits(32) & ~0xFFFF
+    got = s.search(headers, int_to_hash(target_int), base, 1 << 16)
+    N = _native()
+    for v in range(k):
+        ref = sorted(N.cpu_scan_sha256d(headers[v], int_to_hash(target_int), base, 1 << 16))
+        assert sorted(n for n, vv in got if vv == v) == ref and len(ref) > 100
+    with pytest.raises(ValueError):
+        s.prepare([headers[0]] * (k - 1), bytes(32))
