@@ -237,7 +237,9 @@ void GpuMiner::loop() {
       const uint8_t* hs[kSha256dMaxK];
       for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
       if (!sha256d_prepare_k(hs, s.nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
-      s.count = batch_;
+      // Keep one launch's duration (job-switch latency) independent of K: nonces per
+      // variant = batch / 2 or / 4 (batch is a power of two that tiles 2^32, so this still tiles it).
+      s.count = batch_ >= 4 ? batch_ / (s.nvar == 2 ? 2 : 4) : batch_;
       OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_k_, stream));
     } else {
       Sha256dParams p;
