@@ -55,6 +55,7 @@ def _metric(body: str, name: str, labels: str = "") -> float | None:
 @pytest.mark.parametrize("algorithm,difficulty,min_hashrate", [
     ("sha256d", 0.25, 1e9),   # ~16 GH/s per GPU: ~15 shares/s before vardiff settles
     ("scrypt", 16.0, 1e6),    # ~16.7 MH/s per GPU, scrypt diff1 = 0xffff << 224: ~16 shares/s
+    ("x11", 0.005, 1e8),      # ~380 MH/s per GPU, Bitcoin diff1: ~18 shares/s, validated by the pool's CPU chain
 ])
 def test_cli_run_mines_against_local_pool(tmp_path, algorithm, difficulty, min_hashrate):
     with _PoolThread(difficulty, algorithm) as pool:
