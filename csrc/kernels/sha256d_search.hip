@@ -99,29 +99,6 @@ extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search(
   }
 }
 
-// Multi-variant launch: blockIdx.y selects a job variant (version / ntime /
-// extranonce2 roll), each with its own folded params; hits carry the variant.
-// out[0]: count; out[1 + 2*i] = nonce, out[2 + 2*i] = variant index.
-extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search_multi(
-    const otedama::Sha256dParams* __restrict__ params, uint32_t base, uint64_t count,
-    uint32_t* __restrict__ out, uint32_t cap) {
-  const otedama::Sha256dParams p = params[blockIdx.y];
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint64_t off = tid; off < count; off += stride) {
-    const uint32_t nonce = base + static_cast<uint32_t>(off);
-    const uint32_t w3 = __builtin_bswap32(nonce);
-    const uint32_t h7 = sha256d_h7(p, w3);
-    if (__builtin_bswap32(h7) <= p.target_hi) {
-      const uint32_t slot = atomicAdd(out, 1u);
-      if (slot < cap) {
-        out[1 + 2 * slot] = nonce;
-        out[2 + 2 * slot] = blockIdx.y;
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------- K-variant search
 // K header variants that differ only in block 1 (BIP320 version rolling; SV2 standard channels) share
 // block 2 of the first hash — merkle tail, ntime, nbits, nonce — so they share its message schedule
@@ -226,14 +203,6 @@ hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint6
     case 4: hipLaunchKernelGGL(otd_sha256d_search_k<4>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_sha256d_search_multi(const Sha256dParams* d_params, int nvariants, uint32_t base,
-                                       uint64_t count, uint32_t* out, uint32_t cap, int grid,
-                                       hipStream_t stream) {
-  hipLaunchKernelGGL(otd_sha256d_search_multi, dim3(grid, nvariants), dim3(256), 0, stream, d_params,
-                     base, count, out, cap);
   return hipGetLastError();
 }
 
