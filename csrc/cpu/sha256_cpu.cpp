@@ -105,6 +105,62 @@ static void sha256_compress_shani(uint32_t state[8], const uint8_t block[64]) {
   _mm_storeu_si128((__m128i*)&state[4], STATE1);
 }
 
+// N independent compressions interleaved (N = 2): sha256rnds2 is latency-bound in a single chain
+// (each pair of rounds depends on the previous one), so two nonces in flight roughly double the
+// per-core SHA-256d rate of the CPU miner. Same schedule as sha256_compress_shani, per lane.
+template <int N>
+__attribute__((target("sha,sse4.1"))) static void sha256_compress_shani_xn(uint32_t* const state[N],
+                                                                          const uint8_t* const block[N]) {
+  const __m128i MASK = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  const __m128i* K = (const __m128i*)kSha256K;
+  __m128i S0[N], S1[N], A0[N], A1[N], M0[N], M1[N], M2[N], M3[N], MSG[N], TMP[N];
+  for (int l = 0; l < N; ++l) {
+    TMP[l] = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&state[l][0]), 0xB1);
+    S1[l] = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&state[l][4]), 0x1B);
+    S0[l] = _mm_alignr_epi8(TMP[l], S1[l], 8);
+    S1[l] = _mm_blend_epi16(S1[l], TMP[l], 0xF0);
+    A0[l] = S0[l]; A1[l] = S1[l];
+    M0[l] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block[l] + 0)), MASK);
+    M1[l] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block[l] + 16)), MASK);
+    M2[l] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block[l] + 32)), MASK);
+    M3[l] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(block[l] + 48)), MASK);
+  }
+#define QR(Mi, k)                                                    \
+  for (int l = 0; l < N; ++l) {                                      \
+    MSG[l] = _mm_add_epi32(Mi[l], _mm_loadu_si128(K + (k)));         \
+    S1[l] = _mm_sha256rnds2_epu32(S1[l], S0[l], MSG[l]);             \
+    MSG[l] = _mm_shuffle_epi32(MSG[l], 0x0E);                        \
+    S0[l] = _mm_sha256rnds2_epu32(S0[l], S1[l], MSG[l]);             \
+  }
+#define SCHED(Ma, Mb, Mc, Md)                                         \
+  for (int l = 0; l < N; ++l) {                                       \
+    TMP[l] = _mm_alignr_epi8(Md[l], Mc[l], 4); Ma[l] = _mm_add_epi32(Ma[l], TMP[l]); \
+    Ma[l] = _mm_sha256msg2_epu32(Ma[l], Md[l]); Mc[l] = _mm_sha256msg1_epu32(Mc[l], Md[l]); \
+  }
+  QR(M0, 0);
+  QR(M1, 1); for (int l = 0; l < N; ++l) M0[l] = _mm_sha256msg1_epu32(M0[l], M1[l]);
+  QR(M2, 2); for (int l = 0; l < N; ++l) M1[l] = _mm_sha256msg1_epu32(M1[l], M2[l]);
+  QR(M3, 3);
+  for (int k = 4; k < 16; k += 4) {
+    SCHED(M0, M1, M2, M3); QR(M0, k);
+    SCHED(M1, M2, M3, M0); QR(M1, k + 1);
+    SCHED(M2, M3, M0, M1); QR(M2, k + 2);
+    SCHED(M3, M0, M1, M2); QR(M3, k + 3);
+  }
+#undef QR
+#undef SCHED
+  for (int l = 0; l < N; ++l) {
+    S0[l] = _mm_add_epi32(S0[l], A0[l]);
+    S1[l] = _mm_add_epi32(S1[l], A1[l]);
+    TMP[l] = _mm_shuffle_epi32(S0[l], 0x1B);
+    S1[l] = _mm_shuffle_epi32(S1[l], 0xB1);
+    S0[l] = _mm_blend_epi16(TMP[l], S1[l], 0xF0);
+    S1[l] = _mm_alignr_epi8(S1[l], TMP[l], 8);
+    _mm_storeu_si128((__m128i*)&state[l][0], S0[l]);
+    _mm_storeu_si128((__m128i*)&state[l][4], S1[l]);
+  }
+}
+
 static bool detect_sha_ni() {
   unsigned a, b, c, d;
   bool ok = false;
@@ -124,6 +180,17 @@ bool cpu_has_sha_ni() {
 void sha256_compress(uint32_t state[8], const uint8_t block[64]) {
   if (cpu_has_sha_ni()) sha256_compress_shani(state, block);
   else sha256_compress_portable(state, block);
+}
+
+void sha256_compress_x2(uint32_t s0[8], const uint8_t b0[64], uint32_t s1[8], const uint8_t b1[64]) {
+  if (cpu_has_sha_ni()) {
+    uint32_t* const st[2] = {s0, s1};
+    const uint8_t* const bl[2] = {b0, b1};
+    sha256_compress_shani_xn<2>(st, bl);
+  } else {
+    sha256_compress_portable(s0, b0);
+    sha256_compress_portable(s1, b1);
+  }
 }
 
 void sha256(const uint8_t* data, size_t len, uint8_t out[32]) {

@@ -34,6 +34,8 @@ static inline uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 void sha256_compress_portable(uint32_t state[8], const uint8_t block[64]);
 // Dispatches to SHA-NI when the CPU has it, else portable.
 void sha256_compress(uint32_t state[8], const uint8_t block[64]);
+// Two independent compressions, interleaved on SHA-NI (latency hiding); same results as two calls.
+void sha256_compress_x2(uint32_t s0[8], const uint8_t b0[64], uint32_t s1[8], const uint8_t b1[64]);
 bool cpu_has_sha_ni();
 
 // Full SHA-256 of an arbitrary message.

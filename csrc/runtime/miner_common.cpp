@@ -257,7 +257,34 @@ std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t
   std::vector<uint32_t> hits;
   uint8_t h[32];
   const uint32_t thi = load_le32(target + 28);
-  for (uint64_t i = 0; i < count; ++i) {
+  uint64_t i = 0;
+  // Two nonces per step through the interleaved compressor (SHA-NI latency hiding).
+  uint8_t blkB[64], dblkB[64];
+  std::memcpy(blkB, blk2, 64);
+  std::memcpy(dblkB, dblk, 64);
+  for (; i + 2 <= count; i += 2) {
+    const uint32_t n0 = start + uint32_t(i), n1 = n0 + 1;
+    store_le32(blk2 + 12, n0);
+    store_le32(blkB + 12, n1);
+    uint32_t s0[8], s1[8];
+    std::memcpy(s0, mid, 32);
+    std::memcpy(s1, mid, 32);
+    sha256_compress_x2(s0, blk2, s1, blkB);
+    for (int w = 0; w < 8; ++w) { store_be32(dblk + 4 * w, s0[w]); store_be32(dblkB + 4 * w, s1[w]); }
+    std::memcpy(s0, kSha256IV, 32);
+    std::memcpy(s1, kSha256IV, 32);
+    sha256_compress_x2(s0, dblk, s1, dblkB);
+    // H7 (big-endian word 7 = LE bytes 28..31 of the digest) first: the early reject
+    if (__builtin_bswap32(s0[7]) <= thi) {
+      for (int w = 0; w < 8; ++w) store_be32(h + 4 * w, s0[w]);
+      if (le256_leq(h, target)) hits.push_back(n0);
+    }
+    if (__builtin_bswap32(s1[7]) <= thi) {
+      for (int w = 0; w < 8; ++w) store_be32(h + 4 * w, s1[w]);
+      if (le256_leq(h, target)) hits.push_back(n1);
+    }
+  }
+  for (; i < count; ++i) {
     const uint32_t nonce = start + uint32_t(i);
     store_le32(blk2 + 12, nonce);
     sha256d_from_mid(mid, blk2, dblk, h);
