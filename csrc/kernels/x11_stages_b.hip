@@ -1,8 +1,8 @@
-// X11 stages 7-11 on gfx950: Luffa-512, CubeHash16/32-512, SHAvite-3-512,
-// SIMD-512, ECHO-512 (all on the 64-byte output of the previous stage), plus the
-// chain launcher and the target compare fused into the ECHO stage.
+// X11 stages 9-11 on gfx950: SHAvite-3-512, SIMD-512, ECHO-512 (all on the 64-byte
+// output of the previous stage), plus the chain launcher and the target compare fused
+// into the ECHO stage.
 //
-// Luffa / CubeHash / SHAvite / ECHO: one lane per nonce. The padding blocks of
+// SHAvite / ECHO: one lane per nonce. The padding blocks of
 // the fixed 64-byte inputs are folded into constants (SHAvite and ECHO are a
 // single compression; their counters are the constant 512).
 // SIMD: eight lanes per nonce. Lane j owns NTT columns 2j and 2j+1, which are
@@ -16,207 +16,6 @@
 
 namespace otedama {
 namespace x11k {
-
-// ------------------------------------------------------------------ Luffa-512
-constexpr u32 kLuffaIv[5][8] = {
-    {0x6d251e69, 0x44b051e0, 0x4eaa6fb4, 0xdbf78465, 0x6e292011, 0x90152df4, 0xee058139, 0xdef610bb},
-    {0xc3b44b95, 0xd9d2f256, 0x70eee9a0, 0xde099fa3, 0x5d9b0557, 0x8fc944b3, 0xcf1ccf0e, 0x746cd581},
-    {0xf7efc89d, 0x5dba5781, 0x04016ce5, 0xad659c05, 0x0306194f, 0x666d1836, 0x24aa230a, 0x8b264ae7},
-    {0x858075d5, 0x36d79cce, 0xe571f7d7, 0x204b1f67, 0x35870c6a, 0x57e9e923, 0x14bcb808, 0x7cde72ce},
-    {0x6c68e9be, 0x5ec41e22, 0xc825b7c7, 0xaffb4363, 0xf5df3999, 0x0fc688f1, 0xb07224cc, 0x03e86cea}};
-constexpr u32 kLuffaRc0[5][8] = {
-    {0x303994a6, 0xc0e65299, 0x6cc33a12, 0xdc56983e, 0x1e00108f, 0x7800423d, 0x8f5b7882, 0x96e1db12},
-    {0xb6de10ed, 0x70f47aae, 0x0707a3d4, 0x1c1e8f51, 0x707a3d45, 0xaeb28562, 0xbaca1589, 0x40a46f3e},
-    {0xfc20d9d2, 0x34552e25, 0x7ad8818f, 0x8438764a, 0xbb6de032, 0xedb780c8, 0xd9847356, 0xa2c78434},
-    {0xb213afa5, 0xc84ebe95, 0x4e608a22, 0x56d858fe, 0x343b138f, 0xd0ec4e3d, 0x2ceb4882, 0xb3ad2208},
-    {0xf0d2e9e3, 0xac11d7fa, 0x1bcb66f2, 0x6f2d9bc9, 0x78602649, 0x8edae952, 0x3b6ba548, 0xedae9520}};
-constexpr u32 kLuffaRc4[5][8] = {
-    {0xe0337818, 0x441ba90d, 0x7f34d442, 0x9389217f, 0xe5a8bce6, 0x5274baf4, 0x26889ba7, 0x9a226e9d},
-    {0x01685f3d, 0x05a17cf4, 0xbd09caca, 0xf4272b28, 0x144ae5cc, 0xfaa7ae2b, 0x2e48f1c1, 0xb923c704},
-    {0xe25e72c1, 0xe623bb72, 0x5c58a4a4, 0x1e38e2e7, 0x78e38b9d, 0x27586719, 0x36eda57f, 0x703aace7},
-    {0xe028c9bf, 0x44756f91, 0x7e8fce32, 0x956548be, 0xfe191be2, 0x3cb226e5, 0x5944a28e, 0xa1c4c355},
-    {0x5090d577, 0x2d1925ab, 0xb46496ac, 0xd1925ab0, 0x29131ab6, 0x0fc053c3, 0x3f014f0c, 0xfc053c31}};
-
-// Multiplication by x in GF(2^32)[x]/(the Luffa polynomial) on a 256-bit word.
-__device__ __forceinline__ void luffa_m2(u32 a[8]) {
-  const u32 t = a[7];
-  a[7] = a[6]; a[6] = a[5]; a[5] = a[4];
-  a[4] = a[3] ^ t; a[3] = a[2] ^ t; a[2] = a[1];
-  a[1] = a[0] ^ t; a[0] = t;
-}
-// Bitsliced SubCrumb (4-bit S-box {13,14,0,1,5,10,7,6,11,3,9,12,15,8,2,4}, a0 = bit 0) as four
-// Shannon splits on a3: y_k = a3 ? g1_k(a0,a1,a2) : g0_k(a0,a1,a2), each cofactor and the select one
-// v_bitop3: 12 VALU (the and/or/xor network is 16).
-#define LUFFA_SUBCRUMB(a0, a1, a2, a3)                                                   \
-  do {                                                                                   \
-    const u32 y0_ = bop3<0xCA>(a3, bop3<0x17>(a0, a1, a2), bop3<0x4B>(a0, a1, a2));      \
-    const u32 y1_ = bop3<0xCA>(a3, bop3<0x1B>(a0, a1, a2), bop3<0xB8>(a0, a1, a2));      \
-    const u32 y2_ = bop3<0xCA>(a3, bop3<0xC2>(a0, a1, a2), bop3<0x9B>(a0, a1, a2));      \
-    const u32 y3_ = bop3<0xCA>(a3, bop3<0x67>(a0, a1, a2), bop3<0x31>(a0, a1, a2));      \
-    (a0) = y0_; (a1) = y1_; (a2) = y2_; (a3) = y3_;                                       \
-  } while (0)
-#define LUFFA_MIXWORD(u, v)          \
-  do {                               \
-    (v) ^= (u);                      \
-    (u) = rotl32((u), 2) ^ (v);      \
-    (v) = rotl32((v), 14) ^ (u);     \
-    (u) = rotl32((u), 10) ^ (v);     \
-    (v) = rotl32((v), 1);            \
-  } while (0)
-
-template <int J>
-__device__ __forceinline__ void luffa_Q(u32 a[8]) {
-#pragma unroll
-  for (int k = 4; k < 8; ++k) a[k] = rotl32(a[k], J);
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    LUFFA_SUBCRUMB(a[0], a[1], a[2], a[3]);
-    LUFFA_SUBCRUMB(a[5], a[6], a[7], a[4]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) LUFFA_MIXWORD(a[k], a[k + 4]);
-    a[0] ^= kLuffaRc0[J][r];
-    a[4] ^= kLuffaRc4[J][r];
-  }
-}
-
-// Message injection MI5 followed by the five sub-permutations Q_j.
-__device__ __forceinline__ void luffa_round(u32 V[5][8], const u32 Min[8]) {
-  u32 t[8], M[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { M[k] = Min[k]; t[k] = V[0][k] ^ V[1][k] ^ V[2][k] ^ V[3][k] ^ V[4][k]; }
-  luffa_m2(t);
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) V[j][k] ^= t[k];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[k] = V[0][k];
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    luffa_m2(V[j]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) V[j][k] ^= (j < 4 ? V[j + 1][k] : t[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[k] = V[4][k];
-#pragma unroll
-  for (int j = 4; j >= 0; --j) {
-    luffa_m2(V[j]);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) V[j][k] ^= (j > 0 ? V[j - 1][k] : t[k]);
-  }
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) V[j][k] ^= M[k];
-    if (j < 4) luffa_m2(M);
-  }
-  luffa_Q<0>(V[0]);
-  luffa_Q<1>(V[1]);
-  luffa_Q<2>(V[2]);
-  luffa_Q<3>(V[3]);
-  luffa_Q<4>(V[4]);
-}
-
-__global__ __launch_bounds__(kBlock) void k_luffa512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  u64 h[8];
-  load_hash(Hb, stride, i, h);
-  u32 V[5][8];
-#pragma unroll
-  for (int j = 0; j < 5; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) V[j][k] = kLuffaIv[j][k];
-  // Five rounds: two message blocks (big-endian words), the padding block, two blank
-  // output rounds. Rolled: each round is ~3k instructions.
-#pragma unroll 1
-  for (int b = 0; b < 5; ++b) {
-    u32 M[8];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u64 w = b == 0 ? h[k] : h[4 + k];
-      M[2 * k] = b < 2 ? bswap32(lo32(w)) : 0u;
-      M[2 * k + 1] = b < 2 ? bswap32(hi32(w)) : 0u;
-    }
-    if (b == 2) M[0] = 0x80000000u;
-    luffa_round(V, M);
-    if (b >= 3) {
-      u32 o[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = bswap32(V[0][k] ^ V[1][k] ^ V[2][k] ^ V[3][k] ^ V[4][k]);
-      if (b == 3) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) h[k] = mk64(o[2 * k], o[2 * k + 1]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) h[4 + k] = mk64(o[2 * k], o[2 * k + 1]);
-      }
-    }
-  }
-  store_hash(Hb, stride, i, h);
-}
-#undef LUFFA_SUBCRUMB
-#undef LUFFA_MIXWORD
-
-// ------------------------------------------------------------------ CubeHash-512
-// One round; the word swaps are register renames once two rounds are unrolled
-// (the round's permutation is an involution).
-__device__ __forceinline__ void cube_round(u32 x[32]) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i + 16] += x[i];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] = rotl32(x[i], 7);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { const u32 t = x[i]; x[i] = x[i + 8]; x[i + 8] = t; }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] ^= x[i + 16];
-#pragma unroll
-  for (int i = 16; i < 32; ++i)
-    if (!(i & 2)) { const u32 t = x[i]; x[i] = x[i + 2]; x[i + 2] = t; }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i + 16] += x[i];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] = rotl32(x[i], 11);
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (!(i & 4)) { const u32 t = x[i]; x[i] = x[i + 4]; x[i + 4] = t; }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] ^= x[i + 16];
-#pragma unroll
-  for (int i = 16; i < 32; ++i)
-    if (!(i & 1)) { const u32 t = x[i]; x[i] = x[i + 1]; x[i + 1] = t; }
-}
-__device__ __forceinline__ void cube_rounds(u32 x[32], int n) {
-#pragma unroll 1
-  for (int r = 0; r < n; r += 2) {
-    cube_round(x);
-    cube_round(x);
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_cubehash512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  u64 h[8];
-  load_hash(Hb, stride, i, h);
-  u32 x[32];
-#pragma unroll
-  for (int k = 0; k < 32; ++k) x[k] = x11t::CUBE_IV[k];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { x[2 * k] ^= lo32(h[k]); x[2 * k + 1] ^= hi32(h[k]); }
-  cube_rounds(x, 16);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { x[2 * k] ^= lo32(h[4 + k]); x[2 * k + 1] ^= hi32(h[4 + k]); }
-  cube_rounds(x, 16);
-  x[0] ^= 0x80u;  // padding block
-  cube_rounds(x, 16);
-  x[31] ^= 1u;    // finalization
-  cube_rounds(x, 160);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = mk64(x[2 * k], x[2 * k + 1]);
-  store_hash(Hb, stride, i, h);
-}
 
 // ------------------------------------------------------------------ SHAvite-3-512
 constexpr u32 kShaviteIv[16] = {0x72FCCDD8, 0x79CA4727, 0x128A077B, 0x40D55AEC, 0xD1901A06, 0x430AE307,
@@ -626,8 +425,6 @@ hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint
   const u32 aes_want = (n + kAesBlock - 1) / kAesBlock, aes_cap = (u32)x11_device_cus() * 2 * 4;
   const dim3 aes_grid(aes_want < aes_cap ? aes_want : aes_cap), aes_block(kAesBlock);
   switch (stage) {
-    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n); break;
     case kX11Simd: {
       const dim3 g8((8ull * n + kBlock - 1) / kBlock);
@@ -646,7 +443,7 @@ hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint
 hipError_t x11_launch_stage(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
                             uint32_t* out, uint32_t cap, hipStream_t s) {
   if (stage < 0 || stage >= kX11Stages || n == 0 || stride < n || !H) return hipErrorInvalidValue;
-  if (stage <= kX11Keccak) return x11_launch_stage_a(stage, p, base, H, stride, n, s);
+  if (stage <= kX11Cubehash) return x11_launch_stage_a(stage, p, base, H, stride, n, s);
   return x11_launch_stage_b(stage, p, base, H, stride, n, out, cap, s);
 }
 
@@ -654,15 +451,12 @@ hipError_t x11_launch_stage(int stage, const X11Params& p, uint32_t base, uint64
 // out != null: search mode (ECHO compares, H keeps the SIMD output); else H = digests.
 hipError_t x11_launch_chain(const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
                             uint32_t* out, uint32_t cap, hipStream_t s) {
-  for (int st = kX11Blake; st <= kX11Keccak; ++st) {
-    const hipError_t e = x11_launch_stage_a(st, p, base, H, stride, n, s);
-    if (e != hipSuccess) return e;
-  }
-  for (int st = kX11Luffa; st <= kX11Echo; ++st) {
-    const hipError_t e = x11_launch_stage_b(st, p, base, H, stride, n, out, cap, s);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  // One launch per stage. Fusing the register-only middle (Skein..CubeHash) into one kernel measured
+  // 1.3% slower than separate launches (its register union drops it to 4 waves/SIMD; the HBM round
+  // trips it saves are hidden behind the VALU-bound stages anyway): profiles/r1/x11/NOTES.md.
+  hipError_t e = hipSuccess;
+  for (int st = kX11Blake; e == hipSuccess && st <= kX11Echo; ++st) e = x11_launch_stage(st, p, base, H, stride, n, out, cap, s);
+  return e;
 }
 
 }  // namespace otedama
