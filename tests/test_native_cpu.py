@@ -143,3 +143,23 @@ def test_cpu_miner_pause_with_none_job():
     time.sleep(0.1)
     assert m.stats()["hashes"] == h0
     m.stop()
+
+
+@pytest.mark.parametrize("start,count", [(0, 1), (7, 2), (11, 999), (0xFFFFFF00, 513)])
+def test_cpu_scan_pairs_and_tail_match_python(start, count):
+    """The scan hashes nonces in interleaved pairs plus a scalar tail; any count/start (incl. the 2^32 wrap)
+    gives exactly the hashlib hits, in nonce order."""
+    import random
+
+    rng = random.Random(start ^ count)
+    hdr = bytes(rng.getrandbits(8) for _ in range(76)) + bytes(4)
+    t_int = (1 << 250) - 1
+    tgt = t_int.to_bytes(32, "little")
+    got = N.cpu_scan_sha256d(hdr, tgt, start, count)
+    ref = []
+    for k in range(count):
+        n = (start + k) & 0xFFFFFFFF
+        d = hashlib.sha256(hashlib.sha256(hdr[:76] + n.to_bytes(4, "little")).digest()).digest()
+        if int.from_bytes(d, "little") <= t_int:
+            ref.append(n)
+    assert got == ref
