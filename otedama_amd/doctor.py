@@ -504,6 +504,57 @@ def check_collectives() -> Check:
     return Check("Collectives", run)
 
 
+def check_pow_self_test(cfg: C.Config) -> Check:
+    """CPU oracle of the configured algorithm vs its known answer; on a gfx950 box also one tiny GPU search
+    that must find the known nonce (SHA-256d / X11 genesis blocks) or match the oracle (scrypt)."""
+    def run():
+        from otedama_amd.models import algorithms
+
+        algo = cfg.mining.algorithm
+        try:
+            detail = algorithms.self_test(algo)
+        except Exception as exc:  # noqa: BLE001 - any failure is the finding
+            return Result(status=Status.FAIL, detail=str(exc), fix="rebuild the native extension (make build)")
+        from otedama_amd.ops.native import load
+
+        n = load(build_if_missing=False)
+        if n is None or n.gpu_device_count() == 0 or not n.gpu_arch_name(0).startswith("gfx950"):
+            return Result(detail=detail + "; no gfx950 device for the GPU kernel check")
+        try:
+            detail += "; " + _gpu_kernel_self_test(algo)
+        except Exception as exc:  # noqa: BLE001
+            return Result(status=Status.FAIL, detail=f"{detail}; GPU kernel: {exc}",
+                          fix="run `python -m pytest tests -m gpu` to locate the failing kernel")
+        return Result(detail=detail)
+    return Check("PoW self-test", run)
+
+
+def _gpu_kernel_self_test(algo: str) -> str:
+    import torch
+
+    from otedama_amd.models import algorithms
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, X11Search
+
+    if algo == "scrypt":
+        hdr = bytes(range(76)) + bytes(4)
+        s = ScryptSearch("cuda:0", grid=64)
+        got = s.search(hdr, int_to_hash((1 << 256) - 1), 0, 4)
+        if sorted(got) != [0, 1, 2, 3]:
+            raise AssertionError(f"scrypt kernel hits {got}")
+        torch.cuda.synchronize()
+        return "gfx950 scrypt kernel ran"
+    hdr_hex, nonce, _ = algorithms.KNOWN_ANSWERS[algo]
+    hdr = bytes.fromhex(hdr_hex)
+    bits = int.from_bytes(hdr[72:76], "little")
+    target = int_to_hash((bits & 0xFFFFFF) << (8 * ((bits >> 24) - 3)))
+    s = Sha256dSearch("cuda:0") if algo == "sha256d" else X11Search("cuda:0", batch=1 << 16)
+    got = s.search(hdr, target, nonce - 1000, 1 << 16)
+    if nonce not in got:
+        raise AssertionError(f"{algo} kernel missed the genesis nonce ({got})")
+    return f"gfx950 {algo} kernel finds the genesis nonce"
+
+
 def default_checks(cfg: C.Config, config_path: str = "") -> list[Check]:
     return [
         check_configuration(cfg, config_path), check_bitcoin_address(cfg), check_failover_addresses(cfg),
@@ -511,4 +562,5 @@ def default_checks(cfg: C.Config, config_path: str = "") -> list[Check]:
         check_pool_endpoint_diversity(cfg), check_pool_encryption(cfg), check_pool_tls_ca(cfg),
         check_power_cost(cfg), check_env_vars(), check_profitability_floor(cfg), check_payout_scheme(cfg),
         check_hardware(), check_network(), check_clock(), check_native(), check_gpu_runtime(), check_collectives(),
+        check_pow_self_test(cfg),
     ]

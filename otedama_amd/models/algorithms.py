@@ -49,6 +49,37 @@ ALGORITHMS: dict[str, PowAlgorithm] = {
 }
 
 
+# Published known answers: (80-byte header hex, nonce, hash in display order). Bitcoin and Dash main-net
+# genesis blocks; the scrypt oracle is cross-checked against hashlib.scrypt instead (no published PoW hash).
+KNOWN_ANSWERS: dict[str, tuple[str, int, str]] = {
+    "sha256d": ("0100000000000000000000000000000000000000000000000000000000000000000000003ba3edfd7a7b12b27ac72c3e"
+                "67768f617fc81bc3888a51323a9fb8aa4b1e5e4a29ab5f49ffff001d1dac2b7c", 2083236893,
+                "000000000019d6689c085ae165831e934ff763ae46a2a6c172b3f1b60a8ce26f"),
+    "x11": ("010000000000000000000000000000000000000000000000000000000000000000000000c762a6567f3cc092f0684bb6"
+            "2b7e00a84890b990f07cc71a6bb58d64b98e02e0022ddb52f0ff0f1ec23fb901", 28917698,
+            "00000ffd590b1485b3caadc19b22e6379c733355108f107a430458cdf3407ab6"),
+}
+
+
+def self_test(name: str) -> str:
+    """Run the CPU oracle of `name` against its known answer; returns a short description, raises on mismatch."""
+    algo = get(name)
+    if algo.name in KNOWN_ANSWERS:
+        hdr_hex, _nonce, want = KNOWN_ANSWERS[algo.name]
+        got = algo.hash(bytes.fromhex(hdr_hex))[::-1].hex()
+        if got != want:
+            raise AssertionError(f"{algo.name}: genesis hash {got} != published {want}")
+        return f"{algo.name} CPU oracle reproduces the published genesis hash"
+    hdr = bytes(range(80))
+    ref = hashlib.scrypt(hdr, salt=hdr, n=1024, r=1, p=1, dklen=32)
+    from otedama_amd.ops.native import load
+
+    n = load(build_if_missing=False)
+    if n is not None and n.scrypt_1024_1_1(hdr) != ref:
+        raise AssertionError("scrypt: native C++ scrypt != hashlib.scrypt")
+    return "scrypt native C++ oracle == hashlib.scrypt"
+
+
 def get(name: str) -> PowAlgorithm:
     try:
         return ALGORITHMS[name.lower()]

@@ -4,6 +4,8 @@ import json
 import socket
 import threading
 
+import pytest
+
 from otedama_amd import config as C
 from otedama_amd import doctor as D
 
@@ -136,3 +138,26 @@ def test_default_checks_names():
                  "Profitability floor", "Pool payout schemes", "Hardware", "Network", "System clock accuracy",
                  "Native extension", "GPU runtime", "Collectives"):
         assert want in names
+
+
+@pytest.mark.parametrize("algo", ["sha256d", "scrypt", "x11"])
+def test_pow_self_test_check(algo):
+    from otedama_amd import config as C
+
+    cfg = C.Config()
+    cfg.mining.algorithm = algo
+    r = D.check_pow_self_test(cfg).run()
+    assert r.status == D.Status.PASS, r.detail
+    assert algo in r.detail
+
+
+def test_pow_self_test_detects_a_wrong_oracle(monkeypatch):
+    from otedama_amd import config as C
+    from otedama_amd.models import algorithms
+
+    bad = algorithms.PowAlgorithm("x11", algorithms.ALGORITHMS["x11"].diff1, lambda h: bytes(32), True, "broken")
+    monkeypatch.setitem(algorithms.ALGORITHMS, "x11", bad)
+    cfg = C.Config()
+    cfg.mining.algorithm = "x11"
+    r = D.check_pow_self_test(cfg).run()
+    assert r.status == D.Status.FAIL and "genesis" in r.detail

@@ -254,3 +254,15 @@ def test_sha256d_k_variants_match_cpu(k):
         assert sorted(n for n, vv in got if vv == v) == ref and len(ref) > 100
     with pytest.raises(ValueError):
         s.prepare([headers[0]] * (k - 1), bytes(32))
+
+
+@pytest.mark.parametrize("algo", ["sha256d", "scrypt", "x11"])
+def test_doctor_pow_self_test_runs_the_gpu_kernel(algo):
+    from otedama_amd import config as C
+    from otedama_amd import doctor as D
+
+    cfg = C.Config()
+    cfg.mining.algorithm = algo
+    r = D.check_pow_self_test(cfg).run()
+    assert r.status == D.Status.PASS, r.detail
+    assert "gfx950" in r.detail and "no gfx950" not in r.detail
