@@ -1,0 +1,198 @@
+"""Local pool building blocks without sockets: vardiff, share journal / payouts, block templates and the
+share-validation rules of PoolServer.validate (SURVEY §7.2 step 5, H9 — [NO REFERENCE CODE]: the reference has
+no pool; these are the rules its fake pools do not check, tested the way its engine tests drive fakes)."""
+import hashlib
+import struct
+import time
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from otedama_amd.pool import template as T
+from otedama_amd.pool.journal import Journal, ShareRow
+from otedama_amd.pool.server import BIP320_MASK, EN1_SIZE, EN2_SIZE, MAX_NTIME_FUTURE, PoolOptions, PoolServer
+from otedama_amd.pool.vardiff import Vardiff, VardiffConfig
+
+ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
+
+
+class FakeClock:
+    def __init__(self, t=1000.0):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+# ------------------------------------------------------------------ vardiff
+@settings(max_examples=200, deadline=None)
+@given(d0=st.floats(1e-3, 1e9), interval=st.floats(0.01, 1000.0), n=st.integers(1, 40))
+def test_vardiff_step_is_bounded_and_clamped(d0, interval, n):
+    clk = FakeClock()
+    cfg = VardiffConfig(target_share_seconds=10.0, retarget_seconds=30.0, min_difficulty=1e-6, max_difficulty=1e12)
+    vd = Vardiff(cfg, clock=clk)
+    s = vd.new_state(d0)
+    for _ in range(n):
+        before = s.difficulty
+        clk.t += interval
+        new = vd.on_share(s)
+        if new is not None:
+            assert before / cfg.max_step * (1 - 1e-9) <= new <= before * cfg.max_step * (1 + 1e-9)
+            assert abs(new - before) > cfg.dead_band * before  # inside the dead band nothing changes
+        assert cfg.min_difficulty <= s.difficulty <= cfg.max_difficulty
+
+
+def test_vardiff_converges_on_a_steady_miner():
+    """A miner of fixed hashrate: the share interval settles near the target."""
+    clk = FakeClock()
+    vd = Vardiff(VardiffConfig(target_share_seconds=10.0, retarget_seconds=30.0), diff1_hashes=2.0 ** 32, clock=clk)
+    s = vd.new_state(1.0)
+    hashrate = 5e12
+    for _ in range(400):
+        clk.t += s.difficulty * 2.0 ** 32 / hashrate  # expected time to the next share at this difficulty
+        vd.on_share(s)
+    interval = s.difficulty * 2.0 ** 32 / hashrate
+    assert 10.0 / 1.2 <= interval <= 10.0 * 1.2
+    assert vd.difficulty_for_hashrate(hashrate) == pytest.approx(hashrate * 10.0 / 2.0 ** 32)
+
+
+def test_vardiff_lowers_difficulty_when_shares_stop():
+    clk = FakeClock()
+    cfg = VardiffConfig(retarget_seconds=30.0)
+    vd = Vardiff(cfg, clock=clk)
+    s = vd.new_state(64.0)
+    clk.t += 2 * cfg.retarget_seconds + 1
+    assert vd.maybe_retarget(s) == pytest.approx(64.0 / cfg.max_step)
+
+
+# ------------------------------------------------------------------ journal
+def test_journal_pplns_payouts_are_proportional_and_never_exceed_the_reward():
+    j = Journal()
+    for i in range(300):
+        j.append(ShareRow(time.time(), "a" if i % 3 else "b", "sha256d", "1", 2.0 if i % 3 else 1.0, True))
+    j.append(ShareRow(time.time(), "c", "sha256d", "1", 1000.0, False, "low-difficulty-share"))  # rejected: no pay
+    pay = j.record_block(900_001, "00" * 32, "a", 312_500_000)
+    assert set(pay) == {"a", "b"}
+    assert sum(pay.values()) <= 312_500_000
+    assert pay["a"] / pay["b"] == pytest.approx(4.0, rel=1e-6)  # 200 shares x 2.0 vs 100 x 1.0
+    c = j.counts()
+    assert c == {"accepted": 300, "accepted_work": 500.0, "rejected": 1, "blocks": 1}
+
+
+def test_journal_window_and_solo_fallback():
+    j = Journal()
+    for i in range(50):
+        j.append(ShareRow(time.time(), f"w{i}", "x11", "1", 1.0, True))
+    assert set(j.pplns_window(10)) == {f"w{i}" for i in range(40, 50)}  # the last 10 accepted shares
+    j2 = Journal()
+    assert j2.record_block(1, "ab", "solo", 1000, scheme="prop") == {"solo": 1000}
+
+
+def test_journal_worker_difficulty_survives_reopen(tmp_path):
+    p = str(tmp_path / "pool.sqlite")
+    j = Journal(p)
+    j.save_worker("rig1", 512.0)
+    j.save_worker("rig1", 1024.0)
+    j.append(ShareRow(time.time(), "rig1", "scrypt", "2", 1024.0, True))
+    j.close()
+    j = Journal(p)
+    assert j.load_worker("rig1") == 1024.0 and j.load_worker("nobody") is None
+    assert j.counts()["accepted"] == 1
+
+
+# ------------------------------------------------------------------ templates
+@pytest.mark.parametrize("n,enc", [(0, "00"), (1, "0101"), (16, "0110"), (127, "017f"), (128, "028000"),
+                                   (255, "02ff00"), (256, "020001"), (-1, "0181"), (900_001, "03a1bb0d")])
+def test_script_num_bip34(n, enc):
+    assert T.script_num(n).hex() == enc
+
+
+@pytest.mark.parametrize("n,enc", [(0, "00"), (0xFC, "fc"), (0xFD, "fdfd00"), (0xFFFF, "fdffff"),
+                                   (0x10000, "fe00000100"), (0x1_0000_0000, "ff0000000001000000")])
+def test_varint(n, enc):
+    assert T.varint(n).hex() == enc
+
+
+@settings(max_examples=40, deadline=None)
+@given(n=st.integers(0, 12), seed=st.binary(min_size=1, max_size=8))
+def test_merkle_branches_reproduce_the_full_tree(n, seed):
+    txids = [hashlib.sha256(seed + struct.pack("<I", i)).digest() for i in range(n)]
+    cb = hashlib.sha256(b"coinbase" + seed).digest()
+    assert T.merkle_root_from_branches(cb, T.merkle_branches(txids)) == T.merkle_root_full([cb] + txids)
+
+
+def test_coinbase_parts_make_a_bip34_transaction():
+    src = T.TemplateSource(ADDR, n_txs=3, seed=b"s")
+    blk = src.next_block()
+    c1, c2 = blk.coinbase_parts(EN1_SIZE + EN2_SIZE)
+    tx = c1 + bytes(EN1_SIZE + EN2_SIZE) + c2
+    assert tx[:4] == struct.pack("<I", 1) and tx[4] == 1 and tx[5:37] == bytes(32)
+    script_len = tx[41]
+    script = tx[42:42 + script_len]
+    assert script.startswith(T.script_num(blk.height))  # BIP34 height first
+    assert blk.payout_script in tx and tx.endswith(bytes(4))
+    nxt = src.next_block()
+    assert nxt.height == blk.height + 1 and nxt.prev_hash != blk.prev_hash
+
+
+# ------------------------------------------------------------------ validation rules
+def _pool(algo="sha256d"):
+    p = PoolServer(PoolOptions(algorithm=algo, payout_address=ADDR, initial_difficulty=1e-9, min_difficulty=1e-12))
+    p.new_block()
+    return p
+
+
+def _find_share(p, job, w, en, version=None):
+    version = job.version if version is None else version
+    for nonce in range(1 << 20):
+        v = p.validate(w, job.job_id, en, job.ntime, nonce, version)
+        if v.accepted:
+            return nonce
+    raise AssertionError("no share in 2^20 nonces")
+
+
+def test_validate_accepts_then_rejects_the_duplicate():
+    p = _pool()
+    job = next(iter(p.jobs.values()))
+    w = p.new_worker("rig", BIP320_MASK)
+    en = bytes(EN1_SIZE + EN2_SIZE)
+    nonce = _find_share(p, job, w, en)
+    v = p.validate(w, job.job_id, en, job.ntime, nonce, job.version)
+    assert not v.accepted and v.reason == "duplicate-share"
+
+
+def test_validate_rejection_taxonomy():
+    p = _pool()
+    job = next(iter(p.jobs.values()))
+    w = p.new_worker("rig", BIP320_MASK)
+    en = bytes(EN1_SIZE + EN2_SIZE)
+    assert p.validate(w, "ffff", en, job.ntime, 0, job.version).reason == "stale-job"
+    assert p.validate(w, job.job_id, en, job.ntime, 0, job.version ^ 0x1).reason == "invalid-version-bits"
+    assert p.validate(w, job.job_id, en, job.ntime - 1, 0, job.version).reason == "invalid-ntime"
+    far = int(time.time()) + MAX_NTIME_FUTURE + 120
+    assert p.validate(w, job.job_id, en, far, 0, job.version).reason == "invalid-ntime"
+    w.vd.difficulty = 1e12  # nothing meets this
+    assert p.validate(w, job.job_id, en, job.ntime, 1, job.version).reason == "low-difficulty-share"
+    # BIP320 bits are allowed to roll
+    w.vd.difficulty = 1e-9
+    _find_share(p, job, w, en, version=job.version ^ 0x00002000)
+    # a new block makes every old job stale
+    p.new_block()
+    assert p.validate(w, job.job_id, en, job.ntime, 5, job.version).reason == "stale-job"
+    assert p.reject_reasons["invalid-ntime"] == 2 and p.rejected >= 5
+
+
+@pytest.mark.parametrize("algo", ["scrypt", "x11"])
+def test_validate_recomputes_the_algorithm_hash(algo):
+    from otedama_amd.models.algorithms import get
+
+    p = _pool(algo)
+    job = next(iter(p.jobs.values()))
+    w = p.new_worker("rig", BIP320_MASK)
+    en = b"\x00\x00\x00\x01" + bytes(EN2_SIZE)
+    nonce = _find_share(p, job, w, en)
+    hdr = p.header_for(job, en, job.version, job.ntime, nonce)
+    v = p.validate(w, job.job_id, en, job.ntime, nonce + 1, job.version)  # a different nonce: its own hash
+    assert v.hash == b"" or v.hash == get(algo).hash(p.header_for(job, en, job.version, job.ntime, nonce + 1))
+    assert p.journal.counts()["accepted"] >= 1 and len(hdr) == 80
