@@ -60,6 +60,14 @@ __device__ __forceinline__ u32 bop3(u32 a, u32 b, u32 c) {
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
   return r;
 }
+// Same with a wave-uniform third operand read straight from an SGPR (saves the v_mov an all-"v" constraint
+// forces; VOP3 on gfx950 may read one SGPR).
+template <unsigned TT>
+__device__ __forceinline__ u32 bop3s(u32 a, u32 b, u32 c_uniform) {
+  u32 r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "s"(c_uniform), "i"(TT));
+  return r;
+}
 __device__ __forceinline__ u64 xor3_64(u64 a, u64 b, u64 c) { return mk64(xor3(lo32(a), lo32(b), lo32(c)), xor3(hi32(a), hi32(b), hi32(c))); }
 
 // ---------------------------------------------------------------- bank-private tables
@@ -107,9 +115,10 @@ __device__ __forceinline__ void aes_round_k(const u32* T, u32 lo, u32& x0, u32& 
   x2 = xor3(xor3(c0, rotl32(c1, 8), rotl32(c2, 16)), rotl32(c3, 24), k2);
   x3 = xor3(xor3(d0, rotl32(d1, 8), rotl32(d2, 16)), rotl32(d3, 24), k3);
 }
+// k0 must be wave-uniform (ECHO's counter key): it is read from an SGPR.
 __device__ __forceinline__ void aes_round_key0(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3, u32 k0) {
   AES_COLS_(T, lo, x0, x1, x2, x3);
-  x0 = xor3(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);
+  x0 = bop3s<0x96>(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);  // k0 wave-uniform
   x1 = xor3(b0, rotl32(b1, 8), rotl32(b2, 16)) ^ rotl32(b3, 24);
   x2 = xor3(c0, rotl32(c1, 8), rotl32(c2, 16)) ^ rotl32(c3, 24);
   x3 = xor3(d0, rotl32(d1, 8), rotl32(d2, 16)) ^ rotl32(d3, 24);
