@@ -14,6 +14,7 @@
 #include "otedama/runtime.h"
 #include "otedama/trace.h"
 #include "otedama/sha256.h"
+#include "otedama/sv2_frame.h"
 #include "otedama/x11.h"
 
 namespace py = pybind11;
@@ -182,6 +183,31 @@ PYBIND11_MODULE(_native, m) {
     return to_bytes(o, 64);
   }, py::arg("stage"), py::arg("msg"));
   m.def("x11_luffa_sbox_selfcheck", &x11::luffa_sbox_selfcheck);
+  m.def(
+      "sv2_scan",
+      [](py::buffer b, uint32_t max_frame) {
+        py::buffer_info info = b.request();
+        if (info.itemsize != 1 || info.ndim != 1) throw std::invalid_argument("sv2_scan: need a contiguous byte buffer");
+        const size_t n = (size_t)info.size;
+        if (n > 0xFFFFFFFFull) throw std::invalid_argument("sv2_scan: buffer larger than 4 GiB");
+        // Upper bound on frames in n bytes: every frame has a 6-byte header.
+        std::vector<Sv2FrameRec> recs(n / kSv2HeaderSize + 1);
+        size_t consumed = 0, k = 0;
+        int status = kSv2Ok;
+        {
+          py::gil_scoped_release nogil;
+          k = sv2_scan(static_cast<const uint8_t*>(info.ptr), n, max_frame, recs.data(), recs.size(), &consumed,
+                       &status);
+        }
+        py::list frames(k);
+        for (size_t i = 0; i < k; ++i) {
+          const Sv2FrameRec& r = recs[i];
+          frames[i] = py::make_tuple(r.extension_type, r.msg_type, r.offset, r.length);
+        }
+        return py::make_tuple(frames, consumed, status);
+      },
+      py::arg("buf"), py::arg("max_frame"),
+      "Split complete SV2 frames: ([(extension_type, msg_type, payload_offset, payload_length)], consumed, status)");
   m.def("cpu_scan_sha256d", [](const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     std::vector<uint32_t> hits;

@@ -35,6 +35,7 @@ CXX_SOURCES = [
     "cpu/job_prepare.cpp",
     "cpu/aead.cpp",
     "cpu/x11_cpu.cpp",
+    "cpu/sv2_frame.cpp",
     "runtime/miner_common.cpp",
     "bindings.cpp",
 ]

@@ -61,6 +61,14 @@ def format_float(v: float) -> str:
         return "+Inf" if v > 0 else "-Inf"
     if v == 0:
         return "-0" if math.copysign(1.0, v) < 0 else "0"
+    if 1e-4 <= abs(v) < 1e6:
+        # Fixed-point range of %g: Python's repr is the same shortest round-trip digits, without an exponent.
+        r = repr(v)
+        return r[:-2] if r.endswith(".0") else r
+    return _format_float_exp(v)
+
+
+def _format_float_exp(v: float) -> str:
     from decimal import Decimal
 
     sign, digits, exp = Decimal(repr(abs(v))).as_tuple()
@@ -81,10 +89,12 @@ def format_float(v: float) -> str:
 
 
 class Counter:
-    __slots__ = ("name", "help", "labels", "_v", "_lock")
+    __slots__ = ("name", "help", "labels", "key", "prefix", "_v", "_lock")
 
     def __init__(self, name: str, help: str, labels: dict[str, str] | None):
         self.name, self.help, self.labels = name, help, dict(labels or {})
+        # Labels are fixed for a series' lifetime: its sort key and exposition prefix are rendered once.
+        self.key, self.prefix = _metric_key(name, self.labels), f"{name}{render_labels(self.labels)} "
         self._v = 0
         self._lock = threading.Lock()
 
@@ -101,13 +111,18 @@ class Counter:
     def value(self) -> int:
         return self._v
 
+    def text(self) -> str:
+        return str(self._v)
+
 
 class Gauge:
-    __slots__ = ("name", "help", "labels", "_v", "_lock")
+    __slots__ = ("name", "help", "labels", "key", "prefix", "_v", "_lock", "_fv", "_ft")
 
     def __init__(self, name: str, help: str, labels: dict[str, str] | None):
         self.name, self.help, self.labels = name, help, dict(labels or {})
+        self.key, self.prefix = _metric_key(name, self.labels), f"{name}{render_labels(self.labels)} "
         self._v = 0.0
+        self._fv, self._ft = 0.0, "0"  # last formatted value (Go %g formatting is the costly part of a scrape)
         self._lock = threading.Lock()
 
     def set(self, v: float) -> None:
@@ -120,6 +135,12 @@ class Gauge:
 
     def value(self) -> float:
         return self._v
+
+    def text(self) -> str:
+        v = self._v
+        if v != self._fv or math.copysign(1.0, v) != math.copysign(1.0, self._fv):  # NaN always re-formats
+            self._ft, self._fv = format_float(v), v
+        return self._ft
 
 
 class Registry:
@@ -171,19 +192,17 @@ class Registry:
 
     def write_text(self, w: TextIO) -> None:
         with self._lock:
-            entries = [(c.name, _metric_key(c.name, c.labels), c.help, "counter", c.labels, str(c.value()))
-                       for c in self._counters.values()]
-            entries += [(g.name, _metric_key(g.name, g.labels), g.help, "gauge", g.labels, format_float(g.value()))
-                        for g in self._gauges.values()]
+            entries = [(c.name, c.key, c.help, "counter", c.prefix, c.text()) for c in self._counters.values()]
+            entries += [(g.name, g.key, g.help, "gauge", g.prefix, g.text()) for g in self._gauges.values()]
             fns = list(self._collectors)
         entries.sort(key=lambda e: (e[0], e[1]))
         out: list[str] = []
         seen: set[str] = set()
-        for name, _key, help_, kind, labels, text in entries:
+        for name, _key, help_, kind, prefix, text in entries:
             if name not in seen:
                 seen.add(name)
                 out.append(f"# HELP {name} {escape_help(help_)}\n# TYPE {name} {kind}\n")
-            out.append(f"{name}{render_labels(labels)} {text}\n")
+            out.append(f"{prefix}{text}\n")
         w.write("".join(out))
         for fn in fns:
             fn(w)

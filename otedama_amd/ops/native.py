@@ -26,10 +26,13 @@ def load(build_if_missing: bool = True):
         # satisfied by torch's copies (same sonames). Loading the extension
         # first pulls /opt/rocm's runtime and torch then adds a second one, and
         # two HSA runtimes in one process cannot both enumerate the GPU.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # A host without /dev/kfd has no GPU for either runtime to enumerate, so a CPU-only process skips the
+        # ~2 s torch import (startup to first hash stays well under the reference's 1 s budget).
+        if os.path.exists("/dev/kfd") or os.environ.get("OTEDAMA_IMPORT_TORCH_FIRST") == "1":
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         try:
             _mod = importlib.import_module("otedama_amd._native")
             return _mod

@@ -1,5 +1,19 @@
-"""Multi-GPU node parallelism: one rank per GPU over torch.distributed (RCCL)."""
-from otedama_amd.parallel.comm import DistInfo, NodeComm, barrier, init_from_env, shutdown
-from otedama_amd.parallel.partition import Stripe, apply_stripe, stripe_for
+"""Multi-GPU node parallelism: one rank per GPU over torch.distributed (RCCL).
 
-__all__ = ["DistInfo", "NodeComm", "barrier", "init_from_env", "shutdown", "Stripe", "apply_stripe", "stripe_for"]
+Exports resolve lazily (PEP 562) so that importing the stripe planner from the engine does not pull in torch:
+a CPU-only ``otedama run`` starts in well under a second.
+"""
+import importlib
+
+_EXPORTS = {
+    "DistInfo": "comm", "NodeComm": "comm", "barrier": "comm", "init_from_env": "comm", "shutdown": "comm",
+    "Stripe": "partition", "apply_stripe": "partition", "stripe_for": "partition",
+}
+__all__ = list(_EXPORTS)
+
+
+def __getattr__(name):
+    mod = _EXPORTS.get(name)
+    if mod is None:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    return getattr(importlib.import_module(f"{__name__}.{mod}"), name)

@@ -38,7 +38,7 @@ from otedama_amd.pool.template import BlockTemplate, TemplateSource, merkle_root
 from otedama_amd.pool.vardiff import Vardiff, VardiffConfig, VardiffState
 from otedama_amd.poolproto.stratumv1 import prevhash_to_stratum
 from otedama_amd.stratum import messages as M
-from otedama_amd.stratum.frame import read_frame_async
+from otedama_amd.stratum.frame import FrameReader
 
 BIP320_MASK = 0x1FFFE000
 EN1_SIZE = 4
@@ -508,6 +508,7 @@ class _V2Conn:
 
     def __init__(self, pool: PoolServer, reader, writer):
         self.pool, self.reader, self.writer = pool, reader, writer
+        self.frames = FrameReader(reader)
         self.dialect = pool.opts.dialect
         self.version_rolling = False
         self.channels: dict[int, tuple[_Worker, bytes]] = {}  # channel id -> (worker, extranonce prefix)
@@ -542,7 +543,7 @@ class _V2Conn:
     async def run(self) -> None:
         try:
             while True:
-                f = await asyncio.wait_for(read_frame_async(self.reader), 600)
+                f = await asyncio.wait_for(self.frames.read_frame(), 600)
                 msg = M.dispatch_frame(f, self.dialect)
                 await self._handle(msg)
                 await self.writer.drain()

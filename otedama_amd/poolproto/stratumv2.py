@@ -40,7 +40,7 @@ from otedama_amd.poolproto.base import (
 )
 from otedama_amd.stratum import messages as M
 from otedama_amd.stratum import tls
-from otedama_amd.stratum.frame import read_frame_async
+from otedama_amd.stratum.frame import FrameReader
 
 SUBMIT_MAP_CAP = 1024
 BIP320_MASK = 0x1FFFE000
@@ -50,6 +50,7 @@ class V2Session(Session):
     def __init__(self, reader, writer, creds: Credentials, protocol: ProtocolID, endpoint: str,
                  dialect: str = M.REFERENCE, algorithm: str = "sha256d"):
         self.reader, self.writer = reader, writer
+        self.frames = FrameReader(reader)
         self.creds = creds
         self._protocol = protocol
         self.endpoint = endpoint
@@ -95,7 +96,7 @@ class V2Session(Session):
             await asyncio.wait_for(self.writer.drain(), 10.0)  # write deadline (run.go:1251)
 
     async def _recv(self, timeout: float = 30.0) -> M.Message:
-        f = await asyncio.wait_for(read_frame_async(self.reader), timeout)
+        f = await asyncio.wait_for(self.frames.read_frame(), timeout)
         return M.dispatch_frame(f, self.dialect)
 
     async def handshake(self) -> None:

@@ -133,3 +133,23 @@ def test_registry_text_exposition_escaping_and_order():
     assert 'otedama_a_total{pool="x\\"y\\\\z\\n"} 1' in out
     assert "# TYPE otedama_a_total counter" in out and "# TYPE otedama_b gauge" in out
     assert "otedama_nan NaN" in out and "otedama_inf +Inf" in out
+
+
+@settings(max_examples=400, deadline=None)
+@given(v=st.floats(1e-4, 1e6, exclude_max=True), neg=st.booleans())
+def test_format_float_fast_path_matches_the_decimal_path(v, neg):
+    v = -v if neg else v
+    assert M.format_float(v) == M._format_float_exp(v)
+
+
+def test_gauge_text_cache_follows_value_changes():
+    g = M.Registry().new_gauge("otedama_t", "t")
+    assert g.text() == "0"
+    g.set(-0.0)
+    assert g.text() == "-0"
+    g.set(1.5e7)
+    assert g.text() == "1.5e+07"
+    g.set(float("nan"))
+    assert g.text() == "NaN"
+    g.set(2.0)
+    assert g.text() == "2"

@@ -4,6 +4,7 @@ Mirrors stratum/{frame,messages}_fuzz_test.go, poolproto/stratumv1/parse_test.go
 arbitration/engine_property_test.go, rates/fetcher_test.go, i18n/*_test.go,
 daemon/service_test.go, and adds vardiff + merkle checks for the pool.
 """
+import asyncio
 import http.server
 import threading
 
@@ -20,7 +21,8 @@ from otedama_amd.poolproto.stratumv1 import parse_notify, prevhash_from_stratum,
 from otedama_amd.provider import sats_per_second
 from otedama_amd.rates import Fetcher, Source
 from otedama_amd.stratum import messages as M
-from otedama_amd.stratum.frame import Frame, FrameError, Header, decode_header, encode_frame, iter_frames
+from otedama_amd.stratum.frame import (Frame, FrameError, FrameReader, FrameScanner, Header, decode_header,
+                                       encode_frame, iter_frames)
 
 
 # ------------------------------------------------------------------ frames / messages
@@ -63,6 +65,63 @@ def test_frame_header_u24_and_unknown():
     assert isinstance(msg, M.UnknownMessage)
     with pytest.raises(FrameError):
         decode_header(b"\x00\x00")
+
+
+_frame = st.builds(lambda ext, t, p: Frame(Header(ext, t, len(p)), p),
+                   st.integers(0, 0xFFFF), st.integers(0, 255), st.binary(min_size=4, max_size=300))
+
+
+@settings(max_examples=150, deadline=None)
+@given(frames=st.lists(_frame, max_size=12), cuts=st.lists(st.integers(0, 4000), max_size=8), native=st.booleans())
+def test_frame_scanner_matches_iter_frames_under_any_chunking(frames, cuts, native):
+    raw = b"".join(encode_frame(f) for f in frames)
+    pos = sorted({c % (len(raw) + 1) for c in cuts} | {0, len(raw)})
+    sc = FrameScanner(native=native)
+    got = []
+    for a, b in zip(pos, pos[1:]):
+        got += sc.feed(raw[a:b])
+    assert got == frames == list(iter_frames(raw)) and sc.pending == 0
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(min_size=0, max_size=120), st.integers(7, 64))
+def test_native_and_python_scanners_agree(data, max_frame):
+    from otedama_amd.ops.native import load
+    from otedama_amd.stratum.frame import _scan_py
+
+    mod = load(build_if_missing=False)
+    if mod is None:
+        pytest.skip("native extension not built")
+    recs, consumed, status = mod.sv2_scan(data, max_frame)
+    assert (recs, consumed, status) == _scan_py(data, max_frame)
+
+
+def test_frame_scanner_errors_after_the_good_frames():
+    good = encode_frame(Frame(Header(0, 1, 2), b"ok"))
+    bad_channel = bytes([0, 0x80, 0x20, 2, 0, 0]) + b"xy"      # channel bit, 2-byte payload
+    sc = FrameScanner()
+    assert [f.payload for f in sc.feed(good + bad_channel)] == [b"ok"]
+    with pytest.raises(FrameError, match="channel message requires payload"):
+        sc.feed(b"")
+    huge = bytes([0, 0, 1, 0xFF, 0xFF, 0xFF])                  # 16 MiB + 5 > max frame, rejected on the header
+    with pytest.raises(FrameError, match="exceeds MaxFrameSize"):
+        FrameScanner(max_frame_size=1 << 20).feed(huge)
+    with pytest.raises(FrameError):
+        FrameScanner(max_frame_size=0)
+
+
+def test_frame_reader_chunks_and_eof():
+    async def main():
+        r = asyncio.StreamReader()
+        frames = [Frame(Header(0, 0x20, n), bytes([n & 0xFF]) * n) for n in (0, 5, 1000, 70000)]
+        r.feed_data(b"".join(encode_frame(f) for f in frames) + encode_frame(frames[1])[:4])
+        r.feed_eof()
+        fr = FrameReader(r, chunk=4096)
+        assert [await fr.read_frame() for _ in frames] == frames
+        with pytest.raises(asyncio.IncompleteReadError):
+            await fr.read_frame()
+
+    asyncio.run(main())
 
 
 # ------------------------------------------------------------------ V1 parsing
