@@ -200,7 +200,7 @@ void sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
   while (len - off >= 64) { sha256_compress(st, data + off); off += 64; }
   uint8_t tail[128] = {0};
   size_t rem = len - off;
-  std::memcpy(tail, data + off, rem);
+  if (rem) std::memcpy(tail, data + off, rem);  // data may be null when len == 0
   tail[rem] = 0x80;
   size_t tl = (rem + 9 <= 64) ? 64 : 128;
   uint64_t bits = uint64_t(len) * 8;

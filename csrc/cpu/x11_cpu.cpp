@@ -149,7 +149,7 @@ void blake512(const u8* msg, size_t len, u8 out[64]) {
     u64 total = (u64)len * 8;
     u8 buf[256];
     memset(buf, 0, sizeof buf);
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     if (rem == 128) {  // full last block: padding goes in a block of its own
         blake512_compress(h, buf, total);
         memset(buf, 0, 128);
@@ -278,7 +278,7 @@ void bmw512(const u8* msg, size_t len, u8 out[64]) {
     u8 buf[256];
     memset(buf, 0, sizeof buf);
     size_t rem = len - off;
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     buf[rem] = 0x80;
     if (rem + 1 > 120) {
         for (int i = 0; i < 16; ++i) M[i] = ld64le(buf + 8 * i);
@@ -344,7 +344,7 @@ void groestl512(const u8* msg, size_t len, u8 out[64]) {
     size_t rem = len - off;
     u8 buf[256];
     memset(buf, 0, sizeof buf);
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     buf[rem] = 0x80;
     size_t nb = (rem + 1 + 8 <= 128) ? 1 : 2;
     blocks += nb;
@@ -398,7 +398,7 @@ static void skein_ubi(u64 h[8], const u8* msg, size_t len, u64 type) {
         bool final = off + n == len;
         u8 blk[64];
         memset(blk, 0, 64);
-        memcpy(blk, msg + off, n);
+        if (n) memcpy(blk, msg + off, n);
         u64 m[8], o[8];
         for (int i = 0; i < 8; ++i) m[i] = ld64le(blk + 8 * i);
         u64 tw[2] = {(u64)(off + n), (type << 56) | (first ? (1ULL << 62) : 0) | (final ? (1ULL << 63) : 0)};
@@ -519,7 +519,7 @@ void jh512(const u8* msg, size_t len, u8 out[64]) {
     size_t rem = len - off;
     u8 buf[128];
     memset(buf, 0, sizeof buf);
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     buf[rem] = 0x80;
     size_t nb = rem == 0 ? 1 : 2;
     st64be(buf + 64 * nb - 8, (u64)len * 8);  // 128-bit length, high 64 bits zero
@@ -806,7 +806,7 @@ void shavite512(const u8* msg, size_t len, u8 out[64]) {
     u64 total = (u64)len * 8;
     u8 buf[256];
     memset(buf, 0, sizeof buf);
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     buf[rem] = 0x80;
     auto tail = [&](u8* b) {
         st32le(b + 110, (u32)total); st32le(b + 114, (u32)(total >> 32));
@@ -972,7 +972,7 @@ void echo512(const u8* msg, size_t len, u8 out[64]) {
     u64 total = (u64)len * 8;
     u8 buf[256];
     memset(buf, 0, sizeof buf);
-    memcpy(buf, msg + off, rem);
+    if (rem) memcpy(buf, msg + off, rem);  // msg may be null when len == 0
     buf[rem] = 0x80;
     auto tail = [&](u8* b) { b[110] = 0x00; b[111] = 0x02; st64le(b + 112, total); st64le(b + 120, 0); };
     if (rem + 1 <= 110) {

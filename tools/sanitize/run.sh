@@ -29,4 +29,11 @@ for name in tsan asan; do
   fi
   [ "$rc" -eq 0 ] || { echo "$name run failed (rc=$rc)"; exit "$rc"; }
 done
-echo "sanitize: tsan + asan/ubsan clean"
+# libFuzzer (ASan + UBSan) over the SV2 frame scanner and the CPU hash paths.
+fz="$OUT/fuzz_native"
+"$CXX" -std=c++17 -O1 -g -march=x86-64-v2 "-I$ROOT/csrc/include" -fsanitize=fuzzer,address,undefined \
+  -fno-sanitize-recover=undefined -mllvm -asan-globals=0 "$ROOT/tools/sanitize/fuzz_native.cpp" \
+  "$ROOT/csrc/cpu/sv2_frame.cpp" "$ROOT/csrc/cpu/sha256_cpu.cpp" "$ROOT/csrc/cpu/x11_cpu.cpp" -o "$fz" -lcrypto
+echo "== fuzz: $fz ${SECS}s"
+(cd "$OUT" && "$fz" -max_total_time="$SECS" -max_len=2048 -print_final_stats=1) || { echo "fuzz failed"; exit 1; }
+echo "sanitize: tsan + asan/ubsan + fuzz clean"
