@@ -81,54 +81,56 @@ __device__ __forceinline__ u32 lds_addr(u32 w, int k, u32 laneoff) {
   return __builtin_amdgcn_perm(w, laneoff, 0x0c0c0000u | ((4u + (u32)k) << 8));
 }
 
-// AES: T0 only (T1..T3 are byte rotations), 64 copies, dword 64x + l = T0[x] (ds_read_b32 banks
-// are (a/4) mod 32 per 32-lane half: lane l -> bank l mod 32). 64 KiB.
+// AES: T0 and T1 = rotl8(T0) (T2, T3 are their rotl16), 32 copies each in one 64 KiB image: the 256-byte row
+// of entry x holds T0[x] for lanes l mod 32 in bytes 0..127 and T1[x] in bytes 128..255. ds_read_b32 serves lanes
+// {0-31} and {32-63} in separate LDS cycles with bank (a/4) mod 32, so lane l -> bank l mod 32 for either table:
+// conflict-free. A column is T0[b0] ^ T1[b1] ^ rotl16(T0[b2] ^ T1[b3]): one rotate instead of three.
 constexpr u32 kAesPrivWords = 256 * 64;
 __device__ __forceinline__ void aes_priv_fill(u32* T) {
   for (u32 c = threadIdx.x; c < kAesPrivWords / 4; c += blockDim.x) {
-    const u32 v = x11t::AES_T0[c >> 4];
+    const u32 t0 = x11t::AES_T0[c >> 4];
+    const u32 v = (c & 15u) < 8u ? t0 : rotl32(t0, 8);
     reinterpret_cast<uint4*>(T)[c] = make_uint4(v, v, v, v);
   }
   __syncthreads();
 }
-__device__ __forceinline__ u32 aes_laneoff() { return (threadIdx.x & 63u) << 2; }
+__device__ __forceinline__ u32 aes_laneoff() { return (threadIdx.x & 31u) << 2; }
 __device__ __forceinline__ u32 aes_lk(const u32* T, u32 lo, u32 w, int k) {
   return *reinterpret_cast<const u32*>(reinterpret_cast<const char*>(T) + lds_addr(w, k, lo));
 }
-// AES round (SubBytes, ShiftRows, MixColumns) on four LE column words, then AddRoundKey:
-// the key words ride in the second xor3 of each column, so a keyed round costs no more than
-// a keyless one.
+// AES round (SubBytes, ShiftRows, MixColumns) on four LE column words, then AddRoundKey.
 #define AES_COLS_(T, lo, x0, x1, x2, x3)                                                                   \
-  const u32 a0 = aes_lk(T, lo, x0, 0), a1 = aes_lk(T, lo, x1, 1), a2 = aes_lk(T, lo, x2, 2),          \
-            a3 = aes_lk(T, lo, x3, 3);                                                                \
-  const u32 b0 = aes_lk(T, lo, x1, 0), b1 = aes_lk(T, lo, x2, 1), b2 = aes_lk(T, lo, x3, 2),          \
-            b3 = aes_lk(T, lo, x0, 3);                                                                \
-  const u32 c0 = aes_lk(T, lo, x2, 0), c1 = aes_lk(T, lo, x3, 1), c2 = aes_lk(T, lo, x0, 2),          \
-            c3 = aes_lk(T, lo, x1, 3);                                                                \
-  const u32 d0 = aes_lk(T, lo, x3, 0), d1 = aes_lk(T, lo, x0, 1), d2 = aes_lk(T, lo, x1, 2),          \
-            d3 = aes_lk(T, lo, x2, 3)
+  const u32 lo1_ = (lo) | 0x80u;                                                                        \
+  const u32 a0 = aes_lk(T, lo, x0, 0), a1 = aes_lk(T, lo1_, x1, 1), a2 = aes_lk(T, lo, x2, 2),        \
+            a3 = aes_lk(T, lo1_, x3, 3);                                                              \
+  const u32 b0 = aes_lk(T, lo, x1, 0), b1 = aes_lk(T, lo1_, x2, 1), b2 = aes_lk(T, lo, x3, 2),        \
+            b3 = aes_lk(T, lo1_, x0, 3);                                                              \
+  const u32 c0 = aes_lk(T, lo, x2, 0), c1 = aes_lk(T, lo1_, x3, 1), c2 = aes_lk(T, lo, x0, 2),        \
+            c3 = aes_lk(T, lo1_, x1, 3);                                                              \
+  const u32 d0 = aes_lk(T, lo, x3, 0), d1 = aes_lk(T, lo1_, x0, 1), d2 = aes_lk(T, lo, x1, 2),        \
+            d3 = aes_lk(T, lo1_, x2, 3)
 __device__ __forceinline__ void aes_round_k(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3, u32 k0, u32 k1,
                                             u32 k2, u32 k3) {
   AES_COLS_(T, lo, x0, x1, x2, x3);
-  x0 = xor3(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);
-  x1 = xor3(xor3(b0, rotl32(b1, 8), rotl32(b2, 16)), rotl32(b3, 24), k1);
-  x2 = xor3(xor3(c0, rotl32(c1, 8), rotl32(c2, 16)), rotl32(c3, 24), k2);
-  x3 = xor3(xor3(d0, rotl32(d1, 8), rotl32(d2, 16)), rotl32(d3, 24), k3);
+  x0 = xor3(a0, a1, k0) ^ rotl32(a2 ^ a3, 16);
+  x1 = xor3(b0, b1, k1) ^ rotl32(b2 ^ b3, 16);
+  x2 = xor3(c0, c1, k2) ^ rotl32(c2 ^ c3, 16);
+  x3 = xor3(d0, d1, k3) ^ rotl32(d2 ^ d3, 16);
 }
-// k0 must be wave-uniform (ECHO's counter key): it is read from an SGPR.
+// k0 is ECHO's wave-uniform counter key.
 __device__ __forceinline__ void aes_round_key0(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3, u32 k0) {
   AES_COLS_(T, lo, x0, x1, x2, x3);
-  x0 = bop3s<0x96>(xor3(a0, rotl32(a1, 8), rotl32(a2, 16)), rotl32(a3, 24), k0);  // k0 wave-uniform
-  x1 = xor3(b0, rotl32(b1, 8), rotl32(b2, 16)) ^ rotl32(b3, 24);
-  x2 = xor3(c0, rotl32(c1, 8), rotl32(c2, 16)) ^ rotl32(c3, 24);
-  x3 = xor3(d0, rotl32(d1, 8), rotl32(d2, 16)) ^ rotl32(d3, 24);
+  x0 = xor3(a0, a1, rotl32(a2 ^ a3, 16)) ^ k0;
+  x1 = xor3(b0, b1, rotl32(b2 ^ b3, 16));
+  x2 = xor3(c0, c1, rotl32(c2 ^ c3, 16));
+  x3 = xor3(d0, d1, rotl32(d2 ^ d3, 16));
 }
 __device__ __forceinline__ void aes_round(const u32* T, u32 lo, u32& x0, u32& x1, u32& x2, u32& x3) {
   AES_COLS_(T, lo, x0, x1, x2, x3);
-  x0 = xor3(a0, rotl32(a1, 8), rotl32(a2, 16)) ^ rotl32(a3, 24);
-  x1 = xor3(b0, rotl32(b1, 8), rotl32(b2, 16)) ^ rotl32(b3, 24);
-  x2 = xor3(c0, rotl32(c1, 8), rotl32(c2, 16)) ^ rotl32(c3, 24);
-  x3 = xor3(d0, rotl32(d1, 8), rotl32(d2, 16)) ^ rotl32(d3, 24);
+  x0 = xor3(a0, a1, rotl32(a2 ^ a3, 16));
+  x1 = xor3(b0, b1, rotl32(b2 ^ b3, 16));
+  x2 = xor3(c0, c1, rotl32(c2 ^ c3, 16));
+  x3 = xor3(d0, d1, rotl32(d2 ^ d3, 16));
 }
 #undef AES_COLS_
 
