@@ -60,14 +60,6 @@ __device__ __forceinline__ u32 bop3(u32 a, u32 b, u32 c) {
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(TT));
   return r;
 }
-// Same with a wave-uniform third operand read straight from an SGPR (saves the v_mov an all-"v" constraint
-// forces; VOP3 on gfx950 may read one SGPR).
-template <unsigned TT>
-__device__ __forceinline__ u32 bop3s(u32 a, u32 b, u32 c_uniform) {
-  u32 r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "s"(c_uniform), "i"(TT));
-  return r;
-}
 __device__ __forceinline__ u64 xor3_64(u64 a, u64 b, u64 c) { return mk64(xor3(lo32(a), lo32(b), lo32(c)), xor3(hi32(a), hi32(b), hi32(c))); }
 
 // ---------------------------------------------------------------- bank-private tables
