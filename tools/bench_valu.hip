@@ -27,7 +27,7 @@
 
 #define CLOBBERS                                                                                               \
   "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", \
-      "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "s8", "vcc"
+      "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "s8", "s10", "s11", "vcc"
 
 template <int OP>
 __device__ __forceinline__ void body() {
