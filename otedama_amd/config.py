@@ -45,6 +45,7 @@ class PoolConfig:
     password: str = ""
     payout_scheme: str = ""
     tls_ca_file: str = ""
+    sv2_extended_channel: bool = False  # SV2 only: extended channel (miner-side extranonce rolling)
 
 
 @dataclass

@@ -510,7 +510,8 @@ class Engine:
         creds = Credentials(user=user, password=(pc.password if pc else "") or "x", tls_root_cas_pem=ca,
                             worker=user, version_rolling=self.cfg.mining.version_rolling,
                             device="gfx950" if gpu else "cpu", hardware="v3.0.0",
-                            nominal_hashrate=self.current_hashrate)
+                            nominal_hashrate=self.current_hashrate,
+                            extended_channel=bool(pc.sv2_extended_channel) if pc is not None else False)
         session = await self._dial(url, creds)
         self._session = session
         self.connected = True

@@ -504,7 +504,9 @@ class _V1Conn:
 
 
 class _V2Conn:
-    """One Stratum V2 miner connection (standard channels)."""
+    """One Stratum V2 miner connection: standard channels (header-only jobs, merkle root per channel) and
+    extended channels (coinbase prefix/suffix + merkle path; the miner rolls EN2_SIZE extranonce bytes after the
+    pool's EN1_SIZE prefix and submits them in SubmitSharesExtended)."""
 
     def __init__(self, pool: PoolServer, reader, writer):
         self.pool, self.reader, self.writer = pool, reader, writer
@@ -512,6 +514,7 @@ class _V2Conn:
         self.dialect = pool.opts.dialect
         self.version_rolling = False
         self.channels: dict[int, tuple[_Worker, bytes]] = {}  # channel id -> (worker, extranonce prefix)
+        self.extended: set[int] = set()
         self._next_channel = 1
         self.setup = False
 
@@ -528,9 +531,15 @@ class _V2Conn:
             pass
 
     def _job_msgs(self, ch: int, job: PoolJob, prefix: bytes, future: bool) -> list[M.Message]:
-        root = self.pool.merkle_root_for(job, prefix)
-        j = M.NewMiningJob(ch, job.job_int, has_min_ntime=not future, min_ntime=0 if future else job.ntime,
-                           version=job.version, merkle_root=root)
+        if ch in self.extended:
+            j = M.NewExtendedMiningJob(ch, job.job_int, has_min_ntime=not future, min_ntime=0 if future else job.ntime,
+                                       version=job.version, version_rolling_allowed=self.version_rolling,
+                                       merkle_path=list(job.branches), coinbase_prefix=job.coinb1,
+                                       coinbase_suffix=job.coinb2)
+        else:
+            root = self.pool.merkle_root_for(job, prefix)
+            j = M.NewMiningJob(ch, job.job_int, has_min_ntime=not future, min_ntime=0 if future else job.ntime,
+                               version=job.version, merkle_root=root)
         if future:
             return [j, M.SetNewPrevHash(ch, job.job_int, job.block.prev_hash, job.ntime, job.block.nbits)]
         return [j]
@@ -566,30 +575,43 @@ class _V2Conn:
             self.version_rolling = bool(msg.flags & M.FLAG_REQUIRES_VERSION_ROLLING) and \
                 self.pool.opts.allow_version_rolling
             self._send(M.SetupConnectionSuccess(2, M.FLAG_REQUIRES_VERSION_ROLLING if self.version_rolling else 0))
-        elif isinstance(msg, M.OpenMiningChannel):
+        elif isinstance(msg, (M.OpenMiningChannel, M.OpenExtendedMiningChannel)):
+            extended = isinstance(msg, M.OpenExtendedMiningChannel)
             if not self.setup or not msg.user:
                 self._send(M.OpenMiningChannelError(msg.req_id, "unknown-user" if self.setup else "setup-required"))
                 return
+            if extended and msg.min_extranonce_size > EN2_SIZE:
+                self._send(M.OpenMiningChannelError(msg.req_id, "min-extranonce-size-too-large"))
+                return
             ch = self._next_channel
             self._next_channel += 1
-            prefix = self.pool.next_extranonce(EN1_SIZE + EN2_SIZE)
+            prefix = self.pool.next_extranonce(EN1_SIZE if extended else EN1_SIZE + EN2_SIZE)
             w = self.pool.new_worker(msg.user, BIP320_MASK if self.version_rolling else 0)
             if msg.nominal_hashrate > 0 and self.pool.journal.load_worker(msg.user) is None:
                 w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
                 w.prev_difficulty = w.vd.difficulty
             self.channels[ch] = (w, prefix)
-            self._send(M.OpenMiningChannelSuccess(
-                msg.req_id, ch, self.pool.share_target(w.vd.difficulty), prefix,
-                extranonce2_size=0))
+            target = self.pool.share_target(w.vd.difficulty)
+            if extended:
+                self.extended.add(ch)
+                self._send(M.OpenExtendedMiningChannelSuccess(msg.req_id, ch, target, EN2_SIZE, prefix))
+            else:
+                self._send(M.OpenMiningChannelSuccess(msg.req_id, ch, target, prefix, extranonce2_size=0))
             if self.pool.jobs:
                 for m in self._job_msgs(ch, next(reversed(self.pool.jobs.values())), prefix, future=True):
                     self._send(m)
-        elif isinstance(msg, M.SubmitSharesStandard):
+        elif isinstance(msg, (M.SubmitSharesStandard, M.SubmitSharesExtended)):
             ent = self.channels.get(msg.channel_id)
-            if ent is None:
+            extended = isinstance(msg, M.SubmitSharesExtended)
+            if ent is None or extended != (msg.channel_id in self.extended):
                 self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, "invalid-channel-id"))
                 return
             w, prefix = ent
+            if extended:
+                if len(msg.extranonce) != EN2_SIZE:
+                    self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, "invalid-extranonce-size"))
+                    return
+                prefix = prefix + msg.extranonce
             v = await self.pool.validate_async(w, f"{msg.job_id:x}", prefix, msg.ntime, msg.nonce, msg.nversion)
             if v.accepted:
                 self._send(M.SubmitSharesSuccess(msg.channel_id, msg.sequence_number, 1, max(int(v.difficulty), 1)))
@@ -607,3 +629,4 @@ class _V2Conn:
                 self._send(M.SetTarget(msg.channel_id, self.pool.share_target(w.vd.difficulty)))
         elif isinstance(msg, M.CloseChannel):
             self.channels.pop(msg.channel_id, None)
+            self.extended.discard(msg.channel_id)

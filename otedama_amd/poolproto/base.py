@@ -168,6 +168,7 @@ class Credentials:
     firmware: str = "main"
     device: str = "gfx950"
     nominal_hashrate: float = 0.0
+    extended_channel: bool = False   # SV2: open an extended channel and roll extranonce under the pool's prefix
 
 
 class Session(abc.ABC):

@@ -43,6 +43,7 @@ from otedama_amd.stratum import tls
 from otedama_amd.stratum.frame import FrameReader
 
 SUBMIT_MAP_CAP = 1024
+EXTENDED_MIN_EXTRANONCE = 4   # bytes of extranonce the native runtime rolls per extended channel
 BIP320_MASK = 0x1FFFE000
 
 
@@ -62,6 +63,8 @@ class V2Session(Session):
         self.share_target = b"\xff" * 32
         self.version_mask = 0
         self.extranonce_prefix = b""
+        self.extended = False          # extended channel: jobs carry the coinbase, submits carry our extranonce
+        self.extranonce_size = 0
         self._jobs: dict[int, M.NewMiningJob] = {}
         self._active: M.NewMiningJob | None = None
         self._active_ntime = 0
@@ -113,16 +116,29 @@ class V2Session(Session):
             raise HandshakeFailed(f"expected SetupConnectionSuccess, got {type(resp).__name__}")
         if self.creds.version_rolling and resp.flags & M.FLAG_REQUIRES_VERSION_ROLLING:
             self.version_mask = BIP320_MASK
-        await self.send(M.OpenMiningChannel(req_id=1, user=self.creds.user,
-                                            nominal_hashrate=float(self.creds.nominal_hashrate)))
+        if self.creds.extended_channel:
+            await self.send(M.OpenExtendedMiningChannel(req_id=1, user=self.creds.user,
+                                                        nominal_hashrate=float(self.creds.nominal_hashrate),
+                                                        min_extranonce_size=EXTENDED_MIN_EXTRANONCE))
+            want = M.OpenExtendedMiningChannelSuccess
+        else:
+            await self.send(M.OpenMiningChannel(req_id=1, user=self.creds.user,
+                                                nominal_hashrate=float(self.creds.nominal_hashrate)))
+            want = M.OpenMiningChannelSuccess
         resp = await self._recv()
         if isinstance(resp, M.OpenMiningChannelError):
             raise HandshakeFailed(f"pool rejected OpenMiningChannel: {resp.error}")
-        if not isinstance(resp, M.OpenMiningChannelSuccess):
-            raise HandshakeFailed(f"expected OpenMiningChannelSuccess, got {type(resp).__name__}")
+        if not isinstance(resp, want):
+            raise HandshakeFailed(f"expected {want.__name__}, got {type(resp).__name__}")
         self.channel_id = resp.channel_id
         self.share_target = resp.target
-        self.extranonce_prefix = resp.extranonce
+        if self.creds.extended_channel:
+            if not 0 < resp.extranonce_size <= 8:
+                raise HandshakeFailed(f"extended channel: unsupported extranonce size {resp.extranonce_size}")
+            self.extended = True
+            self.extranonce_prefix, self.extranonce_size = resp.extranonce_prefix, resp.extranonce_size
+        else:
+            self.extranonce_prefix = resp.extranonce
 
     def start(self) -> None:
         self._task = asyncio.ensure_future(self._read_loop())
@@ -139,15 +155,23 @@ class V2Session(Session):
             await self._teardown()
 
     # ---------------------------------------------------------- state machine
-    def _start_job(self, j: M.NewMiningJob, ntime: int) -> None:
+    def _start_job(self, j, ntime: int) -> None:
         self._active, self._active_ntime = j, ntime
-        put_drop_oldest(self.jobs, Job(
-            job_id=str(j.job_id), version=j.version, prev_hash=self._prev_hash, merkle_root=j.merkle_root,
-            ntime=ntime, nbits=self._nbits, clean_jobs=True, target=self.share_target,
-            version_mask=self.version_mask, channel_id=self.channel_id, algorithm=self.algorithm))
+        if isinstance(j, M.NewExtendedMiningJob):  # coinbase + merkle path: the miner builds the root per extranonce
+            job = Job(job_id=str(j.job_id), version=j.version, prev_hash=self._prev_hash, merkle_root=None,
+                      ntime=ntime, nbits=self._nbits, clean_jobs=True, target=self.share_target,
+                      version_mask=self.version_mask if j.version_rolling_allowed else 0, channel_id=self.channel_id,
+                      coinb1=j.coinbase_prefix, coinb2=j.coinbase_suffix, extranonce1=self.extranonce_prefix,
+                      extranonce2_size=self.extranonce_size, merkle_branches=list(j.merkle_path),
+                      algorithm=self.algorithm)
+        else:
+            job = Job(job_id=str(j.job_id), version=j.version, prev_hash=self._prev_hash, merkle_root=j.merkle_root,
+                      ntime=ntime, nbits=self._nbits, clean_jobs=True, target=self.share_target,
+                      version_mask=self.version_mask, channel_id=self.channel_id, algorithm=self.algorithm)
+        put_drop_oldest(self.jobs, job)
 
     def _handle(self, msg: M.Message) -> None:
-        if isinstance(msg, M.NewMiningJob):
+        if isinstance(msg, (M.NewMiningJob, M.NewExtendedMiningJob)):
             self._jobs[msg.job_id] = msg
             self.last_job_received_at = time.time()
             if msg.has_min_ntime and self._have_prev:
@@ -209,8 +233,12 @@ class V2Session(Session):
                 if not f.done():
                     f.set_result(ShareResult(False, "unacknowledged (submit map overflow)"))
         try:
-            await self.send(M.SubmitSharesStandard(self.channel_id, seq, job_id, sub.nonce, sub.ntime,
-                                                   sub.version))
+            if self.extended:
+                await self.send(M.SubmitSharesExtended(self.channel_id, seq, job_id, sub.nonce, sub.ntime,
+                                                       sub.version, bytes(sub.extranonce2)))
+            else:
+                await self.send(M.SubmitSharesStandard(self.channel_id, seq, job_id, sub.nonce, sub.ntime,
+                                                       sub.version))
         except (OSError, asyncio.TimeoutError) as exc:
             self._pending.pop(seq, None)
             raise PoolProtoError(f"stratumv2: submit: {exc}") from exc

@@ -35,14 +35,18 @@ MSG_RECONNECT = 0x04
 MSG_OPEN_MINING_CHANNEL = 0x10
 MSG_OPEN_MINING_CHANNEL_SUCCESS = 0x11
 MSG_OPEN_MINING_CHANNEL_ERROR = 0x12
+MSG_OPEN_EXTENDED_MINING_CHANNEL = 0x13
+MSG_OPEN_EXTENDED_MINING_CHANNEL_SUCCESS = 0x14
 MSG_NEW_MINING_JOB = 0x15
 MSG_UPDATE_CHANNEL = 0x16
 MSG_CLOSE_CHANNEL = 0x18
 MSG_SET_EXTRANONCE_PREFIX = 0x19
 MSG_SUBMIT_SHARES_STANDARD = 0x1A
+MSG_SUBMIT_SHARES_EXTENDED = 0x1B
 MSG_SUBMIT_SHARES_SUCCESS = 0x1C
 MSG_SUBMIT_SHARES_ERROR = 0x1E          # reference id (spec: 0x1d)
 MSG_SUBMIT_SHARES_ERROR_SPEC = 0x1D
+MSG_NEW_EXTENDED_MINING_JOB = 0x1F
 MSG_SET_NEW_PREV_HASH = 0x20
 MSG_SET_TARGET = 0x21
 
@@ -120,6 +124,17 @@ def b0_32(v: bytes) -> bytes:
     if len(v) > 32:
         raise MessageError(f"stratum: byte slice too long for B0_32 ({len(v)} > 32)")
     return bytes([len(v)]) + v
+
+
+def b0_64k(v: bytes) -> bytes:
+    if len(v) > 0xFFFF:
+        raise MessageError(f"stratum: byte slice too long for B0_64K ({len(v)} > 65535)")
+    return struct.pack("<H", len(v)) + v
+
+
+def _b0_64k(r: "_R", what: str) -> bytes:
+    n = r.u16(what)
+    return bytes(r.take(n, what)) if n else b""
 
 
 def _u256(v: bytes, what: str) -> bytes:
@@ -296,6 +311,86 @@ class OpenMiningChannelError(Message):
 
 
 @dataclass
+class OpenExtendedMiningChannel(Message):
+    MSG_TYPE: ClassVar[int] = MSG_OPEN_EXTENDED_MINING_CHANNEL
+    req_id: int = 0
+    user: str = ""
+    nominal_hashrate: float = 0.0
+    max_target: bytes = field(default=b"\xff" * 32)
+    min_extranonce_size: int = 0
+
+    def encode(self, dialect=REFERENCE):
+        return (struct.pack("<I", self.req_id) + str0_255(self.user) + struct.pack("<f", self.nominal_hashrate)
+                + _u256(self.max_target, "max_target") + struct.pack("<H", self.min_extranonce_size))
+
+    @classmethod
+    def decode(cls, payload, dialect=REFERENCE):
+        r = _R(payload, "OpenExtendedMiningChannel")
+        return cls(r.u32("ReqID"), r.str0_255("User"), r.f32("NominalHashrate"), bytes(r.take(32, "MaxTarget")),
+                   r.u16("MinExtranonceSize"))
+
+
+@dataclass
+class OpenExtendedMiningChannelSuccess(Message):
+    MSG_TYPE: ClassVar[int] = MSG_OPEN_EXTENDED_MINING_CHANNEL_SUCCESS
+    req_id: int = 0
+    channel_id: int = 0
+    target: bytes = field(default=b"\xff" * 32)
+    extranonce_size: int = 0          # bytes the miner rolls after the prefix
+    extranonce_prefix: bytes = b""
+
+    def encode(self, dialect=REFERENCE):
+        return (struct.pack("<II", self.req_id, self.channel_id) + _u256(self.target, "target")
+                + struct.pack("<H", self.extranonce_size) + b0_32(self.extranonce_prefix))
+
+    @classmethod
+    def decode(cls, payload, dialect=REFERENCE):
+        r = _R(payload, "OpenExtendedMiningChannelSuccess")
+        return cls(r.u32("ReqID"), r.u32("ChannelID"), bytes(r.take(32, "Target")), r.u16("ExtranonceSize"),
+                   r.b0_255("ExtranoncePrefix"))
+
+
+@dataclass
+class NewExtendedMiningJob(Message):
+    MSG_TYPE: ClassVar[int] = MSG_NEW_EXTENDED_MINING_JOB
+    CHANNEL_MSG: ClassVar[bool] = True
+    channel_id: int = 0
+    job_id: int = 0
+    has_min_ntime: bool = False
+    min_ntime: int = 0
+    version: int = 0
+    version_rolling_allowed: bool = True
+    merkle_path: list = field(default_factory=list)   # U256 branch hashes, leaf (coinbase) side first
+    coinbase_prefix: bytes = b""
+    coinbase_suffix: bytes = b""
+
+    def encode(self, dialect=REFERENCE):
+        if len(self.merkle_path) > 255:
+            raise MessageError("stratum: NewExtendedMiningJob: merkle path longer than 255")
+        b = struct.pack("<II", self.channel_id, self.job_id)
+        b += (b"\x01" + struct.pack("<I", self.min_ntime)) if self.has_min_ntime else b"\x00"
+        b += struct.pack("<IB", self.version & 0xFFFFFFFF, 1 if self.version_rolling_allowed else 0)
+        b += bytes([len(self.merkle_path)]) + b"".join(_u256(h, "merkle_path") for h in self.merkle_path)
+        return b + b0_64k(self.coinbase_prefix) + b0_64k(self.coinbase_suffix)
+
+    @classmethod
+    def decode(cls, payload, dialect=REFERENCE):
+        r = _R(payload, "NewExtendedMiningJob")
+        m = cls(r.u32("ChannelID"), r.u32("JobID"))
+        opt = r.u8("MinNTime")
+        if opt == 1:
+            m.has_min_ntime, m.min_ntime = True, r.u32("MinNTime")
+        elif opt != 0:
+            raise MessageError(f"stratum: NewExtendedMiningJob: invalid OPTION count {opt} for min_ntime")
+        m.version = r.u32("Version")
+        m.version_rolling_allowed = r.u8("VersionRollingAllowed") != 0
+        m.merkle_path = [bytes(r.take(32, "MerklePath")) for _ in range(r.u8("MerklePath"))]
+        m.coinbase_prefix = _b0_64k(r, "CoinbaseTxPrefix")
+        m.coinbase_suffix = _b0_64k(r, "CoinbaseTxSuffix")
+        return m
+
+
+@dataclass
 class NewMiningJob(Message):
     MSG_TYPE: ClassVar[int] = MSG_NEW_MINING_JOB
     CHANNEL_MSG: ClassVar[bool] = True
@@ -448,6 +543,29 @@ class SubmitSharesStandard(Message):
 
 
 @dataclass
+class SubmitSharesExtended(Message):
+    MSG_TYPE: ClassVar[int] = MSG_SUBMIT_SHARES_EXTENDED
+    CHANNEL_MSG: ClassVar[bool] = True
+    channel_id: int = 0
+    sequence_number: int = 0
+    job_id: int = 0
+    nonce: int = 0
+    ntime: int = 0
+    nversion: int = 0
+    extranonce: bytes = b""
+
+    def encode(self, dialect=REFERENCE):
+        return struct.pack("<6I", self.channel_id, self.sequence_number, self.job_id, self.nonce & 0xFFFFFFFF,
+                           self.ntime & 0xFFFFFFFF, self.nversion & 0xFFFFFFFF) + b0_32(self.extranonce)
+
+    @classmethod
+    def decode(cls, payload, dialect=REFERENCE):
+        r = _R(payload, "SubmitSharesExtended")
+        vals = [r.u32(w) for w in ("ChannelID", "SequenceNumber", "JobID", "Nonce", "NTime", "Version")]
+        return cls(*vals, r.b0_255("Extranonce"))
+
+
+@dataclass
 class SubmitSharesSuccess(Message):
     MSG_TYPE: ClassVar[int] = MSG_SUBMIT_SHARES_SUCCESS
     CHANNEL_MSG: ClassVar[bool] = True
@@ -511,7 +629,8 @@ class UnknownMessage(Message):
 _BY_TYPE = {cls.MSG_TYPE: cls for cls in (
     SetupConnection, SetupConnectionSuccess, SetupConnectionError, Reconnect, OpenMiningChannel,
     OpenMiningChannelSuccess, OpenMiningChannelError, NewMiningJob, UpdateChannel, CloseChannel,
-    SetExtranoncePrefix, SetNewPrevHash, SetTarget, SubmitSharesStandard, SubmitSharesSuccess, SubmitSharesError)}
+    SetExtranoncePrefix, SetNewPrevHash, SetTarget, SubmitSharesStandard, SubmitSharesSuccess, SubmitSharesError,
+    OpenExtendedMiningChannel, OpenExtendedMiningChannelSuccess, NewExtendedMiningJob, SubmitSharesExtended)}
 
 
 def wrap_message(msg: Message, dialect: str = REFERENCE) -> Frame:

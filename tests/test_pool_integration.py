@@ -154,3 +154,38 @@ def test_setup_connection_error_is_fatal():
         srv.close()
 
     asyncio.run(_with_pool(body))
+
+
+def test_sv2_extended_channel_rolls_extranonce():
+    """SV2 extended channel (spec §5.3.5-5.3.7/5.3.11/5.3.14): the job carries the coinbase and merkle path, the
+    miner rolls its own extranonce after the pool's prefix, SubmitSharesExtended carries it, and the pool rebuilds
+    the coinbase from prefix + extranonce before re-hashing."""
+    async def body(pool):
+        creds = Credentials(user=ADDR, version_rolling=True, extended_channel=True)
+        s = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", creds)
+        assert s.extended and s.extranonce_size == 4 and len(s.extranonce_prefix) == 4
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        assert job.merkle_root is None and job.coinb1 and job.extranonce1 == s.extranonce_prefix
+        assert job.extranonce2_size == 4 and job.version_mask != 0
+        nonce, ver, nt, en2, hdr = None, None, None, None, None
+        for v in range(1, 64):  # variants with a non-zero extranonce2
+            hdr, ver, nt, en2 = N.variant_header(job.template(), v)
+            if en2:
+                hits = N.cpu_scan_sha256d(hdr, job.template()["target"], 0, 1 << 20)
+                if hits:
+                    nonce = hits[0]
+                    break
+        assert nonce is not None
+        en2b = en2.to_bytes(8, "little")[:4]
+        r = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, en2b))
+        assert r.accepted, r
+        r2 = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, en2b))
+        assert not r2.accepted and "duplicate" in r2.reason
+        r3 = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, en2b[:3]))
+        assert not r3.accepted and r3.reason == "invalid-extranonce-size"
+        other = bytes(b ^ 0xFF for b in en2b)  # same nonce under another extranonce: a different header
+        r4 = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver, other))
+        assert not r4.accepted and "difficulty" in r4.reason
+        await s.close()
+
+    asyncio.run(_with_pool(body))

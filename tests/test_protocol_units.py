@@ -57,6 +57,22 @@ def test_message_roundtrips(ch, job, nonce, ntime, ver, h32):
             assert M.dispatch_frame(f, dialect) == m
 
 
+@settings(max_examples=60, deadline=None)
+@given(ch=st.integers(0, 2 ** 32 - 1), job=st.integers(0, 2 ** 32 - 1), ntime=st.integers(0, 2 ** 32 - 1),
+       path=st.lists(st.binary(min_size=32, max_size=32), max_size=12), pre=st.binary(max_size=300),
+       suf=st.binary(max_size=300), en=st.binary(max_size=32), opt=st.booleans())
+def test_extended_channel_messages_roundtrip(ch, job, ntime, path, pre, suf, en, opt):
+    msgs = [M.OpenExtendedMiningChannel(ch, "u.w", 2.0 ** 40, bytes(range(32)), len(en)),
+            M.OpenExtendedMiningChannelSuccess(ch, job, bytes(32), len(en), en),
+            M.NewExtendedMiningJob(ch, job, opt, ntime if opt else 0, 0x20000000, opt, path, pre, suf),
+            M.SubmitSharesExtended(ch, job, job, ntime, ntime, 0x20002000, en)]
+    for m in msgs:
+        for dialect in (M.REFERENCE, M.SPEC):
+            (f,) = list(iter_frames(M.encode_message(m, dialect)))
+            assert f.header.channel_msg == m.CHANNEL_MSG
+            assert M.dispatch_frame(f, dialect) == m
+
+
 def test_frame_header_u24_and_unknown():
     f = Frame(Header(0, 0x7F, 3), b"abc")
     raw = encode_frame(f)
