@@ -52,15 +52,17 @@ def _metric(body: str, name: str, labels: str = "") -> float | None:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("algorithm,difficulty,min_hashrate", [
-    ("sha256d", 0.25, 1e9),   # ~16 GH/s per GPU: ~15 shares/s before vardiff settles
-    ("scrypt", 16.0, 1e6),    # ~16.7 MH/s per GPU, scrypt diff1 = 0xffff << 224: ~16 shares/s
-    ("x11", 0.005, 1e8),      # ~380 MH/s per GPU, Bitcoin diff1: ~18 shares/s, validated by the pool's CPU chain
+@pytest.mark.parametrize("algorithm,difficulty,min_hashrate,extended", [
+    ("sha256d", 0.25, 1e9, False),   # ~16 GH/s per GPU: ~15 shares/s before vardiff settles
+    ("scrypt", 16.0, 1e6, False),    # ~16.7 MH/s per GPU, scrypt diff1 = 0xffff << 224: ~16 shares/s
+    ("x11", 0.005, 1e8, False),      # ~390 MH/s per GPU, Bitcoin diff1: ~18 shares/s, validated by the pool's CPU chain
+    ("sha256d", 0.25, 1e9, True),    # SV2 extended channel: the GPU miner rolls extranonce in the coinbase
 ])
-def test_cli_run_mines_against_local_pool(tmp_path, algorithm, difficulty, min_hashrate):
+def test_cli_run_mines_against_local_pool(tmp_path, algorithm, difficulty, min_hashrate, extended):
     with _PoolThread(difficulty, algorithm) as pool:
         cfg = tmp_path / "config.yaml"
-        cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: stratum+v2://{pool.addr_sv2}\n"
+        ext = "    sv2_extended_channel: true\n" if extended else ""
+        cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: stratum+v2://{pool.addr_sv2}\n{ext}"
                        f"mining:\n  algorithm: {algorithm}\n  batch_nonces: 134217728\n")
         env = dict(os.environ, HOME=str(tmp_path), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(tmp_path / "d"))
         proc = subprocess.Popen([sys.executable, "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
