@@ -116,6 +116,7 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["dropped"] = s.dropped;
   d["launches"] = s.launches;
   d["rejected_candidates"] = s.rejected_candidates;
+  d["variant_launches"] = s.variant_launches;
   d["busy_seconds"] = s.busy_seconds;
   d["faulted"] = s.faulted;
   d["error"] = s.error;

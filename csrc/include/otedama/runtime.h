@@ -72,6 +72,7 @@ struct MinerStats {
   uint64_t dropped = 0;     // shares dropped because the queue was full
   uint64_t launches = 0;
   uint64_t rejected_candidates = 0;  // top-word ties that failed the full compare
+  uint64_t variant_launches = 0;     // SHA-256d launches that searched K > 1 header variants (shared block 2)
   double busy_seconds = 0;           // device (or thread) time spent hashing
   bool faulted = false;              // the device thread died on a HIP error
   std::string error;

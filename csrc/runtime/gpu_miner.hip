@@ -172,6 +172,7 @@ void GpuMiner::loop() {
     stats_.rejected_candidates += bad;
     stats_.busy_seconds += ms * 1e-3;
     stats_.launches += 1;
+    if (multi) stats_.variant_launches += 1;
     s.busy = false;
     s.job.reset();
   };

@@ -62,15 +62,14 @@ void merkle_root_from_coinbase(const JobTemplate& j, uint64_t en2, uint8_t root[
   }
 }
 
+// Digit order of the variant index, lowest first: BIP320 version bits, then extranonce2, then ntime. Neighbouring
+// stripe positions therefore differ only in the version word (block 1 of the header) and share bytes 64..79, so
+// the K-variant SHA-256d kernel can group them and reuse one block-2 message schedule, also on Stratum V1 jobs
+// with a coinbase (extranonce2 rolls only after the 2^popcount(mask) version variants of one merkle root are
+// used). ntime rolls last: it moves the header clock forward, which pools bound.
 void JobTemplate::variant_header(uint64_t v, uint8_t out[80], uint32_t* version, uint32_t* ntime,
                                  uint64_t* extranonce2) const {
   std::memcpy(out, header, 80);
-  const uint64_t es = en2_space(*this);
-  uint64_t en2 = 0;
-  if (es > 1) {
-    if (es == ~0ull) { en2 = v; v = 0; }
-    else { en2 = v % es; v /= es; }
-  }
   const uint32_t vb = popcount32(version_mask);
   uint32_t ver = load_le32(header);
   if (vb) {
@@ -79,6 +78,12 @@ void JobTemplate::variant_header(uint64_t v, uint8_t out[80], uint32_t* version,
     v /= vs;
     ver = (ver & ~version_mask) | deposit_bits(bits, version_mask);
     store_le32(out, ver);
+  }
+  const uint64_t es = en2_space(*this);
+  uint64_t en2 = 0;
+  if (es > 1) {
+    if (es == ~0ull) { en2 = v; v = 0; }
+    else { en2 = v % es; v /= es; }
   }
   uint32_t nt = load_le32(header + 68);
   if (ntime_roll) {

@@ -39,6 +39,8 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs.string("payout-scheme", "pplns", "Block payout accounting: pplns | prop.")
     fs.string("http-addr", "", "Address for /metrics /healthz /api/v1/pool (empty disables).")
     fs.string("dialect", "reference", "SV2 wire dialect: reference | spec.")
+    fs.bool("sv2-noise", False, "Encrypt SV2 connections with Noise NX (miners pin the printed authority key).")
+    fs.string("noise-authority-key", "", "Hex secp256k1 secret signing the Noise certificate (empty = fresh per run).")
     fs.float("duration", 0.0, "Stop after this many seconds (0 = run until signalled).")
     rc = parse_subcommand(fs, args, stdout, stderr)
     if rc is not None:
@@ -54,6 +56,16 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         err = validate_bitcoin_address(fs["payout-address"])
         if err:
             stderr.write(f"pool: payout address invalid: {err}\n")
+            return EXIT_CONFIG
+    if fs["noise-authority-key"]:
+        from otedama_amd.btccrypto import N as CURVE_ORDER
+
+        try:
+            key = bytes.fromhex(fs["noise-authority-key"])
+        except ValueError:
+            key = b""
+        if len(key) != 32 or not 0 < int.from_bytes(key, "big") < CURVE_ORDER:
+            stderr.write("pool: --noise-authority-key must be 64 hex characters (a secp256k1 secret in [1, n))\n")
             return EXIT_CONFIG
     try:
         return asyncio.run(_serve(fs, algos, stdout))
@@ -78,7 +90,8 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
                            target_share_seconds=fs["share-seconds"], retarget_seconds=fs["retarget-seconds"],
                            block_interval=fs["block-interval"], job_interval=fs["job-interval"],
                            journal_path=journal or ":memory:", payout_scheme=fs["payout-scheme"],
-                           dialect=fs["dialect"])
+                           dialect=fs["dialect"], noise=fs["sv2-noise"],
+                           noise_authority_secret=int(fs["noise-authority-key"] or "0", 16))
 
         def log(level, msg):
             stdout.write(f"[{level}] {msg}\n")

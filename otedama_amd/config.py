@@ -38,6 +38,13 @@ class ConfigError(ValueError):
     pass
 
 
+def _is_xonly_hex(s: str) -> bool:
+    try:
+        return len(s) == 64 and len(bytes.fromhex(s)) == 32
+    except ValueError:
+        return False
+
+
 @dataclass
 class PoolConfig:
     url: str = ""
@@ -46,6 +53,8 @@ class PoolConfig:
     payout_scheme: str = ""
     tls_ca_file: str = ""
     sv2_extended_channel: bool = False  # SV2 only: extended channel (miner-side extranonce rolling)
+    noise: bool = False                 # SV2 only: Noise NX encryption (spec §4); implied by pool_pubkey
+    pool_pubkey: str = ""               # SV2 only: pinned authority key (64 hex chars, x-only secp256k1)
 
 
 @dataclass
@@ -124,6 +133,10 @@ class Config:
                 err = validate_pool_url(p.url)
                 if err:
                     issues.append(f"pools[{i}].url invalid: {err}")
+            if (p.noise or p.pool_pubkey) and p.url and not p.url.startswith(("stratum+v2://", "stratum+v2tls://")):
+                issues.append(f"pools[{i}]: noise / pool_pubkey apply to stratum+v2 URLs only")
+            if p.pool_pubkey and not _is_xonly_hex(p.pool_pubkey):
+                issues.append(f"pools[{i}].pool_pubkey must be 64 hex characters (x-only secp256k1 key)")
             if p.payout_scheme not in PAYOUT_SCHEMES:
                 issues.append(f"pools[{i}].payout_scheme {p.payout_scheme!r} is not one of fpps, pplns, tides, solo")
         if not 0 <= self.arbitration_hysteresis_pct < 1.0:

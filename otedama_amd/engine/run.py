@@ -52,7 +52,7 @@ from otedama_amd.engine.stats import (
 from otedama_amd.metrics import Registry, runtime_collector
 from otedama_amd.models.algorithms import get as get_algorithm
 from otedama_amd.poolproto import Credentials, FatalPoolError, Job, ShareSubmission
-from otedama_amd.poolproto.base import from_url, lookup
+from otedama_amd.poolproto.base import extranonce2_bytes, from_url, lookup
 from otedama_amd.provider import AkashProvider, MiningProvider
 from otedama_amd.utils.clock import SYSTEM, Clock
 from otedama_amd.utils.trace import mark as trace_mark
@@ -511,7 +511,9 @@ class Engine:
                             worker=user, version_rolling=self.cfg.mining.version_rolling,
                             device="gfx950" if gpu else "cpu", hardware="v3.0.0",
                             nominal_hashrate=self.current_hashrate,
-                            extended_channel=bool(pc.sv2_extended_channel) if pc is not None else False)
+                            extended_channel=bool(pc.sv2_extended_channel) if pc is not None else False,
+                            noise=bool(pc.noise) if pc is not None else False,
+                            pool_pubkey=bytes.fromhex(pc.pool_pubkey) if pc is not None and pc.pool_pubkey else b"")
         session = await self._dial(url, creds)
         self._session = session
         self.connected = True
@@ -577,7 +579,7 @@ class Engine:
                 if s["job_id"] not in self._valid_jobs:
                     self.m.stale_skipped.inc()
                     continue
-                en2 = s["extranonce2"].to_bytes(8, "little")[: s["extranonce2_size"]] if s["extranonce2_size"] else b""
+                en2 = extranonce2_bytes(s["extranonce2"], s["extranonce2_size"])
                 key = (s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
                 if key in self._submitted:  # defence in depth: never send a pool a duplicate
                     continue

@@ -66,6 +66,11 @@ class PoolOptions:
     coinbase_message: str = "/otedama-mi355x/"
     dialect: str = M.REFERENCE
     allow_version_rolling: bool = True
+    # SV2 Noise NX (spec §4): the SV2 listener runs the responder handshake, sending a certificate for its static key
+    # signed by the authority key (0 = a fresh authority per process; its x-only public key is `noise_authority_pub`).
+    noise: bool = False
+    noise_authority_secret: int = 0
+    noise_cert_seconds: int = 365 * 86400
 
 
 @dataclass
@@ -140,6 +145,15 @@ class PoolServer:
         self.addr_sv2 = ""
         self.addr_v1 = ""
         self.blocks_found = 0
+        self.noise_authority_pub = b""
+        if self.opts.noise:
+            from otedama_amd.stratum import noise
+
+            auth_priv, self.noise_authority_pub = noise.keypair(self.opts.noise_authority_secret or None)
+            self._noise_static, static_pub = noise.keypair()
+            now = int(time.time())
+            self._noise_cert = noise.certificate_payload(static_pub, auth_priv, now - 3600,
+                                                         now + self.opts.noise_cert_seconds)
         self.accepted = 0
         self.rejected = 0
         self.reject_reasons: dict[str, int] = {}
@@ -180,6 +194,9 @@ class PoolServer:
             self.addr_v1 = f"{a[0]}:{a[1]}"
         self._tasks.append(asyncio.ensure_future(self._refresh_loop()))
         self.log("info", f"pool[{self.algo.name}]: listening sv2={self.addr_sv2 or '-'} v1={self.addr_v1 or '-'}")
+        if self.opts.noise:
+            self.log("info", f"pool[{self.algo.name}]: sv2 Noise NX on; authority pubkey "
+                             f"{self.noise_authority_pub.hex()}")
 
     async def stop(self) -> None:
         for t in self._tasks:
@@ -295,10 +312,13 @@ class PoolServer:
             return self._reject(worker, job_id, "invalid-version-bits")
         if ntime < job.ntime or ntime > max(time.time(), job.ntime) + MAX_NTIME_FUTURE:
             return self._reject(worker, job_id, "invalid-ntime")
-        key = (job_id, extranonce, ntime, nonce, version)
-        if key in self._seen:
+        # Duplicates are keyed on the full 80-byte header, not on the job id: every job of one block shares the
+        # coinbase parts and merkle branches, so one (extranonce, ntime, nonce, version) submitted under several
+        # live job ids is the same work and is credited once.
+        hdr = self.header_for(job, extranonce, version, ntime, nonce)
+        if hdr in self._seen:
             return self._reject(worker, job_id, "duplicate-share")
-        return job, key, self.header_for(job, extranonce, version, ntime, nonce)
+        return job, hdr, hdr
 
     def _finish(self, worker: _Worker, job_id: str, job: PoolJob, key: tuple, h: bytes) -> Verdict:
         # re-checked after the (possibly off-loop) hash: a new block or an identical concurrent submit
@@ -374,6 +394,15 @@ class PoolServer:
             self.m_clients.set(len(self._v1) + len(self._v2))
 
     async def _serve_v2(self, reader, writer) -> None:
+        if self.opts.noise:
+            from otedama_amd.stratum import noise
+
+            try:
+                reader, writer = await noise.server_handshake(reader, writer, self._noise_static, self._noise_cert)
+            except (noise.NoiseError, asyncio.IncompleteReadError, asyncio.TimeoutError, ConnectionError, OSError):
+                writer.close()
+                self.reject_reasons["noise-handshake"] = self.reject_reasons.get("noise-handshake", 0) + 1
+                return
         c = _V2Conn(self, reader, writer)
         self._v2.add(c)
         self.m_clients.set(len(self._v1) + len(self._v2))

@@ -93,6 +93,15 @@ def split_host_port(hostport: str, default_port: int) -> tuple[str, int]:
     return host, int(port)
 
 
+def extranonce2_bytes(value: int, size: int) -> bytes:
+    """Wire bytes of a rolled extranonce2: little-endian, exactly `size` bytes. The native runtime rolls at most the
+    low 8 bytes and zero-fills the rest of the coinbase field (csrc/runtime/miner_common.cpp
+    merkle_root_from_coinbase), so a pool asking for extranonce2_size > 8 gets the same zero padding here."""
+    if size <= 0:
+        return b""
+    return (value & 0xFFFFFFFFFFFFFFFF).to_bytes(max(8, size), "little")[:size]
+
+
 @dataclass
 class Job:
     job_id: str
@@ -169,6 +178,7 @@ class Credentials:
     device: str = "gfx950"
     nominal_hashrate: float = 0.0
     extended_channel: bool = False   # SV2: open an extended channel and roll extranonce under the pool's prefix
+    noise: bool = False              # SV2: Noise NX channel encryption (implied by a pinned pool_pubkey)
 
 
 class Session(abc.ABC):

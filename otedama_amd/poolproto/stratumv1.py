@@ -22,6 +22,7 @@ mining.configure and the rolled bits are submitted as the 6th parameter.
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import json
 import time
 
@@ -222,10 +223,11 @@ class V1Session(Session):
             d = parse_difficulty(params)
             if d is not None and d > 0:
                 self._difficulty = d
-                if self.last_job is not None:  # re-issue the active job with the new share target
-                    j = self.last_job
-                    j.clean_jobs = False
-                    self._emit_job(j, requeue=True)
+                if self.last_job is not None:
+                    # Re-issue the active job with the new share target as a COPY: the original may still be
+                    # queued (notify(clean=true) + set_difficulty in one read) and must keep its clean flag
+                    # and target, or the engine never drops the previous prevhash's work.
+                    self._emit_job(dataclasses.replace(self.last_job, clean_jobs=False))
         elif method == "mining.set_extranonce":
             r = parse_set_extranonce(params)
             if r:
@@ -242,7 +244,7 @@ class V1Session(Session):
             self.last_reconnect = parse_reconnect(params)
             asyncio.ensure_future(self.close())
 
-    def _emit_job(self, job: Job, requeue: bool = False) -> None:
+    def _emit_job(self, job: Job) -> None:
         job.extranonce1 = self.extranonce1
         job.extranonce2_size = self.extranonce2_size
         job.version_mask = self.version_mask

@@ -273,6 +273,29 @@ class V2Session(Session):
             self._task.cancel()
 
 
+async def noise_connect(reader, writer, creds: Credentials, timeout: float, log=None):
+    """Noise NX initiator over an open (TCP or TLS) stream; returns the encrypted reader/writer pair.
+
+    With `creds.pool_pubkey` (the pool's 32-byte x-only authority key) the responder's static key must carry a
+    certificate signed by that authority and valid now (SV2 spec §4.5 SignatureNoiseMessage); anything else is a
+    FatalPoolError so the engine fails over instead of mining on an unauthenticated channel. Without a pinned key
+    the channel is encrypted but the pool is not authenticated, which is logged."""
+    from otedama_amd.stratum import noise
+
+    try:
+        er, ew, payload, static = await noise.client_handshake(reader, writer, timeout=timeout)
+    except (noise.NoiseError, asyncio.IncompleteReadError, asyncio.TimeoutError) as exc:
+        writer.close()
+        raise HandshakeFailed(f"noise handshake: {exc}") from exc
+    if creds.pool_pubkey:
+        if not noise.verify_certificate(payload, static, creds.pool_pubkey, int(time.time())):
+            writer.close()
+            raise FatalPoolError("noise: pool certificate does not verify against the pinned authority key")
+    elif log is not None:
+        log("warn", "stratumv2: Noise channel is encrypted but the pool is not authenticated (no pool_pubkey)")
+    return er, ew
+
+
 class V2Dialer(Dialer):
     def __init__(self, use_tls: bool = False, dialect: str = M.REFERENCE, dial_fn=None):
         self.use_tls = use_tls
@@ -292,6 +315,8 @@ class V2Dialer(Dialer):
         else:
             reader, writer = await tls.open_connection(host, port, self.use_tls, creds.tls_root_cas_pem or None,
                                                        timeout)
+        if creds.noise or creds.pool_pubkey:
+            reader, writer = await noise_connect(reader, writer, creds, timeout, log)
         s = V2Session(reader, writer, creds, self.protocol, f"{host}:{port}", self.dialect, algorithm)
         if log is not None:
             s.log = log

@@ -157,6 +157,17 @@ def test_config_layering_and_validation(tmp_path, monkeypatch):
     assert C.validate_pool_url("stratum+tcp://pool.example:3333") is None
 
 
+def test_config_pool_noise_fields_validate():
+    good = "ab" * 32
+    C.Config(bitcoin_address=ADDR, pools=[C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey=good)]).validate()
+    C.Config(bitcoin_address=ADDR, pools=[C.PoolConfig(url="stratum+v2tls://p:3336", noise=True)]).validate()
+    for bad in (C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey="xyz"),
+                C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey="ab" * 31),
+                C.PoolConfig(url="stratum+tcp://p:3333", noise=True)):
+        with pytest.raises(C.ConfigError):
+            C.Config(bitcoin_address=ADDR, pools=[bad]).validate()
+
+
 def test_config_example_loads():
     cfg, warn = C.load_config_file(str(ROOT / "config.yaml.example"))
     assert warn is None

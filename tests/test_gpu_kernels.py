@@ -266,3 +266,37 @@ def test_doctor_pow_self_test_runs_the_gpu_kernel(algo):
     r = D.check_pow_self_test(cfg).run()
     assert r.status == D.Status.PASS, r.detail
     assert "gfx950" in r.detail and "no gfx950" not in r.detail
+
+
+def test_gpu_miner_groups_v1_coinbase_variants():
+    """A Stratum V1 job with a coinbase (extranonce2_size 4) and a BIP320 mask takes the K-variant kernel: the
+    variant digits put version bits lowest, so neighbouring stripe positions share the merkle root and block 2.
+    Every share re-hashes to its reported hash from the rebuilt coinbase / merkle root."""
+    from otedama_amd.models.header import int_to_hash, sha256d
+
+    N = _native()
+    coinb1, coinb2, en1 = os.urandom(40), os.urandom(50), os.urandom(4)
+    branches = [os.urandom(32), os.urandom(32)]
+    hdr = os.urandom(76) + bytes(4)
+    tgt = int_to_hash((1 << 232) - 1)
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28)
+    m.set_job({"header": hdr, "target": tgt, "epoch": 4, "job_id": "v1", "version_mask": 0x1FFFE000,
+               "coinb1": coinb1, "coinb2": coinb2, "extranonce1": en1, "extranonce2_size": 4,
+               "merkle_branches": branches})
+    m.start()
+    deadline = time.time() + 20
+    shares = []
+    while time.time() < deadline and len(shares) < 10:
+        shares += m.poll(256)
+        time.sleep(0.02)
+    m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["launches"] >= 2 and st["variant_launches"] == st["launches"], st
+    assert len(shares) >= 3, st
+    for s in shares:
+        root = sha256d(coinb1 + en1 + s["extranonce2"].to_bytes(4, "little") + coinb2)
+        for b in branches:
+            root = sha256d(root + b)
+        h80 = struct.pack("<I", s["version"]) + hdr[4:36] + root + hdr[68:76] + struct.pack("<I", s["nonce"])
+        assert sha256d(h80) == s["hash"] and int.from_bytes(s["hash"], "little") <= int.from_bytes(tgt, "little")

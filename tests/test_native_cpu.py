@@ -163,3 +163,26 @@ def test_cpu_scan_pairs_and_tail_match_python(start, count):
         if int.from_bytes(d, "little") <= t_int:
             ref.append(n)
     assert got == ref
+
+
+def test_v1_coinbase_variants_group_by_version_first():
+    """Stratum V1 job with a coinbase (extranonce2_size 4) and a BIP320 mask: neighbouring variant indexes differ
+    only in the version word, so they share header bytes 36..79 (merkle root, ntime, nbits) and the K-variant
+    SHA-256d kernel can group them; extranonce2 rolls once per 2^popcount(mask) versions, ntime last."""
+    mask = 0x1FFFE000
+    coinb1, coinb2, en1 = os.urandom(40), os.urandom(50), bytes.fromhex("f8002c90")
+    j = _job(coinb1=coinb1, coinb2=coinb2, extranonce1=en1, extranonce2_size=4, merkle_branches=[os.urandom(32)],
+             version_mask=mask, ntime_roll=3)
+    assert N.variant_space(j) == (1 << 32) * (1 << 16) * 4
+    h0, v0, nt0, e0 = N.variant_header(j, 0)
+    for v in range(1, 4):
+        h, ver, nt, en2 = N.variant_header(j, v)
+        assert h[36:] == h0[36:] and en2 == e0 == 0 and nt == nt0 and ver != v0
+    h, ver, nt, en2 = N.variant_header(j, 1 << 16)
+    assert en2 == 1 and ver == v0 and nt == nt0 and h[36:68] != h0[36:68]
+    h, ver, nt, en2 = N.variant_header(j, (1 << 16) * (1 << 32))
+    assert en2 == 0 and ver == v0 and nt == nt0 + 1
+    # a device stripe (stride = world size) still groups within the version digit
+    stride = 8
+    hs = [N.variant_header(j, 3 + k * stride)[0] for k in range(4)]
+    assert all(x[36:] == hs[0][36:] for x in hs)

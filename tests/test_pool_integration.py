@@ -168,7 +168,8 @@ def test_sv2_extended_channel_rolls_extranonce():
         assert job.merkle_root is None and job.coinb1 and job.extranonce1 == s.extranonce_prefix
         assert job.extranonce2_size == 4 and job.version_mask != 0
         nonce, ver, nt, en2, hdr = None, None, None, None, None
-        for v in range(1, 64):  # variants with a non-zero extranonce2
+        per_en2 = 1 << bin(job.version_mask).count("1")  # version bits are the lowest variant digit
+        for v in range(per_en2, 64 * per_en2, per_en2 // 2):  # variants with a non-zero extranonce2
             hdr, ver, nt, en2 = N.variant_header(job.template(), v)
             if en2:
                 hits = N.cpu_scan_sha256d(hdr, job.template()["target"], 0, 1 << 20)
@@ -189,3 +190,38 @@ def test_sv2_extended_channel_rolls_extranonce():
         await s.close()
 
     asyncio.run(_with_pool(body))
+
+
+def test_sv2_over_noise_with_pinned_authority():
+    """Noise NX wired end to end: the pool's SV2 listener runs the responder with a certificate signed by its
+    authority key; the client pins that key, the whole SV2 session (setup, channel, job, share, verdict) runs over
+    the encrypted channel, and a wrong pinned key is a FatalPoolError before any SV2 message is sent."""
+    from otedama_amd.poolproto import FatalPoolError
+    from otedama_amd.stratum import noise
+
+    async def body(pool):
+        assert len(pool.noise_authority_pub) == 32
+        creds = Credentials(user=ADDR, pool_pubkey=pool.noise_authority_pub)
+        s = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", creds)
+        assert isinstance(s.reader, noise.EncryptedReader)
+        job = await asyncio.wait_for(s.jobs.get(), 5)
+        nonce, ver, nt, _en2, _hdr = _find_share(job)
+        r = await s.submit(ShareSubmission(job.job_id, nonce, nt, ver))
+        assert r.accepted, r
+        await s.close()
+        _, wrong = noise.keypair()
+        with pytest.raises(FatalPoolError):
+            await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR, pool_pubkey=wrong))
+        # encrypted but unauthenticated (no pinned key) still works, with a warning
+        logs = []
+        s2 = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR, noise=True),
+                                   log=lambda lvl, m: logs.append((lvl, m)))
+        assert any("not authenticated" in m for _, m in logs)
+        await asyncio.wait_for(s2.jobs.get(), 5)
+        await s2.close()
+        # a plaintext client against a Noise listener fails the handshake instead of hanging
+        with pytest.raises(Exception):
+            await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR), timeout=2.0)
+        assert pool.accepted == 1
+
+    asyncio.run(_with_pool(body, noise=True))

@@ -162,6 +162,28 @@ def test_validate_accepts_then_rejects_the_duplicate():
     assert not v.accepted and v.reason == "duplicate-share"
 
 
+def test_same_header_under_two_live_job_ids_is_credited_once():
+    """Jobs of one block share coinbase parts and branches; only ntime differs and the miner picks it. The same
+    (extranonce, ntime, nonce, version) submitted under a second non-clean job id is the same header and work."""
+    p = _pool()
+    first = next(iter(p.jobs.values()))
+    second = p.new_job(clean=False)
+    assert second.job_id != first.job_id and second.coinb1 == first.coinb1
+    w = p.new_worker("rig", BIP320_MASK)
+    en = bytes(EN1_SIZE + EN2_SIZE)
+    ntime = max(first.ntime, second.ntime)
+    for nonce in range(1 << 20):
+        if p.validate(w, first.job_id, en, ntime, nonce, first.version).accepted:
+            break
+    else:
+        raise AssertionError("no share in 2^20 nonces")
+    assert p.header_for(first, en, first.version, ntime, nonce) == p.header_for(second, en, first.version, ntime,
+                                                                                 nonce)
+    v = p.validate(w, second.job_id, en, ntime, nonce, first.version)
+    assert not v.accepted and v.reason == "duplicate-share"
+    assert p.journal.counts()["accepted"] == 1
+
+
 def test_validate_rejection_taxonomy():
     p = _pool()
     job = next(iter(p.jobs.values()))

@@ -335,3 +335,28 @@ def test_hal_capabilities_match_kernels():
     assert set(algorithms.ALGORITHMS) == {"sha256d", "scrypt", "x11"}
     with pytest.raises(ValueError, match="unknown algorithm"):
         algorithms.get("x17")
+
+
+def test_extranonce2_bytes_matches_the_native_coinbase_for_every_size():
+    """The submitted extranonce2 must be the bytes the native runtime put in the coinbase (low 8 bytes rolled,
+    the rest zero), including extranonce2_size > 8 (the old serialisation sent only 8 bytes there)."""
+    from otedama_amd.ops.native import load
+    from otedama_amd.poolproto.base import extranonce2_bytes
+
+    assert extranonce2_bytes(0x1234, 0) == b""
+    assert extranonce2_bytes(0x0102030405060708, 4) == bytes([8, 7, 6, 5])
+    assert extranonce2_bytes(0x0102030405060708, 12) == bytes([8, 7, 6, 5, 4, 3, 2, 1, 0, 0, 0, 0])
+    N = load()
+    if N is None:
+        return
+    import hashlib
+
+    def sha256d(b):
+        return hashlib.sha256(hashlib.sha256(b).digest()).digest()
+
+    coinb1, coinb2, en1 = b"\x01" * 41, b"\x02" * 30, b"\xaa\xbb\xcc\xdd"
+    for size in (1, 4, 8, 12, 16):
+        j = {"header": bytes(80), "target": b"\xff" * 32, "epoch": 1, "job_id": "1", "coinb1": coinb1,
+             "coinb2": coinb2, "extranonce1": en1, "extranonce2_size": size, "merkle_branches": []}
+        en2 = 0xA1B2C3D4E5F60718 & ((1 << (8 * min(size, 8))) - 1)
+        assert N.merkle_root(j, en2) == sha256d(coinb1 + en1 + extranonce2_bytes(en2, size) + coinb2)

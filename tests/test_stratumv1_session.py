@@ -114,6 +114,10 @@ def test_set_difficulty_reissues_the_active_job():
         again = await asyncio.wait_for(s.jobs.get(), 5)
         assert again.job_id == first.job_id and not again.clean_jobs
         assert hash_to_int(again.target) == hash_to_int(target_from_difficulty(8.0))
+        # the queued original is a different object and keeps its clean flag and the target it was issued with
+        assert again is not first
+        assert first.clean_jobs
+        assert hash_to_int(first.target) == hash_to_int(target_from_difficulty(1.0))
         assert s.suggested_difficulty() == 8.0
         await s.close()
         await pool.stop()
