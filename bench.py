@@ -60,7 +60,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
-    ap.add_argument("--sha-variants", type=int, default=4,
+    ap.add_argument("--sha-variants", type=int, default=8,
                     help="BIP320 version variants per SHA-256d launch sharing the block-2 schedule (1 = single midstate)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
@@ -85,7 +85,7 @@ def main() -> int:
 
     job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1
     stripe = stripe_for(info.rank, info.world_size)
-    K = max(1, min(args.sha_variants, N.SHA256D_MAX_K))
+    K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
     search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
     world = info.world_size
     slot_words = 1 + (2 if K > 1 else 1) * search.cap

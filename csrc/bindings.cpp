@@ -240,6 +240,12 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   });
   m.attr("SHA256D_MAX_K") = kSha256dMaxK;
+  {
+    py::list ks;
+    for (int k = 2; k <= kSha256dMaxK; ++k)
+      if (sha256d_k_floor(k) == k) ks.append(k);
+    m.attr("SHA256D_K_VALUES") = py::tuple(ks);
+  }
   m.def("sha256d_prepare_k", [](const py::list& headers, const py::bytes& t) {
     std::string ts = need(t, 32, "target");
     std::vector<std::string> hs;
@@ -248,7 +254,7 @@ PYBIND11_MODULE(_native, m) {
     for (auto& h : hs) ptrs.push_back(reinterpret_cast<const uint8_t*>(h.data()));
     Sha256dParamsK p;
     if (!sha256d_prepare_k(ptrs.data(), (int)ptrs.size(), reinterpret_cast<const uint8_t*>(ts.data()), &p))
-      throw std::invalid_argument("need 2..SHA256D_MAX_K headers with identical bytes 64..75");
+      throw std::invalid_argument("need K headers (K in SHA256D_K_VALUES) with identical bytes 64..75");
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   }, py::arg("headers"), py::arg("target"));
   m.def("scrypt_prepare", [](const py::bytes& h, const py::bytes& t) {
@@ -341,7 +347,7 @@ PYBIND11_MODULE(_native, m) {
   py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")
       .def(py::init<int, std::string, uint64_t, int, size_t, int>(), py::arg("device"), py::arg("device_id"),
            py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024,
-           py::arg("sha_variants") = 4);
+           py::arg("sha_variants") = 8);
   py::class_<CpuMiner, MinerBase, std::shared_ptr<CpuMiner>>(m, "CpuMiner")
       .def(py::init<int, std::string, size_t>(), py::arg("threads"), py::arg("device_id") = "cpu-0",
            py::arg("queue_cap") = 1024);

@@ -53,7 +53,7 @@ void scrypt_prepare(const uint8_t header80[80], const uint8_t target32[32], Scry
 namespace otedama {
 
 bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t target32[32], Sha256dParamsK* out) {
-  if (k < 2 || k > kSha256dMaxK) return false;
+  if (k < 2 || k > kSha256dMaxK || sha256d_k_floor(k) != k) return false;
   for (int v = 1; v < k; ++v)
     for (int i = 64; i < 76; ++i)
       if (headers80[v][i] != headers80[0][i]) return false;

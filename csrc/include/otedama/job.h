@@ -25,10 +25,14 @@ struct Sha256dParams {
 // and a 32-byte little-endian target.
 void sha256d_prepare(const uint8_t header80[80], const uint8_t target32[32], Sha256dParams* out);
 
-// K (2..4) header variants with identical bytes 64..79 (block 2 of the first hash: merkle tail,
+// K (2..16) header variants with identical bytes 64..79 (block 2 of the first hash: merkle tail,
 // ntime, nbits, nonce) and different block 1 (BIP320 version rolling): one shared block-2 message
 // schedule per nonce, K midstates (sha256d_search_k).
-constexpr int kSha256dMaxK = 4;
+constexpr int kSha256dMaxK = 16;
+// The K values sha256d_search_k is instantiated for; sha256d_k_floor(k) is the largest one <= k (1 if k < 2).
+constexpr int sha256d_k_floor(int k) {
+  return k >= 16 ? 16 : k >= 12 ? 12 : k >= 8 ? 8 : k >= 6 ? 6 : k >= 4 ? 4 : k >= 3 ? 3 : k >= 2 ? 2 : 1;
+}
 struct Sha256dVariant {
   uint32_t mid[8];
   uint32_t st3[8];
@@ -40,7 +44,7 @@ struct Sha256dParamsK {
   int32_t k;
   Sha256dVariant var[kSha256dMaxK];
 };
-// Returns false (and leaves *out undefined) unless 2 <= k <= kSha256dMaxK and every header has the
+// Returns false (and leaves *out undefined) unless k is an instantiated K (sha256d_k_floor(k) == k) and every header has the
 // same bytes 64..75.
 bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t target32[32], Sha256dParamsK* out);
 

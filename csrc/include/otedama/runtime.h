@@ -126,8 +126,9 @@ class MinerBase {
 // One host thread per GPU: double-buffered batches on a private HIP stream.
 class GpuMiner : public MinerBase {
  public:
-  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling), 1..4.
-  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 4);
+  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling), 1..16
+  // (rounded down to an instantiated K: 2, 3, 4, 6, 8, 12, 16).
+  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 8);
   ~GpuMiner() override;
   void start() override;
   void stop() override;

@@ -105,10 +105,55 @@ extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search(
 // W16..W63 (~460 VALU per nonce): each lane computes W once and advances K states in lockstep
 // (the overt-AsicBoost observation, applied per lane). Hash 2 depends on each variant's digest and
 // runs per variant. Every variant still scans the full nonce range with its own fixed midstate.
+//
+// Register budget (hipcc -Rpass-analysis=kernel-resource-usage, gfx950): the per-variant constants
+// (18 words each) are re-read from the kernarg segment with s_load on every nonce instead of being
+// hoisted out of the nonce loop. Hoisted, they overflow the 102 SGPRs and spill into VGPR lanes
+// (133 v_readlane/v_writelane per loop trip at K=4, 700 at K=8). Re-read, K=4 needs 79 VGPRs and no
+// lane spills, and K=8 fits 121 VGPRs (4 waves/SIMD). Static VALU per variant-hash: K=4 2202, K=8 2146,
+// K=16 2115. The file is built with a raised -pragma-unroll-threshold (otedama_amd/_build.py): at
+// K >= 6 the round loop is otherwise left rolled and W[]/state arrays go to scratch.
 namespace {
 
+using KParamsK = const __attribute__((address_space(4))) otedama::Sha256dParamsK;
+
+// Hash 2 of one variant from its first-hash state: returns H7.
+template <class M>
+__device__ __forceinline__ uint32_t sha256_h7_of_state(const M& mid, uint32_t a0, uint32_t b0, uint32_t c0,
+                                                       uint32_t d0, uint32_t e0, uint32_t f0, uint32_t g0, uint32_t h0) {
+  uint32_t X[61];
+  X[0] = mid[0] + a0; X[1] = mid[1] + b0; X[2] = mid[2] + c0; X[3] = mid[3] + d0;
+  X[4] = mid[4] + e0; X[5] = mid[5] + f0; X[6] = mid[6] + g0; X[7] = mid[7] + h0;
+  X[8] = 0x80000000u;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) X[i] = 0u;
+  X[15] = 256u;
+  uint32_t a = kIV[0], b = kIV[1], c = kIV[2], d = kIV[3], e = kIV[4], f = kIV[5], g = kIV[6], h = kIV[7];
+#pragma unroll
+  for (int t = 0; t < 61; ++t) {
+    if (t >= 16) X[t] = ss1(X[t - 2], t >= 18) + X[t - 7] + ss0(X[t - 15], t <= 22 || t >= 31) + X[t - 16];
+    const uint32_t t1 = h + bS1(e) + ch(e, f, g) + (Kf(t) + X[t]);
+    const uint32_t ne = d + t1;
+    const uint32_t na = t1 + bS0(a) + maj(a, b, c);
+    h = g; g = f; f = e; e = ne; d = c; c = b; b = a; a = na;
+  }
+  return e + kIV[7];
+}
+
+// Hash 2 of variants V..K-1 by compile-time recursion: a runtime loop over the variants is not
+// unrolled for large K, and its A[v]..H[v] indexing would then live in scratch.
+template <int V, int K>
+__device__ __forceinline__ void hash2_all(KParamsK& p, const uint32_t* A, const uint32_t* B, const uint32_t* C,
+                                          const uint32_t* D, const uint32_t* E, const uint32_t* F, const uint32_t* G,
+                                          const uint32_t* H, uint32_t* h7) {
+  if constexpr (V < K) {
+    h7[V] = sha256_h7_of_state(p.var[V].mid, A[V], B[V], C[V], D[V], E[V], F[V], G[V], H[V]);
+    hash2_all<V + 1, K>(p, A, B, C, D, E, F, G, H, h7);
+  }
+}
+
 template <int K>
-__device__ __forceinline__ void sha256d_h7_k(const otedama::Sha256dParamsK& p, uint32_t w3, uint32_t h7[K]) {
+__device__ __forceinline__ void sha256d_h7_k(KParamsK& p, uint32_t w3, uint32_t h7[K]) {
   uint32_t W[64];
   W[0] = p.w0; W[1] = p.w1; W[2] = p.w2; W[3] = w3;
   W[4] = 0x80000000u;
@@ -120,7 +165,7 @@ __device__ __forceinline__ void sha256d_h7_k(const otedama::Sha256dParamsK& p, u
   uint32_t A[K], B[K], C[K], D[K], E[K], F[K], G[K], H[K];
 #pragma unroll
   for (int v = 0; v < K; ++v) {  // round 3: T1 = pre3 + nonce
-    const otedama::Sha256dVariant& q = p.var[v];
+    const auto& q = p.var[v];
     const uint32_t t1 = q.pre3 + w3;
     H[v] = q.st3[6]; G[v] = q.st3[5]; F[v] = q.st3[4]; E[v] = q.st3[3] + t1;
     D[v] = q.st3[2]; C[v] = q.st3[1]; B[v] = q.st3[0]; A[v] = t1 + q.t2_3;
@@ -136,27 +181,7 @@ __device__ __forceinline__ void sha256d_h7_k(const otedama::Sha256dParamsK& p, u
       H[v] = G[v]; G[v] = F[v]; F[v] = E[v]; E[v] = D[v] + t1; D[v] = C[v]; C[v] = B[v]; B[v] = A[v]; A[v] = t1 + t2;
     }
   }
-#pragma unroll
-  for (int v = 0; v < K; ++v) {
-    const otedama::Sha256dVariant& q = p.var[v];
-    uint32_t X[61];
-    X[0] = q.mid[0] + A[v]; X[1] = q.mid[1] + B[v]; X[2] = q.mid[2] + C[v]; X[3] = q.mid[3] + D[v];
-    X[4] = q.mid[4] + E[v]; X[5] = q.mid[5] + F[v]; X[6] = q.mid[6] + G[v]; X[7] = q.mid[7] + H[v];
-    X[8] = 0x80000000u;
-#pragma unroll
-    for (int i = 9; i < 15; ++i) X[i] = 0u;
-    X[15] = 256u;
-    uint32_t a = kIV[0], b = kIV[1], c = kIV[2], d = kIV[3], e = kIV[4], f = kIV[5], g = kIV[6], h = kIV[7];
-#pragma unroll
-    for (int t = 0; t < 61; ++t) {
-      if (t >= 16) X[t] = ss1(X[t - 2], t >= 18) + X[t - 7] + ss0(X[t - 15], t <= 22 || t >= 31) + X[t - 16];
-      const uint32_t t1 = h + bS1(e) + ch(e, f, g) + (Kf(t) + X[t]);
-      const uint32_t ne = d + t1;
-      const uint32_t na = t1 + bS0(a) + maj(a, b, c);
-      h = g; g = f; f = e; e = ne; d = c; c = b; b = a; a = na;
-    }
-    h7[v] = e + kIV[7];
-  }
+  hash2_all<0, K>(p, A, B, C, D, E, F, G, H, h7);
 }
 
 }  // namespace
@@ -165,12 +190,16 @@ __device__ __forceinline__ void sha256d_h7_k(const otedama::Sha256dParamsK& p, u
 template <int K>
 __global__ __launch_bounds__(256) void otd_sha256d_search_k(const otedama::Sha256dParamsK p, uint32_t base,
                                                             uint64_t count, uint32_t* __restrict__ out, uint32_t cap) {
+  (void)p;  // read through the kernarg segment pointer below (p is the first kernel argument, offset 0)
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint64_t off = tid; off < count; off += stride) {
     const uint32_t nonce = base + static_cast<uint32_t>(off);
+    // Opaque per trip: the compiler cannot hoist the (scalar) parameter loads out of the loop.
+    KParamsK* pp = (KParamsK*)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(pp));
     uint32_t h7[K];
-    sha256d_h7_k<K>(p, __builtin_bswap32(nonce), h7);
+    sha256d_h7_k<K>(*pp, __builtin_bswap32(nonce), h7);
 #pragma unroll
     for (int v = 0; v < K; ++v) {
       if (__builtin_bswap32(h7[v]) <= p.target_hi) {
@@ -183,9 +212,16 @@ __global__ __launch_bounds__(256) void otd_sha256d_search_k(const otedama::Sha25
     }
   }
 }
-template __global__ void otd_sha256d_search_k<2>(const otedama::Sha256dParamsK, uint32_t, uint64_t, uint32_t*, uint32_t);
-template __global__ void otd_sha256d_search_k<3>(const otedama::Sha256dParamsK, uint32_t, uint64_t, uint32_t*, uint32_t);
-template __global__ void otd_sha256d_search_k<4>(const otedama::Sha256dParamsK, uint32_t, uint64_t, uint32_t*, uint32_t);
+#define OTD_SHA_K_INSTANCE(K) \
+  template __global__ void otd_sha256d_search_k<K>(const otedama::Sha256dParamsK, uint32_t, uint64_t, uint32_t*, uint32_t);
+OTD_SHA_K_INSTANCE(2)
+OTD_SHA_K_INSTANCE(3)
+OTD_SHA_K_INSTANCE(4)
+OTD_SHA_K_INSTANCE(6)
+OTD_SHA_K_INSTANCE(8)
+OTD_SHA_K_INSTANCE(12)
+OTD_SHA_K_INSTANCE(16)
+#undef OTD_SHA_K_INSTANCE
 
 namespace otedama {
 
@@ -198,9 +234,11 @@ hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t
 hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
                                    int grid, hipStream_t stream) {
   switch (p.k) {
-    case 2: hipLaunchKernelGGL(otd_sha256d_search_k<2>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
-    case 3: hipLaunchKernelGGL(otd_sha256d_search_k<3>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
-    case 4: hipLaunchKernelGGL(otd_sha256d_search_k<4>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
+#define OTD_SHA_K_CASE(K) \
+  case K: hipLaunchKernelGGL(otd_sha256d_search_k<K>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
+    OTD_SHA_K_CASE(2) OTD_SHA_K_CASE(3) OTD_SHA_K_CASE(4) OTD_SHA_K_CASE(6) OTD_SHA_K_CASE(8) OTD_SHA_K_CASE(12)
+    OTD_SHA_K_CASE(16)
+#undef OTD_SHA_K_CASE
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -130,9 +130,9 @@ void GpuMiner::loop() {
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
   // X11: eleven stage kernels per batch over a 64 B/nonce digest buffer (512 MiB at 2^23).
   const uint32_t x11_batch = 1u << 23;
-  // K-variant SHA-256d kernel: 4 waves/SIMD (K states per lane), best at 8 blocks of 256 per CU
-  // (tools/bench_sha_k.py: K=4 18.3 GH/s vs 16.3 single-midstate).
-  grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 8;
+  // K-variant SHA-256d kernel (K states per lane, 4-6 waves/SIMD): 16 blocks of 256 per CU
+  // (tools/bench_sha_k.py sweeps K and the grid; profiles/r2/).
+  grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
 
   uint64_t cur_gen = ~0ull;
   uint64_t k = 0;       // variant-stripe position
@@ -208,7 +208,7 @@ void GpuMiner::loop() {
         if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
         ++kv;
       }
-      s.nvar = kv;
+      s.nvar = sha256d_k_floor(kv);  // kernels exist for K in {2,3,4,6,8,12,16}
     }
     s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch"
                           : job->algo == Algo::kX11  ? "otd.x11.batch"
@@ -238,9 +238,12 @@ void GpuMiner::loop() {
       const uint8_t* hs[kSha256dMaxK];
       for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
       if (!sha256d_prepare_k(hs, s.nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
-      // Keep one launch's duration (job-switch latency) independent of K: nonces per
-      // variant = batch / 2 or / 4 (batch is a power of two that tiles 2^32, so this still tiles it).
-      s.count = batch_ >= 4 ? batch_ / (s.nvar == 2 ? 2 : 4) : batch_;
+      // Keep one launch's duration (job-switch latency) about independent of K: nonces per
+      // variant = batch / (largest power of two <= K); batch is a power of two that tiles 2^32, so this
+      // still tiles it.
+      uint64_t div = 1;
+      while (div * 2 <= (uint64_t)s.nvar && div * 2 <= batch_) div *= 2;
+      s.count = batch_ / div;
       OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_k_, stream));
     } else {
       Sha256dParams p;

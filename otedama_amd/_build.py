@@ -72,6 +72,12 @@ def _compile(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
 
 
+# Per-source extra hipcc flags. sha256d_search.hip: the K-variant kernels (K up to 16) unroll 60 rounds x K
+# states; above LLVM's default pragma-unroll budget the round loop stays rolled and the message schedule and
+# state arrays go to scratch (see the kernel's header comment).
+EXTRA_FLAGS = {"kernels/sha256d_search.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
+
+
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:
     import pybind11
 
@@ -89,7 +95,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         obj = BUILD / (rel.replace("/", "_") + ".o")
         objs.append(obj)
         if force or _stale(obj, src, deps):
-            tasks.append([hipcc, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)])
+            tasks.append([hipcc, f"--offload-arch={ARCH}", *common, *EXTRA_FLAGS.get(rel, []), "-c", str(src), "-o",
+                          str(obj)])
     for rel in CXX_SOURCES:
         src = CSRC / rel
         if not src.exists():

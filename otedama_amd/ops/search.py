@@ -21,7 +21,7 @@ from otedama_amd.ops.native import require_native
 # Blocks of 256 lanes per CU that stay resident for the SHA-256d kernel
 # (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
 SHA256D_BLOCKS_PER_CU = 6
-SHA256D_K_BLOCKS_PER_CU = 8  # K-variant kernel: 99-121 VGPRs (4 waves/SIMD); grid sweep 4/6/8 per CU: 18.0/18.2/18.3 GH/s
+SHA256D_K_BLOCKS_PER_CU = 16  # K-variant kernel: K=8 121 VGPRs (4 waves/SIMD); 4/8/12/16 per CU: 18.05/18.48/18.72/18.80 GH/s
 SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
 
 
@@ -100,8 +100,8 @@ class Sha256dSearchK:
 
     def __init__(self, device="cuda:0", k: int = 4, cap: int = 1024, grid: int | None = None):
         self.native = require_native()
-        if not 2 <= k <= self.native.SHA256D_MAX_K:
-            raise ValueError(f"k must be in [2, {self.native.SHA256D_MAX_K}]")
+        if k not in self.native.SHA256D_K_VALUES:
+            raise ValueError(f"k must be one of {self.native.SHA256D_K_VALUES}")
         self.k = k
         self.device = torch.device(device)
         self.cap = cap

@@ -235,7 +235,7 @@ def test_gpu_fault_retires_device_and_survivor_takes_the_stripe():
     assert any("re-split" in m for m in logs)
 
 
-@pytest.mark.parametrize("k", [2, 3, 4])
+@pytest.mark.parametrize("k", [2, 3, 4, 6, 8, 12, 16])
 def test_sha256d_k_variants_match_cpu(k):
     """K BIP320 version variants sharing block 2: every variant's hits equal the CPU scan of its own header."""
     from otedama_amd.models.header import int_to_hash

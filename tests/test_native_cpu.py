@@ -110,6 +110,25 @@ def test_prepare_sizes():
     assert len(N.scrypt_prepare(GEN, bytes(32))) == N.SCRYPT_PARAMS_SIZE
 
 
+def test_sha256d_prepare_k_accepts_only_instantiated_k():
+    """The K-variant kernel exists for K in SHA256D_K_VALUES; prepare refuses other K and headers whose block 2
+    (bytes 64..75) differs, since the variants share that block's message schedule."""
+    assert N.SHA256D_K_VALUES == (2, 3, 4, 6, 8, 12, 16) and N.SHA256D_MAX_K == 16
+    hdrs = [struct.pack("<I", 0x20000000 | (v << 13)) + GEN[4:] for v in range(16)]
+    for k in range(1, 18):
+        if k in N.SHA256D_K_VALUES:
+            blob = N.sha256d_prepare_k(hdrs[:k], bytes(32))
+            # w0..w17 + target_hi + k, then SHA256D_MAX_K variants of 18 words
+            assert len(blob) == 4 * (7 + 18 * N.SHA256D_MAX_K)
+            assert struct.unpack_from("<i", blob, 24)[0] == k
+        else:
+            with pytest.raises(ValueError):
+                N.sha256d_prepare_k((hdrs * 2)[:k], bytes(32))
+    bad = hdrs[:3] + [hdrs[3][:70] + b"\xff" + hdrs[3][71:]]
+    with pytest.raises(ValueError):
+        N.sha256d_prepare_k(bad, bytes(32))
+
+
 def test_cpu_miner_runtime_emits_verified_shares():
     m = N.CpuMiner(2, "cpu-0")
     tgt = int_to_hash((1 << 244) - 1)

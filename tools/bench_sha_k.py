@@ -1,6 +1,7 @@
-"""SHA-256d: single-midstate kernel vs the K-variant shared-schedule kernel, full 2^32 nonces per launch.
+"""SHA-256d: single-midstate kernel vs the K-variant shared-schedule kernel over K and the grid.
 
-python tools/bench_sha_k.py   -> one JSON line per (kernel, grid): GH/s per GPU (hashes = K x 2^32 per launch)
+python tools/bench_sha_k.py [--count LOG2] [--ks 4,8,16] [--bpc 4,8]
+  -> one JSON line per (kernel, grid): GH/s per GPU (hashes = K x count per launch)
 """
 from __future__ import annotations
 
@@ -13,12 +14,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main() -> int:
+    import argparse
+
     import torch
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--count", type=int, default=32, help="log2 nonces per variant per launch")
+    ap.add_argument("--ks", default="2,3,4,6,8,12,16")
+    ap.add_argument("--bpc", default="4,6,8", help="blocks of 256 per CU")
+    a = ap.parse_args()
+    count = 1 << a.count
 
     from otedama_amd.ops.search import Sha256dSearch, Sha256dSearchK
 
     tail = bytes(range(4, 76)) + bytes(4)
-    headers = [struct.pack("<I", 0x20000000 | (v << 13)) + tail for v in range(4)]
+    headers = [struct.pack("<I", 0x20000000 | (v << 13)) + tail for v in range(16)]
     target = bytes(32)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -35,13 +45,13 @@ def main() -> int:
 
     s1 = Sha256dSearch("cuda:0")
     p1 = s1.prepare(headers[0], target)
-    print(json.dumps({"kernel": "k1", "grid": s1.grid, "ghs": round(run(lambda: s1.launch(p1, 0, 1 << 32), 1 << 32) / 1e9, 3)}),
+    print(json.dumps({"kernel": "k1", "grid": s1.grid, "ghs": round(run(lambda: s1.launch(p1, 0, count), count) / 1e9, 3)}),
           flush=True)
-    for k in (2, 3, 4):
-        for bpc in (4, 6, 8):
+    for k in map(int, a.ks.split(",")):
+        for bpc in map(int, a.bpc.split(",")):
             s = Sha256dSearchK("cuda:0", k=k, grid=cus * bpc)
             p = s.prepare(headers[:k], target)
-            rate = run(lambda: s.launch(p, 0, 1 << 32), k << 32)
+            rate = run(lambda: s.launch(p, 0, count), k * count)
             print(json.dumps({"kernel": f"k{k}", "grid": s.grid, "ghs": round(rate / 1e9, 3)}), flush=True)
     return 0
 
