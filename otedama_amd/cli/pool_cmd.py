@@ -5,6 +5,9 @@ each gets its own SV2 + V1 listener pair (ports increment per algorithm), its
 own vardiff / diff1 constant and share journal, and all publish into one
 /metrics registry — the "mixed SHA-256d + scrypt workers" pool of BASELINE.json
 config 5.
+
+Settings come from flags, then the config file's ``pool_server`` section (plus ``http_addr``), then the flag
+defaults: an explicitly given flag always wins.
 """
 from __future__ import annotations
 
@@ -22,6 +25,30 @@ def _bump(addr: str, k: int) -> str:
         return ""
     h, _, p = addr.rpartition(":")
     return f"{h}:{int(p) + k}" if p and int(p) else addr
+
+
+def apply_config_file(fs: FlagSet, stderr: TextIO) -> None:
+    """Fill every flag the user did not give from the config file's pool_server section."""
+    from otedama_amd.cli.main import load_config
+
+    cfg = load_config(fs, stderr)
+    ps = cfg.pool_server
+    pairs = (("algorithms", ps.algorithm), ("listen-sv2", ps.listen_sv2), ("listen-v1", ps.listen_v1),
+             ("difficulty", ps.initial_difficulty), ("share-seconds", ps.target_share_seconds),
+             ("retarget-seconds", ps.vardiff_retarget_seconds), ("journal", ps.journal_path),
+             ("http-addr", cfg.http_addr))
+    default = type(ps)()
+    for flag, value in pairs:
+        unset_in_file = flag != "http-addr" and value == getattr(default, _FILE_FIELD[flag])
+        if flag in fs.set_flags or unset_in_file or value in ("", None):
+            continue
+        fs.values[flag] = value
+    fs.values["coinbase-message"] = ps.coinbase_message
+
+
+_FILE_FIELD = {"algorithms": "algorithm", "listen-sv2": "listen_sv2", "listen-v1": "listen_v1",
+               "difficulty": "initial_difficulty", "share-seconds": "target_share_seconds",
+               "retarget-seconds": "vardiff_retarget_seconds", "journal": "journal_path"}
 
 
 def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
@@ -42,9 +69,11 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs.bool("sv2-noise", False, "Encrypt SV2 connections with Noise NX (miners pin the printed authority key).")
     fs.string("noise-authority-key", "", "Hex secp256k1 secret signing the Noise certificate (empty = fresh per run).")
     fs.float("duration", 0.0, "Stop after this many seconds (0 = run until signalled).")
+    fs.string("config", "", "Path to the YAML config file (default: $OTEDAMA_CONFIG or ~/.config/otedama/config.yaml).")
     rc = parse_subcommand(fs, args, stdout, stderr)
     if rc is not None:
         return rc
+    apply_config_file(fs, stderr)
     algos = [a.strip() for a in fs["algorithms"].split(",") if a.strip()]
     for a in algos:
         if a not in ("sha256d", "scrypt", "x11"):
@@ -91,6 +120,7 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
                            block_interval=fs["block-interval"], job_interval=fs["job-interval"],
                            journal_path=journal or ":memory:", payout_scheme=fs["payout-scheme"],
                            dialect=fs["dialect"], noise=fs["sv2-noise"],
+                           coinbase_message=fs.values.get("coinbase-message", PoolOptions.coinbase_message),
                            noise_authority_secret=int(fs["noise-authority-key"] or "0", 16))
 
         def log(level, msg):

@@ -239,9 +239,11 @@ def resolve_with_origins(from_file: Config, env: dict[str, str] | None, flags: F
             setattr(cfg, name, getattr(f, name))
             o[name] = ValueOrigin.FILE
     # zero-value caveat: a numeric 0 in the file means "unset" (config.go:427-457)
+    # (a field the file never set keeps its origin DEFAULT even when the dataclass default is non-zero)
     for name in ("arbitration_hysteresis_pct", "min_yield_sats_per_sec", "curtail_below_btc_usd", "power_watts",
                  "electricity_price_per_kwh"):
-        if getattr(f, name) != 0:
+        set_in_file = name in file_keys if file_keys is not None else getattr(f, name) != getattr(cfg, name)
+        if getattr(f, name) != 0 and set_in_file:
             setattr(cfg, name, getattr(f, name))
             o[name] = ValueOrigin.FILE
     if f.mining != MiningConfig():
