@@ -24,6 +24,7 @@ from __future__ import annotations
 import asyncio
 import dataclasses
 import json
+import math
 import time
 
 from otedama_amd.models.header import target_from_difficulty
@@ -49,6 +50,7 @@ MAX_LINE_BYTES = 64 << 10
 READ_DEADLINE = 300.0
 WRITE_DEADLINE = 10.0
 BIP320_MASK = 0x1FFFE000
+MAX_EXTRANONCE2_SIZE = 32  # bytes; a larger (or negative) size from a pool is treated as malformed
 USER_AGENT = "Otedama/3.0.0-mi355x"
 
 
@@ -132,6 +134,12 @@ def parse_subscribe_result(result) -> tuple[str, int]:
         raise HandshakeFailed(f"stratumv1: extranonce1 not a string: {type(en1).__name__}")
     if not isinstance(size, (int, float)) or isinstance(size, bool):
         raise HandshakeFailed(f"stratumv1: extranonce2_size not a number: {type(size).__name__}")
+    if not 0 <= size <= MAX_EXTRANONCE2_SIZE or size != int(size):
+        raise HandshakeFailed(f"stratumv1: extranonce2_size {size} out of range [0, {MAX_EXTRANONCE2_SIZE}]")
+    try:
+        bytes.fromhex(en1)
+    except ValueError:
+        raise HandshakeFailed(f"stratumv1: extranonce1 is not hex: {en1[:32]!r}") from None
     return en1, int(size)
 
 
@@ -212,16 +220,17 @@ class V1Session(Session):
             if fut is not None and not fut.done():
                 fut.set_result((msg.get("result"), msg.get("error")))
             return
-        params = msg.get("params")
+        try:
+            self._dispatch_method(method, msg.get("params"))
+        except (ValueError, TypeError, OverflowError):
+            return  # a malformed notification is dropped; it never ends the session
+
+    def _dispatch_method(self, method, params) -> None:
         if method == "mining.notify":
-            try:
-                job = parse_notify(params)
-            except (ValueError, TypeError):
-                return
-            self._emit_job(job)
+            self._emit_job(parse_notify(params))
         elif method == "mining.set_difficulty":
             d = parse_difficulty(params)
-            if d is not None and d > 0:
+            if d is not None and d > 0 and math.isfinite(d):
                 self._difficulty = d
                 if self.last_job is not None:
                     # Re-issue the active job with the new share target as a COPY: the original may still be
@@ -230,9 +239,9 @@ class V1Session(Session):
                     self._emit_job(dataclasses.replace(self.last_job, clean_jobs=False))
         elif method == "mining.set_extranonce":
             r = parse_set_extranonce(params)
-            if r:
-                self.extranonce1 = bytes.fromhex(r[0])
-                self.extranonce2_size = r[1]
+            if r and 0 <= r[1] <= MAX_EXTRANONCE2_SIZE:
+                en1 = bytes.fromhex(r[0])
+                self.extranonce1, self.extranonce2_size = en1, r[1]
         elif method == "mining.set_version_mask":
             if isinstance(params, list) and params and isinstance(params[0], str):
                 self.version_mask = int(params[0], 16) & BIP320_MASK
