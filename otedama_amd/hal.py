@@ -18,9 +18,10 @@ render nodes that the HIP driver already owns are not reported twice.
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
 import os
+import queue
 import threading
+import time
 from dataclasses import dataclass, field
 from enum import Enum
 from typing import Callable, Protocol
@@ -244,28 +245,45 @@ class Detector:
         self.timeout = timeout
 
     def detect(self) -> list:
+        """Enumerate every driver concurrently (registry.go:138-201). A driver that fails is logged and skipped;
+        one that is still running after ``timeout`` is logged and abandoned (its daemon thread is not joined),
+        and the devices of the drivers that finished are returned."""
         drivers = self.registry.drivers()
         if not drivers:
             return []
-        out = []
-        with cf.ThreadPoolExecutor(max_workers=len(drivers)) as ex:
-            futs = {ex.submit(d.enumerate): d for d in drivers}
-            for fut in cf.as_completed(futs, timeout=self.timeout):
-                d = futs[fut]
-                try:
-                    devs = fut.result()
-                except Exception as exc:  # noqa: BLE001 - partial failure tolerated
+        results: queue.Queue = queue.Queue()
+
+        def run(d):
+            try:
+                results.put((d, d.enumerate(), None))
+            except Exception as exc:  # noqa: BLE001 - partial failure tolerated
+                results.put((d, None, exc))
+
+        for d in drivers:
+            threading.Thread(target=run, args=(d,), name=f"otedama-hal-{d.name()}", daemon=True).start()
+        out, pending = [], {d.name() for d in drivers}
+        deadline = time.monotonic() + self.timeout
+        while pending:
+            try:
+                d, devs, exc = results.get(timeout=max(0.0, deadline - time.monotonic()))
+            except queue.Empty:
+                for name in sorted(pending):
                     if self.logger:
-                        self.logger(d.name(), "enumerate failed", exc)
+                        self.logger(name, "enumerate timed out", TimeoutError(f"no result after {self.timeout} s"))
+                break
+            pending.discard(d.name())
+            if exc is not None:
+                if self.logger:
+                    self.logger(d.name(), "enumerate failed", exc)
+                continue
+            for dev in devs or []:
+                try:
+                    dev.identity().validate()
+                except HalError as exc:
+                    if self.logger:
+                        self.logger(d.name(), "device rejected due to invalid identity", exc)
                     continue
-                for dev in devs or []:
-                    try:
-                        dev.identity().validate()
-                    except HalError as exc:
-                        if self.logger:
-                            self.logger(d.name(), "device rejected due to invalid identity", exc)
-                        continue
-                    out.append(dev)
+                out.append(dev)
         out.sort(key=lambda d: d.identity().id)
         return out
 
