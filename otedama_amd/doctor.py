@@ -15,11 +15,11 @@ path) are module attributes so tests can point them at loopback servers.
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
 import email.utils
 import json
 import os
 import socket
+import threading
 import time
 import urllib.request
 from dataclasses import dataclass, field
@@ -27,7 +27,7 @@ from enum import IntEnum
 from typing import Callable, TextIO
 
 from otedama_amd import config as C
-from otedama_amd.poolproto.base import from_url, split_host_port, strip_scheme, ProtocolID
+from otedama_amd.poolproto.base import from_url, split_host_port, strip_scheme
 
 
 class Status(IntEnum):
@@ -110,17 +110,27 @@ class Runner:
         self.timeout = timeout
 
     def run(self) -> Report:
+        """One daemon thread per check (doctor.go:226-244). A check still running at ``timeout`` is reported as
+        FAIL "check timed out" and abandoned; the report never waits for it."""
         t0 = time.monotonic()
         results: list[Result | None] = [None] * len(self.checks)
-        with cf.ThreadPoolExecutor(max_workers=max(len(self.checks), 1)) as ex:
-            futs = {ex.submit(self._one, c): i for i, c in enumerate(self.checks)}
-            done, pending = cf.wait(futs, timeout=self.timeout)
-            for f in done:
-                results[futs[f]] = f.result()
-            for f in pending:
-                i = futs[f]
-                results[i] = Result(self.checks[i].name, Status.FAIL, "check timed out", "", self.timeout)
-        return Report([r for r in results if r is not None], time.monotonic() - t0)
+        done = threading.Semaphore(0)
+
+        def run_one(i: int, c: Check) -> None:
+            results[i] = self._one(c)
+            done.release()
+
+        for i, c in enumerate(self.checks):
+            threading.Thread(target=run_one, args=(i, c), name=f"otedama-doctor-{i}", daemon=True).start()
+        deadline = t0 + self.timeout
+        for _ in self.checks:
+            if not done.acquire(timeout=max(0.0, deadline - time.monotonic())):
+                break
+        out = []
+        for i, c in enumerate(self.checks):
+            r = results[i]
+            out.append(r if r is not None else Result(c.name, Status.FAIL, "check timed out", "", self.timeout))
+        return Report(out, time.monotonic() - t0)
 
     @staticmethod
     def _one(c: Check) -> Result:
@@ -394,7 +404,10 @@ def check_payout_scheme(cfg: C.Config) -> Check:
             return Result(status=Status.SKIP, detail="no pools configured; using built-in default")
         lines, unknown = [], False
         for p in cfg.pools:
-            host = strip_scheme(p.url) if from_url(p.url) != ProtocolID.UNKNOWN else p.url
+            try:
+                host = strip_scheme(p.url)
+            except Exception:  # noqa: BLE001 - unknown scheme or empty host: show the raw URL
+                host = p.url
             if p.payout_scheme in desc:
                 lines.append(f"{host}: {desc[p.payout_scheme]}")
             else:
@@ -452,7 +465,10 @@ def check_clock() -> Check:
             return Result(status=Status.SKIP, detail=f"clock probe unavailable: {exc}")
         if not date:
             return Result(status=Status.SKIP, detail="probe returned no Date header")
-        skew = abs(time.time() - email.utils.parsedate_to_datetime(date).timestamp())
+        try:
+            skew = abs(time.time() - email.utils.parsedate_to_datetime(date).timestamp())
+        except (TypeError, ValueError):
+            return Result(status=Status.SKIP, detail=f"probe returned an unparseable Date header {date[:40]!r}")
         if skew > 120:
             return Result(status=Status.WARN, detail=f"local clock is {skew:.0f}s off server time",
                           fix="enable NTP (timedatectl set-ntp true); share nTime and TLS depend on it")
