@@ -40,7 +40,8 @@ from otedama_amd.poolproto.base import (
 )
 from otedama_amd.stratum import messages as M
 from otedama_amd.stratum import tls
-from otedama_amd.stratum.frame import FrameReader
+from otedama_amd.stratum.frame import FrameError, FrameReader
+from otedama_amd.stratum.noise import NoiseError
 
 SUBMIT_MAP_CAP = 1024
 EXTENDED_MIN_EXTRANONCE = 4   # bytes of extranonce the native runtime rolls per extended channel
@@ -148,9 +149,9 @@ class V2Session(Session):
             while not self._closed:
                 msg = await self._recv(timeout=300.0)
                 self._handle(msg)
-        except (asyncio.IncompleteReadError, asyncio.TimeoutError, ConnectionError, OSError, M.MessageError,
-                EOFError):
-            pass
+        except (asyncio.IncompleteReadError, asyncio.TimeoutError, ConnectionError, OSError, FrameError, EOFError,
+                NoiseError):
+            pass  # FrameError: oversized / malformed frame or undecodable message; NoiseError: bad Noise tag
         finally:
             await self._teardown()
 

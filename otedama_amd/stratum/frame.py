@@ -187,6 +187,11 @@ class FrameScanner:
         """Bytes held for a frame that is not complete yet."""
         return len(self._buf)
 
+    @property
+    def error(self) -> FrameError | None:
+        """The bad-header error found after the frames the last ``feed`` returned (raised by the next ``feed``)."""
+        return self._err
+
     def feed(self, data: bytes) -> list[Frame]:
         if self._err is not None:
             raise self._err
@@ -219,6 +224,10 @@ class FrameReader:
 
     async def read_frame(self) -> Frame:
         while not self._ready:
+            if self._scanner.error is not None:
+                # a bad header arrived in the same read as the frames already returned: fail now instead of
+                # waiting on the socket for data that would only be rejected
+                raise self._scanner.error
             data = await self.reader.read(self.chunk)
             if not data:
                 raise asyncio.IncompleteReadError(b"", self._scanner.pending or HEADER_SIZE)

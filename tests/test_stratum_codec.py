@@ -359,3 +359,18 @@ def test_setup_connection_flag_bits():
 def test_non_utf8_strings_decode_with_replacement():
     payload = struct.pack("<I", 1) + bytes([3]) + b"\xff\xfe\xfd"
     assert M.SetupConnectionError.decode(payload).error == "�" * 3
+
+
+def test_frame_reader_raises_a_buffered_bad_header_without_waiting_for_more_data():
+    good = M.encode_message(M.SetTarget(1, U256))
+    bad = F.Header(0, 0x15, F.MAX_MESSAGE_LENGTH).encode()
+
+    async def go():
+        r = asyncio.StreamReader()
+        r.feed_data(good + bad)  # one socket read carries a good frame and an oversized header; no EOF follows
+        fr = F.FrameReader(r)
+        assert M.dispatch_frame(await fr.read_frame()) == M.SetTarget(1, U256)
+        with pytest.raises(F.FrameError, match="MaxFrameSize"):
+            await asyncio.wait_for(fr.read_frame(), 1.0)
+
+    asyncio.run(go())
