@@ -119,8 +119,12 @@ def main() -> int:
         if record:
             hits_log.append((hdr, gathered[info.rank].clone()))
 
+    # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
+    # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
+    if (args.steps + args.warmup) * K * world > 1 << 16:
+        raise SystemExit("bench.py: (steps + warmup) x variants x GPUs exceeds the 2^16 version-rolling space")
     for i in range(args.warmup):
-        step(1000 + i, False)
+        step(args.steps + i, False)
     torch.cuda.synchronize(dev)
     barrier(info)
     torch.cuda.synchronize(dev)
