@@ -2,7 +2,7 @@
 //
 // Why: every hash kernel here is VALU-issue bound, and the per-op cost decides which form of a round is
 // cheapest (VOP2 pairs vs VOP3 fused ops, operand VGPR banks, SGPR operands). Each wave runs `iters`
-// bodies of 32 independent instructions of one op (tools/bench_valu_bodies.h) on fixed registers; B blocks
+// bodies of kBodyLen (64) independent instructions of one op (tools/bench_valu_bodies.h) on fixed registers; B blocks
 // of 256 threads per CU put B waves on every SIMD. Reported per (op, B):
 //   cyc  = s_memtime cycles of a block / (B * instructions per wave)  -> SIMD cycles per wave-instruction
 //   wall = same from hipEvent time at the device's max clock
@@ -64,7 +64,7 @@ int main() {
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   const double clk_hz = prop.clockRate * 1e3;
-  const int iters = 2048, max_b = 8;
+  const int iters = 1024, max_b = 8;
   unsigned long long* cyc;
   uint32_t* out;
   CHECK(hipMalloc(&cyc, sizeof(unsigned long long) * cus * max_b));
@@ -94,7 +94,7 @@ int main() {
         best_ms = std::min(best_ms, (double)ms);
         best_cyc = std::min(best_cyc, mean);
       }
-      const double instr_per_wave = (double)iters * 32;
+      const double instr_per_wave = (double)iters * kBodyLen;
       const double cyc_per = best_cyc / (b * instr_per_wave);
       const double wall_per = best_ms * 1e-3 * clk_hz / (b * instr_per_wave);
       std::printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"cyc_per_instr\": %.3f, \"wall_cyc_per_instr\": %.3f}",
