@@ -64,8 +64,12 @@ class WordList:
             raise SeedError(f"lightning: wordlist has {len(words)} words, need 2048")
         index: dict[str, int] = {}
         for i, w in enumerate(words):
-            if not w:
+            if not isinstance(w, str) or not w:
                 raise SeedError(f"lightning: wordlist entry {i} is empty")
+            try:
+                w.encode("utf-8")
+            except UnicodeEncodeError:  # lone surrogates, e.g. bytes decoded with surrogateescape
+                raise SeedError(f"lightning: wordlist entry at index {i} is not valid UTF-8") from None
             if w in index:
                 raise SeedError(f"lightning: wordlist contains duplicate word {w!r}")
             index[w] = i
@@ -97,6 +101,7 @@ def english_wordlist() -> WordList:
 
 
 def entropy_to_mnemonic(e: bytes, wl: WordList | None = None) -> list[str]:
+    """BIP-39 words for `e`; `wl` defaults to the pinned English list (the reference requires a non-nil list)."""
     validate_entropy(e)
     wl = wl or english_wordlist()
     ent = len(e) * 8
@@ -111,17 +116,22 @@ def mnemonic_to_entropy(words: list[str] | str, wl: WordList | None = None) -> b
         words = words.split()
     wl = wl or english_wordlist()
     n = len(words)
+    if n == 0:
+        raise SeedError("lightning: mnemonic is empty")
     if n not in (12, 15, 18, 21, 24):
         raise SeedError(f"lightning: mnemonic has {n} words (want 12, 15, 18, 21 or 24)")
     v = 0
-    for w in words:
-        v = (v << 11) | wl.index(w)
+    for i, w in enumerate(words):
+        try:
+            v = (v << 11) | wl.index(w)
+        except SeedError as exc:
+            raise SeedError(f"lightning: word {i}: {exc}") from None
     total = n * 11
     cs = total // 33
     ent = total - cs
     e = (v >> cs).to_bytes(ent // 8, "big")
     if (v & ((1 << cs) - 1)) != hashlib.sha256(e).digest()[0] >> (8 - cs):
-        raise SeedError("lightning: mnemonic checksum mismatch")
+        raise SeedError("lightning: mnemonic checksum mismatch; check for transcription errors")
     return e
 
 

@@ -59,8 +59,14 @@ def derive_key(passphrase: str, salt: bytes) -> bytes:
 def encrypt_seed(seed: bytes, passphrase: str, reader: Reader | None = None) -> EncryptedSeed:
     if not passphrase:
         raise SeedError("lightning: passphrase must not be empty")
-    salt = _read_exact(reader, 16)
-    nonce = _read_exact(reader, 12)
+    try:
+        salt = _read_exact(reader, 16)
+    except SeedError as exc:
+        raise SeedError(f"lightning: salt generation failed: {exc}") from exc
+    try:
+        nonce = _read_exact(reader, 12)
+    except SeedError as exc:
+        raise SeedError(f"lightning: nonce generation failed: {exc}") from exc
     key = derive_key(passphrase, salt)
     return EncryptedSeed(VERSION, salt, nonce, aead.seal(aead.AES256GCM, key, nonce, seed))
 

@@ -40,9 +40,16 @@ class WalletManager:
         self.wordlist = wordlist or S.english_wordlist()
         self._seed = b""
         self._mnemonic: list[str] | None = None
-        self.data_dir.mkdir(mode=0o700, parents=True, exist_ok=True)
-        if not (self.data_dir / WALLET_FILE).exists():
+        try:
+            self.data_dir.mkdir(mode=0o700, parents=True, exist_ok=True)
+        except OSError as exc:
+            raise WalletError(f"lightning: create data dir {data_dir!r}: {exc}") from exc
+        try:
+            (self.data_dir / WALLET_FILE).stat()
+        except FileNotFoundError:
             self._create(passphrase, mnemonic_passphrase, reader)
+        except OSError as exc:
+            raise WalletError(f"lightning: stat wallet file: {exc}") from exc
         else:
             self._load(passphrase)
 
@@ -63,11 +70,17 @@ class WalletManager:
         return self._mnemonic is not None
 
     def _create(self, passphrase: str, mnemonic_passphrase: str, reader) -> None:
-        entropy = S.generate_entropy(S.DEFAULT_ENTROPY_BITS, reader)
-        words = S.entropy_to_mnemonic(entropy, self.wordlist)
+        try:
+            entropy = S.generate_entropy(S.DEFAULT_ENTROPY_BITS, reader)
+        except S.SeedError as exc:
+            raise WalletError(f"lightning: generate entropy: {exc}") from exc
+        try:
+            words = S.entropy_to_mnemonic(entropy, self.wordlist)
+        except S.SeedError as exc:
+            raise WalletError(f"lightning: entropy to mnemonic: {exc}") from exc
         seed = S.mnemonic_to_seed(words, mnemonic_passphrase)
-        self._seed, self._mnemonic = seed, words
         self._save(seed, passphrase, reader)
+        self._seed, self._mnemonic = seed, words
         try:
             fp = self.data_dir / FINGERPRINT_FILE
             fp.write_text(S.fingerprint(seed))
@@ -86,14 +99,21 @@ class WalletManager:
             raise WalletError(f"lightning: unmarshal wallet: {exc}") from exc
 
     def _load(self, passphrase: str) -> None:
+        es = self._read()  # read / unmarshal errors are reported as such (wallet.go:207-215)
         try:
-            self._seed = SS.decrypt_seed(self._read(), passphrase)
+            self._seed = SS.decrypt_seed(es, passphrase)
         except S.SeedError:
             raise WalletError("lightning: wallet unlock failed — check your passphrase") from None
 
     def _save(self, seed: bytes, passphrase: str, reader) -> None:
-        raw = SS.encrypt_seed(seed, passphrase, reader).marshal()
-        fd, tmp = tempfile.mkstemp(prefix=".wallet-", suffix=".tmp", dir=self.data_dir)
+        try:
+            raw = SS.encrypt_seed(seed, passphrase, reader).marshal()
+        except S.SeedError as exc:
+            raise WalletError(f"lightning: encrypt seed: {exc}") from exc
+        try:
+            fd, tmp = tempfile.mkstemp(prefix=".wallet-", suffix=".tmp", dir=self.data_dir)
+        except OSError as exc:
+            raise WalletError(f"lightning: create temp wallet file: {exc}") from exc
         try:
             with os.fdopen(fd, "wb") as f:
                 f.write(raw)
@@ -101,19 +121,22 @@ class WalletManager:
                 os.fsync(f.fileno())
             os.chmod(tmp, 0o600)
             os.replace(tmp, self.data_dir / WALLET_FILE)
-        except BaseException:
+        except BaseException as exc:
             try:
                 os.unlink(tmp)
             except OSError:
                 pass
+            if isinstance(exc, OSError):
+                raise WalletError(f"lightning: write wallet file: {exc}") from exc
             raise
 
     def change_passphrase(self, old: str, new: str, reader: S.Reader | None = None) -> None:
         if not new:
             raise WalletError("lightning: new passphrase must not be empty")
+        es = self._read()
         try:
-            seed = SS.decrypt_seed(self._read(), old)
-        except SS.WrongPassphrase:
+            seed = SS.decrypt_seed(es, old)
+        except S.SeedError:
             raise WalletError("lightning: incorrect old passphrase") from None
         self._save(seed, new, reader)
 
