@@ -101,7 +101,10 @@ def base58check_encode(payload: bytes) -> str:
 def validate_base58_address(addr: str) -> AddressType:
     if not addr or addr.startswith(("bc1", "BC1")) or not addr.startswith(("1", "3")):
         raise NotBase58("btccrypto: not a base58 address")
-    raw = base58_decode(addr)
+    try:
+        raw = base58_decode(addr)
+    except BtcCryptoError as exc:
+        raise BtcCryptoError(f"btccrypto: {exc}") from None
     if len(raw) != 25:
         raise BtcCryptoError(f"btccrypto: base58 address decodes to {len(raw)} bytes, want 25")
     payload, checksum = raw[:21], raw[21:]
