@@ -20,7 +20,7 @@ def hashrate_string(hps: float) -> str:
     for name, scale in units:
         if hps >= scale:
             return f"{hps / scale:.2f} {name}"
-    return f"{hps:.2f} H/s"
+    return f"{hps:.0f} H/s"  # worker.go:296: whole hashes below 1 kH/s
 
 
 class HashrateWindow:
