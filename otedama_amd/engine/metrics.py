@@ -168,6 +168,8 @@ class EngineMetrics:
         g.set(hps)
 
     def set_active_payout(self, masked: str) -> None:
+        if not masked:  # metrics.go:513: an empty address never creates a series
+            return
         with self._lock:
             for addr, g in self._payout_info.items():
                 g.set(1 if addr == masked else 0)

@@ -142,12 +142,15 @@ class WalletManager:
 
 
 def recovery_phrase_banner(mnemonic: list[str] | None, fingerprint: str) -> str:
+    """The one-time recovery-phrase block (engine/setup.go:175-197); "" when there is nothing to show."""
     if not mnemonic:
         return ""
     bar = "=" * 72
     return (f"\n{bar}\n  WALLET RECOVERY PHRASE — SHOWN ONCE, NEVER AGAIN\n{bar}\n\n"
             f"  {' '.join(mnemonic)}\n\n  Fingerprint: {fingerprint}\n\n"
-            f"  Write these {len(mnemonic)} words on paper, in order, and keep them\n"
-            "  offline. They are the ONLY way to recover the wallet if wallet.dat\n"
-            "  is lost. Otedama will not display them again.\n"
+            f"  Write these {len(mnemonic)} words on paper, in order, and store them somewhere\n"
+            "  safe and offline. They are the ONLY way to recover your funds if\n"
+            "  wallet.dat is lost or the disk fails.\n\n"
+            "  This phrase is not saved to disk and is not written to any log.\n"
+            "  Otedama cannot show it to you again.\n"
             f"{bar}\n\n")
