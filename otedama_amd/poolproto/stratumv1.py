@@ -163,6 +163,7 @@ class V1Session(Session):
         self._write_lock = asyncio.Lock()
         self._task: asyncio.Task | None = None
         self.last_job: Job | None = None
+        self._job_versions: dict[str, int] = {}  # job id -> notify version (BIP310 submit param), bounded
 
     @property
     def protocol(self) -> ProtocolID:
@@ -263,6 +264,10 @@ class V1Session(Session):
 
         job.target = target_from_difficulty(diff, get_algo(self.algorithm).diff1)
         self.last_job = job
+        self._job_versions.pop(job.job_id, None)
+        self._job_versions[job.job_id] = job.version
+        while len(self._job_versions) > 64:
+            self._job_versions.pop(next(iter(self._job_versions)))
         if job.clean_jobs:
             while not self.jobs.empty():
                 self.jobs.get_nowait()
@@ -319,8 +324,10 @@ class V1Session(Session):
         worker = sub.worker or self.creds.worker or self.creds.user
         en2 = sub.extranonce2.hex() if sub.extranonce2 else "00" * self.extranonce2_size
         params = [worker, sub.job_id, en2, f"{sub.ntime & 0xFFFFFFFF:08x}", f"{sub.nonce & 0xFFFFFFFF:08x}"]
-        if self.version_mask and sub.version and self.last_job is not None and sub.version != self.last_job.version:
-            # BIP310: the pool rebuilds (job_version & ~mask) | (version_bits & mask)
+        base = self._job_versions.get(sub.job_id)
+        if self.version_mask and sub.version and sub.version != base:
+            # BIP310: the pool rebuilds (job_version & ~mask) | (version_bits & mask) from the version of the
+            # share's OWN job (several non-clean jobs with different versions can be live at once)
             params.append(f"{sub.version & self.version_mask:08x}")
         t0 = time.perf_counter()
         result, err = await self._call("mining.submit", params, timeout=timeout)
@@ -375,6 +382,8 @@ class V1Dialer(Dialer):
         if not rest:
             raise PoolProtoError(f"stratumv1: empty host in {url!r}")
         host, port = split_host_port(rest, 3333)
+        if not host:
+            raise PoolProtoError(f"stratumv1: empty host in {url!r}")
         if self.dial_fn is not None:
             reader, writer = await self.dial_fn(host, port)
         else:
