@@ -461,7 +461,13 @@ class _V1Conn:
                 except ValueError:
                     continue
                 if isinstance(msg, dict):
-                    await self._handle(msg)
+                    try:
+                        await self._handle(msg)
+                    except (ValueError, TypeError, AttributeError, KeyError, IndexError):
+                        # malformed parameters (e.g. a non-string configure mask): answer, keep the connection
+                        if msg.get("id") is not None:
+                            self._write({"id": msg.get("id"), "result": None,
+                                         "error": [20, "invalid parameters", None]})
         except (asyncio.IncompleteReadError, asyncio.LimitOverrunError, asyncio.TimeoutError, ConnectionError,
                 OSError):
             pass
