@@ -60,8 +60,11 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
+    ap.add_argument("--sha-kernel", choices=("v", "k"), default="v",
+                    help="v: 64 version variants per wave, block-2 schedule on the scalar unit (default); "
+                         "k: --sha-variants variants per lane")
     ap.add_argument("--sha-variants", type=int, default=8,
-                    help="BIP320 version variants per SHA-256d launch sharing the block-2 schedule (1 = single midstate)")
+                    help="k kernel: BIP320 version variants per launch sharing the block-2 schedule (1 = single midstate)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
@@ -70,7 +73,7 @@ def main() -> int:
     args = ap.parse_args()
 
     from otedama_amd.ops import native
-    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, Sha256dSearchK
+    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, Sha256dSearchK, Sha256dSearchV
     from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
     from otedama_amd.utils.trace import span
 
@@ -85,9 +88,19 @@ def main() -> int:
 
     job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1
     stripe = stripe_for(info.rank, info.world_size)
-    K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
-    search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
     world = info.world_size
+    use_v = args.sha_kernel == "v"
+    if use_v:
+        # One step = 64 version variants (one wave's lanes) x 2^29 nonces = 2^35 hashes, the same work as the K=8
+        # step (8 x 2^32); 8 consecutive steps tile the full 2^32 nonces of one 64-variant group.
+        K = N.SHA256D_V_GROUP
+        V_COUNT = 1 << 29
+        steps_per_group = (1 << 32) // V_COUNT
+        search = Sha256dSearchV(dev, grid=args.grid or None)
+    else:
+        V_COUNT, steps_per_group = 1 << 32, 1
+        K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
+        search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
     slot_words = 1 + (2 if K > 1 else 1) * search.cap
     gathered = torch.zeros(world, slot_words, dtype=torch.int32, device=dev)
     counters_hashes = 0
@@ -99,6 +112,15 @@ def main() -> int:
             return hdrs, N.sha256d_prepare_k(hdrs, job["target"])
         return hdrs, N.sha256d_prepare(hdrs[0], job["target"])
 
+    v_groups: dict[int, tuple[list[bytes], object]] = {}
+
+    def v_group(q: int):
+        # variant group q of this rank: stripe positions 64q .. 64q+63; the table is uploaded once, before timing
+        if q not in v_groups:
+            hdrs = [N.variant_header(job, stripe.start + (q * K + j) * stripe.stride)[0] for j in range(K)]
+            v_groups[q] = (hdrs, search.prepare(hdrs, job["target"]))
+        return v_groups[q]
+
     hits_log: list[tuple[list[bytes], torch.Tensor]] = []
 
     def step(i: int, record: bool) -> None:
@@ -109,20 +131,29 @@ def main() -> int:
         nonlocal counters_hashes
         if world > 1:  # R1: job blob fan-out (kept on device; decoded only on job change)
             comm._run(lambda: torch.distributed.broadcast(comm._job, src=0))
-        hdr, params = variant_params(i)
-        r = search.launch(params, 0, 1 << 32)  # K1: full 2^32 nonce space
+        if use_v:  # K1: 64 variants x one eighth of the nonce space (W3 window)
+            hdr, prep = v_group(i // steps_per_group)
+            r = search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT)
+        else:
+            hdr, params = variant_params(i)
+            r = search.launch(params, 0, 1 << 32)  # K1: full 2^32 nonce space
         if world > 1:  # R2: on-device hit buffers, gathered on the comm stream
             comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered.view(-1), r.buf.view(-1)))
         else:
             gathered[0].copy_(r.buf)
-        counters_hashes += K << 32
+        counters_hashes += K * (V_COUNT if use_v else 1 << 32)
         if record:
             hits_log.append((hdr, gathered[info.rank].clone()))
 
     # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
     # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
-    if (args.steps + args.warmup) * K * world > 1 << 16:
+    positions = ((args.steps + args.warmup + steps_per_group - 1) // steps_per_group + 1) * K if use_v \
+        else (args.steps + args.warmup) * K
+    if positions * world > 1 << 16:
         raise SystemExit("bench.py: (steps + warmup) x variants x GPUs exceeds the 2^16 version-rolling space")
+    if use_v:  # variant tables for every step, timed and warmup, built and uploaded before the timed region
+        for i in range(args.steps + args.warmup):
+            v_group(i // steps_per_group)
     for i in range(args.warmup):
         step(args.steps + i, False)
     torch.cuda.synchronize(dev)
@@ -131,7 +162,8 @@ def main() -> int:
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, True)
-    total = comm.allreduce_counters((args.steps * K) << 32)[0] if world > 1 else (args.steps * K) << 32  # R3
+    step_hashes = K * (V_COUNT if use_v else 1 << 32)
+    total = comm.allreduce_counters(args.steps * step_hashes)[0] if world > 1 else args.steps * step_hashes  # R3
     torch.cuda.synchronize(dev)
     barrier(info)
     torch.cuda.synchronize(dev)
@@ -253,11 +285,17 @@ def main() -> int:
             "data": "synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1",
             "config": {
                 "model": "sha256d",
-                "global_batch": (K << 32) * world,
+                "global_batch": step_hashes * world,
                 "seq_len": 80,
-                "parallelism": f"dp{world} (nonce-space: per-rank variant stripe, full 2^32 nonces per variant per step)",
-                "algorithm": ("SHA-256d nonce search, fixed midstate per variant; "
-                              f"{K} BIP320 version variants per launch share the block-2 message schedule"),
+                "parallelism": (f"dp{world} (nonce-space: per-rank variant stripe; "
+                                + ("64 variants x 2^29 nonces per step, 8 steps tile 2^32 per variant)" if use_v
+                                   else "full 2^32 nonces per variant per step)")),
+                "algorithm": ("SHA-256d nonce search, fixed midstate per variant; " + (
+                    "64 BIP320 version variants per wave (one per lane) share the block-2 message schedule, "
+                    "computed on the scalar unit" if use_v else
+                    f"{K} BIP320 version variants per launch share the block-2 message schedule")),
+                "sha_kernel": "otd_sha256d_search_v<8>" if use_v else (f"otd_sha256d_search_k<{K}>" if K > 1
+                                                                       else "otd_sha256d_search"),
                 "variants_per_step": K,
                 "grid": search.grid,
             },

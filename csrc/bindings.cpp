@@ -25,6 +25,8 @@ void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, ui
                        uintptr_t stream);
 void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                          uintptr_t stream);
+void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
+                         uint32_t cap, int grid, uintptr_t stream);
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
 void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
@@ -257,6 +259,20 @@ PYBIND11_MODULE(_native, m) {
       throw std::invalid_argument("need K headers (K in SHA256D_K_VALUES) with identical bytes 64..75");
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   }, py::arg("headers"), py::arg("target"));
+  m.attr("SHA256D_V_GROUP") = kSha256dVGroup;
+  m.def("sha256d_prepare_v", [](const py::list& headers, const py::bytes& t) {
+    std::string ts = need(t, 32, "target");
+    std::vector<std::string> hs;
+    for (auto& h : headers) hs.push_back(need(h.cast<py::bytes>(), 80, "header"));
+    std::vector<const uint8_t*> ptrs;
+    for (auto& h : hs) ptrs.push_back(reinterpret_cast<const uint8_t*>(h.data()));
+    Sha256dParamsV p;
+    std::vector<Sha256dVariant> vars(hs.size());
+    if (!sha256d_prepare_v(ptrs.data(), (int)ptrs.size(), reinterpret_cast<const uint8_t*>(ts.data()), &p, vars.data()))
+      throw std::invalid_argument("need a positive multiple of 64 headers with identical bytes 64..75");
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(&p), sizeof p),
+                          py::bytes(reinterpret_cast<const char*>(vars.data()), vars.size() * sizeof(Sha256dVariant)));
+  }, py::arg("headers"), py::arg("target"));
   m.def("scrypt_prepare", [](const py::bytes& h, const py::bytes& t) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     ScryptParams p;
@@ -298,6 +314,17 @@ PYBIND11_MODULE(_native, m) {
     py_launch_sha256d_k(p, base, count, out, cap, grid, stream);
   }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
      py::arg("stream"));
+  m.def("launch_sha256d_v", [](const py::bytes& params, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
+                               uint32_t cap, int grid, uintptr_t stream, bool occupancy8) {
+    std::string ps = need(params, sizeof(Sha256dParamsV), "params");
+    Sha256dParamsV p; std::memcpy(&p, ps.data(), sizeof p);
+    p.occupancy8 = occupancy8 ? 1u : 0u;
+    if (p.groups == 0 || count == 0 || count > (1ull << 32)) throw std::invalid_argument("bad groups / count");
+    if (grid <= 0 || (uint64_t(grid) * 4u) % p.groups != 0 || vars == 0 || out == 0)
+      throw std::invalid_argument("grid * 4 must be a multiple of the variant groups; vars/out must be set");
+    py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream);
+  }, py::arg("params"), py::arg("vars"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"),
+     py::arg("grid"), py::arg("stream"), py::arg("occupancy8") = false);
   m.def("launch_scrypt", [](const py::bytes& params, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch,
                             int gap, uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
     std::string ps = need(params, sizeof(ScryptParams), "params");

@@ -73,6 +73,28 @@ bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t ta
   return true;
 }
 
+bool sha256d_prepare_v(const uint8_t* const headers80[], int n, const uint8_t target32[32], Sha256dParamsV* p,
+                       Sha256dVariant* vars) {
+  if (n <= 0 || n % kSha256dVGroup != 0) return false;
+  for (int v = 1; v < n; ++v)
+    for (int i = 64; i < 76; ++i)
+      if (headers80[v][i] != headers80[0][i]) return false;
+  for (int v = 0; v < n; ++v) {
+    Sha256dParams q;
+    sha256d_prepare(headers80[v], target32, &q);
+    if (v == 0) {
+      p->w0 = q.w0; p->w1 = q.w1; p->w2 = q.w2; p->w16 = q.w16; p->w17 = q.w17;
+      p->target_hi = q.target_hi;
+    }
+    for (int i = 0; i < 8; ++i) { vars[v].mid[i] = q.mid[i]; vars[v].st3[i] = q.st3[i]; }
+    vars[v].pre3 = q.pre3;
+    vars[v].t2_3 = q.t2_3;
+  }
+  p->groups = uint32_t(n / kSha256dVGroup);
+  p->occupancy8 = 0;
+  return true;
+}
+
 void x11_prepare(const uint8_t header80[80], const uint8_t target32[32], X11Params* p) {
   for (int k = 0; k < 9; ++k) p->m[k] = (uint64_t(load_be32(header80 + 8 * k)) << 32) | load_be32(header80 + 8 * k + 4);
   p->m9_hi = uint64_t(load_be32(header80 + 72)) << 32;

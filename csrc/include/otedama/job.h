@@ -48,6 +48,19 @@ struct Sha256dParamsK {
 // same bytes 64..75.
 bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t target32[32], Sha256dParamsK* out);
 
+// Version-parallel search (sha256d_search_v): 64 * groups variants with identical bytes 64..75, one per lane;
+// the per-variant blocks live in device memory (vars[64 * groups]), the shared block-2 words in the kernarg.
+constexpr int kSha256dVGroup = 64;  // variants per wave (wave64 lanes)
+struct Sha256dParamsV {
+  uint32_t w0, w1, w2, w16, w17;
+  uint32_t target_hi;
+  uint32_t groups;  // variant groups of 64
+  uint32_t occupancy8;  // launch the 8-waves/SIMD build (launch-time choice, not part of the job)
+};
+// Fills *p and vars[0..n) (n a positive multiple of 64); false unless every header has the same bytes 64..75.
+bool sha256d_prepare_v(const uint8_t* const headers80[], int n, const uint8_t target32[32], Sha256dParamsV* p,
+                       Sha256dVariant* vars);
+
 // Scrypt (N, r=1, p=1) job parameters: the 76-byte header prefix; the nonce is
 // appended per lane as bytes 76..79.
 // The HMAC key is the whole 80-byte header (> 64 B, so K' = SHA-256(header)),

@@ -25,6 +25,7 @@ ARCH = os.environ.get("OTEDAMA_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = [
     "kernels/sha256d_search.hip",
+    "kernels/sha256d_search_v.hip",
     "kernels/scrypt_search.hip",
     "kernels/x11_stages_a.hip",
     "kernels/x11_stages_b.hip",
@@ -75,7 +76,8 @@ def _compile(cmd: list[str], verbose: bool) -> None:
 # Per-source extra hipcc flags. sha256d_search.hip: the K-variant kernels (K up to 16) unroll 60 rounds x K
 # states; above LLVM's default pragma-unroll budget the round loop stays rolled and the message schedule and
 # state arrays go to scratch (see the kernel's header comment).
-EXTRA_FLAGS = {"kernels/sha256d_search.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
+EXTRA_FLAGS = {"kernels/sha256d_search.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"],
+               "kernels/sha256d_search_v.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
 
 
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> Path:

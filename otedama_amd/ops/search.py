@@ -7,6 +7,8 @@ read back with :meth:`SearchResult.nonces` after a synchronize.
 
 Kernels (csrc/kernels):
   * ``otd_sha256d_search``   — SHA-256d nonce search (K1)
+  * ``otd_sha256d_search_k`` — K version variants per lane sharing the block-2 schedule
+  * ``otd_sha256d_search_v`` — 64 version variants per wave, block-2 schedule on the scalar unit
   * ``otd_scrypt_*``         — scrypt N=1024,r=1,p=1 three-stage search (K5)
   * ``x11k::k_*512_*``       — X11 eleven-stage chain, one kernel per stage (K6)
 """
@@ -22,6 +24,10 @@ from otedama_amd.ops.native import require_native
 # (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
 SHA256D_BLOCKS_PER_CU = 6
 SHA256D_K_BLOCKS_PER_CU = 16  # K-variant kernel: K=8 121 VGPRs (4 waves/SIMD); 4/8/12/16 per CU: 18.05/18.48/18.72/18.80 GH/s
+# Version-parallel kernel, 8-waves/SIMD build: 64 blocks of 256 per CU (tools/bench_sha_v.py sweep, profiles/r2/sha_v:
+# 8/16/32/64/96/128 per CU -> 18.37/18.73/19.00/19.61/19.58/19.61 GH/s; more resident-block rounds keep the waves'
+# scalar/vector phases apart).
+SHA256D_V_BLOCKS_PER_CU = 64
 SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
 
 
@@ -122,6 +128,57 @@ class Sha256dSearchK:
         out[:1].zero_()
         self.native.launch_sha256d_k(params, base & 0xFFFFFFFF, int(count), out.data_ptr(), self.cap, self.grid,
                                      stream.cuda_stream)
+        return SearchResultK(out, self.cap)
+
+    def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:
+        r = self.launch(self.prepare(headers, target32), base, count)
+        torch.cuda.synchronize(self.device)
+        return r.hits()
+
+
+@dataclass
+class PreparedV:
+    params: bytes         # Sha256dParamsV (kernarg)
+    vars: torch.Tensor    # uint8 device copy of the Sha256dVariant table (72 B per variant)
+    n: int                # variants (multiple of 64)
+
+
+class Sha256dSearchV:
+    """Version-parallel SHA-256d (csrc/kernels/sha256d_search_v.hip): the 64 lanes of a wave are 64 header
+    variants with identical bytes 64..79 and the wave walks W3 (the big-endian nonce word) together, so the
+    first hash's message schedule runs on the scalar unit. Hits are (nonce, variant index) pairs; a launch over
+    W3 in [base, base + count) covers the nonces bswap(W3) of that range for every variant."""
+
+    def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, occupancy8: bool = True):
+        self.native = require_native()
+        self.group = self.native.SHA256D_V_GROUP
+        self.occupancy8 = occupancy8
+        self.device = torch.device(device)
+        self.cap = cap
+        self.grid = grid or default_grid(self.device, SHA256D_V_BLOCKS_PER_CU)
+        self.out = torch.zeros(1 + 2 * cap, dtype=torch.int32, device=self.device)
+
+    def prepare(self, headers: list[bytes], target32: bytes) -> PreparedV:
+        if not headers or len(headers) % self.group:
+            raise ValueError(f"need a positive multiple of {self.group} headers")
+        groups = len(headers) // self.group
+        if (self.grid * 4) % groups:
+            raise ValueError(f"grid*4 ({self.grid * 4}) must be a multiple of the variant groups ({groups})")
+        params, table = self.native.sha256d_prepare_v(list(headers), target32)
+        vars_dev = torch.frombuffer(bytearray(table), dtype=torch.uint8).to(self.device)
+        return PreparedV(params, vars_dev, len(headers))
+
+    def launch(self, prep: PreparedV, base: int = 0, count: int = 1 << 32, out: torch.Tensor | None = None,
+               stream: torch.cuda.Stream | None = None) -> SearchResultK:
+        out = self.out if out is None else out
+        if out.numel() < 1 + 2 * self.cap or out.dtype != torch.int32 or out.device != self.device:
+            raise ValueError("out must be an int32 tensor of >= 1+2*cap elements on the search device")
+        if prep.vars.device != self.device:
+            raise ValueError("variant table must live on the search device")
+        stream = stream or torch.cuda.current_stream(self.device)
+        out[:1].zero_()
+        self.native.launch_sha256d_v(prep.params, prep.vars.data_ptr(), base & 0xFFFFFFFF, int(count),
+                                     out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8)
         return SearchResultK(out, self.cap)
 
     def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:

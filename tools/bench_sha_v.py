@@ -1,0 +1,94 @@
+"""SHA-256d: K-variant kernel (K=8, schedule per lane on the VALU) vs the version-parallel kernel (64 variants per
+wave, schedule on the scalar unit), with a bit-exactness check of the latter against the CPU first.
+
+python tools/bench_sha_v.py [--count LOG2] [--groups 1,2] [--bpc 8,16,24]
+  -> one JSON line per (kernel, grid, groups): GH/s per GPU
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import struct
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def headers_for(n: int) -> list[bytes]:
+    tail = bytes(range(4, 76)) + bytes(4)
+    return [struct.pack("<I", 0x20000000 | ((v & 0xFFFF) << 13)) + tail for v in range(n)]
+
+
+def check(dev: str) -> dict:
+    """Easy target: every hit of a small W3 window must be a true share, and every true share must be hit."""
+    from otedama_amd.ops.search import Sha256dSearchV
+
+    s = Sha256dSearchV(dev)
+    hs = headers_for(64)
+    target = (((1 << 248) - 1)).to_bytes(32, "little")  # ~1 in 256
+    base, count = 0x12345600, 2048
+    got = sorted(s.search(hs, target, base, count))
+    want = []
+    for vi, h in enumerate(hs):
+        for w3 in range(base, base + count):
+            nonce = int.from_bytes(w3.to_bytes(4, "big"), "little")
+            d = hashlib.sha256(hashlib.sha256(h[:76] + nonce.to_bytes(4, "little")).digest()).digest()
+            if int.from_bytes(d, "little") <= int.from_bytes(target, "little"):
+                want.append((nonce, vi))
+    return {"check": "sha256d_v_vs_cpu", "hits": len(got), "expected": len(sorted(want)), "ok": got == sorted(want)}
+
+
+def main() -> int:
+    import argparse
+
+    import torch
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--count", type=int, default=29, help="log2 nonces (W3 values) per variant per launch")
+    ap.add_argument("--groups", default="1,2")
+    ap.add_argument("--bpc", default="7,14,21,24,28")
+    ap.add_argument("--bpc8", default="8,16,24,32")
+    ap.add_argument("--no-check", action="store_true")
+    a = ap.parse_args()
+    count = 1 << a.count
+    if not a.no_check:
+        r = check("cuda:0")
+        print(json.dumps(r), flush=True)
+        if not r["ok"]:
+            return 1
+
+    from otedama_amd.ops.search import Sha256dSearchK, Sha256dSearchV
+
+    target = bytes(32)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def run(launch, hashes, reps=3):
+        launch()
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(reps):
+            launch()
+        ev1.record()
+        torch.cuda.synchronize()
+        return hashes * reps / (ev0.elapsed_time(ev1) * 1e-3)
+
+    sk = Sha256dSearchK("cuda:0", k=8)
+    pk = sk.prepare(headers_for(8), target)
+    kcount = 1 << 32
+    print(json.dumps({"kernel": "k8", "grid": sk.grid, "ghs": round(run(lambda: sk.launch(pk, 0, kcount), 8 * kcount) / 1e9, 3)}),
+          flush=True)
+    for occ8 in (False, True):
+        for g in map(int, a.groups.split(",")):
+            for bpc in map(int, (a.bpc8 if occ8 else a.bpc).split(",")):
+                s = Sha256dSearchV("cuda:0", grid=cus * bpc, occupancy8=occ8)
+                p = s.prepare(headers_for(64 * g), target)
+                rate = run(lambda: s.launch(p, 0, count), 64 * g * count)
+                print(json.dumps({"kernel": "v8" if occ8 else "v", "groups": g, "grid": s.grid,
+                                  "ghs": round(rate / 1e9, 3)}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
