@@ -126,9 +126,11 @@ class MinerBase {
 // One host thread per GPU: double-buffered batches on a private HIP stream.
 class GpuMiner : public MinerBase {
  public:
-  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling), 1..16
-  // (rounded down to an instantiated K: 2, 3, 4, 6, 8, 12, 16).
-  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 8);
+  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling): 64 (default) = the
+  // version-parallel kernel, one variant per lane of a wave (sha256d_search_v); 1..16 = the K-variant kernel
+  // (rounded down to an instantiated K: 2, 3, 4, 6, 8, 12, 16). A job whose variant space cannot supply 64
+  // variants with a common block 2 falls back to the K kernel with what it can supply.
+  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 64);
   ~GpuMiner() override;
   void start() override;
   void stop() override;
@@ -138,7 +140,9 @@ class GpuMiner : public MinerBase {
   uint64_t batch_;
   int grid_;
   int sha_k_;
+  bool sha_v_;  // version-parallel kernel enabled
   int grid_k_ = 0;
+  int grid_v_ = 0;
   std::thread th_;
 };
 

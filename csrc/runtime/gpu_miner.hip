@@ -52,17 +52,20 @@ struct Slot {
   std::shared_ptr<const JobTemplate> job;
   uint64_t gen = 0;
   uint64_t count = 0;  // nonces per variant
-  int nvar = 1;        // > 1: K-variant SHA-256d launch, hits carry the variant index
-  uint8_t header[kSha256dMaxK][80];
-  uint32_t version[kSha256dMaxK] = {0}, ntime[kSha256dMaxK] = {0};
-  uint64_t en2[kSha256dMaxK] = {0};
+  int nvar = 1;        // > 1: K-variant / version-parallel SHA-256d launch, hits carry the variant index
+  uint8_t header[kSha256dVGroup][80];
+  uint32_t version[kSha256dVGroup] = {0}, ntime[kSha256dVGroup] = {0};
+  uint64_t en2[kSha256dVGroup] = {0};
+  Sha256dVariant* d_vars = nullptr;  // version-parallel kernel: per-lane variant table (device)
+  Sha256dVariant* h_vars = nullptr;  // pinned staging copy
   TraceId range = 0;  // roctx: enqueue -> host verification of this batch
 };
 }  // namespace
 
 GpuMiner::GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants)
     : MinerBase(std::move(device_id), queue_cap), device_(device), batch_(batch_nonces), grid_(grid),
-      sha_k_(sha_variants < 1 ? 1 : sha_variants > kSha256dMaxK ? kSha256dMaxK : sha_variants) {
+      sha_k_(sha_variants < 1 ? 1 : sha_variants > kSha256dMaxK ? kSha256dMaxK : sha_variants),
+      sha_v_(sha_variants >= kSha256dVGroup) {
   if (batch_ == 0 || batch_ > (1ull << 32)) batch_ = 1ull << 30;
   // Batches must tile the 2^32 nonce range exactly.
   while ((1ull << 32) % batch_) --batch_;
@@ -113,6 +116,8 @@ void GpuMiner::loop() {
       if (s.h_out) (void)hipHostFree(s.h_out);
       if (s.start) (void)hipEventDestroy(s.start);
       if (s.done) (void)hipEventDestroy(s.done);
+      if (s.d_vars) (void)hipFree(s.d_vars);
+      if (s.h_vars) (void)hipHostFree(s.h_vars);
     }
     if (scratch) (void)hipFree(scratch);
     if (xbuf) (void)hipFree(xbuf);
@@ -125,6 +130,10 @@ void GpuMiner::loop() {
     OTD_HIP(hipHostMalloc(&s.h_out, (1 + 2 * kHitCap) * sizeof(uint32_t), hipHostMallocDefault));
     OTD_HIP(hipEventCreate(&s.start));
     OTD_HIP(hipEventCreate(&s.done));
+    if (sha_v_) {
+      OTD_HIP(hipMalloc(&s.d_vars, kSha256dVGroup * sizeof(Sha256dVariant)));
+      OTD_HIP(hipHostMalloc(&s.h_vars, kSha256dVGroup * sizeof(Sha256dVariant), hipHostMallocDefault));
+    }
   }
   // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
   // 13.6-14.0 for the per-lane kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md).
@@ -136,6 +145,12 @@ void GpuMiner::loop() {
   // K-variant SHA-256d kernel (K states per lane, 4-6 waves/SIMD): 16 blocks of 256 per CU
   // (tools/bench_sha_k.py sweeps K and the grid; profiles/r2/).
   grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
+  // Version-parallel kernel (8-waves/SIMD build): 64 blocks of 256 per CU (tools/bench_sha_v.py, profiles/r2/sha_v).
+  grid_v_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 64;
+  // Host variant table of the current 64-variant group, rebuilt only when the group changes (once per 2^32 nonces).
+  uint64_t v_table_gen = ~0ull, v_table_k = ~0ull;
+  Sha256dParamsV v_params{};
+  Sha256dVariant v_table[kSha256dVGroup];
 
   uint64_t cur_gen = ~0ull;
   uint64_t k = 0;       // variant-stripe position
@@ -200,7 +215,23 @@ void GpuMiner::loop() {
     s.gen = gen;
     s.nvar = 1;
     job->variant_header(v, s.header[0], &s.version[0], &s.ntime[0], &s.en2[0]);
-    if (job->algo == Algo::kSha256d && sha_k_ > 1) {
+    bool use_v = false;
+    if (job->algo == Algo::kSha256d && sha_v_) {
+      // 64 consecutive stripe positions with a common block 2 -> one variant per lane of the version-parallel
+      // kernel. The group is all-or-nothing (a partial group takes the K path below) and depends only on
+      // (job, k), so every launch of a group uses the same kernel and W3/nonce space.
+      int kv = 1;
+      while (kv < kSha256dVGroup) {
+        const uint64_t vk = job->variant_start + (k + kv) * job->variant_stride;
+        if (vk >= job->variant_space()) break;
+        job->variant_header(vk, s.header[kv], &s.version[kv], &s.ntime[kv], &s.en2[kv]);
+        if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
+        ++kv;
+      }
+      use_v = kv == kSha256dVGroup;
+      if (use_v) s.nvar = kSha256dVGroup;
+    }
+    if (!use_v && job->algo == Algo::kSha256d && sha_k_ > 1) {
       // Group the next stripe positions whose headers differ only in block 1 (version rolling): they share
       // the block-2 message schedule in sha256d_search_k. Stops at the first one that differs in 64..75.
       int kv = 1;
@@ -236,6 +267,23 @@ void GpuMiner::loop() {
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = remaining < x11_batch ? remaining : x11_batch;
       OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), s.d_out, kHitCap, stream));
+    } else if (use_v) {
+      if (v_table_gen != gen || v_table_k != k) {
+        const uint8_t* hs[kSha256dVGroup];
+        for (int j = 0; j < kSha256dVGroup; ++j) hs[j] = s.header[j];
+        if (!sha256d_prepare_v(hs, kSha256dVGroup, job->target, &v_params, v_table))
+          throw std::runtime_error("sha256d_prepare_v");
+        v_params.occupancy8 = 1;
+        v_table_gen = gen;
+        v_table_k = k;
+      }
+      std::memcpy(s.h_vars, v_table, sizeof v_table);
+      OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, sizeof v_table, hipMemcpyHostToDevice, stream));
+      // W3 (big-endian nonce word) windows tile [0, 2^32) exactly like the nonce windows of the other kernels;
+      // the kernel reports nonce = bswap(W3). Launch duration stays batch_ hashes.
+      s.count = batch_ / kSha256dVGroup;
+      OTD_HIP(launch_sha256d_search_v(v_params, s.d_vars, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_v_,
+                                      stream));
     } else if (s.nvar > 1) {
       Sha256dParamsK p;
       const uint8_t* hs[kSha256dMaxK];

@@ -269,8 +269,9 @@ def test_doctor_pow_self_test_runs_the_gpu_kernel(algo):
 
 
 def test_gpu_miner_groups_v1_coinbase_variants():
-    """A Stratum V1 job with a coinbase (extranonce2_size 4) and a BIP320 mask takes the K-variant kernel: the
-    variant digits put version bits lowest, so neighbouring stripe positions share the merkle root and block 2.
+    """A Stratum V1 job with a coinbase (extranonce2_size 4) and a BIP320 mask takes the version-parallel kernel:
+    the variant digits put version bits lowest, so 64 neighbouring stripe positions share the merkle root and
+    block 2.
     Every share re-hashes to its reported hash from the rebuilt coinbase / merkle root."""
     from otedama_amd.models.header import int_to_hash, sha256d
 
@@ -300,3 +301,84 @@ def test_gpu_miner_groups_v1_coinbase_variants():
             root = sha256d(root + b)
         h80 = struct.pack("<I", s["version"]) + hdr[4:36] + root + hdr[68:76] + struct.pack("<I", s["nonce"])
         assert sha256d(h80) == s["hash"] and int.from_bytes(s["hash"], "little") <= int.from_bytes(tgt, "little")
+
+
+def _v_headers(n, seed=b"v"):
+    tail = hashlib.sha256(seed).digest() * 3
+    return [struct.pack("<I", 0x20000000 | ((v & 0xFFFF) << 13)) + tail[:72] + bytes(4) for v in range(n)]
+
+
+@pytest.mark.parametrize("groups,base", [(1, 0x12345600), (2, 0xFFFFFC00)])
+def test_sha256d_v_kernel_matches_cpu(groups, base):
+    """Version-parallel kernel: for every variant (lane) and every W3 of the window (incl. the 2^32 wrap), the
+    reported (nonce = bswap(W3), variant) pairs are exactly the CPU's shares."""
+    from otedama_amd.ops.search import Sha256dSearchV
+
+    s = Sha256dSearchV("cuda:0", grid=512)
+    hs = _v_headers(64 * groups)
+    target_int = (1 << 248) - 1
+    count = 1024
+    got = sorted(s.search(hs, target_int.to_bytes(32, "little"), base, count))
+    want = []
+    for vi, h in enumerate(hs):
+        for i in range(count):
+            w3 = (base + i) & 0xFFFFFFFF
+            nonce = int.from_bytes(w3.to_bytes(4, "big"), "little")
+            d = hashlib.sha256(hashlib.sha256(h[:76] + nonce.to_bytes(4, "little")).digest()).digest()
+            if int.from_bytes(d, "little") <= target_int:
+                want.append((nonce, vi))
+    assert got == sorted(want) and len(want) > 100
+
+
+def test_sha256d_v_kernel_both_builds_and_grid_contract():
+    from otedama_amd.ops.search import Sha256dSearchV
+
+    hs = _v_headers(128, b"w")
+    tgt = ((1 << 248) - 1).to_bytes(32, "little")
+    a = sorted(Sha256dSearchV("cuda:0", grid=256, occupancy8=False).search(hs, tgt, 7, 512))
+    b = sorted(Sha256dSearchV("cuda:0", grid=256, occupancy8=True).search(hs, tgt, 7, 512))
+    assert a == b and a
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", grid=1).prepare(_v_headers(64 * 8), tgt)  # 4 waves cannot split 8 groups
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", grid=256).prepare(hs[:63], tgt)
+
+
+def test_gpu_miner_kernel_selection():
+    """Default GpuMiner: version-rolling jobs take the version-parallel kernel (64 variants per launch); with
+    sha_variants=8 they take the K-variant kernel; a job without a version mask runs single-midstate."""
+    from otedama_amd.models.header import int_to_hash
+
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    tgt = int_to_hash((1 << 236) - 1)
+
+    def run(miner, job, want):
+        miner.set_job(job)
+        miner.start()
+        deadline = time.time() + 15
+        shares = []
+        while time.time() < deadline and len(shares) < want:
+            shares += miner.poll(256)
+            time.sleep(0.02)
+        miner.stop()
+        st = miner.stats()
+        assert not st["faulted"], st
+        for s in shares:
+            h80 = bytearray(hdr)
+            struct.pack_into("<I", h80, 0, s["version"])
+            struct.pack_into("<I", h80, 76, s["nonce"])
+            d = hashlib.sha256(hashlib.sha256(bytes(h80)).digest()).digest()
+            assert d == s["hash"] and int.from_bytes(d, "little") <= int.from_bytes(tgt, "little")
+        return st, shares
+
+    job = {"header": hdr, "target": tgt, "epoch": 1, "job_id": "a", "version_mask": 0x1FFFE000}
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), job, 8)
+    assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 4
+    assert st["hashes"] % ((1 << 28) // 64 * 64) == 0
+    assert len({s["version"] for s in shares}) >= 2
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28, sha_variants=8), job, 4)
+    assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 2
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), dict(job, version_mask=0), 2)
+    assert st["variant_launches"] == 0 and st["launches"] >= 2
+    assert all(s["version"] == struct.unpack_from("<I", hdr, 0)[0] for s in shares)
