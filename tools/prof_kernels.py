@@ -24,4 +24,18 @@ if algo in ("both", "scrypt"):
     for i in range(4):
         sc.launch(sp, i * sc.batch)
     torch.cuda.synchronize()
+if algo == "sha_v":  # K=8 vs version-parallel, equal work: 4 x 2^35 hashes each
+    from otedama_amd.ops.search import Sha256dSearchK, Sha256dSearchV
+
+    tail = bytes(range(4, 76)) + bytes(4)
+    hs = [(0x20000000 | (v << 13)).to_bytes(4, "little") + tail for v in range(64)]
+    sk = Sha256dSearchK("cuda:0", k=8)
+    pk = sk.prepare(hs[:8], tgt)
+    for _ in range(4):
+        sk.launch(pk, 0, 1 << 32)
+    sv = Sha256dSearchV("cuda:0")
+    pv = sv.prepare(hs, tgt)
+    for i in range(4):
+        sv.launch(pv, i << 29, 1 << 29)
+    torch.cuda.synchronize()
 print("done")
