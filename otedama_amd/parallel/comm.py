@@ -24,7 +24,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
-JOB_BLOB_BYTES = 4096
+JOB_BLOB_BYTES = 64 << 10  # a real V1 job (coinbase parts + 12 merkle branches, hex in JSON) can pass 4 KiB
 SHARE_SLOTS = 64
 SHARE_WORDS = 9  # epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_hi, rank|device, found_at_us
 COUNTER_WORDS = 4  # hashes, shares, dropped, faulted

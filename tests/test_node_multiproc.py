@@ -111,3 +111,28 @@ def test_nodecomm_single_rank_paths(n):
     got = c.gather_shares([{"epoch": 3, "nonce": 7, "ntime": 1, "version": 2, "extranonce2": 1 << 40,
                             "found_at": 12.5}])
     assert got[0]["extranonce2"] == 1 << 40 and got[0]["found_at"] == 12.5 and got[0]["epoch"] == 3
+
+
+def _blob_worker(rank: int, port: int, out_path: str) -> None:
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from otedama_amd.parallel.comm import NodeComm, init_from_env, shutdown
+
+    info = init_from_env(backend="gloo", use_gpu=False)
+    comm = NodeComm(info)
+    big = dict(_job(), coinb1=bytes(range(150)), coinb2=bytes(i % 251 for i in range(2000)), extranonce1=b"\x01\x02",
+               extranonce2_size=8, merkle_branches=[bytes([i]) * 32 for i in range(13)])
+    got = comm.broadcast_job(big if rank == 0 else None)
+    shutdown(info)
+    if rank == 1:
+        with open(out_path, "w") as f:
+            json.dump({"same": got == big, "keys": sorted(got)}, f)
+
+
+def test_node_broadcasts_a_large_v1_job(tmp_path):
+    """R1 carries a full Stratum V1 job (2 KB coinb2, 13 merkle branches): well past the old 4 KiB blob once
+    hex-encoded in JSON."""
+    out = tmp_path / "blob.json"
+    mp.start_processes(_blob_worker, args=(_port(), str(out)), nprocs=WORLD, join=True, start_method="spawn")
+    r = json.loads(out.read_text())
+    assert r["same"], r
