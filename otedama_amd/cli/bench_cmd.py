@@ -45,7 +45,7 @@ def bench_gpu(device: int = 0, reps: int = 3, scrypt_batches: int = 4) -> dict:
     import torch
 
     from otedama_amd.ops.native import require_native
-    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch
+    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, Sha256dSearchV
 
     N = require_native()
     hdr = os.urandom(76) + bytes(4)
@@ -58,6 +58,16 @@ def bench_gpu(device: int = 0, reps: int = 3, scrypt_batches: int = 4) -> dict:
         s.launch(p, 0, 1 << 32)
     torch.cuda.synchronize()
     sha = reps * (1 << 32) / (time.perf_counter() - t0)
+    # version rolling (BIP320): 64 variants per wave, one per lane, block-2 schedule on the scalar unit
+    sv = Sha256dSearchV(f"cuda:{device}")
+    pv = sv.prepare([bytes([v & 0xFF, (v >> 8) | 0x20, 0, 0x20]) + hdr[4:] for v in range(64)], bytes(32))
+    sv.launch(pv, 0, 1 << 22)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(reps):
+        sv.launch(pv, i << 29, 1 << 29)
+    torch.cuda.synchronize()
+    sha_v = reps * 64 * (1 << 29) / (time.perf_counter() - t0)
     sc = ScryptSearch(f"cuda:{device}")
     sp = N.scrypt_prepare(hdr, bytes(32))
     sc.launch(sp, 0)
@@ -67,7 +77,8 @@ def bench_gpu(device: int = 0, reps: int = 3, scrypt_batches: int = 4) -> dict:
         sc.launch(sp, i * sc.batch)
     torch.cuda.synchronize()
     scr = scrypt_batches * sc.batch / (time.perf_counter() - t0)
-    return {"device": device, "arch": N.gpu_arch_name(device), "sha256d_hps": sha, "scrypt_hps": scr,
+    return {"device": device, "arch": N.gpu_arch_name(device), "sha256d_hps": sha,
+            "sha256d_version_rolling_hps": sha_v, "scrypt_hps": scr,
             "scrypt_scratch_gib": sc.scratch_bytes / 2 ** 30}
 
 
