@@ -129,6 +129,30 @@ def test_sha256d_prepare_k_accepts_only_instantiated_k():
         N.sha256d_prepare_k(bad, bytes(32))
 
 
+def test_sha256d_prepare_v_table_matches_single_prepare():
+    """Version-parallel layout: the kernarg block carries the shared block-2 words and the group count; the table
+    holds, per variant, exactly the mid / st3 / pre3 / t2_3 words the single-midstate prepare computes."""
+    assert N.SHA256D_V_GROUP == 64
+    hdrs = [struct.pack("<I", 0x20000000 | (v << 13)) + GEN[4:] for v in range(128)]
+    tgt = int_to_hash((1 << 240) - 1)
+    params, table = N.sha256d_prepare_v(hdrs, tgt)
+    w0, w1, w2, w16, w17, target_hi, groups, occ8 = struct.unpack("<8I", params)
+    assert groups == 2 and occ8 == 0 and len(table) == 128 * 18 * 4
+    for v in (0, 1, 63, 64, 127):
+        single = N.sha256d_prepare(hdrs[v], tgt)
+        mid_st3 = single[:64]
+        sw0, sw1, sw2, sw16, sw17, pre3, t2_3, sth = struct.unpack_from("<8I", single, 64)
+        assert (w0, w1, w2, w16, w17, target_hi) == (sw0, sw1, sw2, sw16, sw17, sth)
+        row = table[72 * v: 72 * (v + 1)]
+        assert row[:64] == mid_st3 and struct.unpack_from("<2I", row, 64) == (pre3, t2_3)
+    for n in (0, 1, 63, 65, 100):
+        with pytest.raises(ValueError):
+            N.sha256d_prepare_v((hdrs * 2)[:n], tgt)
+    bad = hdrs[:63] + [hdrs[63][:66] + b"\xee" + hdrs[63][67:]]
+    with pytest.raises(ValueError):
+        N.sha256d_prepare_v(bad, tgt)
+
+
 def test_cpu_miner_runtime_emits_verified_shares():
     m = N.CpuMiner(2, "cpu-0")
     tgt = int_to_hash((1 << 244) - 1)
