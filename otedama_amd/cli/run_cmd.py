@@ -104,7 +104,9 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         from otedama_amd.parallel.comm import NodeComm, init_from_env
 
         info = init_from_env()
-        cfg.mining.gpus = str(info.local_rank)
+        # the rank's HIP ordinal (init_from_env maps local ranks onto the visible GPUs; on an 8-GPU node it is the
+        # local rank, on a 1-GPU rehearsal over gloo every rank shares GPU 0)
+        cfg.mining.gpus = str(info.device.index if info.device.type == "cuda" else info.local_rank)
         cfg.mining.cpu_threads = 0  # equal device count per rank keeps the stripes disjoint
         if info.rank > 0:
             return _run_node_worker(cfg, info, NodeComm(info), stdout)
@@ -133,10 +135,11 @@ def _run_node_worker(cfg, info, comm, stdout) -> int:
     from otedama_amd.parallel.node import NodeWorker
 
     devs = hal.Detector(hal.default_registry(0)).detect()
-    devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == info.local_rank]
+    gpu = info.device.index if info.device.type == "cuda" else info.local_rank
+    devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == gpu]
     local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0, rank=info.rank,
                      world_size=info.world_size)
-    stdout.write(f"[info] node: rank {info.rank}/{info.world_size} mining on GPU {info.local_rank} "
+    stdout.write(f"[info] node: rank {info.rank}/{info.world_size} mining on GPU {gpu} "
                  f"({len(local)} device(s))\n")
     try:
         NodeWorker(local, comm).run()

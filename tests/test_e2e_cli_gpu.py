@@ -105,3 +105,60 @@ def test_cli_run_mines_against_local_pool(tmp_path, algorithm, difficulty, min_h
                 proc.kill()
                 rc = proc.wait(10)
         assert rc == 0, "".join(lines[-40:])
+
+
+@pytest.mark.gpu
+def test_cli_node_mode_two_ranks_share_one_gpu(tmp_path):
+    """torchrun node mode through the real CLI: rank 0 runs the engine (pool session, HTTP), rank 1 a NodeWorker;
+    on this 1-GPU box both ranks hash disjoint variant stripes on GPU 0 and talk over gloo (an 8-GPU node uses
+    RCCL, one GPU per rank). Rank 1's shares reach the pool through rank 0 (R2) and are accepted."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with _PoolThread(0.25, "sha256d") as pool:
+        cfg = tmp_path / "config.yaml"
+        cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: stratum+v2://{pool.addr_sv2}\n"
+                       f"mining:\n  batch_nonces: 134217728\n")
+        env = dict(os.environ, HOME=str(tmp_path), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(tmp_path / "d"),
+                   OTEDAMA_DIST_BACKEND="gloo")
+        proc = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                                 "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "otedama_amd", "run",
+                                 "--config", str(cfg), "--no-tui", "--http-addr", "127.0.0.1:0"],
+                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT,
+                                start_new_session=True)
+        lines, http = [], None
+        try:
+            deadline = time.time() + 150
+            while time.time() < deadline and http is None:
+                line = proc.stdout.readline()
+                if not line:
+                    break
+                lines.append(line)
+                m = re.search(r"http: listening on (\S+)", line)
+                if m:
+                    http = m.group(1)
+            assert http, "".join(lines)
+            threading.Thread(target=lambda: [lines.append(x) for x in proc.stdout], daemon=True).start()
+            body, rank1 = "", 0
+            deadline = time.time() + 60
+            while time.time() < deadline:
+                time.sleep(2)
+                with urllib.request.urlopen(f"http://{http}/metrics", timeout=5) as r:
+                    body = r.read().decode()
+                acc = _metric(body, "otedama_shares_total", '{status="accepted"}') or 0
+                rank1 = _metric(body, "otedama_device_shares_found_total", '{device="rank1"}') or 0
+                if acc >= 10 and rank1 >= 2:
+                    break
+            assert acc >= 10 and rank1 >= 2, body + "".join(lines[-40:])
+            assert any("node: rank 1/2 mining on GPU 0 (1 device(s))" in x for x in lines), "".join(lines[-40:])
+            assert pool.m_accepted.value() >= acc
+        finally:
+            os.killpg(proc.pid, signal.SIGTERM)
+            try:
+                proc.wait(60)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+                proc.wait(10)
