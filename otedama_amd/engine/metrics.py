@@ -4,7 +4,8 @@ Parity: internal/engine/metrics.go:22-581 — every series name, type and label
 set is kept so existing dashboards and alerts keep working; lazily created
 label sets (reject reason, per-device shares, payout info, last reject) are
 bounded exactly as there. MI355X additions are per-device series
-(otedama_device_hashrate_hashes_per_second{device}, kernel busy ratio) and the
+(otedama_device_hashrate_hashes_per_second{device}, otedama_device_busy_ratio{device},
+otedama_device_kernel_launches_total{device}), the node's collective tick (otedama_node_*) and the
 local-pool series in otedama_amd.pool.server. docs/METRICS.md lists every name
 (enforced by tests/test_metrics_doc.py, the analogue of metrics_doc_test.go).
 """
@@ -112,11 +113,19 @@ class EngineMetrics:
                                                   "difficulty x 2^32 / hashrate.")
         self.stale_skipped = C("otedama_shares_stale_skipped_total",
                                "Shares found for a job the pool already invalidated (not submitted).")
+        self.node_collective_seconds = G("otedama_node_collective_seconds",
+                                         "Multi-GPU node: wall time of the last R1/R2/R3 collective tick on rank 0 "
+                                         "(0 outside node mode).")
+        self.node_ranks = G("otedama_node_ranks", "Multi-GPU node: ranks (one per GPU) in the torchrun job; 1 when "
+                                                  "running standalone.")
+        self.node_ranks.set(1)
         self._lock = threading.Lock()
         self._reject_reason: dict[str, object] = {}
         self._last_reject: dict[str, object] = {}
         self._device_found: dict[str, object] = {}
         self._device_hashrate: dict[str, object] = {}
+        self._device_busy: dict[str, object] = {}
+        self._device_launches: dict[str, object] = {}
         self._payout_info: dict[str, object] = {}
 
     def reject_reason(self, category: str):
@@ -166,6 +175,32 @@ class EngineMetrics:
                                        "Per-device hashrate (GPU kernel or CPU threads).", {"device": device})
                 self._device_hashrate[device] = g
         g.set(hps)
+
+    def set_device_busy(self, device: str, ratio: float) -> None:
+        with self._lock:
+            g = self._device_busy.get(device)
+            if g is None:
+                if len(self._device_busy) >= 64:
+                    return
+                g = self.reg.new_gauge("otedama_device_busy_ratio",
+                                       "Fraction of the last stats interval the device spent executing search "
+                                       "kernels (GPU: HIP event time of its launches; CPU: thread time / threads).",
+                                       {"device": device})
+                self._device_busy[device] = g
+        g.set(ratio)
+
+    def add_device_launches(self, device: str, n: int) -> None:
+        if n <= 0:
+            return
+        with self._lock:
+            c = self._device_launches.get(device)
+            if c is None:
+                if len(self._device_launches) >= 64:
+                    return
+                c = self.reg.new_counter("otedama_device_kernel_launches_total",
+                                         "Search-kernel launches (batches) completed by the device.", {"device": device})
+                self._device_launches[device] = c
+        c.add(n)
 
     def set_active_payout(self, masked: str) -> None:
         if not masked:  # metrics.go:513: an empty address never creates a series

@@ -71,7 +71,8 @@ class MinerSet:
         cpus = [d for d in devices if d.identity().family == Family.CPU]
         if cpus and algorithm == "sha256d" and (cpu_threads > 0 or not gpus):
             threads = cpu_threads or cpus[0].threads
-            self.miners.append(DeviceMiner(cpus[0], N.CpuMiner(threads, cpus[0].identity().id, queue_cap)))
+            self.miners.append(DeviceMiner(cpus[0], N.CpuMiner(threads, cpus[0].identity().id, queue_cap),
+                                           extra={"threads": max(int(threads or 1), 1)}))
         self.rank, self.world_size = rank, world_size
         self.stall_samples = max(1, stall_samples)
         self._restripe_pending = False
@@ -184,7 +185,13 @@ class MinerSet:
         return out
 
     def device_stats(self) -> dict[str, dict]:
-        return {m.id: m.native.stats() for m in self.miners}
+        out = {}
+        for m in self.miners:
+            st = m.native.stats()
+            if "threads" in m.extra:  # CPU: busy_seconds sums thread time
+                st["threads"] = m.extra["threads"]
+            out[m.id] = st
+        return out
 
     def total_hashes(self) -> int:
         return sum(s["hashes"] for s in self.device_stats().values())

@@ -157,6 +157,7 @@ class Engine:
         self._uptime = UptimeAccountant()
         self._sats = SatsAccountant()
         self._last_dropped = 0
+        self._busy_prev: dict[str, tuple[float, float, int]] = {}  # device -> (busy_seconds, at, launches)
         self.dashboard = opts.dashboard
 
     # ---------------------------------------------------------------- API
@@ -635,7 +636,13 @@ class Engine:
         for dev, err in self.miners.retire_faulted():
             self.log("error", f"engine: device {dev} faulted: {err}")
         stalled_devs = self.miners.stalled()
-        self.m.devices_faulted.set(sum(1 for s in self.miners.device_stats().values() if s["faulted"]))
+        dstats = self.miners.device_stats()
+        self._publish_device_activity(dstats, now)
+        link = getattr(self.miners, "link", None)
+        if link is not None:
+            self.m.node_ranks.set(link.world)
+            self.m.node_collective_seconds.set(getattr(link, "last_tick_seconds", 0.0))
+        self.m.devices_faulted.set(sum(1 for s in dstats.values() if s["faulted"]))
         self.m.devices_stalled.set(len(stalled_devs))
         self.m.devices_active.set(len(self.miners.live()) - len(stalled_devs))
         if self.curtailed:
@@ -669,6 +676,24 @@ class Engine:
             publish_difficulty(self.m, session.suggested_difficulty(), rate, float(2 ** 256) / self.algorithm.diff1)
         if self.dashboard is not None:
             self.dashboard.update(self.stats())
+
+
+    def _publish_device_activity(self, dstats: dict, now: float) -> None:
+        """Per-device busy ratio and launch counts from the native miners' cumulative stats (remote node ranks
+        report only hash/share counters and are skipped)."""
+        for dev, st in dstats.items():
+            if "busy_seconds" not in st:
+                continue
+            busy, launches = float(st["busy_seconds"]), int(st.get("launches", 0))
+            prev = self._busy_prev.get(dev)
+            self._busy_prev[dev] = (busy, now, launches)
+            if prev is None:
+                continue
+            dt = now - prev[1]
+            if dt > 0:
+                threads = max(int(st.get("threads", 1) or 1), 1)
+                self.m.set_device_busy(dev, min(max((busy - prev[0]) / (dt * threads), 0.0), 1.0))
+            self.m.add_device_launches(dev, launches - prev[2])
 
 
 def update_stream(streams: dict[str, arb.Stream], q) -> str:

@@ -44,6 +44,7 @@ class _Link:
         self.rank = comm.info.rank
         self.world = comm.info.world_size
         self.rows: list[list[int]] = [[0, 0, 0, 0] for _ in range(self.world)]
+        self.last_tick_seconds = 0.0  # wall time of the last R1/R2/R3 round (otedama_node_collective_seconds)
         self._seen_seq = 0
         self.error: BaseException | None = None
 
@@ -54,6 +55,7 @@ class _Link:
 
     def step(self, ctl_words: list[int] | None, job: dict | None, outgoing: list[dict]) -> tuple:
         """One tick; returns (stop, job_or_None_if_unchanged, changed, gathered_shares)."""
+        t0 = time.perf_counter()
         with span("otd.node.tick"):
             with span("otd.node.R1_control"):
                 ctl = self.comm.broadcast_control(ctl_words or [0, 0, 0, 0])
@@ -68,6 +70,7 @@ class _Link:
                 shares = self.comm.gather_shares(outgoing)
             with span("otd.node.R3_counters"):
                 self.rows = self.comm.gather_counters(self.local_counters())
+        self.last_tick_seconds = time.perf_counter() - t0
         return bool(stop), new_job, changed, shares
 
 

@@ -1364,3 +1364,40 @@ def test_detect_devices_honours_gpu_selection(monkeypatch):
         cfg.mining.gpus = sel
         eng, _ = make_engine(cfg)
         assert [d.identity().id for d in eng._detect_devices()] == want, sel
+
+
+def test_tick_stats_publishes_device_busy_ratio_and_launches():
+    class Miners(FakeMiners):
+        def __init__(self):
+            super().__init__(["gpu-0", "cpu-0", "rank1"])
+            self.busy = {"gpu-0": 0.0, "cpu-0": 0.0}
+            self.launches = 0
+
+        def device_stats(self):
+            return {"gpu-0": {"faulted": False, "busy_seconds": self.busy["gpu-0"], "launches": self.launches},
+                    "cpu-0": {"faulted": False, "busy_seconds": self.busy["cpu-0"], "launches": 0, "threads": 4},
+                    "rank1": {"faulted": False, "hashes": 5}}
+    clock = Clock()
+    eng, _ = make_engine(clock=clock)
+    eng.miners = Miners()
+    tick(eng, clock, 1, 1)
+    eng.miners.busy = {"gpu-0": 9.5, "cpu-0": 20.0}
+    eng.miners.launches = 340
+    tick(eng, clock, 10, 1)
+    text = eng.registry.render()
+    assert 'otedama_device_busy_ratio{device="gpu-0"} 0.95' in text
+    assert 'otedama_device_busy_ratio{device="cpu-0"} 0.5' in text       # 20 thread-seconds / (10 s x 4 threads)
+    assert 'otedama_device_kernel_launches_total{device="gpu-0"} 340' in text
+    assert 'device="rank1"' not in text.split("otedama_device_busy_ratio")[-1].split("\n")[0]
+
+
+def test_tick_stats_publishes_node_collective_tick():
+    class Link:
+        world = 8
+        last_tick_seconds = 0.0004
+    clock = Clock()
+    eng, _ = make_engine(clock=clock)
+    assert eng.m.node_ranks.value() == 1
+    eng.miners.link = Link()
+    tick(eng, clock, 1, 1)
+    assert eng.m.node_ranks.value() == 8 and eng.m.node_collective_seconds.value() == pytest.approx(0.0004)
