@@ -64,7 +64,7 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs.float("job-interval", 30.0, "Seconds between job refreshes (new ntime).")
     fs.string("journal", "", "SQLite share journal path (empty = in-memory).")
     fs.string("payout-scheme", "pplns", "Block payout accounting: pplns | prop.")
-    fs.string("http-addr", "", "Address for /metrics /healthz /api/v1/pool (empty disables).")
+    fs.string("http-addr", "", "Address for /metrics /healthz /api/v1/{pool,workers,blocks} (empty disables).")
     fs.string("dialect", "reference", "SV2 wire dialect: reference | spec.")
     fs.bool("sv2-noise", False, "Encrypt SV2 connections with Noise NX (miners pin the printed authority key).")
     fs.string("noise-authority-key", "", "Hex secp256k1 secret signing the Noise certificate (empty = fresh per run).")
@@ -133,7 +133,9 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
     srv = None
     if fs["http-addr"]:
         srv = HTTPServer(fs["http-addr"], reg, api={"pool": lambda: [p.stats() for p in pools],
-                                                    "stats": lambda: [p.stats() for p in pools]})
+                                                    "stats": lambda: [p.stats() for p in pools],
+                                                    "workers": lambda: [w for p in pools for w in p.workers()],
+                                                    "blocks": lambda: [b for p in pools for b in p.blocks()]})
         srv.start()
         srv.set_ready(True)
         stdout.write(f"[info] http: listening on {srv.addr}\n")

@@ -125,6 +125,31 @@ class Journal:
                                  [(bid, w, a) for w, a in payouts.items()])
         return payouts
 
+    def worker_summary(self, limit: int = 100) -> list[dict]:
+        """Per-worker totals from the journal (all time), busiest first: the /api/v1/workers payload."""
+        self.flush()
+        with self._lock:
+            rows = self._db.execute(
+                "SELECT s.worker, SUM(s.accepted), SUM(1 - s.accepted), COALESCE(SUM(CASE WHEN s.accepted=1 "
+                "THEN s.difficulty END), 0), MAX(s.ts), SUM(s.block), w.difficulty FROM shares s LEFT JOIN workers w "
+                "ON w.worker = s.worker GROUP BY s.worker ORDER BY 4 DESC LIMIT ?", (limit,)).fetchall()
+        return [{"worker": w, "accepted": int(a or 0), "rejected": int(r or 0), "accepted_work": float(work),
+                 "last_share": float(ts or 0.0), "blocks": int(b or 0), "saved_difficulty": d}
+                for w, a, r, work, ts, b, d in rows]
+
+    def recent_blocks(self, limit: int = 20) -> list[dict]:
+        """Blocks found, newest first, each with its payout split: the /api/v1/blocks payload."""
+        with self._lock:
+            blocks = self._db.execute("SELECT id, ts, height, hash, worker, reward, scheme FROM blocks "
+                                      "ORDER BY id DESC LIMIT ?", (limit,)).fetchall()
+            out = []
+            for bid, ts, height, h, worker, reward, scheme in blocks:
+                pays = self._db.execute("SELECT worker, amount FROM payouts WHERE block_id=? ORDER BY amount DESC",
+                                        (bid,)).fetchall()
+                out.append({"height": height, "hash": h, "found_by": worker, "ts": ts, "reward": reward,
+                            "scheme": scheme, "payouts": [{"worker": w, "amount": a} for w, a in pays]})
+        return out
+
     def close(self) -> None:
         self.flush()
         self._db.close()

@@ -374,6 +374,28 @@ class PoolServer:
             self.journal.save_worker(w.name, new)
         return new
 
+    def _live_workers(self) -> list[_Worker]:
+        # called from the HTTP server thread: list() snapshots each container in one C-level call under the GIL
+        live = [c.worker for c in list(self._v1) if c.worker is not None]
+        for c in list(self._v2):
+            live += [w for w, _prefix in list(c.channels.values())]
+        return live
+
+    def workers(self, limit: int = 100) -> list[dict]:
+        """Journal totals per worker, merged with the live sessions' vardiff state (GET /api/v1/workers)."""
+        rows = {r["worker"]: dict(r, algorithm=self.algo.name, connected=0, difficulty=r["saved_difficulty"])
+                for r in self.journal.worker_summary(limit)}
+        for w in self._live_workers():
+            r = rows.setdefault(w.name, {"worker": w.name, "algorithm": self.algo.name, "accepted": 0, "rejected": 0,
+                                         "accepted_work": 0.0, "last_share": 0.0, "blocks": 0,
+                                         "saved_difficulty": None, "connected": 0})
+            r["connected"] += 1
+            r["difficulty"] = w.vd.difficulty
+        return sorted(rows.values(), key=lambda r: (-r["accepted_work"], r["worker"]))[:limit]
+
+    def blocks(self, limit: int = 20) -> list[dict]:
+        return [dict(b, algorithm=self.algo.name) for b in self.journal.recent_blocks(limit)]
+
     def stats(self) -> dict:
         return {
             "algorithm": self.algo.name, "height": self.block.height if self.block else 0,

@@ -582,3 +582,29 @@ def test_pool_metrics_track_clients_and_verdicts():
         assert st["clients_v1"] == 1 and st["accepted"] == 1 and st["rejected"] == 1
         c.close()
     run(with_pool(body))
+
+
+def test_pool_workers_and_blocks_api():
+    """GET /api/v1/workers and /api/v1/blocks payloads: journal totals merged with the live vardiff state, and the
+    blocks found with their payout split."""
+    async def body(pool):
+        c = await V1Raw.connect(pool)
+        n = await c.handshake(user=ADDR + ".rigA")
+        jid, en2 = n["params"][0], bytes(4)
+        nonce, ntime, _, _ = mine(pool, jid, c.en1 + en2)
+        await c.call("mining.submit", ["w", jid, en2.hex(), f"{ntime:08x}", f"{nonce:08x}"])
+        await c.call("mining.submit", ["w", jid, en2.hex(), f"{ntime:08x}", f"{nonce:08x}"])  # duplicate
+        ws = pool.workers()
+        assert len(ws) == 1
+        w = ws[0]
+        assert w["worker"] == ADDR + ".rigA" and w["accepted"] == 1 and w["rejected"] == 1 and w["connected"] == 1
+        assert w["difficulty"] == pytest.approx(2e-5) and w["accepted_work"] == pytest.approx(2e-5)
+        assert w["algorithm"] == "sha256d"
+        assert pool.blocks() == []
+        pool.journal.record_block(840000, "00" * 32, ADDR + ".rigA", 312_500_000, "pplns")
+        b = pool.blocks()
+        assert b[0]["height"] == 840000 and b[0]["payouts"] == [{"worker": ADDR + ".rigA", "amount": 312_500_000}]
+        c.close()
+        await asyncio.sleep(0.1)
+        assert pool.workers()[0]["connected"] == 0   # journal totals outlive the session
+    run(with_pool(body))
