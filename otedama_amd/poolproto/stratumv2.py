@@ -210,6 +210,15 @@ class V2Session(Session):
             ent = self._pending.pop(msg.sequence_number, None)
             if ent is not None and not ent[0].done():
                 ent[0].set_result(ShareResult(False, msg.error, latency_ms=(time.perf_counter() - ent[1]) * 1e3))
+        elif isinstance(msg, M.SetExtranoncePrefix):
+            # spec §5.3.9: a new prefix for this channel's extranonce space. On an extended channel the active job
+            # is re-issued (clean) so the miner rebuilds every coinbase under the new prefix; a standard channel's
+            # merkle roots come from the pool and change with its next job.
+            if msg.channel_id == self.channel_id:
+                self.extranonce_prefix = bytes(msg.extranonce_prefix)
+                self.log("info", "engine: extranonce prefix updated by pool")
+                if self.extended and self._active is not None and self._have_prev:
+                    self._start_job(self._active, self._active_ntime)
         elif isinstance(msg, M.Reconnect):
             put_drop_oldest(self.notices, f"pool requested reconnect to {msg.new_host}:{msg.new_port} (not followed)")
             asyncio.ensure_future(self.close())

@@ -352,6 +352,41 @@ def test_extended_channel_submit_carries_the_extranonce():
     run(go())
 
 
+def test_set_extranonce_prefix_reissues_the_extended_job():
+    async def script(pool):
+        await pool.send(M.NewExtendedMiningJob(7, 3, False, 0, 0x20000000, True, [ROOT], b"\x01" * 10, b"\x02" * 10))
+        await pool.send(M.SetNewPrevHash(7, 3, PREV, 10, 0x1d00ffff))
+        await asyncio.sleep(0.1)
+        await pool.send(M.SetExtranoncePrefix(99, b"\xee"))           # another channel: ignored
+        await pool.send(M.SetExtranoncePrefix(7, b"\x0a\x0b\x0c"))
+        await asyncio.sleep(0.3)
+
+    async def go():
+        pool = Pool(open_reply=M.OpenExtendedMiningChannelSuccess(1, 7, T1, 4, b"\x09\x09"), script=script)
+        s = await _dial(pool, extended_channel=True)
+        first = await _next_job(s)
+        again = await _next_job(s)
+        assert first.extranonce1 == b"\x09\x09"
+        assert again.job_id == "3" and again.clean_jobs and again.extranonce1 == b"\x0a\x0b\x0c"
+        assert s.extranonce_prefix == b"\x0a\x0b\x0c" and s.jobs.empty()
+        await s.close()
+        await pool.stop()
+    run(go())
+
+
+def test_set_extranonce_prefix_on_a_standard_channel_only_records_it():
+    async def go():
+        pool = Pool(script=_script(M.NewMiningJob(7, 3, False, 0, 0x20000000, ROOT), M.SetNewPrevHash(7, 3, PREV, 10,
+                    0x1d00ffff), 0.1, M.SetExtranoncePrefix(7, b"\x05" * 8)))
+        s = await _dial(pool)
+        await _next_job(s)
+        await asyncio.sleep(0.3)
+        assert s.jobs.empty() and s.extranonce_prefix == b"\x05" * 8
+        await s.close()
+        await pool.stop()
+    run(go())
+
+
 @pytest.mark.parametrize("size", [0, 9])
 def test_extended_channel_rejects_unsupported_extranonce_sizes(size):
     async def go():
