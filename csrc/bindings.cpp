@@ -26,7 +26,7 @@ void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, ui
 void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                          uintptr_t stream);
 void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                         uint32_t cap, int grid, uintptr_t stream);
+                         uint32_t cap, int grid, uintptr_t stream, int block);
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
 void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
@@ -315,16 +315,17 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
      py::arg("stream"));
   m.def("launch_sha256d_v", [](const py::bytes& params, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                               uint32_t cap, int grid, uintptr_t stream, bool occupancy8) {
+                               uint32_t cap, int grid, uintptr_t stream, bool occupancy8, int block) {
     std::string ps = need(params, sizeof(Sha256dParamsV), "params");
     Sha256dParamsV p; std::memcpy(&p, ps.data(), sizeof p);
     p.occupancy8 = occupancy8 ? 1u : 0u;
     if (p.groups == 0 || count == 0 || count > (1ull << 32)) throw std::invalid_argument("bad groups / count");
-    if (grid <= 0 || (uint64_t(grid) * 4u) % p.groups != 0 || vars == 0 || out == 0)
-      throw std::invalid_argument("grid * 4 must be a multiple of the variant groups; vars/out must be set");
-    py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream);
+    if (block != 64 && block != 256) throw std::invalid_argument("block must be 64 or 256 threads");
+    if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % p.groups != 0 || vars == 0 || out == 0)
+      throw std::invalid_argument("the wave count must be a multiple of the variant groups; vars/out must be set");
+    py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream, block);
   }, py::arg("params"), py::arg("vars"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"),
-     py::arg("grid"), py::arg("stream"), py::arg("occupancy8") = false);
+     py::arg("grid"), py::arg("stream"), py::arg("occupancy8") = false, py::arg("block") = 256);
   m.def("launch_scrypt", [](const py::bytes& params, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch,
                             int gap, uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
     std::string ps = need(params, sizeof(ScryptParams), "params");

@@ -51,8 +51,8 @@ using VarPtr = const otedama::Sha256dVariant* __restrict__;
 }  // namespace
 
 // out[0]: candidate count (may exceed cap); out[1 + 2i] = nonce (header byte order), out[2 + 2i] = variant index.
-// Grid contract (checked on the host): gridDim.x * 4 is a multiple of p.groups, so every variant group gets the
-// same number of waves and each wave's nonce stride is uniform.
+// Grid contract (checked on the host): the wave count gridDim.x * blockDim.x / 64 is a multiple of p.groups, so every
+// variant group gets the same number of waves and each wave's nonce stride is uniform.
 // MINW = 0: default build, 63 VGPRs / 106 SGPRs -> 7 waves/SIMD (SGPR-limited);
 // MINW = 8: 8 waves/SIMD, the SGPR budget drops and more schedule words live in VGPR lanes (v_readlane).
 // The body sits in the kernel itself: routed through a device function taking the params by reference, the
@@ -61,8 +61,9 @@ template <int MINW>
 __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v(
     const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, uint32_t* __restrict__ out,
     uint32_t cap) {
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  const uint32_t waves = gridDim.x * 4u;
+  const uint32_t wpb = blockDim.x >> 6;  // waves per block (256 or 64 threads)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  const uint32_t waves = gridDim.x * wpb;
   const uint32_t groups = p.groups;
   const uint32_t g = wave % groups;
   const uint32_t first = wave / groups;
@@ -137,12 +138,13 @@ template __global__ void otd_sha256d_search_v<8>(const otedama::Sha256dParamsV, 
 namespace otedama {
 
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
-                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream) {
-  if (p.groups == 0 || grid <= 0 || (uint64_t(grid) * 4u) % p.groups != 0) return hipErrorInvalidValue;
+                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block) {
+  if (block != 64 && block != 256) return hipErrorInvalidValue;
+  if (p.groups == 0 || grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % p.groups != 0) return hipErrorInvalidValue;
   if (p.occupancy8)
-    hipLaunchKernelGGL(otd_sha256d_search_v<8>, dim3(grid), dim3(256), 0, stream, p, vars, base, count, out, cap);
+    hipLaunchKernelGGL(otd_sha256d_search_v<8>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, out, cap);
   else
-    hipLaunchKernelGGL(otd_sha256d_search_v<0>, dim3(grid), dim3(256), 0, stream, p, vars, base, count, out, cap);
+    hipLaunchKernelGGL(otd_sha256d_search_v<0>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, out, cap);
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t
 hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
                                    int grid, hipStream_t stream);
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
-                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
+                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block = 256);
 
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
                                 int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
@@ -332,9 +332,10 @@ void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count,
 }
 
 void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                         uint32_t cap, int grid, uintptr_t stream) {
+                         uint32_t cap, int grid, uintptr_t stream, int block) {
   OTD_HIP(launch_sha256d_search_v(p, reinterpret_cast<const Sha256dVariant*>(vars), base, count,
-                                  reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream)));
+                                  reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream),
+                                  block));
 }
 
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,

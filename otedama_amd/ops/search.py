@@ -149,10 +149,14 @@ class Sha256dSearchV:
     first hash's message schedule runs on the scalar unit. Hits are (nonce, variant index) pairs; a launch over
     W3 in [base, base + count) covers the nonces bswap(W3) of that range for every variant."""
 
-    def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, occupancy8: bool = True):
+    def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, occupancy8: bool = True,
+                 block: int = 256):
         self.native = require_native()
         self.group = self.native.SHA256D_V_GROUP
         self.occupancy8 = occupancy8
+        if block not in (64, 256):
+            raise ValueError("block must be 64 or 256 threads")
+        self.block = block
         self.device = torch.device(device)
         self.cap = cap
         self.grid = grid or default_grid(self.device, SHA256D_V_BLOCKS_PER_CU)
@@ -162,8 +166,9 @@ class Sha256dSearchV:
         if not headers or len(headers) % self.group:
             raise ValueError(f"need a positive multiple of {self.group} headers")
         groups = len(headers) // self.group
-        if (self.grid * 4) % groups:
-            raise ValueError(f"grid*4 ({self.grid * 4}) must be a multiple of the variant groups ({groups})")
+        waves = self.grid * self.block // 64
+        if waves % groups:
+            raise ValueError(f"the wave count ({waves}) must be a multiple of the variant groups ({groups})")
         params, table = self.native.sha256d_prepare_v(list(headers), target32)
         vars_dev = torch.frombuffer(bytearray(table), dtype=torch.uint8).to(self.device)
         return PreparedV(params, vars_dev, len(headers))
@@ -178,7 +183,8 @@ class Sha256dSearchV:
         stream = stream or torch.cuda.current_stream(self.device)
         out[:1].zero_()
         self.native.launch_sha256d_v(prep.params, prep.vars.data_ptr(), base & 0xFFFFFFFF, int(count),
-                                     out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8)
+                                     out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8,
+                                     self.block)
         return SearchResultK(out, self.cap)
 
     def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:

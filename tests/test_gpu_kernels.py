@@ -337,9 +337,14 @@ def test_sha256d_v_kernel_both_builds_and_grid_contract():
     tgt = ((1 << 248) - 1).to_bytes(32, "little")
     a = sorted(Sha256dSearchV("cuda:0", grid=256, occupancy8=False).search(hs, tgt, 7, 512))
     b = sorted(Sha256dSearchV("cuda:0", grid=256, occupancy8=True).search(hs, tgt, 7, 512))
-    assert a == b and a
+    c = sorted(Sha256dSearchV("cuda:0", grid=1024, block=64).search(hs, tgt, 7, 512))  # one wave per block
+    assert a == b == c and a
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", grid=1).prepare(_v_headers(64 * 8), tgt)  # 4 waves cannot split 8 groups
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", grid=3, block=64).prepare(hs, tgt)  # 3 waves cannot split 2 groups
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", block=128)
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", grid=256).prepare(hs[:63], tgt)
 

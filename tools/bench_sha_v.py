@@ -20,11 +20,11 @@ def headers_for(n: int) -> list[bytes]:
     return [struct.pack("<I", 0x20000000 | ((v & 0xFFFF) << 13)) + tail for v in range(n)]
 
 
-def check(dev: str) -> dict:
+def check(dev: str, block: int = 256) -> dict:
     """Easy target: every hit of a small W3 window must be a true share, and every true share must be hit."""
     from otedama_amd.ops.search import Sha256dSearchV
 
-    s = Sha256dSearchV(dev)
+    s = Sha256dSearchV(dev, block=block)
     hs = headers_for(64)
     target = (((1 << 248) - 1)).to_bytes(32, "little")  # ~1 in 256
     base, count = 0x12345600, 2048
@@ -36,7 +36,7 @@ def check(dev: str) -> dict:
             d = hashlib.sha256(hashlib.sha256(h[:76] + nonce.to_bytes(4, "little")).digest()).digest()
             if int.from_bytes(d, "little") <= int.from_bytes(target, "little"):
                 want.append((nonce, vi))
-    return {"check": "sha256d_v_vs_cpu", "hits": len(got), "expected": len(sorted(want)), "ok": got == sorted(want)}
+    return {"check": "sha256d_v_vs_cpu", "block": block, "hits": len(got), "expected": len(sorted(want)), "ok": got == sorted(want)}
 
 
 def main() -> int:
@@ -50,6 +50,7 @@ def main() -> int:
     ap.add_argument("--bpc", default="7,14,21,24,28")
     ap.add_argument("--bpc8", default="8,16,24,32")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--block64-bpc", default="", help="also time 64-thread blocks at these 64-thread blocks per CU")
     a = ap.parse_args()
     count = 1 << a.count
     if not a.no_check:
@@ -81,12 +82,22 @@ def main() -> int:
           flush=True)
     for occ8 in (False, True):
         for g in map(int, a.groups.split(",")):
-            for bpc in map(int, (a.bpc8 if occ8 else a.bpc).split(",")):
+            for bpc in [int(x) for x in (a.bpc8 if occ8 else a.bpc).split(",") if x]:
                 s = Sha256dSearchV("cuda:0", grid=cus * bpc, occupancy8=occ8)
                 p = s.prepare(headers_for(64 * g), target)
                 rate = run(lambda: s.launch(p, 0, count), 64 * g * count)
                 print(json.dumps({"kernel": "v8" if occ8 else "v", "groups": g, "grid": s.grid,
                                   "ghs": round(rate / 1e9, 3)}), flush=True)
+    if a.block64_bpc and not a.no_check:
+        r = check("cuda:0", block=64)
+        print(json.dumps(r), flush=True)
+        if not r["ok"]:
+            return 1
+    for bpc in [int(x) for x in a.block64_bpc.split(",") if x]:
+        s = Sha256dSearchV("cuda:0", grid=cus * bpc, block=64)
+        p = s.prepare(headers_for(64), target)
+        rate = run(lambda: s.launch(p, 0, count), 64 * count)
+        print(json.dumps({"kernel": "v8", "block": 64, "grid": s.grid, "ghs": round(rate / 1e9, 3)}), flush=True)
     return 0
 
 
