@@ -381,5 +381,6 @@ PYBIND11_MODULE(_native, m) {
            py::arg("queue_cap") = 1024);
 
   m.attr("SHA256D_PARAMS_SIZE") = sizeof(Sha256dParams);
+  m.attr("SHA256D_V_PARAMS_SIZE") = sizeof(Sha256dParamsV);
   m.attr("SCRYPT_PARAMS_SIZE") = sizeof(ScryptParams);
 }

@@ -75,7 +75,8 @@ class Sha256dSearch:
         if out.numel() < 1 + self.cap or out.dtype != torch.int32 or out.device != self.device:
             raise ValueError("out must be an int32 tensor of >= 1+cap elements on the search device")
         stream = stream or torch.cuda.current_stream(self.device)
-        out[:1].zero_()
+        with torch.cuda.stream(stream):  # the count reset must precede the kernel on the launch stream
+            out[:1].zero_()
         self.native.launch_sha256d(params, base & 0xFFFFFFFF, int(count), out.data_ptr(), self.cap, self.grid,
                                    stream.cuda_stream)
         return SearchResult(out, self.cap)
@@ -125,7 +126,8 @@ class Sha256dSearchK:
         if out.numel() < 1 + 2 * self.cap or out.dtype != torch.int32 or out.device != self.device:
             raise ValueError("out must be an int32 tensor of >= 1+2*cap elements on the search device")
         stream = stream or torch.cuda.current_stream(self.device)
-        out[:1].zero_()
+        with torch.cuda.stream(stream):  # the count reset must precede the kernel on the launch stream
+            out[:1].zero_()
         self.native.launch_sha256d_k(params, base & 0xFFFFFFFF, int(count), out.data_ptr(), self.cap, self.grid,
                                      stream.cuda_stream)
         return SearchResultK(out, self.cap)
@@ -180,8 +182,15 @@ class Sha256dSearchV:
             raise ValueError("out must be an int32 tensor of >= 1+2*cap elements on the search device")
         if prep.vars.device != self.device:
             raise ValueError("variant table must live on the search device")
-        stream = stream or torch.cuda.current_stream(self.device)
-        out[:1].zero_()
+        if prep.vars.numel() != prep.n * 72 or len(prep.params) != self.native.SHA256D_V_PARAMS_SIZE:
+            raise ValueError("prepared table does not match its parameter block")
+        cur = torch.cuda.current_stream(self.device)
+        if stream is None:
+            stream = cur
+        elif stream != cur:
+            stream.wait_stream(cur)  # prepare() uploaded the variant table on the current stream
+        with torch.cuda.stream(stream):
+            out[:1].zero_()
         self.native.launch_sha256d_v(prep.params, prep.vars.data_ptr(), base & 0xFFFFFFFF, int(count),
                                      out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8,
                                      self.block)
@@ -231,7 +240,8 @@ class ScryptSearch:
         if not 0 < count <= self.batch:
             raise ValueError(f"count must be in [1, {self.batch}]")
         stream = stream or torch.cuda.current_stream(self.device)
-        self.out[:1].zero_()
+        with torch.cuda.stream(stream):
+            self.out[:1].zero_()
         self.native.launch_scrypt(params, base & 0xFFFFFFFF, int(count), self.xbuf.data_ptr(),
                                   self.scratch.data_ptr(), self.gap, self.out.data_ptr(), self.cap, self.grid,
                                   stream.cuda_stream)
@@ -270,7 +280,8 @@ class X11Search:
         if not 0 < count <= self.batch:
             raise ValueError(f"count must be in [1, {self.batch}]")
         stream = stream or torch.cuda.current_stream(self.device)
-        self.out[:1].zero_()
+        with torch.cuda.stream(stream):
+            self.out[:1].zero_()
         self.native.launch_x11(params, base & 0xFFFFFFFF, self.H.data_ptr(), self.batch, int(count),
                                self.out.data_ptr(), self.cap, stream.cuda_stream)
         return SearchResult(self.out, self.cap)

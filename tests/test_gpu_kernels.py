@@ -349,6 +349,24 @@ def test_sha256d_v_kernel_both_builds_and_grid_contract():
         Sha256dSearchV("cuda:0", grid=256).prepare(hs[:63], tgt)
 
 
+def test_sha256d_v_launch_on_a_side_stream():
+    """A launch on a caller's stream waits for the variant-table upload (done on the current stream) and resets
+    the hit count on the launch stream itself, so its hits equal the default-stream launch."""
+    import torch
+
+    from otedama_amd.ops.search import Sha256dSearchV
+
+    hs = _v_headers(64, b"s")
+    tgt = ((1 << 248) - 1).to_bytes(32, "little")
+    s = Sha256dSearchV("cuda:0", grid=256)
+    want = sorted(s.search(hs, tgt, 1000, 512))
+    side = torch.cuda.Stream(device="cuda:0")
+    out = torch.full((1 + 2 * s.cap,), 7, dtype=torch.int32, device="cuda:0")  # stale count must be cleared
+    r = s.launch(s.prepare(hs, tgt), 1000, 512, out=out, stream=side)
+    side.synchronize()
+    assert sorted(r.hits()) == want and want
+
+
 def test_gpu_miner_kernel_selection():
     """Default GpuMiner: version-rolling jobs take the version-parallel kernel (64 variants per launch); with
     sha_variants=8 they take the K-variant kernel; a job without a version mask runs single-midstate."""
