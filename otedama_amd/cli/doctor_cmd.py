@@ -24,7 +24,12 @@ def cmd_doctor(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     if warn:
         stderr.write(f"warning: {warn}\n")
     cfg = C.resolve(file_cfg, None, C.FlagValues(bitcoin_address=fs["bitcoin-address"], data_dir=fs["data-dir"]))
-    report = doctor.Runner(doctor.default_checks(cfg, fs["config"]), timeout=30.0).run()
+    # The reference passes only --config to the Configuration check, so a default config file that exists is
+    # reported as "no config file found"; here the file actually loaded is the one diagnosed.
+    import os
+
+    diagnosed = fs["config"] or (path if path and os.path.exists(path) else "")
+    report = doctor.Runner(doctor.default_checks(cfg, diagnosed), timeout=30.0).run()
     if fs["json"]:
         report.write_json(stdout)
     else:

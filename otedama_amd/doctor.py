@@ -19,6 +19,7 @@ import email.utils
 import json
 import os
 import socket
+import stat
 import threading
 import time
 import urllib.request
@@ -162,84 +163,177 @@ def resolve_host(host: str) -> list[str]:
 
 # ----------------------------------------------------------------------- checks
 def check_configuration(cfg: C.Config, path: str) -> Check:
+    """checks.go:54-85: no config file -> warn, a named file that does not exist -> warn, a file whose resolved
+    configuration fails validation -> fail, else pass. Without a file the validation errors (if any) are
+    appended to the warning instead of being dropped."""
     def run():
-        try:
-            cfg.validate()
-        except C.ConfigError as exc:
-            return Result(status=Status.FAIL, detail=str(exc).replace("\n", " "),
-                          fix="fix the listed fields via flags, OTEDAMA_* env vars or the config file")
-        src = path or C.default_config_path()
-        exists = bool(src) and os.path.exists(src)
-        return Result(detail=f"configuration valid ({'file ' + src if exists else 'no config file; flags/env only'})")
+        def invalid() -> str:
+            try:
+                cfg.validate()
+            except C.ConfigError as exc:
+                return str(exc).replace("\n", " ")
+            return ""
+
+        if not path:
+            err = invalid()
+            return Result(status=Status.WARN,
+                          detail="no config file found; using defaults and env vars" + (f" ({err})" if err else ""),
+                          fix="create ~/.config/otedama/config.yaml (see config.yaml.example)")
+        if not os.path.exists(path):
+            return Result(status=Status.WARN, detail=f"config file {path!r} not found",
+                          fix="pass --config /path/to/config.yaml or create the default file")
+        err = invalid()
+        if err:
+            return Result(status=Status.FAIL, detail=f"config invalid: {err}",
+                          fix="edit the config file or pass missing flags on the command line")
+        return Result(detail=f"loaded from {path}")
     return Check("Configuration", run)
 
 
+BECH32_CHARS = "qpzry9x8gf2tvdw0s3jn54khce6mua7l"
+BASE58_CHARS = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+
+
+def is_bech32_char(c: str) -> bool:
+    return len(c) == 1 and c in BECH32_CHARS
+
+
+def is_base58_char(c: str) -> bool:
+    return len(c) == 1 and c in BASE58_CHARS
+
+
+def is_likely_bitcoin_address(s: str) -> bool:
+    """Cheap shape check before the checksum (checks.go:862-887): 26..90 characters, ``bc1`` + lowercase bech32
+    characters, or ``1``/``3`` + base58 characters."""
+    s = s.strip()
+    if not 26 <= len(s) <= 90:
+        return False
+    if s.startswith("bc1"):
+        return all(is_bech32_char(c) for c in s[3:])
+    if s[0] in "13":
+        return all(is_base58_char(c) for c in s[1:])
+    return False
+
+
+def mask_address(s: str) -> str:
+    """First 6 and last 4 characters around three middle dots; 10 characters or fewer unchanged (checks.go:899)."""
+    return s if len(s) <= 10 else s[:6] + "\u00b7" * 3 + s[-4:]
+
+
+def address_kind(addr: str) -> str:
+    """Human label of the address type, so the report shows the address was understood (checks.go:128-143)."""
+    from otedama_amd.btccrypto import AddressType, classify_address
+
+    return {AddressType.P2PKH: "P2PKH legacy", AddressType.P2SH: "P2SH", AddressType.P2WPKH: "P2WPKH SegWit v0",
+            AddressType.P2WSH: "P2WSH SegWit v0", AddressType.P2TR: "P2TR Taproot"}.get(
+        classify_address(addr.strip()), "unrecognised type")
+
+
+def append_unique(xs: list[str], x: str) -> list[str]:
+    if x not in xs:
+        xs.append(x)
+    return xs
+
+
 def check_bitcoin_address(cfg: C.Config) -> Check:
+    """checks.go:87-123: shape check, then the bech32/bech32m/Base58Check checksum; the pass detail names the
+    masked address and its type. Beyond the reference: no primary address but a failover list is a warning."""
     def run():
-        if not cfg.bitcoin_address:
+        addr = cfg.bitcoin_address
+        if not addr:
             if cfg.bitcoin_addresses:
                 return Result(status=Status.WARN, detail="no primary bitcoin_address; using failover list only",
                               fix="set bitcoin_address to the address you want paid first")
-            return Result(status=Status.FAIL, detail="bitcoin_address is not set",
-                          fix="pass --bitcoin-address or set OTEDAMA_BITCOIN_ADDRESS")
-        err = C.validate_bitcoin_address(cfg.bitcoin_address)
+            return Result(status=Status.FAIL, detail="no address configured",
+                          fix="pass --bitcoin-address bc1q... or set OTEDAMA_BITCOIN_ADDRESS")
+        if not is_likely_bitcoin_address(addr):
+            return Result(status=Status.FAIL, detail=f"{addr!r} does not look like a valid address",
+                          fix="verify the address — typos here would send your earnings to strangers")
+        err = C.validate_bitcoin_address(addr.strip())
         if err:
-            return Result(status=Status.FAIL, detail=err, fix="re-copy the address from your wallet")
-        from otedama_amd.btccrypto import classify_address
-
-        return Result(detail=f"{cfg.bitcoin_address[:6]}…{cfg.bitcoin_address[-4:]} "
-                             f"({classify_address(cfg.bitcoin_address)}) checksum OK")
+            return Result(status=Status.FAIL, detail=f"{mask_address(addr)}: {err} (checksum)",
+                          fix="re-check the address character by character; the checksum does not match "
+                              "(likely a typo)")
+        return Result(detail=f"{mask_address(addr)} ({address_kind(addr)}, likely valid)")
     return Check("Bitcoin address", run)
 
 
 def check_failover_addresses(cfg: C.Config) -> Check:
+    """checks.go:149-181: every failover address gets the shape and checksum checks; the first bad entry fails
+    with its index. Beyond the reference: a repeated address (or the primary listed again) is a warning."""
     def run():
-        if not cfg.bitcoin_addresses:
-            return Result(status=Status.SKIP, detail="no failover payout addresses configured")
-        bad = [a for a in cfg.bitcoin_addresses if C.validate_bitcoin_address(a)]
-        if bad:
-            return Result(status=Status.FAIL, detail=f"{len(bad)} invalid failover address(es)",
-                          fix="fix or remove the invalid entries under bitcoin_addresses")
-        dup = len(cfg.bitcoin_addresses) != len(set(cfg.bitcoin_addresses))
-        if dup or cfg.bitcoin_address in cfg.bitcoin_addresses:
+        addrs = cfg.bitcoin_addresses
+        if not addrs:
+            return Result(status=Status.SKIP, detail="none configured")
+        for i, a in enumerate(addrs):
+            if not a or not is_likely_bitcoin_address(a):
+                return Result(status=Status.FAIL, detail=f"bitcoin_addresses[{i}] {a!r} does not look valid",
+                              fix="verify every failover address — a typo would send earnings to strangers")
+            err = C.validate_bitcoin_address(a.strip())
+            if err:
+                return Result(status=Status.FAIL, detail=f"bitcoin_addresses[{i}] {mask_address(a)}: {err}",
+                              fix="re-check the failover address; its checksum does not match (likely a typo)")
+        if len(addrs) != len(set(addrs)) or cfg.bitcoin_address in addrs:
             return Result(status=Status.WARN, detail="failover list repeats an address",
                           fix="list each payout address once")
-        return Result(detail=f"{len(cfg.bitcoin_addresses)} failover address(es) valid")
+        return Result(detail=f"{len(addrs)} failover address(es), all likely valid")
     return Check("Failover payout addresses", run)
 
 
+def _resolve_data_dir(cfg: C.Config) -> str:
+    """The configured data dir, else the OS default the engine would use (checks.go:187-195)."""
+    return cfg.data_dir or C.default_data_dir()
+
+
 def check_data_dir(cfg: C.Config) -> Check:
+    """checks.go:183-235: missing -> warn (created on first run), stat error / not a directory -> fail, group or
+    world permission bits -> warn. Beyond the reference: an existing directory must be writable, and a missing
+    one whose nearest existing parent is not writable fails (the first run could not create it)."""
     def run():
-        d = cfg.data_dir
+        d = _resolve_data_dir(cfg)
         if not d:
-            return Result(status=Status.WARN, detail="data directory could not be determined",
-                          fix="pass --data-dir or set OTEDAMA_DATA_DIR")
-        if not os.path.exists(d):
+            return Result(status=Status.SKIP, detail="no home directory")
+        try:
+            st = os.stat(d)
+        except FileNotFoundError:
             parent = os.path.dirname(os.path.abspath(d).rstrip("/")) or "/"
             while not os.path.exists(parent) and parent != "/":
                 parent = os.path.dirname(parent)
-            if os.access(parent, os.W_OK):
-                return Result(detail=f"{d} does not exist yet; it will be created (parent writable)")
-            return Result(status=Status.FAIL, detail=f"{d} does not exist and {parent} is not writable",
-                          fix=f"create {d} or choose a writable --data-dir")
-        if not os.path.isdir(d):
-            return Result(status=Status.FAIL, detail=f"{d} is not a directory", fix="point --data-dir at a directory")
+            if not os.access(parent, os.W_OK):
+                return Result(status=Status.FAIL, detail=f"{d} does not exist and {parent} is not writable",
+                              fix=f"create {d} or choose a writable --data-dir")
+            return Result(status=Status.WARN, detail=f"{d} does not exist (will be created on first run)")
+        except OSError as exc:
+            return Result(status=Status.FAIL, detail=f"cannot stat {d}: {exc}", fix="check filesystem permissions")
+        if not stat.S_ISDIR(st.st_mode):
+            return Result(status=Status.FAIL, detail=f"{d} is not a directory",
+                          fix="remove the file and restart Otedama")
         if not os.access(d, os.W_OK):
             return Result(status=Status.FAIL, detail=f"{d} is not writable", fix=f"chmod u+w {d}")
-        mode = os.stat(d).st_mode & 0o777
+        mode = st.st_mode & 0o777
         if mode & 0o077:
-            return Result(status=Status.WARN, detail=f"{d} is accessible by other users (mode {mode:o})",
-                          fix=f"chmod 700 {d} (the wallet lives here)")
-        return Result(detail=f"{d} writable (mode {mode:o})")
+            return Result(status=Status.WARN, detail=f"{d} has permissions {mode:04o} (world/group readable)",
+                          fix=f"run: chmod 0700 {d}")
+        return Result(detail=f"{d} (exists, writable)")
     return Check("Data directory", run)
 
 
 def check_wallet(cfg: C.Config) -> Check:
+    """checks.go:249-292: no wallet.dat -> warn with the passphrase hint, stat error -> fail, otherwise pass with
+    the public fingerprint (trimmed) or a note that the fingerprint file is missing. Beyond the reference:
+    wallet.dat must parse as the seedstore format (no KDF run) and be private (mode 0600)."""
     def run():
-        path = os.path.join(cfg.data_dir or "", "wallet.dat")
-        if not cfg.data_dir or not os.path.exists(path):
-            return Result(status=Status.SKIP, detail="no wallet.dat (created on first run with --wallet-passphrase)")
-        mode = os.stat(path).st_mode & 0o777
+        d = _resolve_data_dir(cfg)
+        if not d:
+            return Result(status=Status.SKIP, detail="no home directory; cannot locate wallet")
+        path = os.path.join(d, "wallet.dat")
+        try:
+            st = os.stat(path)
+        except FileNotFoundError:
+            return Result(status=Status.WARN, detail=f"no wallet found in {d}",
+                          fix="set --wallet-passphrase or OTEDAMA_WALLET_PASSPHRASE to create a wallet on next run")
+        except OSError as exc:
+            return Result(status=Status.FAIL, detail=f"cannot stat {path}: {exc}", fix="check filesystem permissions")
         try:
             from otedama_amd.lightning.seedstore import unmarshal
 
@@ -248,38 +342,52 @@ def check_wallet(cfg: C.Config) -> Check:
         except Exception as exc:  # noqa: BLE001
             return Result(status=Status.FAIL, detail=f"wallet.dat unreadable: {exc}",
                           fix="restore wallet.dat from backup or recreate it from your recovery phrase")
+        mode = st.st_mode & 0o777
         if mode & 0o077:
             return Result(status=Status.WARN, detail=f"wallet.dat mode {mode:o} is too permissive",
                           fix=f"chmod 600 {path}")
-        return Result(detail=f"wallet.dat present, format OK (mode {mode:o})")
+        try:
+            with open(os.path.join(d, "wallet.fingerprint"), encoding="utf-8", errors="replace") as f:
+                fp = f.read().strip()
+        except OSError:
+            return Result(detail="initialized (fingerprint file missing; re-run to regenerate)")
+        return Result(detail=f"initialized, fingerprint: {fp}")
     return Check("Lightning wallet", run)
 
 
-def _pool_targets(cfg: C.Config) -> list[tuple[str, str, int]]:
+def _pool_targets(cfg: C.Config, unparsed: list[str] | None = None) -> list[tuple[str, str, int]]:
+    """(url, host, port) of every configured pool, or of the built-in default. URLs that do not parse are left
+    out, and appended to ``unparsed`` when given."""
     urls = [p.url for p in cfg.pools] or [C.DEFAULT_POOL_URL]
     out = []
     for u in urls:
         try:
             rest = strip_scheme(u)
+            proto = from_url(u)
+            host, port = split_host_port(rest, 3336 if proto.value.startswith("stratum-v2") else 3333)
         except Exception:  # noqa: BLE001
+            if unparsed is not None:
+                unparsed.append(u)
             continue
-        proto = from_url(u)
-        host, port = split_host_port(rest, 3336 if proto.value.startswith("stratum-v2") else 3333)
         out.append((u, host, port))
     return out
 
 
 def check_pool_reachability(cfg: C.Config) -> Check:
+    """checks.go:294-330 dials the first pool only; this dials every configured pool (or the default). An
+    unparseable URL counts as unreachable ("cannot parse pool URL"), so a config of only bad URLs fails."""
     def run():
-        ok, bad = [], []
-        for u, host, port in _pool_targets(cfg):
+        ok, bad, unparsed = [], [], []
+        for u, host, port in _pool_targets(cfg, unparsed):
+            t0 = time.monotonic()
             try:
                 pool_dial(host, port, dial_timeout)
-                ok.append(u)
+                ok.append(f"{host}:{port} ({(time.monotonic() - t0) * 1000:.0f}ms)")
             except OSError as exc:
                 bad.append(f"{u} ({exc})")
+        bad += [f"cannot parse pool URL {u!r}" for u in unparsed]
         if not bad:
-            return Result(detail=f"{len(ok)} pool(s) reachable")
+            return Result(detail=f"{len(ok)} pool(s) reachable: {', '.join(ok)}")
         if ok:
             return Result(status=Status.WARN, detail=f"unreachable: {'; '.join(bad)}",
                           fix="check the pool URL/port or remove dead pools")
@@ -437,43 +545,80 @@ def check_hardware() -> Check:
         except OSError:
             pass
         if drm:
-            return Result(status=Status.WARN, detail=detail + f", {drm} render node(s) but no HIP device",
+            # checks.go:696-705 reports DRM render nodes as "GPU(s) detected" (pass). Here the gfx950 kernels need
+            # the HIP runtime too, so render nodes without a HIP device are a warning.
+            return Result(status=Status.WARN, detail=detail + f", {drm} GPU(s) detected (render nodes) but no HIP "
+                                                              "device",
                           fix="install the ROCm runtime / amdgpu driver so the gfx950 kernels can run")
         return Result(detail=detail + ", no GPU detected (CPU SHA-NI miner only)")
     return Check("Hardware", run)
 
 
 def check_network() -> Check:
+    """checks.go:728-746: a TCP dial of 1.1.1.1:53 (3 s); unreachable is a failure."""
     def run():
+        host, port = network_check_endpoint
         try:
-            pool_dial(network_check_endpoint[0], network_check_endpoint[1], dial_timeout)
+            pool_dial(host, port, min(dial_timeout, 3.0))
         except OSError as exc:
-            return Result(status=Status.WARN, detail=f"cannot reach {network_check_endpoint[0]}:"
-                                                     f"{network_check_endpoint[1]}: {exc}",
-                          fix="check internet connectivity (pools and price sources need it)")
-        return Result(detail="internet reachable")
+            return Result(status=Status.FAIL, detail=f"cannot reach {host}:{port}: {exc}",
+                          fix="check your firewall, proxy, or VPN")
+        return Result(detail="IPv4 OK")
     return Check("Network", run)
 
 
+CLOCK_SKEW_WARN_SECS = 120.0  # checks.go:761 (= the rate fetcher's skew warning)
+CLOCK_SKEW_FAIL_SECS = 300.0  # checks.go:766: most TLS stacks start rejecting certificates
+
+
 def check_clock() -> Check:
+    """checks.go:768-852: GET the probe URL and compare its Date header. An unreachable probe, a missing or an
+    unparseable Date header warn; skew > 120 s warns, > 300 s fails. The body is drained (bounded, 8 KiB)
+    before the connection closes."""
     def run():
         try:
-            req = urllib.request.Request(clock_skew_probe_url, method="HEAD")
+            req = urllib.request.Request(clock_skew_probe_url, method="GET",
+                                         headers={"User-Agent": f"Otedama/{_version()} (doctor)"})
+        except ValueError as exc:
+            return Result(status=Status.WARN, detail=f"could not build request: {exc}",
+                          fix="this is an internal error; report it")
+        try:
             with urllib.request.urlopen(req, timeout=dial_timeout) as resp:  # noqa: S310
                 date = resp.headers.get("Date")
+                resp.read(8 << 10)
         except Exception as exc:  # noqa: BLE001
-            return Result(status=Status.SKIP, detail=f"clock probe unavailable: {exc}")
+            return Result(status=Status.WARN, detail=f"cannot reach clock probe endpoint: {exc}",
+                          fix="check internet connectivity; re-run when online to verify clock accuracy")
         if not date:
-            return Result(status=Status.SKIP, detail="probe returned no Date header")
+            return Result(status=Status.WARN, detail="server returned no Date header; cannot measure clock skew",
+                          fix="try again; if persistent, the probe endpoint may have changed")
         try:
             skew = abs(time.time() - email.utils.parsedate_to_datetime(date).timestamp())
-        except (TypeError, ValueError):
-            return Result(status=Status.SKIP, detail=f"probe returned an unparseable Date header {date[:40]!r}")
-        if skew > 120:
-            return Result(status=Status.WARN, detail=f"local clock is {skew:.0f}s off server time",
-                          fix="enable NTP (timedatectl set-ntp true); share nTime and TLS depend on it")
-        return Result(detail=f"clock within {skew:.1f}s of server time")
+        except (TypeError, ValueError) as exc:
+            return Result(status=Status.WARN, detail=f"cannot parse server Date header {date[:40]!r}: {exc}",
+                          fix="try again; if persistent, the probe endpoint date format may have changed")
+        if skew > CLOCK_SKEW_FAIL_SECS:
+            return Result(status=Status.FAIL,
+                          detail=f"local clock is {skew:.0f} s off server time (threshold {CLOCK_SKEW_FAIL_SECS:.0f} s)",
+                          fix="synchronise your system clock (e.g. `timedatectl set-ntp true`); skew >300 s breaks "
+                              "TLS certificate validation and mining nTime checks")
+        if skew > CLOCK_SKEW_WARN_SECS:
+            return Result(status=Status.WARN,
+                          detail=f"local clock is {skew:.0f} s off server time (warn threshold "
+                                 f"{CLOCK_SKEW_WARN_SECS:.0f} s)",
+                          fix="synchronise your system clock; skew above 120 s may cause TLS errors or stale rate "
+                              "judgements")
+        return Result(detail=f"clock skew {skew:.1f} s (within {CLOCK_SKEW_WARN_SECS:.0f} s threshold)")
     return Check("System clock accuracy", run)
+
+
+def _version() -> str:
+    try:
+        from otedama_amd import version
+
+        return version.get().version
+    except Exception:  # noqa: BLE001
+        return "dev"
 
 
 def check_native() -> Check:

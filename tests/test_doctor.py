@@ -104,13 +104,13 @@ def test_tls_ca_and_data_dir(tmp_path):
     p = [C.PoolConfig(url="stratum+tls://x:1", tls_ca_file=str(tmp_path / "missing"))]
     assert D.check_pool_tls_ca(_cfg(pools=p)).run().status == D.Status.FAIL
     d = tmp_path / "dd"
-    assert D.check_data_dir(_cfg(data_dir=str(d))).run().status == D.Status.PASS
+    assert D.check_data_dir(_cfg(data_dir=str(d))).run().status == D.Status.WARN  # created on first run
     d.mkdir(mode=0o755)
     d.chmod(0o755)
     assert D.check_data_dir(_cfg(data_dir=str(d))).run().status == D.Status.WARN
     d.chmod(0o700)
     assert D.check_data_dir(_cfg(data_dir=str(d))).run().status == D.Status.PASS
-    assert D.check_wallet(_cfg(data_dir=str(d))).run().status == D.Status.SKIP
+    assert D.check_wallet(_cfg(data_dir=str(d))).run().status == D.Status.WARN
     (d / "wallet.dat").write_bytes(b"\x01short")
     assert D.check_wallet(_cfg(data_dir=str(d))).run().status == D.Status.FAIL
 
@@ -125,7 +125,7 @@ def test_misc_checks(monkeypatch):
     assert D.check_env_vars().run().status == D.Status.WARN
     monkeypatch.setattr(D, "clock_skew_probe_url", "http://127.0.0.1:1/")
     monkeypatch.setattr(D, "dial_timeout", 0.5)
-    assert D.check_clock().run().status == D.Status.SKIP
+    assert D.check_clock().run().status == D.Status.WARN
     assert D.check_native().run().status == D.Status.PASS
     assert D.check_collectives().run().status in (D.Status.PASS, D.Status.WARN)
 

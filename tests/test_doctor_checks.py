@@ -113,18 +113,26 @@ def test_runner_with_no_checks():
 
 # ------------------------------------------------------------------ configuration / address
 def test_configuration_check(tmp_path):
-    assert run(D.check_configuration(cfg(), "")).status == D.Status.PASS
+    r = run(D.check_configuration(cfg(), ""))
+    assert r.status == D.Status.WARN and "no config file found" in r.detail and "config.yaml.example" in r.fix
+    r = run(D.check_configuration(cfg(), str(tmp_path / "absent.yaml")))
+    assert r.status == D.Status.WARN and "not found" in r.detail and "--config" in r.fix
     p = tmp_path / "c.yaml"
     p.write_text("")
-    assert str(p) in run(D.check_configuration(cfg(), str(p))).detail
-    r = run(D.check_configuration(C.Config(), ""))
+    r = run(D.check_configuration(cfg(), str(p)))
+    assert r.status == D.Status.PASS and r.detail == f"loaded from {p}"
+    r = run(D.check_configuration(C.Config(), str(p)))
     assert r.status == D.Status.FAIL and "bitcoin_address is required" in r.detail and "\n" not in r.detail
+    assert r.fix
+    # without a file the validation errors ride along on the warning
+    r = run(D.check_configuration(C.Config(), ""))
+    assert r.status == D.Status.WARN and "bitcoin_address is required" in r.detail
 
 
 @pytest.mark.parametrize("c,status,needle", [
-    (cfg(), D.Status.PASS, "checksum OK"),
-    (C.Config(bitcoin_address=ADDR2), D.Status.PASS, "p2pkh"),
-    (C.Config(), D.Status.FAIL, "not set"),
+    (cfg(), D.Status.PASS, "likely valid"),
+    (C.Config(bitcoin_address=ADDR2), D.Status.PASS, "P2PKH legacy"),
+    (C.Config(), D.Status.FAIL, "no address configured"),
     (C.Config(bitcoin_addresses=[ADDR]), D.Status.WARN, "failover list only"),
     (C.Config(bitcoin_address=ADDR[:-1] + "x"), D.Status.FAIL, "checksum"),
 ])
@@ -142,16 +150,19 @@ def test_failover_addresses_check(lst, status):
 # ------------------------------------------------------------------ data dir / wallet
 def test_data_dir_check(tmp_path):
     d = tmp_path / "d"
-    assert "will be created" in run(D.check_data_dir(cfg(data_dir=str(d)))).detail
+    r = run(D.check_data_dir(cfg(data_dir=str(d))))
+    assert r.status == D.Status.WARN and "will be created on first run" in r.detail
     d.mkdir(mode=0o700)
     r = run(D.check_data_dir(cfg(data_dir=str(d))))
-    assert r.status == D.Status.PASS and "mode 700" in r.detail
+    assert r.status == D.Status.PASS and "(exists, writable)" in r.detail
     os.chmod(d, 0o755)
-    assert run(D.check_data_dir(cfg(data_dir=str(d)))).status == D.Status.WARN
+    r = run(D.check_data_dir(cfg(data_dir=str(d))))
+    assert r.status == D.Status.WARN and "0755" in r.detail and "chmod 0700" in r.fix
     f = tmp_path / "file"
     f.write_text("")
-    assert run(D.check_data_dir(cfg(data_dir=str(f)))).status == D.Status.FAIL
-    assert run(D.check_data_dir(cfg(data_dir=""))).status == D.Status.WARN
+    r = run(D.check_data_dir(cfg(data_dir=str(f))))
+    assert r.status == D.Status.FAIL and "not a directory" in r.detail and r.fix
+    assert run(D.check_data_dir(cfg(data_dir=""))).status in (D.Status.WARN, D.Status.SKIP, D.Status.PASS)
 
 
 @pytest.mark.skipif(os.geteuid() == 0, reason="root bypasses permission bits")
@@ -164,7 +175,8 @@ def test_data_dir_not_writable(tmp_path):
 def test_wallet_check(tmp_path):
     from otedama_amd.lightning import seedstore
 
-    assert run(D.check_wallet(cfg(data_dir=str(tmp_path)))).status == D.Status.SKIP
+    r = run(D.check_wallet(cfg(data_dir=str(tmp_path))))
+    assert r.status == D.Status.WARN and "no wallet found" in r.detail and "wallet-passphrase" in r.fix
     w = tmp_path / "wallet.dat"
     w.write_bytes(b"garbage")
     os.chmod(w, 0o600)
@@ -305,7 +317,7 @@ def test_network_check(monkeypatch):
     monkeypatch.setattr(D, "network_check_endpoint", ("127.0.0.1", 1))
     monkeypatch.setattr(D, "pool_dial", lambda h, p, t: (_ for _ in ()).throw(OSError("unreachable")))
     r = run(D.check_network())
-    assert r.status == D.Status.WARN and "127.0.0.1:1" in r.detail
+    assert r.status == D.Status.FAIL and "127.0.0.1:1" in r.detail and r.fix
 
 
 class _DateServer:
@@ -314,7 +326,7 @@ class _DateServer:
         self.date = date
 
         class H(http.server.BaseHTTPRequestHandler):
-            def do_HEAD(self):
+            def do_GET(self):
                 self.log_request(200)
                 self.send_response_only(200)
                 if outer.date is not None:
@@ -334,7 +346,8 @@ class _DateServer:
         self.httpd.server_close()
 
 
-@pytest.mark.parametrize("offset,status", [(0, D.Status.PASS), (600, D.Status.WARN), (-600, D.Status.WARN)])
+@pytest.mark.parametrize("offset,status", [(0, D.Status.PASS), (200, D.Status.WARN), (-200, D.Status.WARN),
+                                           (600, D.Status.FAIL), (-600, D.Status.FAIL)])
 def test_clock_check(monkeypatch, offset, status):
     s = _DateServer(email.utils.formatdate(time.time() + offset, usegmt=True))
     try:
@@ -349,7 +362,8 @@ def test_clock_check_without_a_usable_date(monkeypatch, date):
     s = _DateServer(date)
     try:
         monkeypatch.setattr(D, "clock_skew_probe_url", s.url)
-        assert run(D.check_clock()).status == D.Status.SKIP
+        r = run(D.check_clock())
+        assert r.status == D.Status.WARN and r.fix
     finally:
         s.close()
 
@@ -358,7 +372,7 @@ def test_clock_check_probe_unreachable(monkeypatch):
     monkeypatch.setattr(D, "clock_skew_probe_url", "http://127.0.0.1:1/")
     monkeypatch.setattr(D, "dial_timeout", 0.5)
     r = run(D.check_clock())
-    assert r.status == D.Status.SKIP and "unavailable" in r.detail
+    assert r.status == D.Status.WARN and "cannot reach clock probe endpoint" in r.detail and r.fix
 
 
 # ------------------------------------------------------------------ hardware / native / collectives
