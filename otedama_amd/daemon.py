@@ -65,9 +65,31 @@ class ServiceStatus:
     details: str = ""
 
 
+_GO_ESCAPES = {"\\": "\\\\", '"': '\\"', "\a": "\\a", "\b": "\\b", "\f": "\\f", "\n": "\\n", "\r": "\\r",
+               "\t": "\\t", "\v": "\\v"}
+
+
+def _go_quote(s: str) -> str:
+    """Go's %q of a string: backslash escapes for quote, backslash and control characters; printable text
+    (including non-ASCII) unchanged."""
+    out = []
+    for c in s:
+        if c in _GO_ESCAPES:
+            out.append(_GO_ESCAPES[c])
+        elif ord(c) < 0x20 or ord(c) == 0x7F:
+            out.append(f"\\x{ord(c):02x}")
+        elif not c.isprintable():
+            out.append(f"\\u{ord(c):04x}" if ord(c) <= 0xFFFF else f"\\U{ord(c):08x}")
+        else:
+            out.append(c)
+    return '"' + "".join(out) + '"'
+
+
 def quote_token(s: str) -> str:
+    """service.go:436-441: a token with a space, tab or double quote is Go-quoted (both systemd ExecStart= and
+    sc.exe binPath= accept C-style escapes); anything else is returned unchanged."""
     if any(c in s for c in ' \t"'):
-        return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
+        return _go_quote(s)
     return s
 
 
@@ -83,7 +105,7 @@ class Manager:
         self.config_path = config_path
         self.data_dir = data_dir
         self.flags = flags or ServiceFlags()
-        self.home = home or os.path.expanduser("~")
+        self.home = home  # None: $HOME / the password database, as os.UserHomeDir
 
     # ------------------------------------------------------------------ argv
     def service_argv(self) -> list[str]:
@@ -105,9 +127,24 @@ class Manager:
     def service_args(self) -> str:
         return " ".join(quote_token(a) for a in self.program_argv()[1:])
 
+    def _home(self) -> Path:
+        home = self.home if self.home is not None else os.environ.get("HOME", "")
+        if not home:
+            raise DaemonError("daemon: home directory not set ($HOME is empty)")
+        return Path(home)
+
+    def _service_dir(self, *parts: str) -> Path:
+        """~/<parts>, created (0755) if missing (service.go:139-149, 241-251)."""
+        d = self._home().joinpath(*parts)
+        try:
+            d.mkdir(mode=0o755, parents=True, exist_ok=True)
+        except OSError as exc:
+            raise DaemonError(f"daemon: create {d}: {exc}") from exc
+        return d
+
     # ------------------------------------------------------------------ systemd
     def systemd_unit_path(self) -> Path:
-        return Path(self.home) / ".config" / "systemd" / "user" / SYSTEMD_UNIT_NAME
+        return self._service_dir(".config", "systemd", "user") / SYSTEMD_UNIT_NAME
 
     def systemd_unit(self) -> str:
         data = self.data_dir or default_data_dir()
@@ -138,11 +175,19 @@ WantedBy=default.target
 
     # ------------------------------------------------------------------ launchd
     def launchd_plist_path(self) -> Path:
-        return Path(self.home) / "Library" / "LaunchAgents" / f"{LAUNCHD_LABEL}.plist"
+        return self._service_dir("Library", "LaunchAgents") / f"{LAUNCHD_LABEL}.plist"
+
+    def launchd_log_dir(self) -> Path:
+        """~/Library/Logs (per-user, not world-readable /tmp); /tmp only when the home directory is unknown or the
+        Logs directory cannot be created (service.go:333-343)."""
+        try:
+            return self._service_dir("Library", "Logs")
+        except DaemonError:
+            return Path("/tmp")
 
     def launchd_plist(self) -> str:
         entries = "".join(f"\t\t<string>{xml_escape(a)}</string>\n" for a in self.program_argv() if a)
-        logs = Path(self.home) / "Library" / "Logs"
+        logs = self.launchd_log_dir()
         return f"""<?xml version="1.0" encoding="UTF-8"?>
 <!DOCTYPE plist PUBLIC "-//Apple//DTD PLIST 1.0//EN"
     "http://www.apple.com/DTDs/PropertyList-1.0.dtd">
@@ -169,15 +214,16 @@ WantedBy=default.target
     def install(self) -> None:
         p = _platform()
         if p == "linux":
-            path = self.systemd_unit_path()
-            path.parent.mkdir(parents=True, exist_ok=True)
-            path.write_text(self.systemd_unit())
-            run_cmd("systemctl", "--user", "daemon-reload")
-            run_cmd("systemctl", "--user", "enable", "--now", SYSTEMD_UNIT_NAME)
+            try:
+                path = self.systemd_unit_path()
+            except DaemonError as exc:
+                raise DaemonError(f"daemon: systemd unit dir: {exc}") from exc
+            _write(path, self.systemd_unit(), "daemon: write systemd unit")
+            _step("daemon: systemctl daemon-reload", "systemctl", "--user", "daemon-reload")
+            _step("daemon: systemctl enable", "systemctl", "--user", "enable", "--now", SYSTEMD_UNIT_NAME)
         elif p == "darwin":
             path = self.launchd_plist_path()
-            path.parent.mkdir(parents=True, exist_ok=True)
-            path.write_text(self.launchd_plist())
+            _write(path, self.launchd_plist(), "daemon: write plist")
             run_cmd("launchctl", "load", "-w", str(path))
         elif p == "windows":
             run_cmd("sc.exe", "create", "Otedama", "binPath=", f'"{self.executable}" {self.service_args()}',
@@ -213,14 +259,37 @@ WantedBy=default.target
         p = _platform()
         if p == "linux":
             out, ok = cmd_output("systemctl", "--user", "is-active", SYSTEMD_UNIT_NAME)
-            return ServiceStatus(self.systemd_unit_path().exists(), ok and out.strip() == "active", 0, out)
+            return ServiceStatus(_exists(self.systemd_unit_path), ok and out.strip() == "active", 0, out)
         if p == "darwin":
             out, ok = cmd_output("launchctl", "list", LAUNCHD_LABEL)
-            return ServiceStatus(self.launchd_plist_path().exists(), ok and "Could not find" not in out, 0, out)
+            return ServiceStatus(_exists(self.launchd_plist_path), ok and "Could not find" not in out, 0, out)
         if p == "windows":
             out, ok = cmd_output("sc.exe", "query", "Otedama")
             return ServiceStatus(ok, ok and "RUNNING" in out, 0, out) if ok else ServiceStatus()
         raise DaemonError(f"daemon: unsupported platform {p!r}")
+
+
+def _exists(path_fn) -> bool:
+    """Status never fails on an unknown home directory: the service is then simply not installed."""
+    try:
+        return path_fn().exists()
+    except DaemonError:
+        return False
+
+
+def _write(path: Path, text: str, what: str) -> None:
+    try:
+        path.write_text(text)
+        os.chmod(path, 0o644)
+    except OSError as exc:
+        raise DaemonError(f"{what}: {exc}") from exc
+
+
+def _step(what: str, name: str, *args: str) -> None:
+    try:
+        run_cmd(name, *args)
+    except DaemonError as exc:
+        raise DaemonError(f"{what}: {exc}") from exc
 
 
 def _platform() -> str:

@@ -61,7 +61,7 @@ def test_all_flags_in_order(tmp_path):
 
 
 @pytest.mark.parametrize("s,want", [("plain", "plain"), ("with space", '"with space"'), ('q"uote', '"q\\"uote"'),
-                                    ("tab\there", '"tab\there"'), ('a b\\c', '"a b\\\\c"'), ("", "")])
+                                    ("tab\there", '"tab\\there"'), ('a b\\c', '"a b\\\\c"'), ("", "")])
 def test_quote_token(s, want):
     assert D.quote_token(s) == want
 
