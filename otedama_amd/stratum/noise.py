@@ -196,10 +196,11 @@ class Responder:
 
 # ------------------------------------------------------------------ framing
 def encode_frame(cs: CipherState, plain: bytes) -> bytes:
-    ct = cs.encrypt(b"", plain)
-    if len(ct) > MAX_FRAME:
-        raise NoiseError(f"noise: message too large: {len(ct)}-byte ciphertext exceeds {MAX_FRAME} "
+    # size check first: a refused frame must not consume a nonce (the peer would never see it)
+    if len(plain) + (TAG if cs.k is not None else 0) > MAX_FRAME:
+        raise NoiseError(f"noise: message too large: {len(plain) + TAG}-byte ciphertext exceeds {MAX_FRAME} "
                          f"(plaintext {len(plain)})")
+    ct = cs.encrypt(b"", plain)
     return struct.pack("<H", len(ct)) + ct
 
 
