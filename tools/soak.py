@@ -1,0 +1,151 @@
+"""Soak run of the production path on one GPU: the local validating pool (in this process) and `otedama run`
+(a child process, native GPU miner) for a fixed time, with job refreshes and new blocks much more often than a
+real pool sends them. Samples /metrics and the miner's RSS every --every seconds and prints one JSON line per
+sample, then a summary line. Exits 1 if any share is rejected, a sample's hashrate falls below 90% of the
+median after warm-up, or the miner's RSS grows by more than --max-rss-growth-mb.
+
+python tools/soak.py [--seconds 180] [--protocol sv2|v1] [--algorithm sha256d]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import re
+import signal
+import statistics
+import subprocess
+import sys
+import threading
+import time
+import urllib.request
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
+
+
+def metric(body: str, name: str, labels: str = "") -> float:
+    m = re.search(rf"^{re.escape(name)}{re.escape(labels)} (\S+)$", body, re.M)
+    return float(m.group(1)) if m else 0.0
+
+
+def rss_mb(pid: int) -> float:
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return int(line.split()[1]) / 1024.0
+    except OSError:
+        pass
+    return 0.0
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=180.0)
+    ap.add_argument("--every", type=float, default=10.0)
+    ap.add_argument("--warmup", type=float, default=30.0)
+    ap.add_argument("--protocol", choices=("sv2", "v1"), default="sv2")
+    ap.add_argument("--algorithm", default="sha256d")
+    ap.add_argument("--difficulty", type=float, default=2.0)
+    ap.add_argument("--job-interval", type=float, default=5.0)
+    ap.add_argument("--block-interval", type=float, default=45.0)
+    ap.add_argument("--max-rss-growth-mb", type=float, default=64.0)
+    ap.add_argument("--workdir", default="gpurun_out/soak")
+    a = ap.parse_args()
+
+    from otedama_amd.pool.server import PoolOptions, PoolServer
+
+    work = Path(a.workdir)
+    work.mkdir(parents=True, exist_ok=True)
+    pool = PoolServer(PoolOptions(algorithm=a.algorithm, initial_difficulty=a.difficulty, payout_address=ADDR,
+                                  target_share_seconds=1.0, retarget_seconds=15.0, job_interval=a.job_interval,
+                                  block_interval=a.block_interval))
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+
+    def serve():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(pool.start())
+        ready.set()
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True).start()
+    if not ready.wait(30):
+        print(json.dumps({"error": "pool did not start"}))
+        return 1
+    url = f"stratum+v2://{pool.addr_sv2}" if a.protocol == "sv2" else f"stratum+tcp://{pool.addr_v1}"
+    cfg = work / "config.yaml"
+    cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: {url}\nmining:\n  algorithm: {a.algorithm}\n")
+    env = dict(os.environ, HOME=str(work), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(work / "data"))
+    log = open(work / "miner.log", "w")
+    proc = subprocess.Popen([sys.executable, "-u", "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
+                             "--http-addr", "127.0.0.1:0", "--gpus", "0"], stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
+    http = None
+    t_start = time.time()
+    while time.time() - t_start < 120 and http is None:
+        line = proc.stdout.readline()
+        if not line:
+            break
+        log.write(line)
+        m = re.search(r"http: listening on (\S+)", line)
+        if m:
+            http = m.group(1)
+    threading.Thread(target=lambda: [log.write(x) for x in proc.stdout], daemon=True).start()
+    samples, rc = [], 0
+    try:
+        if http is None:
+            print(json.dumps({"error": "miner did not start", "log": str(work / "miner.log")}))
+            return 1
+        t0 = time.time()
+        while time.time() - t0 < a.seconds:
+            time.sleep(a.every)
+            if proc.poll() is not None:
+                print(json.dumps({"error": f"miner exited with {proc.returncode}"}), flush=True)
+                return 1
+            with urllib.request.urlopen(f"http://{http}/metrics", timeout=5) as r:
+                body = r.read().decode()
+            s = {"t": round(time.time() - t0, 1),
+                 "hashrate_ghs": round(metric(body, "otedama_hashrate_hashes_per_second") / 1e9, 3),
+                 "accepted": metric(body, "otedama_shares_total", '{status="accepted"}'),
+                 "rejected": metric(body, "otedama_shares_total", '{status="rejected"}'),
+                 "p50_submit_ms": metric(body, "otedama_submit_latency_milliseconds", '{quantile="0.5"}'),
+                 "pool_accepted": pool.m_accepted.value(), "pool_rejected": pool.m_rejected.value(),
+                 "blocks": pool.m_blocks.value() if hasattr(pool, "m_blocks") else None,
+                 "rss_mb": round(rss_mb(proc.pid), 1)}
+            samples.append(s)
+            print(json.dumps(s), flush=True)
+    finally:
+        proc.send_signal(signal.SIGTERM)
+        try:
+            exit_code = proc.wait(60)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            exit_code = proc.wait(10)
+        asyncio.run_coroutine_threadsafe(pool.stop(), loop).result(30)
+        loop.call_soon_threadsafe(loop.stop)
+        log.close()
+    steady = [s for s in samples if s["t"] >= a.warmup] or samples
+    rates = [s["hashrate_ghs"] for s in steady]
+    med = statistics.median(rates) if rates else 0.0
+    rss0 = steady[0]["rss_mb"] if steady else 0.0
+    last = samples[-1] if samples else {}
+    summary = {"summary": True, "seconds": a.seconds, "protocol": a.protocol, "algorithm": a.algorithm,
+               "median_hashrate_ghs": med, "min_hashrate_ghs": min(rates) if rates else 0.0,
+               "accepted": last.get("accepted"), "rejected": last.get("rejected"),
+               "pool_accepted": last.get("pool_accepted"), "pool_rejected": last.get("pool_rejected"),
+               "blocks": last.get("blocks"), "rss_growth_mb": round((last.get("rss_mb") or 0.0) - rss0, 1),
+               "miner_exit_code": exit_code}
+    ok = (rates and min(rates) >= 0.9 * med and not last.get("rejected") and not last.get("pool_rejected")
+          and summary["rss_growth_mb"] <= a.max_rss_growth_mb and exit_code == 0)
+    summary["ok"] = bool(ok)
+    print(json.dumps(summary), flush=True)
+    return 0 if ok and rc == 0 else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
