@@ -110,7 +110,7 @@ def main() -> int:
             with urllib.request.urlopen(f"http://{http}/metrics", timeout=5) as r:
                 body = r.read().decode()
             s = {"t": round(time.time() - t0, 1),
-                 "hashrate_ghs": round(metric(body, "otedama_hashrate_hashes_per_second") / 1e9, 3),
+                 "hashrate_ghs": round(metric(body, "otedama_hashrate_hashes_per_second") / 1e9, 6),
                  "accepted": metric(body, "otedama_shares_total", '{status="accepted"}'),
                  "rejected": metric(body, "otedama_shares_total", '{status="rejected"}'),
                  "p50_submit_ms": metric(body, "otedama_submit_latency_milliseconds", '{quantile="0.5"}'),
