@@ -34,8 +34,8 @@ def _job() -> dict:
             "version_mask": 0x1FFFE000}
 
 
-def _worker(rank: int, port: int, out_path: str) -> None:
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+def _worker(rank: int, port: int, out_path: str, world: int = WORLD) -> None:
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     from otedama_amd.engine.miners import MinerSet
     from otedama_amd.parallel.comm import NodeComm, init_from_env, shutdown
@@ -56,7 +56,8 @@ def _worker(rank: int, port: int, out_path: str) -> None:
     shares, deadline = [], time.monotonic() + 20
     while time.monotonic() < deadline:
         shares += node.poll(256)
-        if sum(1 for s in shares if s["device_id"] == "rank1") >= 3 and len(shares) >= 6:
+        per_rank = [sum(1 for s in shares if s["device_id"] == f"rank{r}") for r in range(1, world)]
+        if min(per_rank) >= 3 and len(shares) >= 2 * world:
             break
         time.sleep(0.02)
     node.update_hashrates()
@@ -72,7 +73,7 @@ def _worker(rank: int, port: int, out_path: str) -> None:
     shutdown(info)
     with open(out_path, "w") as f:
         json.dump({"epoch": ep, "shares": shares, "stats": stats, "total": total, "paused_delta": h2 - h1,
-                   "len": len(node)}, f, default=str)
+               "len": len(node)}, f, default=str)
 
 
 def test_node_two_ranks(tmp_path):
@@ -99,6 +100,31 @@ def test_node_two_ranks(tmp_path):
     assert res["paused_delta"] == 0
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def test_node_four_ranks_stripes_and_fan_in(tmp_path):
+    """World size 4 (the 8-GPU node's code path at half the ranks): every remote rank's shares reach rank 0
+    through R2, each rank hashes only its own stripe (variant index = rank mod 4, i.e. the two lowest rolled
+    version bits), and the R3 counters cover all four ranks."""
+    world = 4
+    out = tmp_path / "out4.json"
+    mp.start_processes(_worker, args=(_port(), str(out), world), nprocs=world, join=True, start_method="spawn")
+    res = json.loads(out.read_text())
+    assert res["len"] == world
+    for r in range(1, world):
+        assert res["stats"][f"rank{r}"]["hashes"] > 0
+    job = _job()
+    seen = set()
+    for s in res["shares"]:
+        rank = int(s["device_id"][4:]) if s["device_id"].startswith("rank") else 0
+        seen.add(rank)
+        assert (int(s["version"]) >> 13) & 3 == rank
+        hdr = bytearray(job["header"])
+        hdr[0:4] = int(s["version"]).to_bytes(4, "little")
+        hdr[68:72] = int(s["ntime"]).to_bytes(4, "little")
+        hdr[76:80] = int(s["nonce"]).to_bytes(4, "little")
+        assert int.from_bytes(sha256d(bytes(hdr)), "little") <= 1 << 240
+    assert seen == set(range(world))
 
 
 @pytest.mark.parametrize("n", [1])

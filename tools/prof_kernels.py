@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fixed workload for rocprofv3: SHA-256d full-range launches + scrypt batches."""
+"""Fixed workload for rocprofv3: SHA-256d full-range launches, scrypt batches, the version-parallel kernel, X11."""
 import sys
 
 import torch
@@ -37,5 +37,13 @@ if algo == "sha_v":  # K=8 vs version-parallel, equal work: 4 x 2^35 hashes each
     pv = sv.prepare(hs, tgt)
     for i in range(4):
         sv.launch(pv, i << 29, 1 << 29)
+    torch.cuda.synchronize()
+if algo == "x11":  # the 11-stage chain, 4 batches of 2^23 nonces
+    from otedama_amd.ops.search import X11Search
+
+    xs = X11Search("cuda:0")
+    xp = xs.prepare(hdr, tgt)
+    for i in range(4):
+        xs.launch(xp, i * xs.batch)
     torch.cuda.synchronize()
 print("done")
