@@ -7,8 +7,10 @@ Ryzen 9 7950X (BENCHMARKS.md:46, CPU only).
 
 One rank per GPU (torchrun). One timed step =
   R1  broadcast of the job blob from rank 0 (torch.distributed / RCCL),
-  K1  SHA-256d search of the FULL 2^32 nonce space of this rank's next header
-      variant (fixed midstate per variant; variants striped across ranks),
+  K1  SHA-256d search over this rank's next 64 BIP320 header variants (one per
+      lane of the version-parallel kernel, fixed midstate per variant, variants
+      striped across ranks) x 2^29 nonces; 8 consecutive steps tile the full
+      2^32 nonce space of each variant (--sha-kernel k: K variants x 2^32),
   R2  all_gather of every rank's on-device hit buffer,
   R3  all_reduce of the hash counters.
 Data: synthetic 80-byte block headers (random prev-hash / merkle root), share
