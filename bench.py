@@ -7,10 +7,11 @@ Ryzen 9 7950X (BENCHMARKS.md:46, CPU only).
 
 One rank per GPU (torchrun). One timed step =
   R1  broadcast of the job blob from rank 0 (torch.distributed / RCCL),
-  K1  SHA-256d search over this rank's next 64 BIP320 header variants (one per
+  K1  SHA-256d search over this rank's next 128 BIP320 header variants (two per
       lane of the version-parallel kernel, fixed midstate per variant, variants
-      striped across ranks) x 2^29 nonces; 8 consecutive steps tile the full
-      2^32 nonce space of each variant (--sha-kernel k: K variants x 2^32),
+      striped across ranks) x 2^28 nonces; 16 consecutive steps tile the full
+      2^32 nonce space of each variant (--sha-chains 1: 64 variants x 2^29;
+      --sha-kernel k: K variants x 2^32),
   R2  all_gather of every rank's on-device hit buffer,
   R3  all_reduce of the hash counters.
 Data: synthetic 80-byte block headers (random prev-hash / merkle root), share
@@ -65,6 +66,8 @@ def main() -> int:
     ap.add_argument("--sha-kernel", choices=("v", "k"), default="v",
                     help="v: 64 version variants per wave, block-2 schedule on the scalar unit (default); "
                          "k: --sha-variants variants per lane")
+    ap.add_argument("--sha-chains", type=int, choices=(1, 2), default=2,
+                    help="v kernel: variants per lane (2: 128 variants per wave-group, 4 waves/SIMD; 1: 64, 8 waves)")
     ap.add_argument("--sha-variants", type=int, default=8,
                     help="k kernel: BIP320 version variants per launch sharing the block-2 schedule (1 = single midstate)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
@@ -93,12 +96,19 @@ def main() -> int:
     world = info.world_size
     use_v = args.sha_kernel == "v"
     if use_v:
-        # One step = 64 version variants (one wave's lanes) x 2^29 nonces = 2^35 hashes, the same work as the K=8
-        # step (8 x 2^32); 8 consecutive steps tile the full 2^32 nonces of one 64-variant group.
-        K = N.SHA256D_V_GROUP
-        V_COUNT = 1 << 29
+        # One step = 64 x chains version variants (chains per lane of a wave) x 2^35 / that many nonces = 2^35
+        # hashes, the same work as the K=8 step (8 x 2^32); 8 x chains consecutive steps tile the full 2^32 nonces
+        # of one variant group. Two chains run the 4-waves/SIMD build at 128 blocks/CU (profiles/r2/sha_v2).
+        K = N.SHA256D_V_GROUP * args.sha_chains
+        V_COUNT = (1 << 35) // K
         steps_per_group = (1 << 32) // V_COUNT
-        search = Sha256dSearchV(dev, grid=args.grid or None)
+        if args.sha_chains == 2:
+            from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, default_grid
+
+            search = Sha256dSearchV(dev, grid=args.grid or default_grid(dev, SHA256D_V2_BLOCKS_PER_CU), chains=2,
+                                    occupancy8=False)
+        else:
+            search = Sha256dSearchV(dev, grid=args.grid or None)
     else:
         V_COUNT, steps_per_group = 1 << 32, 1
         K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
@@ -117,7 +127,7 @@ def main() -> int:
     v_groups: dict[int, tuple[list[bytes], object]] = {}
 
     def v_group(q: int):
-        # variant group q of this rank: stripe positions 64q .. 64q+63; the table is uploaded once, before timing
+        # variant group q of this rank: stripe positions Kq .. Kq+K-1; the table is uploaded once, before timing
         if q not in v_groups:
             hdrs = [N.variant_header(job, stripe.start + (q * K + j) * stripe.stride)[0] for j in range(K)]
             v_groups[q] = (hdrs, search.prepare(hdrs, job["target"]))
@@ -290,14 +300,15 @@ def main() -> int:
                 "global_batch": step_hashes * world,
                 "seq_len": 80,
                 "parallelism": (f"dp{world} (nonce-space: per-rank variant stripe; "
-                                + ("64 variants x 2^29 nonces per step, 8 steps tile 2^32 per variant)" if use_v
+                                + (f"{K} variants x 2^{(V_COUNT).bit_length() - 1} nonces per step, {steps_per_group} "
+                                   "steps tile 2^32 per variant)" if use_v
                                    else "full 2^32 nonces per variant per step)")),
                 "algorithm": ("SHA-256d nonce search, fixed midstate per variant; " + (
-                    "64 BIP320 version variants per wave (one per lane) share the block-2 message schedule, "
+                    f"{K} BIP320 version variants per wave ({K // 64} per lane) share the block-2 message schedule, "
                     "computed on the scalar unit" if use_v else
                     f"{K} BIP320 version variants per launch share the block-2 message schedule")),
-                "sha_kernel": "otd_sha256d_search_v<8>" if use_v else (f"otd_sha256d_search_k<{K}>" if K > 1
-                                                                       else "otd_sha256d_search"),
+                "sha_kernel": (("otd_sha256d_search_v2<0>" if K == 128 else "otd_sha256d_search_v<8>") if use_v
+                               else (f"otd_sha256d_search_k<{K}>" if K > 1 else "otd_sha256d_search")),
                 "variants_per_step": K,
                 "grid": search.grid,
             },

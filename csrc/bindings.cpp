@@ -26,7 +26,7 @@ void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, ui
 void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                          uintptr_t stream);
 void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                         uint32_t cap, int grid, uintptr_t stream, int block);
+                         uint32_t cap, int grid, uintptr_t stream, int block, int chains);
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream);
 void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
@@ -260,6 +260,7 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof p);
   }, py::arg("headers"), py::arg("target"));
   m.attr("SHA256D_V_GROUP") = kSha256dVGroup;
+  m.attr("SHA256D_V2_GROUP") = kSha256dV2Group;
   m.def("sha256d_prepare_v", [](const py::list& headers, const py::bytes& t) {
     std::string ts = need(t, 32, "target");
     std::vector<std::string> hs;
@@ -315,17 +316,19 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("params"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"), py::arg("grid"),
      py::arg("stream"));
   m.def("launch_sha256d_v", [](const py::bytes& params, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                               uint32_t cap, int grid, uintptr_t stream, bool occupancy8, int block) {
+                               uint32_t cap, int grid, uintptr_t stream, bool occupancy8, int block, int chains) {
     std::string ps = need(params, sizeof(Sha256dParamsV), "params");
     Sha256dParamsV p; std::memcpy(&p, ps.data(), sizeof p);
     p.occupancy8 = occupancy8 ? 1u : 0u;
     if (p.groups == 0 || count == 0 || count > (1ull << 32)) throw std::invalid_argument("bad groups / count");
     if (block != 64 && block != 256) throw std::invalid_argument("block must be 64 or 256 threads");
-    if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % p.groups != 0 || vars == 0 || out == 0)
+    if (chains != 1 && chains != 2) throw std::invalid_argument("chains must be 1 or 2");
+    if (p.groups % uint32_t(chains) != 0) throw std::invalid_argument("two chains need an even number of 64-variant groups");
+    if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % (p.groups / uint32_t(chains)) != 0 || vars == 0 || out == 0)
       throw std::invalid_argument("the wave count must be a multiple of the variant groups; vars/out must be set");
-    py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream, block);
+    py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream, block, chains);
   }, py::arg("params"), py::arg("vars"), py::arg("base"), py::arg("count"), py::arg("out"), py::arg("cap"),
-     py::arg("grid"), py::arg("stream"), py::arg("occupancy8") = false, py::arg("block") = 256);
+     py::arg("grid"), py::arg("stream"), py::arg("occupancy8") = false, py::arg("block") = 256, py::arg("chains") = 1);
   m.def("launch_scrypt", [](const py::bytes& params, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch,
                             int gap, uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
     std::string ps = need(params, sizeof(ScryptParams), "params");
@@ -375,7 +378,7 @@ PYBIND11_MODULE(_native, m) {
   py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")
       .def(py::init<int, std::string, uint64_t, int, size_t, int>(), py::arg("device"), py::arg("device_id"),
            py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024,
-           py::arg("sha_variants") = 64);
+           py::arg("sha_variants") = 128);
   py::class_<CpuMiner, MinerBase, std::shared_ptr<CpuMiner>>(m, "CpuMiner")
       .def(py::init<int, std::string, size_t>(), py::arg("threads"), py::arg("device_id") = "cpu-0",
            py::arg("queue_cap") = 1024);

@@ -51,6 +51,7 @@ bool sha256d_prepare_k(const uint8_t* const headers80[], int k, const uint8_t ta
 // Version-parallel search (sha256d_search_v): 64 * groups variants with identical bytes 64..75, one per lane;
 // the per-variant blocks live in device memory (vars[64 * groups]), the shared block-2 words in the kernarg.
 constexpr int kSha256dVGroup = 64;  // variants per wave (wave64 lanes)
+constexpr int kSha256dV2Group = 128;  // two-chain version-parallel kernel: two variants per lane
 struct Sha256dParamsV {
   uint32_t w0, w1, w2, w16, w17;
   uint32_t target_hi;

@@ -126,11 +126,13 @@ class MinerBase {
 // One host thread per GPU: double-buffered batches on a private HIP stream.
 class GpuMiner : public MinerBase {
  public:
-  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling): 64 (default) = the
-  // version-parallel kernel, one variant per lane of a wave (sha256d_search_v); 1..16 = the K-variant kernel
-  // (rounded down to an instantiated K: 2, 3, 4, 6, 8, 12, 16). A job whose variant space cannot supply 64
-  // variants with a common block 2 falls back to the K kernel with what it can supply.
-  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants = 64);
+  // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling): 128 (default) = the
+  // two-chain version-parallel kernel (two variants per lane, sha256d_search_v2); 64 = one variant per lane of a
+  // wave (sha256d_search_v); 1..16 = the K-variant kernel (rounded down to an instantiated K: 2, 3, 4, 6, 8, 12,
+  // 16). A job whose variant space cannot supply that many variants with a common block 2 falls back to the next
+  // smaller layout it can supply (128 -> 64 -> K).
+  GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap,
+           int sha_variants = 128);
   ~GpuMiner() override;
   void start() override;
   void stop() override;
@@ -140,9 +142,11 @@ class GpuMiner : public MinerBase {
   uint64_t batch_;
   int grid_;
   int sha_k_;
-  bool sha_v_;  // version-parallel kernel enabled
+  bool sha_v_;   // version-parallel kernel enabled
+  bool sha_v2_;  // two-chain version-parallel kernel enabled (tried first)
   int grid_k_ = 0;
   int grid_v_ = 0;
+  int grid_v2_ = 0;
   std::thread th_;
 };
 

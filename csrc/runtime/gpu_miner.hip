@@ -27,7 +27,8 @@ hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t
 hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
                                    int grid, hipStream_t stream);
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
-                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block = 256);
+                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block = 256,
+                                   int chains = 1);
 
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
                                 int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
@@ -53,9 +54,9 @@ struct Slot {
   uint64_t gen = 0;
   uint64_t count = 0;  // nonces per variant
   int nvar = 1;        // > 1: K-variant / version-parallel SHA-256d launch, hits carry the variant index
-  uint8_t header[kSha256dVGroup][80];
-  uint32_t version[kSha256dVGroup] = {0}, ntime[kSha256dVGroup] = {0};
-  uint64_t en2[kSha256dVGroup] = {0};
+  uint8_t header[kSha256dV2Group][80];
+  uint32_t version[kSha256dV2Group] = {0}, ntime[kSha256dV2Group] = {0};
+  uint64_t en2[kSha256dV2Group] = {0};
   Sha256dVariant* d_vars = nullptr;  // version-parallel kernel: per-lane variant table (device)
   Sha256dVariant* h_vars = nullptr;  // pinned staging copy
   TraceId range = 0;  // roctx: enqueue -> host verification of this batch
@@ -65,7 +66,7 @@ struct Slot {
 GpuMiner::GpuMiner(int device, std::string device_id, uint64_t batch_nonces, int grid, size_t queue_cap, int sha_variants)
     : MinerBase(std::move(device_id), queue_cap), device_(device), batch_(batch_nonces), grid_(grid),
       sha_k_(sha_variants < 1 ? 1 : sha_variants > kSha256dMaxK ? kSha256dMaxK : sha_variants),
-      sha_v_(sha_variants >= kSha256dVGroup) {
+      sha_v_(sha_variants >= kSha256dVGroup), sha_v2_(sha_variants >= kSha256dV2Group) {
   if (batch_ == 0 || batch_ > (1ull << 32)) batch_ = 1ull << 30;
   // Batches must tile the 2^32 nonce range exactly.
   while ((1ull << 32) % batch_) --batch_;
@@ -131,8 +132,8 @@ void GpuMiner::loop() {
     OTD_HIP(hipEventCreate(&s.start));
     OTD_HIP(hipEventCreate(&s.done));
     if (sha_v_) {
-      OTD_HIP(hipMalloc(&s.d_vars, kSha256dVGroup * sizeof(Sha256dVariant)));
-      OTD_HIP(hipHostMalloc(&s.h_vars, kSha256dVGroup * sizeof(Sha256dVariant), hipHostMallocDefault));
+      OTD_HIP(hipMalloc(&s.d_vars, kSha256dV2Group * sizeof(Sha256dVariant)));
+      OTD_HIP(hipHostMalloc(&s.h_vars, kSha256dV2Group * sizeof(Sha256dVariant), hipHostMallocDefault));
     }
   }
   // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
@@ -147,10 +148,15 @@ void GpuMiner::loop() {
   grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
   // Version-parallel kernel (8-waves/SIMD build): 64 blocks of 256 per CU (tools/bench_sha_v.py, profiles/r2/sha_v).
   grid_v_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 64;
-  // Host variant table of the current 64-variant group, rebuilt only when the group changes (once per 2^32 nonces).
+  // Two-chain kernel (4 waves/SIMD build): 128 blocks of 256 per CU (tools/bench_sha_v.py --chains2-bpc,
+  // profiles/r2/sha_v2).
+  grid_v2_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 128;
+  // Host variant table of the current 64/128-variant group, rebuilt only when the group changes (once per 2^32
+  // nonces).
   uint64_t v_table_gen = ~0ull, v_table_k = ~0ull;
+  int v_table_n = 0;
   Sha256dParamsV v_params{};
-  Sha256dVariant v_table[kSha256dVGroup];
+  Sha256dVariant v_table[kSha256dV2Group];
 
   uint64_t cur_gen = ~0ull;
   uint64_t k = 0;       // variant-stripe position
@@ -217,19 +223,26 @@ void GpuMiner::loop() {
     job->variant_header(v, s.header[0], &s.version[0], &s.ntime[0], &s.en2[0]);
     bool use_v = false;
     if (job->algo == Algo::kSha256d && sha_v_) {
-      // 64 consecutive stripe positions with a common block 2 -> one variant per lane of the version-parallel
-      // kernel. The group is all-or-nothing (a partial group takes the K path below) and depends only on
-      // (job, k), so every launch of a group uses the same kernel and W3/nonce space.
+      // 128 (two-chain kernel) or 64 consecutive stripe positions with a common block 2 -> one or two variants per
+      // lane of the version-parallel kernel. A group is all-or-nothing (a shorter run takes the next layout down,
+      // ending at the K path below) and depends only on (job, k), so every launch of a group uses the same kernel
+      // and W3/nonce space.
+      const int want = sha_v2_ ? kSha256dV2Group : kSha256dVGroup;
       int kv = 1;
-      while (kv < kSha256dVGroup) {
+      while (kv < want) {
         const uint64_t vk = job->variant_start + (k + kv) * job->variant_stride;
         if (vk >= job->variant_space()) break;
         job->variant_header(vk, s.header[kv], &s.version[kv], &s.ntime[kv], &s.en2[kv]);
         if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
         ++kv;
       }
-      use_v = kv == kSha256dVGroup;
-      if (use_v) s.nvar = kSha256dVGroup;
+      if (kv >= kSha256dV2Group && sha_v2_) {
+        use_v = true;
+        s.nvar = kSha256dV2Group;
+      } else if (kv >= kSha256dVGroup) {
+        use_v = true;
+        s.nvar = kSha256dVGroup;
+      }
     }
     if (!use_v && job->algo == Algo::kSha256d && sha_k_ > 1) {
       // Group the next stripe positions whose headers differ only in block 1 (version rolling): they share
@@ -268,22 +281,25 @@ void GpuMiner::loop() {
       s.count = remaining < x11_batch ? remaining : x11_batch;
       OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), s.d_out, kHitCap, stream));
     } else if (use_v) {
-      if (v_table_gen != gen || v_table_k != k) {
-        const uint8_t* hs[kSha256dVGroup];
-        for (int j = 0; j < kSha256dVGroup; ++j) hs[j] = s.header[j];
-        if (!sha256d_prepare_v(hs, kSha256dVGroup, job->target, &v_params, v_table))
+      const bool two = s.nvar == kSha256dV2Group;
+      if (v_table_gen != gen || v_table_k != k || v_table_n != s.nvar) {
+        const uint8_t* hs[kSha256dV2Group];
+        for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
+        if (!sha256d_prepare_v(hs, s.nvar, job->target, &v_params, v_table))
           throw std::runtime_error("sha256d_prepare_v");
-        v_params.occupancy8 = 1;
+        v_params.occupancy8 = two ? 0 : 1;  // two chains: the 4-waves/SIMD build; one chain: the 8-wave build
         v_table_gen = gen;
         v_table_k = k;
+        v_table_n = s.nvar;
       }
-      std::memcpy(s.h_vars, v_table, sizeof v_table);
-      OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, sizeof v_table, hipMemcpyHostToDevice, stream));
+      const size_t table_bytes = size_t(s.nvar) * sizeof(Sha256dVariant);
+      std::memcpy(s.h_vars, v_table, table_bytes);
+      OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, table_bytes, hipMemcpyHostToDevice, stream));
       // W3 (big-endian nonce word) windows tile [0, 2^32) exactly like the nonce windows of the other kernels;
       // the kernel reports nonce = bswap(W3). Launch duration stays batch_ hashes.
-      s.count = batch_ / kSha256dVGroup;
-      OTD_HIP(launch_sha256d_search_v(v_params, s.d_vars, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_v_,
-                                      stream));
+      s.count = batch_ >= uint64_t(s.nvar) ? batch_ / uint64_t(s.nvar) : 1;  // powers of two: still tiles 2^32
+      OTD_HIP(launch_sha256d_search_v(v_params, s.d_vars, uint32_t(nonce_off), s.count, s.d_out, kHitCap,
+                                      two ? grid_v2_ : grid_v_, stream, 256, two ? 2 : 1));
     } else if (s.nvar > 1) {
       Sha256dParamsK p;
       const uint8_t* hs[kSha256dMaxK];
@@ -332,10 +348,10 @@ void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count,
 }
 
 void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
-                         uint32_t cap, int grid, uintptr_t stream, int block) {
+                         uint32_t cap, int grid, uintptr_t stream, int block, int chains) {
   OTD_HIP(launch_sha256d_search_v(p, reinterpret_cast<const Sha256dVariant*>(vars), base, count,
                                   reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream),
-                                  block));
+                                  block, chains));
 }
 
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import os
+import struct
 import time
 from typing import TextIO
 
@@ -58,16 +59,19 @@ def bench_gpu(device: int = 0, reps: int = 3, scrypt_batches: int = 4) -> dict:
         s.launch(p, 0, 1 << 32)
     torch.cuda.synchronize()
     sha = reps * (1 << 32) / (time.perf_counter() - t0)
-    # version rolling (BIP320): 64 variants per wave, one per lane, block-2 schedule on the scalar unit
-    sv = Sha256dSearchV(f"cuda:{device}")
-    pv = sv.prepare([bytes([v & 0xFF, (v >> 8) | 0x20, 0, 0x20]) + hdr[4:] for v in range(64)], bytes(32))
+    # version rolling (BIP320): 128 variants per wave-group, two per lane, block-2 schedule on the scalar unit
+    from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, default_grid
+
+    sv = Sha256dSearchV(f"cuda:{device}", grid=default_grid(f"cuda:{device}", SHA256D_V2_BLOCKS_PER_CU), chains=2,
+                        occupancy8=False)
+    pv = sv.prepare([struct.pack("<I", 0x20000000 | (v << 13)) + hdr[4:] for v in range(128)], bytes(32))
     sv.launch(pv, 0, 1 << 22)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(reps):
-        sv.launch(pv, i << 29, 1 << 29)
+        sv.launch(pv, i << 28, 1 << 28)
     torch.cuda.synchronize()
-    sha_v = reps * 64 * (1 << 29) / (time.perf_counter() - t0)
+    sha_v = reps * 128 * (1 << 28) / (time.perf_counter() - t0)
     sc = ScryptSearch(f"cuda:{device}")
     sp = N.scrypt_prepare(hdr, bytes(32))
     sc.launch(sp, 0)

@@ -28,6 +28,10 @@ SHA256D_K_BLOCKS_PER_CU = 16  # K-variant kernel: K=8 121 VGPRs (4 waves/SIMD); 
 # 8/16/32/64/96/128 per CU -> 18.37/18.73/19.00/19.61/19.58/19.61 GH/s; more resident-block rounds keep the waves'
 # scalar/vector phases apart).
 SHA256D_V_BLOCKS_PER_CU = 64
+# Two-chain version-parallel kernel (two variants per lane), 4-waves/SIMD build: 128 blocks per CU (profiles/r2/sha_v2:
+# 16/32/64/128/256 per CU -> 19.12/19.29/19.32/19.36-19.40/19.37-19.42 GH/s, against 19.21-19.30 for the one-chain
+# kernel in the same runs).
+SHA256D_V2_BLOCKS_PER_CU = 128
 SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
 
 
@@ -152,9 +156,14 @@ class Sha256dSearchV:
     W3 in [base, base + count) covers the nonces bswap(W3) of that range for every variant."""
 
     def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, occupancy8: bool = True,
-                 block: int = 256):
+                 block: int = 256, chains: int = 1):
+        """chains=2: two variants per lane on the same nonce (128 per wave); ``occupancy8`` then selects the
+        5-waves/SIMD build of that kernel instead of the 4-wave one."""
         self.native = require_native()
-        self.group = self.native.SHA256D_V_GROUP
+        if chains not in (1, 2):
+            raise ValueError("chains must be 1 or 2")
+        self.chains = chains
+        self.group = self.native.SHA256D_V_GROUP * chains
         self.occupancy8 = occupancy8
         if block not in (64, 256):
             raise ValueError("block must be 64 or 256 threads")
@@ -193,7 +202,7 @@ class Sha256dSearchV:
             out[:1].zero_()
         self.native.launch_sha256d_v(prep.params, prep.vars.data_ptr(), base & 0xFFFFFFFF, int(count),
                                      out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8,
-                                     self.block)
+                                     self.block, self.chains)
         return SearchResultK(out, self.cap)
 
     def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:

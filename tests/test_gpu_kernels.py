@@ -308,13 +308,14 @@ def _v_headers(n, seed=b"v"):
     return [struct.pack("<I", 0x20000000 | ((v & 0xFFFF) << 13)) + tail[:72] + bytes(4) for v in range(n)]
 
 
-@pytest.mark.parametrize("groups,base", [(1, 0x12345600), (2, 0xFFFFFC00)])
-def test_sha256d_v_kernel_matches_cpu(groups, base):
-    """Version-parallel kernel: for every variant (lane) and every W3 of the window (incl. the 2^32 wrap), the
-    reported (nonce = bswap(W3), variant) pairs are exactly the CPU's shares."""
+@pytest.mark.parametrize("groups,base,chains,occ", [(1, 0x12345600, 1, True), (2, 0xFFFFFC00, 1, True),
+                                                  (2, 0x12345600, 2, False), (4, 0xFFFFFC00, 2, True)])
+def test_sha256d_v_kernel_matches_cpu(groups, base, chains, occ):
+    """Version-parallel kernels (one or two variants per lane): for every variant and every W3 of the window
+    (incl. the 2^32 wrap), the reported (nonce = bswap(W3), variant) pairs are exactly the CPU's shares."""
     from otedama_amd.ops.search import Sha256dSearchV
 
-    s = Sha256dSearchV("cuda:0", grid=512)
+    s = Sha256dSearchV("cuda:0", grid=512, chains=chains, occupancy8=occ)
     hs = _v_headers(64 * groups)
     target_int = (1 << 248) - 1
     count = 1024
@@ -345,6 +346,12 @@ def test_sha256d_v_kernel_both_builds_and_grid_contract():
         Sha256dSearchV("cuda:0", grid=3, block=64).prepare(hs, tgt)  # 3 waves cannot split 2 groups
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", block=128)
+    d = sorted(Sha256dSearchV("cuda:0", grid=256, chains=2).search(hs, tgt, 7, 512))  # 128 variants, 2 per lane
+    assert d == a
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", grid=256, chains=2).prepare(hs[:64], tgt)  # two chains need 128 variants
+    with pytest.raises(ValueError):
+        Sha256dSearchV("cuda:0", chains=3)
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", grid=256).prepare(hs[:63], tgt)
 
@@ -368,8 +375,9 @@ def test_sha256d_v_launch_on_a_side_stream():
 
 
 def test_gpu_miner_kernel_selection():
-    """Default GpuMiner: version-rolling jobs take the version-parallel kernel (64 variants per launch); with
-    sha_variants=8 they take the K-variant kernel; a job without a version mask runs single-midstate."""
+    """Default GpuMiner: version-rolling jobs take the two-chain version-parallel kernel (128 variants per launch),
+    or the 64-variant one when the mask supplies fewer; with sha_variants=8 they take the K-variant kernel; a job
+    without a version mask runs single-midstate."""
     from otedama_amd.models.header import int_to_hash
 
     N = _native()
@@ -396,10 +404,15 @@ def test_gpu_miner_kernel_selection():
         return st, shares
 
     job = {"header": hdr, "target": tgt, "epoch": 1, "job_id": "a", "version_mask": 0x1FFFE000}
-    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), job, 8)
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), job, 8)  # default: two variants per lane
     assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 4
-    assert st["hashes"] % ((1 << 28) // 64 * 64) == 0
+    assert st["hashes"] % ((1 << 28) // 128 * 128) == 0
     assert len({s["version"] for s in shares}) >= 2
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28, sha_variants=64), job, 4)  # one per lane
+    assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 2
+    # only 64 versions in the mask: the default miner falls back from 128 to the 64-variant layout
+    st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), dict(job, version_mask=0x7E000), 4)
+    assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 2
     st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28, sha_variants=8), job, 4)
     assert st["variant_launches"] == st["launches"] >= 2 and len(shares) >= 2
     st, shares = run(N.GpuMiner(0, "gpu-0", batch_nonces=1 << 28), dict(job, version_mask=0), 2)

@@ -51,6 +51,7 @@ def main() -> int:
     ap.add_argument("--bpc8", default="8,16,24,32")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--block64-bpc", default="", help="also time 64-thread blocks at these 64-thread blocks per CU")
+    ap.add_argument("--chains2-bpc", default="", help="also time the two-variants-per-lane kernel at these blocks per CU")
     a = ap.parse_args()
     count = 1 << a.count
     if not a.no_check:
@@ -98,6 +99,23 @@ def main() -> int:
         p = s.prepare(headers_for(64), target)
         rate = run(lambda: s.launch(p, 0, count), 64 * count)
         print(json.dumps({"kernel": "v8", "block": 64, "grid": s.grid, "ghs": round(rate / 1e9, 3)}), flush=True)
+    if a.chains2_bpc and not a.no_check:
+        ref = sorted(Sha256dSearchV("cuda:0").search(headers_for(128), (((1 << 248) - 1)).to_bytes(32, "little"),
+                                                     0x12345600, 1024))
+        for occ in (False, True):
+            got = sorted(Sha256dSearchV("cuda:0", chains=2, occupancy8=occ).search(
+                headers_for(128), (((1 << 248) - 1)).to_bytes(32, "little"), 0x12345600, 1024))
+            r = {"check": "sha256d_v2_vs_v", "occ5": occ, "hits": len(got), "expected": len(ref), "ok": got == ref}
+            print(json.dumps(r), flush=True)
+            if not r["ok"]:
+                return 1
+    for occ in (False, True):
+        for bpc in [int(x) for x in a.chains2_bpc.split(",") if x]:
+            s = Sha256dSearchV("cuda:0", grid=cus * bpc, chains=2, occupancy8=occ)
+            p = s.prepare(headers_for(128), target)
+            rate = run(lambda: s.launch(p, 0, count // 2), 128 * (count // 2))
+            print(json.dumps({"kernel": "v2_5w" if occ else "v2_4w", "grid": s.grid, "ghs": round(rate / 1e9, 3)}),
+                  flush=True)
     return 0
 
 
