@@ -322,8 +322,9 @@ PYBIND11_MODULE(_native, m) {
     p.occupancy8 = occupancy8 ? 1u : 0u;
     if (p.groups == 0 || count == 0 || count > (1ull << 32)) throw std::invalid_argument("bad groups / count");
     if (block != 64 && block != 256) throw std::invalid_argument("block must be 64 or 256 threads");
-    if (chains != 1 && chains != 2) throw std::invalid_argument("chains must be 1 or 2");
-    if (p.groups % uint32_t(chains) != 0) throw std::invalid_argument("two chains need an even number of 64-variant groups");
+    if (chains < 1 || chains > 4) throw std::invalid_argument("chains must be 1..4");
+    if (p.groups % uint32_t(chains) != 0)
+      throw std::invalid_argument("chains variants per lane need a multiple of 64 * chains variants");
     if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % (p.groups / uint32_t(chains)) != 0 || vars == 0 || out == 0)
       throw std::invalid_argument("the wave count must be a multiple of the variant groups; vars/out must be set");
     py_launch_sha256d_v(p, vars, base, count, out, cap, grid, stream, block, chains);

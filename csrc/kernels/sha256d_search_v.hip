@@ -136,11 +136,12 @@ template __global__ void otd_sha256d_search_v<8>(const otedama::Sha256dParamsV, 
                                                    uint32_t*, uint32_t);
 
 
-// Two variants per lane (lane l of group g: variants 128g + l and 128g + 64 + l), same nonce: both chains use the one
-// scalar schedule, so the SALU work per hash halves, and the two independent round chains give each wave ILP at
-// lower occupancy (MINW = 0: 111 VGPRs, 4 waves/SIMD; MINW = 5: 96 VGPRs, 5 waves). p.groups counts groups of 128.
-template <int MINW>
-__global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v2(
+// NC variants per lane (lane l of group g: variants 64*NC*g + 64c + l, c < NC), same nonce: all chains use the one
+// scalar schedule, so the SALU work per hash drops NC-fold, and the independent round chains give each wave ILP at
+// lower occupancy. NC = 2: 111 VGPRs, 4 waves/SIMD (MINW = 5: 96 VGPRs, 5 waves); NC = 3: 157 VGPRs, 3 waves;
+// NC = 4: 203 VGPRs, 2 waves. p.groups counts groups of 64*NC variants.
+template <int NC, int MINW>
+__global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_vn(
     const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, uint32_t* __restrict__ out,
     uint32_t cap) {
   const uint32_t wpb = blockDim.x >> 6;
@@ -150,12 +151,12 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
   const uint32_t g = wave % groups;
   const uint32_t first = wave / groups;
   const uint32_t stride = waves / groups;
-  uint32_t vi[2];
-  vi[0] = g * 128u + (threadIdx.x & 63u);
-  vi[1] = vi[0] + 64u;
-  uint32_t mid[2][8], st3[2][8], pre3[2], t2_3[2];
+  uint32_t vi[NC];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < NC; ++c) vi[c] = g * (64u * NC) + 64u * c + (threadIdx.x & 63u);
+  uint32_t mid[NC][8], st3[NC][8], pre3[NC], t2_3[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
     const otedama::Sha256dVariant& v = vars[vi[c]];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { mid[c][i] = v.mid[i]; st3[c][i] = v.st3[i]; }
@@ -171,9 +172,9 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
     W[15] = 640u;
     W[16] = p.w16;
     W[17] = p.w17;
-    uint32_t a[2], b[2], c_[2], d[2], e[2], f[2], gg[2], h[2];
+    uint32_t a[NC], b[NC], c_[NC], d[NC], e[NC], f[NC], gg[NC], h[NC];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const uint32_t t1_3 = pre3[c] + w3;
       h[c] = st3[c][6]; gg[c] = st3[c][5]; f[c] = st3[c][4]; e[c] = st3[c][3] + t1_3;
       d[c] = st3[c][2]; c_[c] = st3[c][1]; b[c] = st3[c][0]; a[c] = t1_3 + t2_3[c];
@@ -183,16 +184,16 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
       if (t >= 18) W[t] = sss1(W[t - 2]) + W[t - 7] + sss0(W[t - 15]) + W[t - 16];
       const uint32_t kw = sha256_k(t) + W[t];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NC; ++c) {
         const uint32_t t1 = h[c] + bS1(e[c]) + ch(e[c], f[c], gg[c]) + kw;
         const uint32_t t2 = bS0(a[c]) + maj(a[c], b[c], c_[c]);
         h[c] = gg[c]; gg[c] = f[c]; f[c] = e[c]; e[c] = d[c] + t1; d[c] = c_[c]; c_[c] = b[c]; b[c] = a[c]; a[c] = t1 + t2;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    uint32_t X[2][61];
+    uint32_t X[NC][61];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NC; ++c) {
       X[c][0] = mid[c][0] + a[c]; X[c][1] = mid[c][1] + b[c]; X[c][2] = mid[c][2] + c_[c]; X[c][3] = mid[c][3] + d[c];
       X[c][4] = mid[c][4] + e[c]; X[c][5] = mid[c][5] + f[c]; X[c][6] = mid[c][6] + gg[c]; X[c][7] = mid[c][7] + h[c];
       X[c][8] = 0x80000000u;
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
 #pragma unroll
     for (int t = 0; t < 61; ++t) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NC; ++c) {
         if (t >= 16) X[c][t] = ss1(X[c][t - 2], t >= 18) + X[c][t - 7] + ss0(X[c][t - 15], t <= 22 || t >= 31) + X[c][t - 16];
         const uint32_t t1 = h[c] + bS1(e[c]) + ch(e[c], f[c], gg[c]) + (sha256_k(t) + X[c][t]);
         const uint32_t ne = d[c] + t1;
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
       }
     }
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const uint32_t h7 = e[c] + kIVv[7];
       if (__builtin_bswap32(h7) <= p.target_hi) {
         const uint32_t slot = atomicAdd(out, 1u);
@@ -226,23 +227,35 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
     }
   }
 }
-template __global__ void otd_sha256d_search_v2<0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t, uint32_t*, uint32_t);
-template __global__ void otd_sha256d_search_v2<5>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t, uint32_t*, uint32_t);
+
+template __global__ void otd_sha256d_search_vn<2, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
+                                                       uint32_t*, uint32_t);
+template __global__ void otd_sha256d_search_vn<2, 5>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
+                                                       uint32_t*, uint32_t);
+template __global__ void otd_sha256d_search_vn<3, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
+                                                       uint32_t*, uint32_t);
+template __global__ void otd_sha256d_search_vn<4, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
+                                                       uint32_t*, uint32_t);
 
 namespace otedama {
 
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
                                    uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block, int chains) {
   if (block != 64 && block != 256) return hipErrorInvalidValue;
-  if (chains == 2) {  // p.groups counts 64-variant groups; the two-chain kernel takes groups of 128
-    if (p.groups == 0 || p.groups % 2 != 0) return hipErrorInvalidValue;
-    Sha256dParamsV p2 = p;
-    p2.groups = p.groups / 2;
-    if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % p2.groups != 0) return hipErrorInvalidValue;
-    if (p.occupancy8)
-      hipLaunchKernelGGL(otd_sha256d_search_v2<5>, dim3(grid), dim3(block), 0, stream, p2, vars, base, count, out, cap);
+  if (chains >= 2 && chains <= 4) {  // p.groups counts 64-variant groups; the kernel takes groups of 64 * chains
+    if (p.groups == 0 || p.groups % uint32_t(chains) != 0) return hipErrorInvalidValue;
+    Sha256dParamsV pn = p;
+    pn.groups = p.groups / uint32_t(chains);
+    if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % pn.groups != 0) return hipErrorInvalidValue;
+    const dim3 g(grid), b(block);
+    if (chains == 2 && p.occupancy8)
+      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 5>), g, b, 0, stream, pn, vars, base, count, out, cap);
+    else if (chains == 2)
+      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
+    else if (chains == 3)
+      hipLaunchKernelGGL((otd_sha256d_search_vn<3, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
     else
-      hipLaunchKernelGGL(otd_sha256d_search_v2<0>, dim3(grid), dim3(block), 0, stream, p2, vars, base, count, out, cap);
+      hipLaunchKernelGGL((otd_sha256d_search_vn<4, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
     return hipGetLastError();
   }
   if (chains != 1) return hipErrorInvalidValue;

@@ -157,11 +157,11 @@ class Sha256dSearchV:
 
     def __init__(self, device="cuda:0", cap: int = 1024, grid: int | None = None, occupancy8: bool = True,
                  block: int = 256, chains: int = 1):
-        """chains=2: two variants per lane on the same nonce (128 per wave); ``occupancy8`` then selects the
-        5-waves/SIMD build of that kernel instead of the 4-wave one."""
+        """chains=2..4: that many variants per lane on the same nonce (64 x chains per wave); with chains=2
+        ``occupancy8`` selects the 5-waves/SIMD build instead of the 4-wave one."""
         self.native = require_native()
-        if chains not in (1, 2):
-            raise ValueError("chains must be 1 or 2")
+        if chains not in (1, 2, 3, 4):
+            raise ValueError("chains must be 1..4")
         self.chains = chains
         self.group = self.native.SHA256D_V_GROUP * chains
         self.occupancy8 = occupancy8

@@ -309,13 +309,14 @@ def _v_headers(n, seed=b"v"):
 
 
 @pytest.mark.parametrize("groups,base,chains,occ", [(1, 0x12345600, 1, True), (2, 0xFFFFFC00, 1, True),
-                                                  (2, 0x12345600, 2, False), (4, 0xFFFFFC00, 2, True)])
+                                                  (2, 0x12345600, 2, False), (4, 0xFFFFFC00, 2, True),
+                                                  (3, 0x12345600, 3, False), (4, 0xFFFFFC00, 4, False)])
 def test_sha256d_v_kernel_matches_cpu(groups, base, chains, occ):
     """Version-parallel kernels (one or two variants per lane): for every variant and every W3 of the window
     (incl. the 2^32 wrap), the reported (nonce = bswap(W3), variant) pairs are exactly the CPU's shares."""
     from otedama_amd.ops.search import Sha256dSearchV
 
-    s = Sha256dSearchV("cuda:0", grid=512, chains=chains, occupancy8=occ)
+    s = Sha256dSearchV("cuda:0", cap=4096, grid=512, chains=chains, occupancy8=occ)  # ~4 hits per variant
     hs = _v_headers(64 * groups)
     target_int = (1 << 248) - 1
     count = 1024
@@ -351,7 +352,7 @@ def test_sha256d_v_kernel_both_builds_and_grid_contract():
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", grid=256, chains=2).prepare(hs[:64], tgt)  # two chains need 128 variants
     with pytest.raises(ValueError):
-        Sha256dSearchV("cuda:0", chains=3)
+        Sha256dSearchV("cuda:0", chains=5)
     with pytest.raises(ValueError):
         Sha256dSearchV("cuda:0", grid=256).prepare(hs[:63], tgt)
 

@@ -52,6 +52,7 @@ def main() -> int:
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--block64-bpc", default="", help="also time 64-thread blocks at these 64-thread blocks per CU")
     ap.add_argument("--chains2-bpc", default="", help="also time the two-variants-per-lane kernel at these blocks per CU")
+    ap.add_argument("--chainsn", default="", help="also time 3/4 variants per lane: 'NC:bpc,bpc;NC:bpc'")
     a = ap.parse_args()
     count = 1 << a.count
     if not a.no_check:
@@ -116,6 +117,24 @@ def main() -> int:
             rate = run(lambda: s.launch(p, 0, count // 2), 128 * (count // 2))
             print(json.dumps({"kernel": "v2_5w" if occ else "v2_4w", "grid": s.grid, "ghs": round(rate / 1e9, 3)}),
                   flush=True)
+    for spec in [x for x in a.chainsn.split(";") if x]:
+        nc, bpcs = spec.split(":")
+        nc = int(nc)
+        hs = headers_for(64 * nc)
+        if not a.no_check:
+            t248 = ((1 << 248) - 1).to_bytes(32, "little")
+            ref = sorted(Sha256dSearchV("cuda:0", cap=4096, grid=768).search(hs, t248, 0x12345600, 1024))  # 3072 waves
+            got = sorted(Sha256dSearchV("cuda:0", cap=4096, chains=nc).search(hs, t248, 0x12345600, 1024))
+            r = {"check": f"sha256d_v{nc}_vs_v", "hits": len(got), "expected": len(ref), "ok": got == ref}
+            print(json.dumps(r), flush=True)
+            if not r["ok"]:
+                return 1
+        for bpc in [int(x) for x in bpcs.split(",") if x]:
+            s = Sha256dSearchV("cuda:0", grid=cus * bpc, chains=nc, occupancy8=False)
+            p = s.prepare(hs, target)
+            n = (1 << 35) // (64 * nc)
+            rate = run(lambda: s.launch(p, 0, n), 64 * nc * n)
+            print(json.dumps({"kernel": f"v{nc}", "grid": s.grid, "ghs": round(rate / 1e9, 3)}), flush=True)
     return 0
 
 
