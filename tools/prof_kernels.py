@@ -38,6 +38,20 @@ if algo == "sha_v":  # K=8 vs version-parallel, equal work: 4 x 2^35 hashes each
     for i in range(4):
         sv.launch(pv, i << 29, 1 << 29)
     torch.cuda.synchronize()
+if algo == "sha_v2":  # one chain (64 variants) vs two chains per lane (128 variants), equal work: 4 x 2^35 hashes
+    from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, Sha256dSearchV, default_grid
+
+    tail = bytes(range(4, 76)) + bytes(4)
+    hs = [(0x20000000 | (v << 13)).to_bytes(4, "little") + tail for v in range(128)]
+    sv = Sha256dSearchV("cuda:0")
+    pv = sv.prepare(hs[:64], tgt)
+    for i in range(4):
+        sv.launch(pv, i << 29, 1 << 29)
+    s2 = Sha256dSearchV("cuda:0", grid=default_grid("cuda:0", SHA256D_V2_BLOCKS_PER_CU), chains=2, occupancy8=False)
+    p2 = s2.prepare(hs, tgt)
+    for i in range(4):
+        s2.launch(p2, i << 28, 1 << 28)
+    torch.cuda.synchronize()
 if algo == "x11":  # the 11-stage chain, 4 batches of 2^23 nonces
     from otedama_amd.ops.search import X11Search
 
