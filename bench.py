@@ -64,7 +64,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", type=int, default=0, help="SHA-256d blocks (0 = CUs x resident blocks)")
     ap.add_argument("--sha-kernel", choices=("v", "k"), default="v",
-                    help="v: 64 version variants per wave, block-2 schedule on the scalar unit (default); "
+                    help="v: 64 x --sha-chains version variants per wave, block-2 schedule on the scalar unit (default); "
                          "k: --sha-variants variants per lane")
     ap.add_argument("--sha-chains", type=int, choices=(1, 2), default=2,
                     help="v kernel: variants per lane (2: 128 variants per wave-group, 4 waves/SIMD; 1: 64, 8 waves)")

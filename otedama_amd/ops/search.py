@@ -8,7 +8,8 @@ read back with :meth:`SearchResult.nonces` after a synchronize.
 Kernels (csrc/kernels):
   * ``otd_sha256d_search``   — SHA-256d nonce search (K1)
   * ``otd_sha256d_search_k`` — K version variants per lane sharing the block-2 schedule
-  * ``otd_sha256d_search_v`` — 64 version variants per wave, block-2 schedule on the scalar unit
+  * ``otd_sha256d_search_v`` / ``_vn<NC>`` — 64 x NC version variants per wave (NC per lane), block-2 schedule on
+    the scalar unit
   * ``otd_scrypt_*``         — scrypt N=1024,r=1,p=1 three-stage search (K5)
   * ``x11k::k_*512_*``       — X11 eleven-stage chain, one kernel per stage (K6)
 """
