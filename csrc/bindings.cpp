@@ -161,6 +161,7 @@ PYBIND11_MODULE(_native, m) {
   m.attr("SCRYPT_COOP") = kScryptCoop;
   m.attr("SCRYPT_LANE_W8") = kScryptLaneW8;
   m.attr("SCRYPT_COOP2") = kScryptCoop2;
+  m.attr("SCRYPT_COOP_SPLIT") = kScryptCoopSplit;
   m.attr("AEAD_AES256GCM") = 0;
   m.attr("AEAD_CHACHA20POLY1305") = 1;
   m.def("scrypt_1024_1_1", [](const py::bytes& h) {
@@ -334,7 +335,8 @@ PYBIND11_MODULE(_native, m) {
                             int gap, uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
     std::string ps = need(params, sizeof(ScryptParams), "params");
     ScryptParams p; std::memcpy(&p, ps.data(), sizeof p);
-    if (gap != 1 && gap != 2 && gap != 4 && gap != kScryptCoop && gap != kScryptLaneW8 && gap != kScryptCoop2)
+    if (gap != 1 && gap != 2 && gap != 4 && gap != kScryptCoop && gap != kScryptLaneW8 && gap != kScryptCoop2 &&
+        gap != kScryptCoopSplit)
       throw std::invalid_argument("gap must be 1, 2, 4, SCRYPT_COOP or SCRYPT_LANE_W8");
     if (grid <= 0 || out == 0 || xbuf == 0 || scratch == 0 || count == 0) throw std::invalid_argument("bad launch args");
     py_launch_scrypt(p, base, count, xbuf, scratch, gap, out, cap, grid, stream);

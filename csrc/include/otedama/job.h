@@ -90,5 +90,6 @@ void x11_prepare(const uint8_t header80[80], const uint8_t target32[32], X11Para
 constexpr int kScryptCoop = 8;
 constexpr int kScryptLaneW8 = 9;   // per-lane ROMix, gap 1, pinned to 8 waves/SIMD
 constexpr int kScryptCoop2 = 11;   // cooperative ROMix, two software-pipelined hashes per lane (gap 1)
+constexpr int kScryptCoopSplit = 12;  // cooperative ROMix, write and lookup phases as two launches (gap 1)
 
 }  // namespace otedama

@@ -320,6 +320,26 @@ __device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffe
   }
 }
 
+// The two ROMix phases as separate launches (see otd_scrypt_romix_coop_phase): PHASE 1 writes the pad, PHASE 2
+// does the 1024 lookups. X crosses the launch boundary through xbuf and the pad stays in HBM.
+template <int LCPOL, int PHASE>
+__device__ __forceinline__ void scrypt_romix_coop_phase(uint32_t X[32], __amdgpu_buffer_rsrc_t rs,
+                                                        uint4* __restrict__ tile, uint32_t lane) {
+  if constexpr (PHASE == 1) {
+    for (uint32_t i = 0; i < 1024; ++i) {
+      coop_store_entry(X, rs, tile, lane, i);
+      blockmix(X);
+    }
+  } else {
+    for (int i = 0; i < 1024; ++i) {
+      coop_v4u R[4];
+      coop_issue<LCPOL>(X, rs, tile, lane, R);
+      coop_consume(X, tile, lane, R);
+      blockmix(X);
+    }
+  }
+}
+
 // Two hashes per lane (A, B), software-pipelined so each stream's BlockMix runs while the other stream's
 // lookup is in flight; the wave only waits when a lookup outlives a whole BlockMix. One tile and one R are
 // shared: at most one lookup is outstanding per wave at any time.
@@ -399,6 +419,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
+// Split-phase cooperative ROMix: the same per-wave pad layout as otd_scrypt_romix_coop, one phase per launch.
+// Every wave of the chip is then in the same phase, so HBM sees pure sequential nt stores (launch 1) and then pure
+// random full-line reads (launch 2) instead of the 1:1 mix that costs ~10% of bandwidth (tools/bench_hbm.hip:
+// stores 5.8, reads 6.2, mixed 5.3-5.5 TB/s). Requires count <= grid * 256: each lane slot owns exactly one
+// hash, whose pad must survive until the second launch.
+template <int LCPOL, int PHASE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop_phase(
+    uint32_t count, uint4* __restrict__ xbuf, uint4* __restrict__ V) {
+  __shared__ uint4 tiles[4 * 256];
+  const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t lane = uint32_t(slot & 63u);
+  const uint64_t wave = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot >> 32))) << 26) |
+                        uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot) >> 6));
+  uint4* Vw = V + wave * (1024ull * 64u * 8u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Vw, (short)0, 1024 * 64 * 128, 0x00020000);
+  uint4* tile = tiles + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256;
+  if (slot < count) {  // count is a multiple of 64: whole waves take this branch together
+    uint32_t X[32];
+    load_entry(xbuf + (slot << 3), X);
+    scrypt_romix_coop_phase<LCPOL, PHASE>(X, rs, tile, lane);
+    store_entry(xbuf + (slot << 3), X);
+  }
+}
+
 // Two-stream cooperative ROMix: wave w owns hashes [128w, 128w+128) (lane l: 128w+l and 128w+64+l) and a
 // 16 MiB pad region (8 MiB per stream). count is a multiple of 128 (launcher rounds up).
 template <int LCPOL>
@@ -466,7 +510,7 @@ namespace otedama {
 // Scratchpad bytes for `grid` ROMix blocks of 256 lane slots at lookup gap `gap`.
 uint64_t scrypt_scratch_bytes(int grid, int gap) {
   if (gap == kScryptCoop2) return uint64_t(grid) * 512ull * 1024ull * 128ull;  // 2 hashes per lane slot
-  if (gap == kScryptCoop || gap == kScryptLaneW8) gap = 1;
+  if (gap == kScryptCoop || gap == kScryptLaneW8 || gap == kScryptCoopSplit) gap = 1;
   return uint64_t(grid) * 256ull * (1024ull / uint64_t(gap)) * 128ull;
 }
 
@@ -480,6 +524,8 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   // The cooperative kernel runs whole waves (shfl + octet loads): round its count up to 64 lanes. xbuf is
   // allocated in multiples of 256 lanes, and lanes past `count` are ignored by pbkdf_out.
   const uint32_t count64 = (count + 63u) & ~63u;
+  // Refuse before anything is enqueued: the split ROMix holds one hash per lane slot across its two launches.
+  if (gap == kScryptCoopSplit && uint64_t(count64) > uint64_t(grid) * 256u) return hipErrorInvalidValue;
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
     case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
@@ -487,6 +533,10 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
       break;
     case kScryptLaneW8:
       hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);
+      break;
+    case kScryptCoopSplit:
+      hipLaunchKernelGGL((otd_scrypt_romix_coop_phase<2, 1>), dim3(grid), dim3(256), 0, stream, count64, X, V);
+      hipLaunchKernelGGL((otd_scrypt_romix_coop_phase<2, 2>), dim3(grid), dim3(256), 0, stream, count64, X, V);
       break;
     case kScryptCoop2:
       hipLaunchKernelGGL(otd_scrypt_romix_coop2<2>, dim3(grid), dim3(256), 0, stream, (count + 127u) & ~127u, X, V);

@@ -219,14 +219,19 @@ class ScryptSearch:
                  lanes_per_slot: int = 1, kernel: str = "coop"):
         """kernel="coop": lane-cooperative full-line ROMix (gap 1 only, the fast path);
         kernel="coop2": the same with two software-pipelined hashes per lane;
+        kernel="split": the cooperative ROMix as two launches (pad writes, then lookups), one hash per lane slot;
         kernel="lane": one lane per hash with lookup gap 1/2/4. Raw native codes
-        (SCRYPT_COOP / SCRYPT_COOP2 / SCRYPT_LANE_W8) may also be passed as ``gap``."""
+        (SCRYPT_COOP / SCRYPT_COOP2 / SCRYPT_COOP_SPLIT / SCRYPT_LANE_W8) may also be passed as ``gap``."""
         self.native = require_native()
-        if kernel not in ("coop", "coop2", "lane"):
-            raise ValueError(f"kernel must be 'coop', 'coop2' or 'lane', got {kernel!r}")
-        if kernel in ("coop", "coop2") and gap == 1:
-            gap = self.native.SCRYPT_COOP if kernel == "coop" else self.native.SCRYPT_COOP2
-        self.kernel = {self.native.SCRYPT_COOP: "coop", self.native.SCRYPT_COOP2: "coop2"}.get(gap, "lane")
+        codes = {"coop": self.native.SCRYPT_COOP, "coop2": self.native.SCRYPT_COOP2,
+                 "split": self.native.SCRYPT_COOP_SPLIT}
+        if kernel not in ("coop", "coop2", "split", "lane"):
+            raise ValueError(f"kernel must be 'coop', 'coop2', 'split' or 'lane', got {kernel!r}")
+        if kernel in codes and gap == 1:
+            gap = codes[kernel]
+        self.kernel = {v: k for k, v in codes.items()}.get(gap, "lane")
+        if self.kernel == "split" and lanes_per_slot != 1:
+            raise ValueError("the split kernel holds one hash per lane slot")
         self.device = torch.device(device)
         self.cap = cap
         self.gap = gap

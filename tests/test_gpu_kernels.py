@@ -95,7 +95,8 @@ def test_sha256d_wraps_nonce_space():
 # native code 9 = per-lane gap 1 pinned to 8 waves/SIMD. n = 200 is not a multiple of 64 (the cooperative
 # kernel rounds its wave count up).
 @pytest.mark.parametrize("gap,n,kernel", [(1, 192, "lane"), (2, 192, "lane"), (4, 192, "lane"), (1, 192, "coop"),
-                                          (1, 200, "coop"), (9, 200, "lane"), (1, 192, "coop2"), (1, 200, "coop2")])
+                                          (1, 200, "coop"), (9, 200, "lane"), (1, 192, "coop2"), (1, 200, "coop2"),
+                                          (1, 192, "split"), (1, 200, "split")])
 def test_scrypt_matches_hashlib(gap, n, kernel):
     from otedama_amd.models.header import int_to_hash
     from otedama_amd.ops.search import ScryptSearch
@@ -129,6 +130,17 @@ def test_scrypt_more_lanes_than_slots(kernel):
         hdr[:76] + struct.pack("<I", n), salt=hdr[:76] + struct.pack("<I", n), n=1024, r=1, p=1, dklen=32),
         "little") <= target_int]
     assert got == ref and 100 < len(ref) < 412
+
+
+def test_scrypt_split_refuses_more_lanes_than_slots():
+    """The split kernel keeps one hash per lane slot across its two launches: a batch larger than the grid's slots
+    is refused rather than silently reusing a pad between the launches."""
+    from otedama_amd.ops.search import ScryptSearch
+
+    with pytest.raises(ValueError):
+        ScryptSearch("cuda:0", grid=1, lanes_per_slot=2, kernel="split")
+    sc = ScryptSearch("cuda:0", grid=1, kernel="split")
+    assert sc.batch == 256
 
 
 def test_gpu_miner_runtime_shares():
