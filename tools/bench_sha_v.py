@@ -53,6 +53,7 @@ def main() -> int:
     ap.add_argument("--block64-bpc", default="", help="also time 64-thread blocks at these 64-thread blocks per CU")
     ap.add_argument("--chains2-bpc", default="", help="also time the two-variants-per-lane kernel at these blocks per CU")
     ap.add_argument("--chainsn", default="", help="also time 3/4 variants per lane: 'NC:bpc,bpc;NC:bpc'")
+    ap.add_argument("--chains2-block64-bpc", default="", help="two chains with one-wave blocks, these blocks per CU")
     a = ap.parse_args()
     count = 1 << a.count
     if not a.no_check:
@@ -117,6 +118,11 @@ def main() -> int:
             rate = run(lambda: s.launch(p, 0, count // 2), 128 * (count // 2))
             print(json.dumps({"kernel": "v2_5w" if occ else "v2_4w", "grid": s.grid, "ghs": round(rate / 1e9, 3)}),
                   flush=True)
+    for bpc in [int(x) for x in a.chains2_block64_bpc.split(",") if x]:
+        s = Sha256dSearchV("cuda:0", grid=cus * bpc, chains=2, occupancy8=False, block=64)
+        p = s.prepare(headers_for(128), target)
+        rate = run(lambda: s.launch(p, 0, count // 2), 128 * (count // 2))
+        print(json.dumps({"kernel": "v2_4w", "block": 64, "grid": s.grid, "ghs": round(rate / 1e9, 3)}), flush=True)
     for spec in [x for x in a.chainsn.split(";") if x]:
         nc, bpcs = spec.split(":")
         nc = int(nc)
