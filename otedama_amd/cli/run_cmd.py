@@ -138,7 +138,7 @@ def _run_node_worker(cfg, info, comm, stdout) -> int:
     gpu = info.device.index if info.device.type == "cuda" else info.local_rank
     devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == gpu]
     local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0, rank=info.rank,
-                     world_size=info.world_size)
+                     world_size=info.world_size, sha_variants=cfg.mining.sha_variants)
     stdout.write(f"[info] node: rank {info.rank}/{info.world_size} mining on GPU {gpu} "
                  f"({len(local)} device(s))\n")
     try:

@@ -70,6 +70,8 @@ class MiningConfig:
     batch_nonces: int = 1 << 29         # per-launch nonce batch (share latency vs launch overhead)
     version_rolling: bool = True        # BIP320 (negotiated with the pool)
     ntime_roll: int = 0
+    sha_variants: int = 128             # SHA-256d header variants per GPU launch: 128 / 64 (version-parallel, two or
+                                        # one per lane), 1..16 (K variants per lane; 1 = single midstate)
 
 
 @dataclass
@@ -152,6 +154,8 @@ class Config:
             issues.append("mining.cpu_threads must be >= 0")
         if not 1 << 16 <= self.mining.batch_nonces <= 1 << 32:
             issues.append("mining.batch_nonces must be in [65536, 2^32]")
+        if self.mining.sha_variants not in (64, 128) and not 1 <= self.mining.sha_variants <= 16:
+            issues.append(f"mining.sha_variants {self.mining.sha_variants} must be 128, 64 or 1..16")
         if self.pool_server.initial_difficulty <= 0:
             issues.append("pool_server.initial_difficulty must be > 0")
         if self.pool_server.target_share_seconds <= 0:

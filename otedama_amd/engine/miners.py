@@ -57,7 +57,7 @@ class DeviceMiner:
 class MinerSet:
     def __init__(self, devices: list, algorithm: str = "sha256d", batch_nonces: int = 1 << 29,
                  cpu_threads: int = 0, rank: int = 0, world_size: int = 1, log=None, queue_cap: int = 4096,
-                 stall_samples: int = 3):
+                 stall_samples: int = 3, sha_variants: int = 128):
         N = require_native()
         self.algorithm = algorithm
         self.log = log or (lambda level, msg: None)
@@ -66,7 +66,8 @@ class MinerSet:
                 and d.capabilities().supports(algorithm)]
         for d in gpus:
             cus = int(d.extra.get("cus", 256))
-            m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6, queue_cap=queue_cap)
+            m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6, queue_cap=queue_cap,
+                           sha_variants=sha_variants)
             self.miners.append(DeviceMiner(d, m))
         cpus = [d for d in devices if d.identity().family == Family.CPU]
         if cpus and algorithm == "sha256d" and (cpu_threads > 0 or not gpus):

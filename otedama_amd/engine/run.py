@@ -230,7 +230,7 @@ class Engine:
             node = self.opts.node_comm
             world = node.info.world_size if node is not None else 1
             self.miners = MinerSet(self.devices, self.algorithm.name, cfg.mining.batch_nonces, cfg.mining.cpu_threads,
-                                   rank=0, world_size=world, log=self.log)
+                                   rank=0, world_size=world, log=self.log, sha_variants=cfg.mining.sha_variants)
             if node is not None and world > 1:
                 from otedama_amd.parallel.node import NodeMinerSet
 

@@ -325,6 +325,9 @@ def test_validate_aggregates_every_issue():
     ({"algorithm": "ethash"}, False), ({"cpu_threads": -1}, False),
     ({"batch_nonces": 1 << 16}, True), ({"batch_nonces": 1 << 32}, True),
     ({"batch_nonces": 1000}, False), ({"batch_nonces": (1 << 32) + 1}, False),
+    ({"sha_variants": 128}, True), ({"sha_variants": 64}, True), ({"sha_variants": 8}, True),
+    ({"sha_variants": 1}, True), ({"sha_variants": 0}, False), ({"sha_variants": 32}, False),
+    ({"sha_variants": 256}, False),
 ])
 def test_validate_mining_section(mining, ok):
     cfg = C.Config(bitcoin_address=ADDR, mining=C.MiningConfig(**mining))
@@ -343,12 +346,12 @@ def test_config_file_round_trip(tmp_path):
     p = tmp_path / "c.yaml"
     p.write_text(f"bitcoin_address: {ADDR}\nlog_level: debug\nlog_format: json\npower_watts: 900\n"
                  "pools:\n  - url: stratum+v2://p.example:3336\n    user: me.rig\n    password: pw\n"
-                 "mining:\n  algorithm: x11\n  batch_nonces: 1048576\n")
+                 "mining:\n  algorithm: x11\n  batch_nonces: 1048576\n  sha_variants: 64\n")
     f, warn = C.load_config_file(str(p))
     assert warn is None
     assert (f.bitcoin_address, f.log_level, f.log_format, f.power_watts) == (ADDR, "debug", "json", 900.0)
     assert f.pools[0].user == "me.rig" and f.pools[0].password == "pw"
-    assert f.mining.algorithm == "x11" and f.mining.batch_nonces == 1 << 20
+    assert f.mining.algorithm == "x11" and f.mining.batch_nonces == 1 << 20 and f.mining.sha_variants == 64
 
 
 def test_missing_config_file_is_ok(tmp_path):
