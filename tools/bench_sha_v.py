@@ -1,7 +1,8 @@
-"""SHA-256d: K-variant kernel (K=8, schedule per lane on the VALU) vs the version-parallel kernel (64 variants per
-wave, schedule on the scalar unit), with a bit-exactness check of the latter against the CPU first.
+"""SHA-256d: K-variant kernel (K=8, schedule per lane on the VALU) vs the version-parallel kernels (64 x NC variants
+per wave, NC per lane, schedule on the scalar unit), with bit-exactness checks against the CPU / the one-chain kernel.
 
-python tools/bench_sha_v.py [--count LOG2] [--groups 1,2] [--bpc 8,16,24]
+python tools/bench_sha_v.py [--count LOG2] [--groups 1,2] [--bpc ...] [--bpc8 ...] [--block64-bpc ...]
+                            [--chains2-bpc ...] [--chains2-block64-bpc ...] [--chainsn "3:bpc,..;4:bpc,.."]
   -> one JSON line per (kernel, grid, groups): GH/s per GPU
 """
 from __future__ import annotations
