@@ -163,34 +163,60 @@ constexpr int kGroestlBlock = 512;
 __device__ __forceinline__ u64 swap64(u64 x) { return mk64(hi32(x), lo32(x)); }
 
 template <bool kQ>
-__device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
+__device__ __forceinline__ void groestl_arc(u64 a[16], u32 r) {  // AddRoundConstant
+  if (!kQ) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] ^= (u64)(((u32)j << 4) ^ r);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = mk64(~lo32(a[j]), hi32(a[j]) ^ ~((((u32)j << 4) ^ r) << 24));
+  }
+}
+
+// Output column j of one round (SubBytes + ShiftBytes + MixBytes). Columns >= kConstFrom of `a` are compile-time
+// constants (round 0 of a one-block message: the padding half), so their lookups come from the constant table and
+// fold away instead of reading LDS.
+template <bool kQ, int kConstFrom>
+__device__ __forceinline__ u64 groestl_col(const u64* T, u32 lo, const u64 a[16], int j) {
   constexpr int SP[8] = {0, 1, 2, 3, 4, 5, 6, 11};
   constexpr int SQ[8] = {1, 3, 5, 11, 0, 2, 4, 6};
+  u64 v[8];
+#pragma unroll
+  for (int row = 0; row < 8; ++row) {
+    const int col = (j + (kQ ? SQ[row] : SP[row])) & 15;
+    const u32 w = row < 4 ? lo32(a[col]) : hi32(a[col]);
+    v[row] = col >= kConstFrom ? x11t::GROESTL_T0[(w >> (8 * (row & 3))) & 0xFF] : groestl_lk(T, lo, w, row & 3);
+  }
+  const u64 L3 = v[3] ^ swap64(v[7]);
+  const u64 L2 = xor3_64(v[2], swap64(v[6]), rotl64(L3, 8));
+  const u64 L1 = xor3_64(v[1], swap64(v[5]), rotl64(L2, 8));
+  return xor3_64(v[0], swap64(v[4]), rotl64(L1, 8));
+}
+
+// kConstFrom: first compile-time-constant column of the input (16: none). kHalfOut: only columns 8..15 of the
+// result are used (the output transform), so the last round computes just those.
+template <bool kQ, int kConstFrom = 16, bool kHalfOut = false>
+__device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
+  u64 t[16];
+  groestl_arc<kQ>(a, 0);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) t[j] = groestl_col<kQ, kConstFrom>(T, lo, a, j);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = t[j];
 #pragma unroll 1
-  for (u32 r = 0; r < 14; ++r) {
-    if (!kQ) {
+  for (u32 r = 1; r < (kHalfOut ? 13u : 14u); ++r) {
+    groestl_arc<kQ>(a, r);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] ^= (u64)(((u32)j << 4) ^ r);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] = mk64(~lo32(a[j]), hi32(a[j]) ^ ~((((u32)j << 4) ^ r) << 24));
-    }
-    u64 t[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      u32 w[8];
-#pragma unroll
-      for (int row = 0; row < 8; ++row) {
-        const u64 src = a[(j + (kQ ? SQ[row] : SP[row])) & 15];
-        w[row] = row < 4 ? lo32(src) : hi32(src);
-      }
-      const u64 L3 = groestl_lk(T, lo, w[3], 3) ^ swap64(groestl_lk(T, lo, w[7], 3));
-      const u64 L2 = xor3_64(groestl_lk(T, lo, w[2], 2), swap64(groestl_lk(T, lo, w[6], 2)), rotl64(L3, 8));
-      const u64 L1 = xor3_64(groestl_lk(T, lo, w[1], 1), swap64(groestl_lk(T, lo, w[5], 1)), rotl64(L2, 8));
-      t[j] = xor3_64(groestl_lk(T, lo, w[0], 0), swap64(groestl_lk(T, lo, w[4], 0)), rotl64(L1, 8));
-    }
+    for (int j = 0; j < 16; ++j) t[j] = groestl_col<kQ, 16>(T, lo, a, j);
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = t[j];
+  }
+  if (kHalfOut) {
+    groestl_arc<kQ>(a, 13);
+#pragma unroll
+    for (int j = 8; j < 16; ++j) t[j] = groestl_col<kQ, 16>(T, lo, a, j);
+#pragma unroll
+    for (int j = 8; j < 16; ++j) a[j] = t[j];
   }
 }
 
@@ -209,14 +235,14 @@ __global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
     for (int k = 0; k < 16; ++k) { p[k] = m[k]; q[k] = m[k]; }
     p[15] ^= iv15;
-    groestl_perm<false>(T, lo, p);
-    groestl_perm<true>(T, lo, q);
+    groestl_perm<false, 8>(T, lo, p);  // columns 8..15 (padding, and h's length word) are constants
+    groestl_perm<true, 8>(T, lo, q);
 #pragma unroll
     for (int k = 0; k < 16; ++k) p[k] ^= q[k];
     p[15] ^= iv15;  // h' = P(h^m) ^ Q(m) ^ h
 #pragma unroll
     for (int k = 0; k < 16; ++k) q[k] = p[k];
-    groestl_perm<false>(T, lo, q);
+    groestl_perm<false, 16, true>(T, lo, q);  // output transform: only columns 8..15 are kept
     u64 out[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) out[k] = q[8 + k] ^ p[8 + k];
