@@ -1,27 +1,39 @@
 #!/usr/bin/env python3
-"""Headline benchmark: whole-node SHA-256d hashes/sec (+ scrypt) on N MI355X.
+"""Headline benchmark: whole-node SHA-256d hashes/sec (+ scrypt, X11) on N MI355X.
 
 BASELINE.json metric: "hashes/sec (whole node) SHA-256d + scrypt at 1/2/4/8
 MI355X; p50 share latency". Reference headline: ~75 MH/s SHA-256d on a whole
 Ryzen 9 7950X (BENCHMARKS.md:46, CPU only).
 
-One rank per GPU (torchrun). One timed step =
-  R1  broadcast of the job blob from rank 0 (torch.distributed / RCCL),
+Ranks: one process per GPU. ``python bench.py --gpus N`` with no torchrun env
+spawns the N ranks itself (otedama_amd/parallel/launch.py: fresh interpreters,
+the parent never touches the GPU) and exits non-zero when fewer than N GPUs
+are visible; under torchrun (WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE.
+
+One timed step on each rank =
+  R1  control broadcast from rank 0 when the variant group changes (the job
+      blob itself went out once, before timing),
   K1  SHA-256d search over this rank's next 128 BIP320 header variants (two per
-      lane of the version-parallel kernel, fixed midstate per variant, variants
+      lane of otd_sha256d_search_vn<2,0>, fixed midstate per variant, variants
       striped across ranks) x 2^28 nonces; 16 consecutive steps tile the full
       2^32 nonce space of each variant (--sha-chains 1: 64 variants x 2^29;
       --sha-kernel k: K variants x 2^32),
-  R2  all_gather of every rank's on-device hit buffer,
-  R3  all_reduce of the hash counters.
+  R2  all_gather of every rank's on-device hit slots, on the comm stream and
+      overlapped with the next step's kernel (double-buffered slots),
+then R3 (all_reduce of the hash counters) once after the last step.
 Data: synthetic 80-byte block headers (random prev-hash / merkle root), share
-target = difficulty 1. Every hit found in the timed region is re-verified on
-the CPU after timing. Weak scaling: per-GPU work is fixed as N grows.
+target = difficulty 1. Every hit of the timed region is de-duplicated by
+(header variant, nonce), re-verified on the CPU, and compared with the Poisson
+expectation (z-score). Weak scaling: per-GPU work is fixed as N grows.
 
-Then scrypt(1024,1,1) is timed the same way (HBM-resident scratchpads), then
-X11 (eleven chained 512-bit hashes, nonce ranges partitioned across ranks), and
-p50 share latency is measured end-to-end (GPU hit -> SV2 SubmitSharesStandard
--> pool validation -> SubmitSharesSuccess) against the in-process local pool.
+Then BASELINE config 2 verbatim (one fixed midstate, full 2^32 nonces, the
+single-header kernel), scrypt(1024,1,1) (HBM-resident scratchpads; hits re-
+verified with hashlib.scrypt), X11 (nonce ranges partitioned across ranks; hits
+re-verified with the C++ chain), and the share-latency probe.
+
+``--cpu-rehearsal`` runs the same rank/launcher/collective code with gloo and
+the native CPU scanner in place of the kernels (tests/test_bench_launcher.py);
+its JSON says so in ``data`` and ``rehearsal``.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -30,11 +42,10 @@ from __future__ import annotations
 import argparse
 import hashlib
 import json
+import math
 import os
 import sys
 import time
-
-import torch
 
 BASELINE_HPS = 75e6  # BENCHMARKS.md:46 (whole 7950X, SHA-256d)
 METRIC = "hashes/sec (whole node) SHA-256d + scrypt at 1/2/4/8 MI355X; p50 share latency"
@@ -57,7 +68,7 @@ def synthetic_job(seed: int = 1) -> dict:
     }
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -70,55 +81,157 @@ def main() -> int:
                     help="v kernel: variants per lane (2: 128 variants per wave-group, 4 waves/SIMD; 1: 64, 8 waves)")
     ap.add_argument("--sha-variants", type=int, default=8,
                     help="k kernel: BIP320 version variants per launch sharing the block-2 schedule (1 = single midstate)")
+    ap.add_argument("--single-midstate-headers", type=int, default=2,
+                    help="BASELINE config 2 pass: headers x full 2^32 nonces each (0 = skip)")
     ap.add_argument("--scrypt-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
     ap.add_argument("--x11-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--no-latency", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="gloo + native CPU scanner instead of the GPU kernels (launcher / collective tests)")
+    ap.add_argument("--cpu-nonces", type=int, default=1 << 12, help="rehearsal: nonces per variant per step")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            return launch(args, sys.argv[1:] if argv is None else list(argv))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} (torchrun "
+              "--nproc-per-node must equal --gpus)", file=sys.stderr)
+        return 2
+    return run_rank(args)
+
+
+def launch(args, argv: list[str]) -> int:
+    """No torchrun env and N > 1: spawn the N ranks here (never exec; this process stays GPU-free)."""
+    from otedama_amd.parallel.launch import run_ranks, visible_gpus
+
+    if not args.cpu_rehearsal and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
+        n = visible_gpus()
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {n}; "
+                  "refusing to report a smaller node as N GPUs", file=sys.stderr)
+            return 2
+    return run_ranks([sys.executable, os.path.abspath(__file__), *argv], args.gpus)
+
+
+# --------------------------------------------------------------------------- search back-ends
+class _CpuSearch:
+    """Rehearsal stand-in for the version-parallel kernel: the native CPU scanner over K variants."""
+
+    def __init__(self, native, k: int, cap: int = 1024):
+        import torch
+
+        self.N, self.k, self.cap, self.grid = native, k, cap, 0
+        self.out = torch.zeros(1 + 2 * cap, dtype=torch.int32)
+
+    def prepare(self, hdrs, target):
+        return (list(hdrs), target)
+
+    def launch(self, prep, base, count, out=None):
+        hdrs, target = prep
+        out = self.out if out is None else out
+        pairs = []
+        for vi, h in enumerate(hdrs):
+            pairs += [(n, vi) for n in self.N.cpu_scan_sha256d(h, target, base & 0xFFFFFFFF, count)]
+        out.zero_()
+        out[0] = len(pairs)
+        for i, (n, vi) in enumerate(pairs[: self.cap]):
+            out[1 + 2 * i] = n - (1 << 32) if n >= 1 << 31 else n
+            out[2 + 2 * i] = vi
+        return out
+
+
+def _sha_name(args, K: int, use_v: bool) -> str:
+    if args.cpu_rehearsal:
+        return "cpu_scan_sha256d (rehearsal)"
+    if use_v:
+        return "otd_sha256d_search_vn<2,0>" if args.sha_chains == 2 else "otd_sha256d_search_v<8>"
+    return f"otd_sha256d_search_k<{K}>" if K > 1 else "otd_sha256d_search"
+
+
+def _poisson(found: int, hashes: int, target_int: int) -> tuple[float, float]:
+    exp = hashes * (target_int + 1) / 2.0 ** 256
+    return exp, ((found - exp) / math.sqrt(exp) if exp > 0 else 0.0)
+
+
+def run_rank(args) -> int:
+    import torch
 
     from otedama_amd.ops import native
-    from otedama_amd.ops.search import ScryptSearch, Sha256dSearch, Sha256dSearchK, Sha256dSearchV
     from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
     from otedama_amd.utils.trace import span
 
-    if not torch.cuda.is_available():
-        print("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU config",
-              file=sys.stderr)
+    cpu = args.cpu_rehearsal
+    if not cpu and not torch.cuda.is_available():
+        print("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU config "
+              "(or --cpu-rehearsal for the launcher/collective rehearsal)", file=sys.stderr)
         return 2
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if not cpu and world_env > 1 and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
+        local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+        if local >= torch.cuda.device_count():
+            print(f"bench.py: rank with LOCAL_RANK={local} has no GPU ({torch.cuda.device_count()} visible)",
+                  file=sys.stderr)
+            return 2
     N = native.require_native()
-    info = init_from_env()
+    info = init_from_env(backend="gloo" if cpu else None, use_gpu=not cpu)
     comm = NodeComm(info)
     dev = info.device
-
-    job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1
-    stripe = stripe_for(info.rank, info.world_size)
     world = info.world_size
-    use_v = args.sha_kernel == "v"
-    if use_v:
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize(dev)
+
+    job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1: the job blob, once
+    if cpu:
+        from otedama_amd.models.header import int_to_hash
+
+        job["target"] = int_to_hash((1 << 244) - 1)  # ~1 hit per 4096 hashes: the rehearsal exercises R2
+    target_int = int.from_bytes(job["target"], "little")
+    stripe = stripe_for(info.rank, info.world_size)
+    use_v = args.sha_kernel == "v" or cpu
+    if cpu:
+        K, V_COUNT = 4, max(1, args.cpu_nonces)
+        steps_per_group = 2
+        search = _CpuSearch(N, K)
+    elif use_v:
         # One step = 64 x chains version variants (chains per lane of a wave) x 2^35 / that many nonces = 2^35
         # hashes, the same work as the K=8 step (8 x 2^32); 8 x chains consecutive steps tile the full 2^32 nonces
         # of one variant group. Two chains run the 4-waves/SIMD build at 128 blocks/CU (profiles/r2/sha_v2).
+        from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, Sha256dSearchV, default_grid
+
         K = N.SHA256D_V_GROUP * args.sha_chains
         V_COUNT = (1 << 35) // K
         steps_per_group = (1 << 32) // V_COUNT
         if args.sha_chains == 2:
-            from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, default_grid
-
             search = Sha256dSearchV(dev, grid=args.grid or default_grid(dev, SHA256D_V2_BLOCKS_PER_CU), chains=2,
                                     occupancy8=False)
         else:
             search = Sha256dSearchV(dev, grid=args.grid or None)
     else:
+        from otedama_amd.ops.search import Sha256dSearch, Sha256dSearchK
+
         V_COUNT, steps_per_group = 1 << 32, 1
         K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
         search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
     slot_words = 1 + (2 if K > 1 else 1) * search.cap
-    gathered = torch.zeros(world, slot_words, dtype=torch.int32, device=dev)
-    counters_hashes = 0
+    # double-buffered hit slots: step i writes outs[i % 2] while R2 of step i-1 reads the other one
+    outs = [torch.zeros(slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
+    gathered = [torch.zeros(world, slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
+    r2_seen = torch.zeros(1, dtype=torch.int64, device=dev)  # hits of every rank that arrived through R2
+    r2_done: list = [None, None]
+    ctl = torch.zeros(4, dtype=torch.int64, device=dev)
 
     def variant_params(step: int) -> tuple[list[bytes], bytes]:
-        # step i of this rank: stripe positions K*i .. K*i + K-1 (version-rolled headers, identical block 2)
         hdrs = [N.variant_header(job, stripe.start + (step * K + j) * stripe.stride)[0] for j in range(K)]
         if K > 1:
             return hdrs, N.sha256d_prepare_k(hdrs, job["target"])
@@ -134,28 +247,43 @@ def main() -> int:
         return v_groups[q]
 
     hits_log: list[tuple[list[bytes], torch.Tensor]] = []
+    last_group = [-1]
 
     def step(i: int, record: bool) -> None:
         with span("otd.bench.sha256d_step"):
             _step(i, record)
 
     def _step(i: int, record: bool) -> None:
-        nonlocal counters_hashes
-        if world > 1:  # R1: job blob fan-out (kept on device; decoded only on job change)
-            comm._run(lambda: torch.distributed.broadcast(comm._job, src=0))
-        if use_v:  # K1: 64 variants x one eighth of the nonce space (W3 window)
-            hdr, prep = v_group(i // steps_per_group)
-            r = search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT)
+        b = i % 2
+        q = i // steps_per_group
+        if world > 1 and q != last_group[0]:  # R1 on change: rank 0 announces the next variant group
+            if info.is_primary:
+                ctl.fill_(q)
+            comm.run_async(lambda: torch.distributed.broadcast(ctl, src=0))
+            last_group[0] = q
+        if r2_done[b] is not None:  # the gather that read this slot two steps ago must be done before reuse
+            torch.cuda.current_stream(dev).wait_event(r2_done[b])
+        out = outs[b]
+        if use_v:  # K1: 128 variants x 1/16 of the nonce space (W3 window)
+            hdr, prep = v_group(q)
+            if cpu:
+                search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT, out)
+            else:
+                search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT, out=out)
         else:
             hdr, params = variant_params(i)
-            r = search.launch(params, 0, 1 << 32)  # K1: full 2^32 nonce space
-        if world > 1:  # R2: on-device hit buffers, gathered on the comm stream
-            comm._run(lambda: torch.distributed.all_gather_into_tensor(gathered.view(-1), r.buf.view(-1)))
-        else:
-            gathered[0].copy_(r.buf)
-        counters_hashes += K * (V_COUNT if use_v else 1 << 32)
+            search.launch(params, 0, 1 << 32, out=out)  # K1: full 2^32 nonce space
         if record:
-            hits_log.append((hdr, gathered[info.rank].clone()))
+            hits_log.append((hdr, out.clone()))
+
+        def r2(o=out, g=gathered[b]):
+            if world > 1:
+                torch.distributed.all_gather_into_tensor(g.view(-1), o)
+            else:
+                g[0].copy_(o)
+            r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
+
+        r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
 
     # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
     # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
@@ -168,22 +296,29 @@ def main() -> int:
             v_group(i // steps_per_group)
     for i in range(args.warmup):
         step(args.steps + i, False)
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(info)
-    torch.cuda.synchronize(dev)
+    sync()
+    r2_seen.zero_()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, True)
     step_hashes = K * (V_COUNT if use_v else 1 << 32)
     total = comm.allreduce_counters(args.steps * step_hashes)[0] if world > 1 else args.steps * step_hashes  # R3
-    torch.cuda.synchronize(dev)
+    sync()
     barrier(info)
-    torch.cuda.synchronize(dev)
-    elapsed = comm.allreduce_max(time.perf_counter() - t0)
+    sync()
+    t_local = time.perf_counter() - t0
+    elapsed = comm.allreduce_max(t_local)
     sha_hps = total / elapsed
+    # per-rank rates + which ranks actually took part in the collectives (RCCL world check)
+    rows = comm.gather_counters([info.rank, args.steps * step_hashes, int(t_local * 1e6), int(r2_seen.item())])
+    ranks_seen = sorted(int(r[0]) for r in rows)
+    per_rank_hps = [r[1] / max(r[2] * 1e-6, 1e-9) for r in sorted(rows)]
 
-    # Re-verify every hit of the timed region on the CPU (full 256-bit compare).
-    found = verified = 0
+    # Re-verify every hit of the timed region on the CPU (full 256-bit compare), de-duplicated by (variant, nonce).
+    found = verified = dups = 0
+    seen: set = set()
     for hdrs, buf in hits_log:
         host = buf.cpu().tolist()
         n = min(host[0] & 0xFFFFFFFF, search.cap)
@@ -194,37 +329,100 @@ def main() -> int:
             if not 0 <= vi < K:
                 continue
             hdr = hdrs[vi]
+            key = (hdr[:76], nonce)
+            if key in seen:
+                dups += 1
+                continue
+            seen.add(key)
             h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
-            if int.from_bytes(h, "little") <= int.from_bytes(job["target"], "little"):
+            if int.from_bytes(h, "little") <= target_int:
                 verified += 1
-    found, verified, _, _ = comm.allreduce_counters(found, verified)
+    found, verified, dups, _ = comm.allreduce_counters(found, verified, dups)
+    expected, z = _poisson(verified, total, target_int)
+    r2_hits = rows[0][3] if rows else 0  # rank 0's R2 view of every rank's hit counts
+
+    # ------------------------------------------- BASELINE config 2 verbatim: one fixed midstate, full 2^32
+    single = {}
+    if args.single_midstate_headers > 0 and not cpu:
+        from otedama_amd.ops.search import Sha256dSearch
+
+        ss = Sha256dSearch(dev)
+        heads = [N.variant_header(job, stripe.start + (positions + j) * stripe.stride)[0]
+                 for j in range(args.single_midstate_headers)]
+        params = [N.sha256d_prepare(h, job["target"]) for h in heads]
+        ss.launch(params[0], 0, 1 << 24)  # warm the kernel
+        sync()
+        barrier(info)
+        sync()
+        souts = []
+        t0 = time.perf_counter()
+        for p in params:
+            souts.append(ss.launch(p, 0, 1 << 32, out=torch.zeros_like(ss.out)).buf)
+        sync()
+        barrier(info)
+        sync()
+        s_el = comm.allreduce_max(time.perf_counter() - t0)
+        s_total = len(params) * (1 << 32) * world
+        s_found = s_ok = 0
+        for h, buf in zip(heads, souts):
+            host = buf.cpu().tolist()
+            for nonce in host[1 : 1 + min(host[0] & 0xFFFFFFFF, ss.cap)]:
+                nonce &= 0xFFFFFFFF
+                s_found += 1
+                d = hashlib.sha256(hashlib.sha256(h[:76] + nonce.to_bytes(4, "little")).digest()).digest()
+                s_ok += int.from_bytes(d, "little") <= target_int
+        s_found, s_ok, _, _ = comm.allreduce_counters(s_found, s_ok)
+        single = {"hashes_per_sec": s_total / s_el, "kernel": "otd_sha256d_search", "headers_per_rank": len(params),
+                  "nonces_per_header": 1 << 32, "grid": ss.grid, "hits_found": s_found, "hits_verified": s_ok,
+                  "hits_expected": _poisson(s_ok, s_total, target_int)[0]}
+        del ss
 
     # ---------------------------------------------------------------- scrypt
     scrypt_hps = None
     ssteps = args.steps if args.scrypt_steps < 0 else args.scrypt_steps
     scrypt_info = {}
-    if ssteps > 0:
+    if ssteps > 0 and not cpu:
         from otedama_amd.models.algorithms import ALGORITHMS
         from otedama_amd.models.header import int_to_hash
+        from otedama_amd.ops.search import ScryptSearch
 
         sc = ScryptSearch(dev, gap=args.scrypt_gap, kernel=args.scrypt_kernel)
-        starget = int_to_hash(ALGORITHMS["scrypt"].diff1)
+        s_int = ALGORITHMS["scrypt"].diff1
+        starget = int_to_hash(s_int)
         hdr, _, _, _ = N.variant_header(job, stripe.start)
         sparams = N.scrypt_prepare(hdr, starget)
         sc.launch(sparams, 0)
-        torch.cuda.synchronize(dev)
+        sync()
         barrier(info)
-        torch.cuda.synchronize(dev)
+        sync()
+        sbufs = []
         t0 = time.perf_counter()
         for i in range(ssteps):
-            sc.launch(sparams, (i * sc.batch) & 0xFFFFFFFF)
-        torch.cuda.synchronize(dev)
+            base = ((i * world + info.rank) * sc.batch) & 0xFFFFFFFF  # ranks partition the nonce range
+            sbufs.append(sc.launch(sparams, base).buf.clone())
+        sync()
         barrier(info)
-        torch.cuda.synchronize(dev)
+        sync()
         selapsed = comm.allreduce_max(time.perf_counter() - t0)
         stotal = comm.allreduce_counters(ssteps * sc.batch)[0] if world > 1 else ssteps * sc.batch
         scrypt_hps = stotal / selapsed
-        scrypt_info = {"kernel": sc.kernel, "lookup_gap": 1 if sc.kernel == "coop" else sc.gap, "lanes": sc.batch, "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2)}
+        # re-verify up to 64 hits per rank with hashlib.scrypt (CPU, ~1 ms each)
+        sfound = sver = schecked = 0
+        for buf in sbufs:
+            host = buf.cpu().tolist()
+            for nonce in host[1 : 1 + min(host[0] & 0xFFFFFFFF, sc.cap)]:
+                sfound += 1
+                if schecked >= 64:
+                    continue
+                schecked += 1
+                h80 = hdr[:76] + (nonce & 0xFFFFFFFF).to_bytes(4, "little")
+                d = hashlib.scrypt(h80, salt=h80, n=1024, r=1, p=1, dklen=32)
+                sver += int.from_bytes(d, "little") <= s_int
+        sfound, sver, schecked, _ = comm.allreduce_counters(sfound, sver, schecked)
+        scrypt_info = {"kernel": sc.kernel, "lookup_gap": 1 if sc.kernel == "coop" else sc.gap, "lanes": sc.batch,
+                       "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2), "hits_found": sfound,
+                       "hits_checked": schecked, "hits_verified": sver,
+                       "hits_expected": _poisson(sfound, stotal, s_int)[0], "hit_target": "scrypt diff 1 (0xFFFF<<224)"}
         del sc
         torch.cuda.empty_cache()
 
@@ -234,7 +432,7 @@ def main() -> int:
     x11_hps = None
     x11_info = {}
     xsteps = args.steps if args.x11_steps < 0 else args.x11_steps
-    if xsteps > 0:
+    if xsteps > 0 and not cpu:
         from otedama_amd.models.header import int_to_hash
         from otedama_amd.ops.search import X11Search
 
@@ -243,18 +441,18 @@ def main() -> int:
         hdr, _, _, _ = N.variant_header(job, stripe.start)
         xparams = N.x11_prepare(hdr, int_to_hash(xtarget_int))
         xs.launch(xparams, 0)
-        torch.cuda.synchronize(dev)
+        sync()
         barrier(info)
-        torch.cuda.synchronize(dev)
-        xhits: list[list[int]] = []
+        sync()
+        xhits: list = []
         t0 = time.perf_counter()
         for i in range(xsteps):
             base = ((i * world + info.rank) * xs.batch) & 0xFFFFFFFF
             r = xs.launch(xparams, base)
             xhits.append(r.buf.clone())
-        torch.cuda.synchronize(dev)
+        sync()
         barrier(info)
-        torch.cuda.synchronize(dev)
+        sync()
         xelapsed = comm.allreduce_max(time.perf_counter() - t0)
         xtotal = comm.allreduce_counters(xsteps * xs.batch)[0] if world > 1 else xsteps * xs.batch
         x11_hps = xtotal / xelapsed
@@ -267,13 +465,14 @@ def main() -> int:
                 xver += int.from_bytes(h, "little") <= xtarget_int
         xfound, xver, _, _ = comm.allreduce_counters(xfound, xver)
         x11_info = {"batch_per_launch": xs.batch, "kernels": "11 stage kernels per batch (tools/bench_x11.py)",
-                    "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20"}
+                    "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20",
+                    "hits_expected": _poisson(xfound, xtotal, xtarget_int)[0]}
         del xs
         torch.cuda.empty_cache()
 
     # ---------------------------------------------------------- share latency
     latency = None
-    if not args.no_latency and info.is_primary:
+    if not args.no_latency and info.is_primary and not cpu:
         try:
             from otedama_amd.engine.latency_probe import measure_share_latency
 
@@ -294,7 +493,9 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": sha_hps / BASELINE_HPS,
             "dtype": "u32",
-            "data": "synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1",
+            "data": ("synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1"
+                     if not cpu else "CPU REHEARSAL (gloo + native CPU scanner, share target 2^-12): not a GPU "
+                                     "measurement"),
             "config": {
                 "model": "sha256d",
                 "global_batch": step_hashes * world,
@@ -304,18 +505,29 @@ def main() -> int:
                                    "steps tile 2^32 per variant)" if use_v
                                    else "full 2^32 nonces per variant per step)")),
                 "algorithm": ("SHA-256d nonce search, fixed midstate per variant; " + (
-                    f"{K} BIP320 version variants per wave ({K // 64} per lane) share the block-2 message schedule, "
-                    "computed on the scalar unit" if use_v else
+                    f"{K} BIP320 version variants per wave ({max(K // 64, 1)} per lane) share the block-2 message "
+                    "schedule, computed on the scalar unit" if use_v else
                     f"{K} BIP320 version variants per launch share the block-2 message schedule")),
-                "sha_kernel": (("otd_sha256d_search_v2<0>" if K == 128 else "otd_sha256d_search_v<8>") if use_v
-                               else (f"otd_sha256d_search_k<{K}>" if K > 1 else "otd_sha256d_search")),
+                "sha_kernel": _sha_name(args, K, use_v),
                 "variants_per_step": K,
                 "grid": search.grid,
             },
+            "world_size": world,
+            "dist_backend": info.backend,
+            "rccl_ranks_seen": ranks_seen,
+            "per_rank_hashes_per_sec": per_rank_hps,
+            "rehearsal": "cpu-gloo" if cpu else (
+                "gloo-shared-gpu" if os.environ.get("OTEDAMA_DIST_BACKEND") == "gloo" and world > 1 else None),
             "sha256d_hashes_per_sec": sha_hps,
             "sha256d_per_gpu_hashes_per_sec": sha_hps / world,
+            "sha256d_single_midstate_hashes_per_sec": single.get("hashes_per_sec"),
+            "sha256d_single_midstate": single,
             "hits_found": found,
             "hits_verified": verified,
+            "hits_duplicate": dups,
+            "hits_expected": expected,
+            "hits_z": z,
+            "hits_r2_gathered": r2_hits,
             "scrypt_hashes_per_sec": scrypt_hps,
             "scrypt": scrypt_info,
             "x11_hashes_per_sec": x11_hps,
@@ -323,7 +535,7 @@ def main() -> int:
             "p50_share_latency_ms": (latency or {}).get("p50_ms") if isinstance(latency, dict) else None,
             "share_latency": latency,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     shutdown(info)
     return 0
 

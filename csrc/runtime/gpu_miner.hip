@@ -292,6 +292,9 @@ void GpuMiner::loop() {
         v_table_k = k;
         v_table_n = s.nvar;
       }
+      // The table is cached per (work, group) but a target-only update (SV2 SetTarget, V1 set_difficulty) keeps
+      // the work generation: the share filter must follow the job's current target on every launch.
+      v_params.target_hi = load_le32(job->target + 28);
       const size_t table_bytes = size_t(s.nvar) * sizeof(Sha256dVariant);
       std::memcpy(s.h_vars, v_table, table_bytes);
       OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, table_bytes, hipMemcpyHostToDevice, stream));

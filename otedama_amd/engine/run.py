@@ -54,6 +54,7 @@ from otedama_amd.models.algorithms import get as get_algorithm
 from otedama_amd.poolproto import Credentials, FatalPoolError, Job, ShareSubmission
 from otedama_amd.poolproto.base import extranonce2_bytes, from_url, lookup
 from otedama_amd.provider import AkashProvider, MiningProvider
+from otedama_amd.utils.bounded import BoundedSet
 from otedama_amd.utils.clock import SYSTEM, Clock
 from otedama_amd.utils.trace import mark as trace_mark
 
@@ -62,6 +63,7 @@ RECONNECT_BACKOFF_MAX = 64.0
 STREAM_STALE_TIMEOUT = 180.0
 DEFAULT_HYSTERESIS = 0.05
 SHARE_POLL_INTERVAL = 0.005
+SUBMIT_KEYS_CAP = 1024  # unacked-submit map bound (internal/engine/run.go:726)
 
 
 @dataclass
@@ -147,7 +149,7 @@ class Engine:
         self.activity: dict[str, float] = {}
         self._active_job: Job | None = None
         self._valid_jobs: set[str] = set()
-        self._submitted: set = set()
+        self._submitted = BoundedSet(SUBMIT_KEYS_CAP)  # run.go:720-726: cap 1024, oldest half dropped
         self._session = None
         self._providers: list = []
         self._rate_fetcher = opts.rate_fetcher

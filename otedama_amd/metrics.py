@@ -115,6 +115,25 @@ class Counter:
         return str(self._v)
 
 
+class FloatCounter(Counter):
+    """Counter of a real-valued quantity (e.g. accepted share difficulty, which is fractional below 1)."""
+
+    __slots__ = ()
+
+    def __init__(self, name: str, help: str, labels: dict[str, str] | None):
+        super().__init__(name, help, labels)
+        self._v = 0.0
+
+    def add(self, delta: float) -> None:
+        if not delta >= 0:
+            raise MetricsError("counter delta must be non-negative")
+        with self._lock:
+            self._v += float(delta)
+
+    def text(self) -> str:
+        return format_float(self._v)
+
+
 class Gauge:
     __slots__ = ("name", "help", "labels", "key", "prefix", "_v", "_lock", "_fv", "_ft")
 
@@ -158,7 +177,9 @@ class Registry:
             if not _LABEL_RE.match(k):
                 raise MetricsError(f"invalid label name {k!r} on metric {name!r} (must match [a-zA-Z_][a-zA-Z0-9_]*)")
 
-    def new_counter(self, name: str, help: str, labels: dict[str, str] | None = None) -> Counter:
+    def new_counter(self, name: str, help: str, labels: dict[str, str] | None = None,
+                    float_value: bool = False) -> Counter:
+        """``float_value``: a FloatCounter (real-valued increments) instead of the reference's uint64 counter."""
         self._validate(name, labels)
         key = _metric_key(name, labels)
         with self._lock:
@@ -166,7 +187,7 @@ class Registry:
                 return self._counters[key]
             if any(g.name == name for g in self._gauges.values()):
                 raise MetricsError(f"name {name!r} already registered as a gauge; cannot also be a counter")
-            c = Counter(name, help, labels)
+            c = (FloatCounter if float_value else Counter)(name, help, labels)
             self._counters[key] = c
             return c
 

@@ -13,7 +13,9 @@ goroutines (internal/miner/worker.go:51-60,279) and a channel fan-in of shares
 
 Payloads are bytes to a few KiB, so the budget is latency, not xGMI bandwidth:
 collectives run on a dedicated comm stream so they overlap the search kernels
-running on the miners' own HIP streams.
+running on the miners' own HIP streams. ``run_async`` is the overlapped form
+(nothing on the compute stream waits for the collective; bench.py double-buffers
+the hit slots it gathers), ``_run`` the blocking one for results read at once.
 """
 from __future__ import annotations
 
@@ -179,15 +181,32 @@ class NodeComm:
         return float(t.item())
 
     def _run(self, fn) -> None:
+        """Blocking form: the collective runs on the comm stream and the current stream waits for it (used where
+        the caller reads the result right away)."""
         if self.stream is None:
             fn()
             return
-        # Comm stream: ordered after the producer (current stream), overlaps the miners' HIP streams.
         cur = torch.cuda.current_stream(self.info.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             fn()
         cur.wait_stream(self.stream)
+
+    def run_async(self, fn):
+        """Overlapped form: the collective is ordered after the work already queued on the current stream (its
+        producer) but nothing on the current stream waits for it. Returns an event recorded on the comm stream
+        (``None`` on CPU, where gloo collectives complete inline); a consumer, or the producer that reuses the
+        collective's buffers, waits on that event only when it needs to."""
+        if self.stream is None:
+            fn()
+            return None
+        cur = torch.cuda.current_stream(self.info.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            fn()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
 
 
 def _encode(obj):

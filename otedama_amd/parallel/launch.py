@@ -1,0 +1,103 @@
+"""One process per GPU without torchrun: spawn N rank processes of a command.
+
+torchrun's agent tears the whole job down when one worker dies, and the driver
+runs ``bench.py --gpus N`` directly; both need a launcher of our own. The
+parent never touches the GPU (counting devices with ``torch.cuda.device_count``
+does not initialise HIP on this image), never ``exec``s, and hands every child
+the torch.distributed env contract (RANK / LOCAL_RANK / WORLD_SIZE /
+LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT). Children run as fresh
+interpreters (``subprocess``), so each one initialises only its own device.
+
+Reference analogue: the per-device worker start-up of
+internal/engine/setup.go:59-77 (goroutines there, processes here: a GPU fault
+that aborts one process cannot take the other GPUs with it).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Sequence
+
+MASTER_ADDR = "127.0.0.1"  # the container hostname may not resolve
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind((MASTER_ADDR, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus() -> int:
+    """HIP devices visible to a child (honours HIP/ROCR/CUDA_VISIBLE_DEVICES) without initialising HIP here."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001 - no torch / no driver: no GPUs
+        return 0
+
+
+def rank_env(rank: int, world: int, port: int, base: dict | None = None, **extra: str) -> dict:
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR=MASTER_ADDR, MASTER_PORT=str(port))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL peer buffers)
+    env.update({k: str(v) for k, v in extra.items()})
+    return env
+
+
+def _stop_all(procs: list[subprocess.Popen], grace: float = 10.0) -> None:
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
+def run_ranks(cmd: Sequence[str], world: int, port: int | None = None, env: dict | None = None,
+              stdout_rank0_only: bool = True, poll: float = 0.1, **extra: str) -> int:
+    """Run ``cmd`` as ``world`` ranks and wait. The first rank to fail stops the others; returns its exit code
+    (0 when every rank succeeded). Only rank 0's stdout is kept when ``stdout_rank0_only`` (one JSON line)."""
+    port = port or free_port()
+    procs: list[subprocess.Popen] = []
+    prev = {}
+
+    def forward(sig, _frame):  # the driver's timeout / Ctrl-C reaches every rank
+        _stop_all(procs, grace=5.0)
+        sys.exit(128 + sig)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            prev[sig] = signal.signal(sig, forward)
+        except ValueError:  # not the main thread
+            pass
+    try:
+        for r in range(world):
+            out = None if (r == 0 or not stdout_rank0_only) else subprocess.DEVNULL
+            procs.append(subprocess.Popen(list(cmd), env=rank_env(r, world, port, env, **extra), stdout=out))
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"launch: rank {r} exited with code {c}; stopping the other ranks", file=sys.stderr)
+                _stop_all(procs)
+                return c if c > 0 else 128 - c
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(poll)
+    finally:
+        _stop_all(procs, grace=5.0)
+        for sig, h in prev.items():
+            signal.signal(sig, h)

@@ -45,6 +45,7 @@ EN1_SIZE = 4
 EN2_SIZE = 4
 MAX_NTIME_FUTURE = 7200
 RETARGET_GRACE = 10.0
+MAX_SHARES_PER_JOB = 1 << 20  # credited headers kept per live job before the job is retired
 
 
 @dataclass
@@ -136,7 +137,9 @@ class PoolServer:
         self.block: BlockTemplate | None = None
         self.jobs: "OrderedDict[str, PoolJob]" = OrderedDict()
         self._job_counter = 0
-        self._seen: set = set()
+        # Headers already credited, per live job: bounded by the 16 retained jobs x MAX_SHARES_PER_JOB and dropped
+        # with the job, instead of one set that only a new block clears.
+        self._seen: dict[str, set] = {}
         self._en_counter = int.from_bytes(os.urandom(2), "little") << 16
         self._v1: set[_V1Conn] = set()
         self._v2: set[_V2Conn] = set()
@@ -173,7 +176,7 @@ class PoolServer:
         self.m_hashrate = r.new_gauge("otedama_pool_hashrate_hashes_per_second",
                                       "Pool hashrate estimated from accepted share work.", lab)
         self.m_work = r.new_counter("otedama_pool_accepted_work_total",
-                                    "Sum of accepted share difficulties.", lab)
+                                    "Sum of accepted share difficulties.", lab, float_value=True)
         self._work_t0 = time.monotonic()
         self._work_sum = 0.0
 
@@ -249,8 +252,10 @@ class PoolServer:
         job = PoolJob(self._job_counter, self.block, self.block.version, max(int(time.time()), self.block.ntime),
                       coinb1, coinb2, self.block.branches(), clean)
         self.jobs[job.job_id] = job
+        self._seen[job.job_id] = set()
         while len(self.jobs) > 16:
-            self.jobs.popitem(last=False)
+            old, _ = self.jobs.popitem(last=False)
+            self._seen.pop(old, None)
         for c in list(self._v1):
             c.send_job(job)
         for c in list(self._v2):
@@ -316,7 +321,7 @@ class PoolServer:
         # coinbase parts and merkle branches, so one (extranonce, ntime, nonce, version) submitted under several
         # live job ids is the same work and is credited once.
         hdr = self.header_for(job, extranonce, version, ntime, nonce)
-        if hdr in self._seen:
+        if self._credited(hdr):
             return self._reject(worker, job_id, "duplicate-share")
         return job, hdr, hdr
 
@@ -324,8 +329,11 @@ class PoolServer:
         # re-checked after the (possibly off-loop) hash: a new block or an identical concurrent submit
         if job.block is not self.block:
             return self._reject(worker, job_id, "stale-job")
-        if key in self._seen:
+        if self._credited(key):
             return self._reject(worker, job_id, "duplicate-share")
+        seen = self._seen.get(job_id)
+        if seen is None or self.jobs.get(job_id) is not job:  # job retired while the share was being hashed
+            return self._reject(worker, job_id, "stale-job")
         hv = hash_to_int(h)
         diff = worker.vd.difficulty
         if hv > hash_to_int(self.share_target(diff)):
@@ -334,12 +342,16 @@ class PoolServer:
                 diff = worker.prev_difficulty
             else:
                 return self._reject(worker, job_id, "low-difficulty-share", h)
-        self._seen.add(key)
+        seen.add(key)
+        if len(seen) >= MAX_SHARES_PER_JOB:  # cap reached: retire the job (later shares for it are stale)
+            self.jobs.pop(job_id, None)
+            self._seen.pop(job_id, None)
+            self.new_job()
         is_block = hv <= hash_to_int(target_from_nbits(job.block.nbits))
         worker.accepted += 1
         self.accepted += 1
         self.m_accepted.inc()
-        self.m_work.add(int(diff)) if diff >= 1 else None
+        self.m_work.add(diff)  # real difficulty, fractional below 1
         self._work_sum += diff
         self.journal.append(ShareRow(time.time(), worker.name, self.algo.name, job_id, diff, True, "", h[::-1].hex(),
                                      is_block))
@@ -352,6 +364,10 @@ class PoolServer:
                              f"payouts={json.dumps(pay)}")
             asyncio.get_event_loop().call_soon(self.new_block)
         return Verdict(True, "", diff, h, is_block)
+
+    def _credited(self, hdr: bytes) -> bool:
+        """Duplicates are keyed on the full header across every live job of the block (see _precheck)."""
+        return any(hdr in s for s in self._seen.values())
 
     def _reject(self, worker: _Worker, job_id: str, reason: str, h: bytes = b"") -> Verdict:
         worker.rejected += 1

@@ -1,0 +1,73 @@
+"""bench.py as the driver runs it: ``python bench.py --gpus N`` with no torchrun env spawns N ranks itself.
+
+The CPU rehearsal (``--cpu-rehearsal``: gloo + the native CPU scanner in place of the kernels) drives the same
+launcher, rank bootstrap, R1/R2/R3 collectives, hit de-duplication and JSON contract as the MI355X run, at the
+world sizes the 8-GPU node uses. On a host with fewer GPUs than ``--gpus`` the GPU run must refuse instead of
+silently reporting a smaller node.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _bench(*args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=e,
+                          cwd=ROOT)
+
+
+def _json(res) -> dict:
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (res.stdout, res.stderr[-3000:])
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_launcher_runs_n_ranks(n):
+    res = _bench("--gpus", str(n), "--steps", "3", "--warmup", "1", "--cpu-rehearsal")
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == n and d["world_size"] == n
+    assert d["rccl_ranks_seen"] == list(range(n))
+    assert d["dist_backend"] == "gloo" and d["rehearsal"] == "cpu-gloo"
+    assert len(d["per_rank_hashes_per_sec"]) == n and all(r > 0 for r in d["per_rank_hashes_per_sec"])
+    # whole-job value = total hashes / max rank time; each rank scans its own stripe
+    assert d["value"] == pytest.approx(d["config"]["global_batch"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3))
+    # every hit found is unique and verifies; R2 delivered every rank's hits to rank 0
+    assert d["hits_duplicate"] == 0
+    assert d["hits_verified"] == d["hits_found"] > 0
+    assert d["hits_r2_gathered"] == d["hits_found"]
+    assert abs(d["hits_z"]) < 6
+
+
+def test_single_rank_rehearsal_keeps_the_json_contract():
+    res = _bench("--steps", "2", "--warmup", "1", "--cpu-rehearsal")
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert KEYS <= set(d) and d["n_gpus"] == 1 and d["rccl_ranks_seen"] == [0]
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert "REHEARSAL" in d["data"]
+
+
+def test_refuses_more_gpus_than_visible():
+    res = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", env={"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+    assert res.returncode != 0
+    assert "visible GPUs" in res.stderr
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_torchrun_world_size_must_match_gpus():
+    res = _bench("--gpus", "2", "--cpu-rehearsal", env={"WORLD_SIZE": "3", "RANK": "0"})
+    assert res.returncode == 2 and "WORLD_SIZE=3" in res.stderr
