@@ -273,8 +273,9 @@ def run_rank(args) -> int:
         else:
             hdr, params = variant_params(i)
             search.launch(params, 0, 1 << 32, out=out)  # K1: full 2^32 nonce space
-        if record:
-            hits_log.append((hdr, out.clone()))
+        if record:  # with the nonce window the step covered (W3 = bswap(nonce) for the v kernel)
+            lo = (i % steps_per_group) * V_COUNT if use_v else 0
+            hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
 
         def r2(o=out, g=gathered[b]):
             if world > 1:
@@ -317,15 +318,17 @@ def run_rank(args) -> int:
     per_rank_hps = [r[1] / max(r[2] * 1e-6, 1e-9) for r in sorted(rows)]
 
     # Re-verify every hit of the timed region on the CPU (full 256-bit compare), de-duplicated by (variant, nonce).
-    found = verified = dups = 0
+    found = verified = dups = outside = 0
     seen: set = set()
-    for hdrs, buf in hits_log:
+    for hdrs, buf, lo, cnt in hits_log:
         host = buf.cpu().tolist()
         n = min(host[0] & 0xFFFFFFFF, search.cap)
         pairs = [(host[1 + 2 * i], host[2 + 2 * i]) for i in range(n)] if K > 1 else [(x, 0) for x in host[1 : 1 + n]]
         for nonce, vi in pairs:
             nonce &= 0xFFFFFFFF
             found += 1
+            w = nonce if cpu or not use_v else int.from_bytes(nonce.to_bytes(4, "little"), "big")
+            outside += not lo <= w < lo + cnt  # a hit outside the window the step was asked to search
             if not 0 <= vi < K:
                 continue
             hdr = hdrs[vi]
@@ -337,7 +340,7 @@ def run_rank(args) -> int:
             h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
             if int.from_bytes(h, "little") <= target_int:
                 verified += 1
-    found, verified, dups, _ = comm.allreduce_counters(found, verified, dups)
+    found, verified, dups, outside = comm.allreduce_counters(found, verified, dups, outside)
     expected, z = _poisson(verified, total, target_int)
     r2_hits = rows[0][3] if rows else 0  # rank 0's R2 view of every rank's hit counts
 
@@ -525,6 +528,7 @@ def run_rank(args) -> int:
             "hits_found": found,
             "hits_verified": verified,
             "hits_duplicate": dups,
+            "hits_outside_window": outside,
             "hits_expected": expected,
             "hits_z": z,
             "hits_r2_gathered": r2_hits,

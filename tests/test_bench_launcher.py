@@ -46,7 +46,7 @@ def test_launcher_runs_n_ranks(n):
     # whole-job value = total hashes / max rank time; each rank scans its own stripe
     assert d["value"] == pytest.approx(d["config"]["global_batch"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3))
     # every hit found is unique and verifies; R2 delivered every rank's hits to rank 0
-    assert d["hits_duplicate"] == 0
+    assert d["hits_duplicate"] == 0 and d["hits_outside_window"] == 0
     assert d["hits_verified"] == d["hits_found"] > 0
     assert d["hits_r2_gathered"] == d["hits_found"]
     assert abs(d["hits_z"]) < 6
