@@ -29,7 +29,9 @@ expectation (z-score). Weak scaling: per-GPU work is fixed as N grows.
 Then BASELINE config 2 verbatim (one fixed midstate, full 2^32 nonces, the
 single-header kernel), scrypt(1024,1,1) (HBM-resident scratchpads; hits re-
 verified with hashlib.scrypt), X11 (nonce ranges partitioned across ranks; hits
-re-verified with the C++ chain), and the share-latency probe.
+re-verified with the C++ chain), the share-latency probe (engine on this GPU,
+pool in a separate process; device hit -> accept from the kernel's own clock)
+and the job-switch probe (set_job -> new work running, SHA-256d and scrypt).
 
 ``--cpu-rehearsal`` runs the same rank/launcher/collective code with gloo and
 the native CPU scanner in place of the kernels (tests/test_bench_launcher.py);
@@ -474,14 +476,22 @@ def run_rank(args) -> int:
         torch.cuda.empty_cache()
 
     # ---------------------------------------------------------- share latency
+    # End-to-end share latency against the local pool in a separate process (default 2^29-nonce batches), then the
+    # job-switch time of the native miner for SHA-256d and scrypt (set_job -> first batch of the new work running).
     latency = None
+    switch: dict = {}
     if not args.no_latency and info.is_primary and not cpu:
-        try:
-            from otedama_amd.engine.latency_probe import measure_share_latency
+        from otedama_amd.engine.latency_probe import measure_job_switch, measure_share_latency
 
+        try:
             latency = measure_share_latency(device_index=dev.index or 0, seconds=6.0)
         except Exception as exc:  # noqa: BLE001 - latency is auxiliary; never fail the headline
             latency = {"error": f"{type(exc).__name__}: {exc}"}
+        for algo in ("sha256d", "scrypt"):
+            try:
+                switch[algo] = measure_job_switch(device_index=dev.index or 0, algorithm=algo)
+            except Exception as exc:  # noqa: BLE001
+                switch[algo] = {"error": f"{type(exc).__name__}: {exc}"}
 
     if info.is_primary:
         out = {
@@ -537,7 +547,11 @@ def run_rank(args) -> int:
             "x11_hashes_per_sec": x11_hps,
             "x11": x11_info,
             "p50_share_latency_ms": (latency or {}).get("p50_ms") if isinstance(latency, dict) else None,
+            "device_hit_to_accept_p50_ms": (latency or {}).get("device_hit_to_accept_p50_ms"),
+            "device_hit_to_accept_p95_ms": (latency or {}).get("device_hit_to_accept_p95_ms"),
             "share_latency": latency,
+            "job_switch_ms": {a: v.get("p50_ms") for a, v in switch.items()} or None,
+            "job_switch": switch or None,
         }
         print(json.dumps(out), flush=True)
     shutdown(info)

@@ -105,6 +105,7 @@ py::list shares_to_list(std::vector<ShareRecord>&& v) {
     d["hash"] = to_bytes(s.hash, 32);
     d["device_id"] = s.device_id;
     d["found_at"] = s.found_at;
+    d["device_found_at"] = s.device_found_at;
     out.append(d);
   }
   return out;
@@ -122,6 +123,14 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["busy_seconds"] = s.busy_seconds;
   d["faulted"] = s.faulted;
   d["error"] = s.error;
+  d["variant_next"] = s.variant_next;
+  d["variant_gen"] = s.variant_gen;
+  d["job_switches"] = s.job_switches;
+  d["last_job_switch_ms"] = s.last_job_switch_ms;
+  d["job_switch_ms"] = s.job_switch_ms;
+  d["aborted_launches"] = s.aborted_launches;
+  d["ring_hits"] = s.ring_hits;
+  d["clock_calib_rtt_us"] = s.clock_calib_rtt_us;
   return d;
 }
 
@@ -376,6 +385,8 @@ PYBIND11_MODULE(_native, m) {
         return shares_to_list(std::move(v));
       }, py::arg("max") = 256)
       .def("stats", [](MinerBase& self) { return stats_to_dict(self.stats()); })
+      .def("share_fd", &MinerBase::share_fd,
+           "eventfd that becomes readable when shares are queued (read 8 bytes to reset, then poll())")
       .def_property_readonly("device_id", &MinerBase::device_id);
 
   py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")

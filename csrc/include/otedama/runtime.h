@@ -62,7 +62,9 @@ struct ShareRecord {
   uint32_t extranonce2_size;
   uint8_t hash[32];
   std::string device_id;
-  double found_at = 0;  // CLOCK_MONOTONIC seconds when the host verified the share
+  double found_at = 0;         // CLOCK_MONOTONIC seconds when the host verified the share
+  double device_found_at = 0;  // CLOCK_MONOTONIC seconds of the kernel's hit (s_memrealtime mapped to host time;
+                               // 0 when the device did not stamp it, e.g. the CPU miner)
 };
 
 struct MinerStats {
@@ -76,6 +78,17 @@ struct MinerStats {
   double busy_seconds = 0;           // device (or thread) time spent hashing
   bool faulted = false;              // the device thread died on a HIP error
   std::string error;
+  // Search-space cursor: first variant index of this device's stripe not yet started, for the work generation
+  // `variant_gen` (a re-split after a device / rank loss starts past every cursor so nothing is searched twice).
+  uint64_t variant_next = 0;
+  uint64_t variant_gen = 0;
+  // Job switches (GPU): set_job() of new work -> the first batch of that work running on the device, in ms.
+  uint64_t job_switches = 0;
+  double last_job_switch_ms = 0;
+  std::vector<double> job_switch_ms;  // most recent samples (<= 64)
+  uint64_t aborted_launches = 0;      // batches stopped early by the device abort word
+  uint64_t ring_hits = 0;             // hits consumed from the host-coherent ring while their launch was running
+  double clock_calib_rtt_us = 0;      // round trip of the device-clock calibration that is in use
 };
 
 // Full-target re-verification of a candidate (host SHA-256d / scrypt).
@@ -83,14 +96,21 @@ bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32
 void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]);
 void merkle_root_from_coinbase(const JobTemplate& job, uint64_t extranonce2, uint8_t root_out[32]);
 
+// Bounded share queue with an eventfd that becomes readable on every push, so a consumer (the asyncio engine
+// through loop.add_reader, a device process's forwarder through poll) wakes on the share instead of polling.
 class ShareQueue {
  public:
-  explicit ShareQueue(size_t cap) : cap_(cap) {}
+  explicit ShareQueue(size_t cap);
+  ~ShareQueue();
+  ShareQueue(const ShareQueue&) = delete;
+  ShareQueue& operator=(const ShareQueue&) = delete;
   bool push(ShareRecord&& s);  // false (and counted) when full
   std::vector<ShareRecord> drain(size_t max);
   size_t size();
   uint64_t dropped() const { return dropped_.load(); }
+  int event_fd() const { return efd_; }
  private:
+  int efd_ = -1;
   std::mutex mu_;
   std::deque<ShareRecord> q_;
   size_t cap_;
@@ -108,9 +128,12 @@ class MinerBase {
   std::vector<ShareRecord> poll(size_t max) { return queue_.drain(max); }
   MinerStats stats();
   const std::string& device_id() const { return device_id_; }
+  int share_fd() const { return queue_.event_fd(); }
 
  protected:
   std::shared_ptr<const JobTemplate> current_job(uint64_t* gen);
+  // Non-blocking: the current job, its work generation and when that generation was set (monotonic seconds).
+  std::shared_ptr<const JobTemplate> peek_job(uint64_t* gen, double* set_at);
   std::string device_id_;
   ShareQueue queue_;
   std::mutex job_mu_;
@@ -118,12 +141,15 @@ class MinerBase {
   std::shared_ptr<const JobTemplate> job_;
   std::shared_ptr<const JobTemplate> last_work_;  // last non-null job (work identity)
   uint64_t job_gen_ = 0;                          // bumps only when the search space changes
+  double job_set_at_ = 0;                         // monotonic time of the last set_job that changed the work
   std::atomic<bool> running_{false};
   std::mutex stats_mu_;
   MinerStats stats_;
 };
 
-// One host thread per GPU: double-buffered batches on a private HIP stream.
+// One host thread per GPU: two batches in flight on a private HIP stream. Hits reach the host while a launch
+// runs (host-coherent ring, otedama/hitsink.h); new work or a pause moves the device abort word so the
+// obsolete batches stop within one grid-stride trip.
 class GpuMiner : public MinerBase {
  public:
   // sha_variants: SHA-256d header variants per launch that share block 2 (version rolling): 128 (default) = the
@@ -147,6 +173,7 @@ class GpuMiner : public MinerBase {
   int grid_k_ = 0;
   int grid_v_ = 0;
   int grid_v2_ = 0;
+  double rt_offset_ = 0;  // host monotonic seconds at device realtime 0 (s_memrealtime, 100 MHz)
   std::thread th_;
 };
 

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 
+#include "otedama/hitsink.h"
 #include "otedama/job.h"
 
 namespace otedama {
@@ -11,10 +12,11 @@ namespace otedama {
 
 // Stage i on the GPU over nonces base .. base + n - 1. H holds the 64-byte
 // intermediate digests as 8 planes of u64 (word w of nonce k at H[w * stride + k]).
-// Stage 0 reads the header from `p`; stage 10 with out != null compares with the
-// target and appends nonces (out[0] = count, out[1..cap]) instead of writing H.
+// Stage 0 reads the header from `p`; stage 10 with sink != null compares with the
+// target and publishes nonces to *sink (otedama/hitsink.h) instead of writing H. Every
+// stage honours the sink's abort word.
 hipError_t x11_launch_stage(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                            uint32_t* out, uint32_t cap, hipStream_t s);
+                            const HitSink* sink, hipStream_t s);
 hipError_t x11_launch_chain(const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                            uint32_t* out, uint32_t cap, hipStream_t s);
+                            const HitSink* sink, hipStream_t s);
 }  // namespace otedama

@@ -1,0 +1,46 @@
+// Device side of otedama::HitSink (csrc/include/otedama/hitsink.h): hit publication and the abort poll.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "otedama/hitsink.h"
+
+namespace otedama_dev {
+
+// Abort word as of now (system-scope relaxed load: the word is uncached device memory written by the host's
+// control stream). Wave-uniform by construction (one address), made provably so for a scalar branch. Without
+// an abort word the batch's own epoch comes back, which never reads as newer.
+__device__ __forceinline__ uint32_t abort_peek(const uint32_t* word, uint32_t epoch) {
+  if (word == nullptr) return epoch;
+  const uint32_t v = __hip_atomic_load(const_cast<uint32_t*>(word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint32_t abort_peek(const otedama::HitSink& s) { return abort_peek(s.abort, s.epoch); }
+
+// True once the host has moved the abort word past this batch's epoch (serial-number compare: wrap-safe).
+__device__ __forceinline__ bool abort_newer(uint32_t word, uint32_t epoch) {
+  return static_cast<int32_t>(word - epoch) > 0;
+}
+
+// One candidate. Miner path: the record is written, fenced at system scope, then tagged, so a host thread
+// polling the tag never reads a half-written record. Ops path: the legacy device-memory slots.
+__device__ __forceinline__ void hit_publish(const otedama::HitSink& s, uint32_t nonce, uint32_t variant) {
+  const uint32_t slot = atomicAdd(s.out, 1u);
+  if (slot >= s.cap) return;
+  if (s.ring != nullptr) {
+    otedama::HitRecord* r = s.ring + slot;
+    r->nonce = nonce;
+    r->variant = variant;
+    r->stamp = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+    __threadfence_system();
+    __hip_atomic_store(&r->tag, s.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else if (s.words == 2) {
+    s.out[1 + 2 * slot] = nonce;
+    s.out[2 + 2 * slot] = variant;
+  } else {
+    s.out[1 + slot] = nonce;
+  }
+}
+
+}  // namespace otedama_dev

@@ -19,6 +19,7 @@
 #include <cstdint>
 
 #include "cdna_bitops.h"
+#include "hitsink_dev.h"
 #include "otedama/job.h"
 
 namespace {
@@ -305,19 +306,26 @@ __device__ __forceinline__ void coop_consume(uint32_t X[32], uint4* __restrict__
   }
 }
 
+// The abort word (otedama/hitsink.h) is polled before each ROMix phase (a wave's hash takes ~32 ms, its phases
+// ~16 ms each): an obsolete batch stops within half a hash instead of finishing two launches. Polling inside the
+// BlockMix loops made the allocator reload spilled values every iteration (64-VGPR budget). Returns false when
+// aborted.
 template <int LCPOL>
-__device__ __forceinline__ void scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
-                                                  uint32_t lane) {
+__device__ __forceinline__ bool scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
+                                                  uint32_t lane, const otedama::HitSink& sink) {
+  if (abort_newer(abort_peek(sink), sink.epoch)) return false;
   for (uint32_t i = 0; i < 1024; ++i) {
     coop_store_entry(X, rs, tile, lane, i);
     blockmix(X);
   }
+  if (abort_newer(abort_peek(sink), sink.epoch)) return false;
   for (int i = 0; i < 1024; ++i) {
     coop_v4u R[4];
     coop_issue<LCPOL>(X, rs, tile, lane, R);
     coop_consume(X, tile, lane, R);
     blockmix(X);
   }
+  return true;
 }
 
 // The two ROMix phases as separate launches (see otd_scrypt_romix_coop_phase): PHASE 1 writes the pad, PHASE 2
@@ -396,7 +404,7 @@ __global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* _
 
 template <int LCPOL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop(uint32_t count, uint4* __restrict__ xbuf,
-                                                             uint4* __restrict__ V) {
+                                                             uint4* __restrict__ V, const otedama::HitSink sink) {
   __shared__ uint4 tiles[4 * 256];  // 4 waves x 4 KiB half-tiles
   const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (uint64_t i = slot; i < count; i += nslots) {
     uint32_t X[32];
     load_entry(xbuf + (i << 3), X);
-    scrypt_romix_coop<LCPOL>(X, rs, tile, lane);
+    if (!scrypt_romix_coop<LCPOL>(X, rs, tile, lane, sink)) return;  // aborted: pbkdf_out publishes nothing
     store_entry(xbuf + (i << 3), X);
   }
 }
@@ -486,19 +494,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
-// out[0]: candidate count; out[1..cap]: nonces.
+// Hits (nonce) to `sink` (ops API: out[0] = candidate count, out[1..cap] = nonces). A batch whose abort word moved
+// on publishes nothing: its ROMix stopped part way and xbuf holds unfinished states.
 extern "C" __global__ __launch_bounds__(256) void otd_scrypt_pbkdf_out(const otedama::ScryptParams p, uint32_t base,
                                                                        uint32_t count, const uint4* __restrict__ xbuf,
-                                                                       uint32_t* __restrict__ out, uint32_t cap) {
+                                                                       const otedama::HitSink sink) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
+  if (abort_newer(abort_peek(sink), sink.epoch)) return;
   uint32_t X[32];
   load_entry(xbuf + (uint64_t(i) << 3), X);
   const uint32_t h7 = scrypt_pbkdf_out(p, base + i, X);
-  if (bswap(h7) <= p.target_hi) {
-    const uint32_t s = atomicAdd(out, 1u);
-    if (s < cap) out[1 + s] = base + i;
-  }
+  if (bswap(h7) <= p.target_hi) hit_publish(sink, base + i, 0u);
 }
 
 template __global__ void otd_scrypt_romix<1>(uint32_t, uint4*, uint4*);
@@ -517,7 +524,7 @@ uint64_t scrypt_scratch_bytes(int grid, int gap) {
 // xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
 // gap: 1/2/4 = per-lane ROMix with that lookup gap; kScryptCoop = lane-cooperative ROMix (gap 1).
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
-                                int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream) {
+                                int gap, const HitSink& sink, int grid, hipStream_t stream) {
   uint4* X = static_cast<uint4*>(xbuf);
   uint4* V = static_cast<uint4*>(scratch);
   const int eg = int((count + 255) / 256);
@@ -529,7 +536,7 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
     case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
-      hipLaunchKernelGGL(otd_scrypt_romix_coop<2>, dim3(grid), dim3(256), 0, stream, count64, X, V);
+      hipLaunchKernelGGL(otd_scrypt_romix_coop<2>, dim3(grid), dim3(256), 0, stream, count64, X, V, sink);
       break;
     case kScryptLaneW8:
       hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);
@@ -546,7 +553,7 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
     case 4: hipLaunchKernelGGL(otd_scrypt_romix<4>, dim3(grid), dim3(256), 0, stream, count, X, V); break;
     default: return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(otd_scrypt_pbkdf_out, dim3(eg), dim3(256), 0, stream, p, base, count, X, out, cap);
+  hipLaunchKernelGGL(otd_scrypt_pbkdf_out, dim3(eg), dim3(256), 0, stream, p, base, count, X, sink);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@
 #include <cstdint>
 
 #include "cdna_bitops.h"
+#include "hitsink_dev.h"
 #include "otedama/job.h"
 
 namespace {
@@ -80,22 +81,26 @@ __device__ __forceinline__ uint32_t sha256d_h7(const otedama::Sha256dParams& p, 
 
 }  // namespace
 
-// out[0]: candidate count (may exceed cap); out[1..cap]: nonces (header byte order).
+// Hits go to `sink` (otedama/hitsink.h; ops API: out[0] = count, out[1..cap] = nonces in header byte order).
 // Nonces are header-order values (bytes 76..79 little-endian); the kernel feeds
 // W3 = bswap(nonce) (one v_perm per nonce) so base/count index the nonce itself.
+// A trip here is one hash per lane (~1 us per wave), so the abort word is polled every kAbortTrips trips.
+constexpr uint32_t kAbortTrips = 32;
 extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search(
-    const otedama::Sha256dParams p, uint32_t base, uint64_t count, uint32_t* __restrict__ out,
-    uint32_t cap) {
+    const otedama::Sha256dParams p, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
+  uint32_t ab = abort_peek(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
+    if (++trip == kAbortTrips) {
+      if (abort_newer(ab, sink.epoch)) break;
+      ab = abort_peek(sink);
+      trip = 0;
+    }
     const uint32_t nonce = base + static_cast<uint32_t>(off);
     const uint32_t w3 = __builtin_bswap32(nonce);
     const uint32_t h7 = sha256d_h7(p, w3);
-    if (__builtin_bswap32(h7) <= p.target_hi) {
-      const uint32_t slot = atomicAdd(out, 1u);
-      if (slot < cap) out[1 + slot] = nonce;
-    }
+    if (__builtin_bswap32(h7) <= p.target_hi) hit_publish(sink, nonce, 0u);
   }
 }
 
@@ -186,14 +191,22 @@ __device__ __forceinline__ void sha256d_h7_k(KParamsK& p, uint32_t w3, uint32_t 
 
 }  // namespace
 
-// out[0]: count; out[1 + 2*i] = nonce, out[2 + 2*i] = variant index (0..K-1).
+// Hits: (nonce, variant index 0..K-1) to `sink` (ops API: out[0] = count, out[1 + 2*i] = nonce, out[2 + 2*i] =
+// variant). One trip is K hashes per lane: the abort word is polled every kAbortTrips / K trips.
 template <int K>
 __global__ __launch_bounds__(256) void otd_sha256d_search_k(const otedama::Sha256dParamsK p, uint32_t base,
-                                                            uint64_t count, uint32_t* __restrict__ out, uint32_t cap) {
+                                                            uint64_t count, const otedama::HitSink sink) {
   (void)p;  // read through the kernarg segment pointer below (p is the first kernel argument, offset 0)
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
+  constexpr uint32_t kTrips = kAbortTrips / K > 0 ? kAbortTrips / K : 1;
+  uint32_t ab = abort_peek(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
+    if (++trip == kTrips) {
+      if (abort_newer(ab, sink.epoch)) break;
+      ab = abort_peek(sink);
+      trip = 0;
+    }
     const uint32_t nonce = base + static_cast<uint32_t>(off);
     // Opaque per trip: the compiler cannot hoist the (scalar) parameter loads out of the loop.
     KParamsK* pp = (KParamsK*)(__builtin_amdgcn_kernarg_segment_ptr());
@@ -202,18 +215,12 @@ __global__ __launch_bounds__(256) void otd_sha256d_search_k(const otedama::Sha25
     sha256d_h7_k<K>(*pp, __builtin_bswap32(nonce), h7);
 #pragma unroll
     for (int v = 0; v < K; ++v) {
-      if (__builtin_bswap32(h7[v]) <= p.target_hi) {
-        const uint32_t slot = atomicAdd(out, 1u);
-        if (slot < cap) {
-          out[1 + 2 * slot] = nonce;
-          out[2 + 2 * slot] = (uint32_t)v;
-        }
-      }
+      if (__builtin_bswap32(h7[v]) <= p.target_hi) hit_publish(sink, nonce, uint32_t(v));
     }
   }
 }
 #define OTD_SHA_K_INSTANCE(K) \
-  template __global__ void otd_sha256d_search_k<K>(const otedama::Sha256dParamsK, uint32_t, uint64_t, uint32_t*, uint32_t);
+  template __global__ void otd_sha256d_search_k<K>(const otedama::Sha256dParamsK, uint32_t, uint64_t, const otedama::HitSink);
 OTD_SHA_K_INSTANCE(2)
 OTD_SHA_K_INSTANCE(3)
 OTD_SHA_K_INSTANCE(4)
@@ -225,17 +232,17 @@ OTD_SHA_K_INSTANCE(16)
 
 namespace otedama {
 
-hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, uint32_t* out,
-                                 uint32_t cap, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(otd_sha256d_search, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap);
+hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, const HitSink& sink, int grid,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(otd_sha256d_search, dim3(grid), dim3(256), 0, stream, p, base, count, sink);
   return hipGetLastError();
 }
 
-hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
-                                   int grid, hipStream_t stream) {
+hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, const HitSink& sink, int grid,
+                                   hipStream_t stream) {
   switch (p.k) {
 #define OTD_SHA_K_CASE(K) \
-  case K: hipLaunchKernelGGL(otd_sha256d_search_k<K>, dim3(grid), dim3(256), 0, stream, p, base, count, out, cap); break;
+  case K: hipLaunchKernelGGL(otd_sha256d_search_k<K>, dim3(grid), dim3(256), 0, stream, p, base, count, sink); break;
     OTD_SHA_K_CASE(2) OTD_SHA_K_CASE(3) OTD_SHA_K_CASE(4) OTD_SHA_K_CASE(6) OTD_SHA_K_CASE(8) OTD_SHA_K_CASE(12)
     OTD_SHA_K_CASE(16)
 #undef OTD_SHA_K_CASE

@@ -19,6 +19,7 @@
 #include <cstdint>
 
 #include "cdna_bitops.h"
+#include "hitsink_dev.h"
 #include "otedama/job.h"
 
 namespace {
@@ -50,7 +51,8 @@ using VarPtr = const otedama::Sha256dVariant* __restrict__;
 
 }  // namespace
 
-// out[0]: candidate count (may exceed cap); out[1 + 2i] = nonce (header byte order), out[2 + 2i] = variant index.
+// Hits (nonce in header byte order, variant index) go to `sink` (otedama/hitsink.h): the host-coherent ring of the
+// native miner, or out[0] = count, out[1 + 2i] = nonce, out[2 + 2i] = variant for the ops API.
 // Grid contract (checked on the host): the wave count gridDim.x * blockDim.x / 64 is a multiple of p.groups, so every
 // variant group gets the same number of waves and each wave's nonce stride is uniform.
 // MINW = 0: default build, 63 VGPRs / 106 SGPRs -> 7 waves/SIMD (SGPR-limited);
@@ -59,8 +61,7 @@ using VarPtr = const otedama::Sha256dVariant* __restrict__;
 // compiler forms fewer v_add3 with the SGPR K+W word (2117 instead of 2084 VALU per hash).
 template <int MINW>
 __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v(
-    const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, uint32_t* __restrict__ out,
-    uint32_t cap) {
+    const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t wpb = blockDim.x >> 6;  // waves per block (256 or 64 threads)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t waves = gridDim.x * wpb;
@@ -78,7 +79,12 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
   }
   const uint32_t pre3 = v.pre3, t2_3 = v.t2_3;
 
+  // Abort poll, one per grid-stride iteration: the load for the next check is issued at the top of each trip and
+  // only waited on at the next trip's top, so its latency hides under a whole iteration of hashing.
+  uint32_t ab = abort_peek(sink);
   for (uint64_t off = first; off < count; off += stride) {
+    if (abort_newer(ab, sink.epoch)) break;
+    ab = abort_peek(sink);
     const uint32_t w3 = base + static_cast<uint32_t>(off);  // wave-uniform
     // ---- hash 1, block 2: rounds 3..63 (schedule on the scalar unit) ----
     uint32_t W[64];
@@ -120,20 +126,14 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
       h = gg; gg = f; f = e; e = ne; d = c; c = b; b = a; a = na;
     }
     const uint32_t h7 = e + kIVv[7];
-    if (__builtin_bswap32(h7) <= p.target_hi) {
-      const uint32_t slot = atomicAdd(out, 1u);
-      if (slot < cap) {
-        out[1 + 2 * slot] = __builtin_bswap32(w3);
-        out[2 + 2 * slot] = vi;
-      }
-    }
+    if (__builtin_bswap32(h7) <= p.target_hi) hit_publish(sink, __builtin_bswap32(w3), vi);
   }
 }
 
 template __global__ void otd_sha256d_search_v<0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                   uint32_t*, uint32_t);
+                                                   const otedama::HitSink);
 template __global__ void otd_sha256d_search_v<8>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                   uint32_t*, uint32_t);
+                                                   const otedama::HitSink);
 
 
 // NC variants per lane (lane l of group g: variants 64*NC*g + 64c + l, c < NC), same nonce: all chains use the one
@@ -142,8 +142,7 @@ template __global__ void otd_sha256d_search_v<8>(const otedama::Sha256dParamsV, 
 // NC = 4: 203 VGPRs, 2 waves. p.groups counts groups of 64*NC variants.
 template <int NC, int MINW>
 __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_vn(
-    const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, uint32_t* __restrict__ out,
-    uint32_t cap) {
+    const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t waves = gridDim.x * wpb;
@@ -162,7 +161,10 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
     for (int i = 0; i < 8; ++i) { mid[c][i] = v.mid[i]; st3[c][i] = v.st3[i]; }
     pre3[c] = v.pre3; t2_3[c] = v.t2_3;
   }
+  uint32_t ab = abort_peek(sink);  // as in otd_sha256d_search_v: one poll per trip, latency hidden by the trip
   for (uint64_t off = first; off < count; off += stride) {
+    if (abort_newer(ab, sink.epoch)) break;
+    ab = abort_peek(sink);
     const uint32_t w3 = base + static_cast<uint32_t>(off);
     uint32_t W[64];
     W[0] = p.w0; W[1] = p.w1; W[2] = p.w2; W[3] = w3;
@@ -217,30 +219,24 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const uint32_t h7 = e[c] + kIVv[7];
-      if (__builtin_bswap32(h7) <= p.target_hi) {
-        const uint32_t slot = atomicAdd(out, 1u);
-        if (slot < cap) {
-          out[1 + 2 * slot] = __builtin_bswap32(w3);
-          out[2 + 2 * slot] = vi[c];
-        }
-      }
+      if (__builtin_bswap32(h7) <= p.target_hi) hit_publish(sink, __builtin_bswap32(w3), vi[c]);
     }
   }
 }
 
 template __global__ void otd_sha256d_search_vn<2, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                       uint32_t*, uint32_t);
+                                                       const otedama::HitSink);
 template __global__ void otd_sha256d_search_vn<2, 5>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                       uint32_t*, uint32_t);
+                                                       const otedama::HitSink);
 template __global__ void otd_sha256d_search_vn<3, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                       uint32_t*, uint32_t);
+                                                       const otedama::HitSink);
 template __global__ void otd_sha256d_search_vn<4, 0>(const otedama::Sha256dParamsV, VarPtr, uint32_t, uint64_t,
-                                                       uint32_t*, uint32_t);
+                                                       const otedama::HitSink);
 
 namespace otedama {
 
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
-                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block, int chains) {
+                                   const HitSink& sink, int grid, hipStream_t stream, int block, int chains) {
   if (block != 64 && block != 256) return hipErrorInvalidValue;
   if (chains >= 2 && chains <= 4) {  // p.groups counts 64-variant groups; the kernel takes groups of 64 * chains
     if (p.groups == 0 || p.groups % uint32_t(chains) != 0) return hipErrorInvalidValue;
@@ -249,21 +245,21 @@ hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant
     if (grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % pn.groups != 0) return hipErrorInvalidValue;
     const dim3 g(grid), b(block);
     if (chains == 2 && p.occupancy8)
-      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 5>), g, b, 0, stream, pn, vars, base, count, out, cap);
+      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 5>), g, b, 0, stream, pn, vars, base, count, sink);
     else if (chains == 2)
-      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
+      hipLaunchKernelGGL((otd_sha256d_search_vn<2, 0>), g, b, 0, stream, pn, vars, base, count, sink);
     else if (chains == 3)
-      hipLaunchKernelGGL((otd_sha256d_search_vn<3, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
+      hipLaunchKernelGGL((otd_sha256d_search_vn<3, 0>), g, b, 0, stream, pn, vars, base, count, sink);
     else
-      hipLaunchKernelGGL((otd_sha256d_search_vn<4, 0>), g, b, 0, stream, pn, vars, base, count, out, cap);
+      hipLaunchKernelGGL((otd_sha256d_search_vn<4, 0>), g, b, 0, stream, pn, vars, base, count, sink);
     return hipGetLastError();
   }
   if (chains != 1) return hipErrorInvalidValue;
   if (p.groups == 0 || grid <= 0 || (uint64_t(grid) * uint32_t(block / 64)) % p.groups != 0) return hipErrorInvalidValue;
   if (p.occupancy8)
-    hipLaunchKernelGGL(otd_sha256d_search_v<8>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, out, cap);
+    hipLaunchKernelGGL(otd_sha256d_search_v<8>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, sink);
   else
-    hipLaunchKernelGGL(otd_sha256d_search_v<0>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, out, cap);
+    hipLaunchKernelGGL(otd_sha256d_search_v<0>, dim3(grid), dim3(block), 0, stream, p, vars, base, count, sink);
   return hipGetLastError();
 }
 

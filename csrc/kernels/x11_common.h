@@ -14,6 +14,7 @@
 
 #include "otedama/job.h"
 #include "cdna_bitops.h"
+#include "hitsink_dev.h"
 #include "x11_tables.h"
 
 namespace otedama {
@@ -156,9 +157,19 @@ enum X11Stage : int {
 // Stage 0 writes H from the header + nonces; stages 1..10 transform H in place.
 // Stage 10 with `out` != null compares against the target and appends nonces
 // instead of writing H (search mode).
+// Abort word of the batch (otedama/hitsink.h): every stage kernel stops early once the host moved it past `epoch`
+// (whole-launch kernels check once per wave, grid-stride kernels once per trip); word == nullptr: never.
+struct X11Abort {
+  const uint32_t* word = nullptr;
+  uint32_t epoch = 0;
+};
+__device__ __forceinline__ bool x11_stop(const X11Abort& a) {
+  return otedama_dev::abort_newer(otedama_dev::abort_peek(a.word, a.epoch), a.epoch);
+}
 hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                              hipStream_t s);
+                              X11Abort ab, hipStream_t s);
+// sink == nullptr: ECHO writes the digests (trace mode); else it compares and publishes hits to *sink.
 hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                              uint32_t* out, uint32_t cap, hipStream_t s);
+                              const HitSink* sink, hipStream_t s);
 
 }  // namespace otedama

@@ -33,11 +33,12 @@ __device__ __forceinline__ void shavite_F(const u32* T, u32 lo, u32 x[4], const 
   aes_round(T, lo, x[0], x[1], x[2], x[3]);
 }
 
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
+    if (x11_stop(ab)) return;  // after the table fill: no block barrier follows
   u64 h[8];
   load_hash(Hb, stride, i, h);
   // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
@@ -221,7 +222,7 @@ constexpr int kSimdBlock = 256;
 constexpr u32 kSimdLds = 624;
 
 // Eight lanes per hash: launch with 8 * n threads.
-__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
   __shared__ __attribute__((aligned(16))) u32 L[kSimdLds];
   for (u32 t = threadIdx.x; t < kSimdLds; t += kSimdBlock) {
     u32 v = 0;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb,
   __syncthreads();
   const u32 t = blockIdx.x * kSimdBlock + threadIdx.x;
   const u32 i = t >> 3, j = t & 7;
-  if (i >= n) return;  // whole 8-lane groups exit together
+  if (i >= n || x11_stop(ab)) return;  // whole 8-lane groups exit together (the abort word is wave-uniform)
   u64 h[8];
   load_hash(Hb, stride, i, h);
   u32 xw[16];
@@ -340,16 +341,17 @@ __device__ __forceinline__ void echo_round(const u32* T, u32 lo, u32 W[16][4], u
 }
 
 // kSearch: compare the top 64 bits of the X11 digest (ECHO output bytes 24..31) with
-// the target and append hits to out[1..cap] (out[0] counts); otherwise write H.
+// the target and publish hits to `sink` (otedama/hitsink.h); otherwise write H.
 // Round 0 only transforms the four message words (the other twelve are nonce-independent:
 // x11t::ECHO_R0); in search mode round 9 only computes the two output rows the compare needs.
 template <bool kSearch>
 __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_echo512_64(u64* __restrict__ Hb, u32 stride, u32 n, u32 base,
-                                                          u64 target_hi, u32* __restrict__ out, u32 cap) {
+                                                          u64 target_hi, const HitSink sink) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
+    if (otedama_dev::abort_newer(otedama_dev::abort_peek(sink), sink.epoch)) return;
     u64 h[8];
     load_hash(Hb, stride, i, h);
     u32 W[16][4];
@@ -382,10 +384,7 @@ __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4)
         t[w - 2] = xor3(r1, r9, w == 2 ? lo32(h[3]) : hi32(h[3]));
       }
       const u64 top = mk64(t[0], t[1]);
-      if (top <= target_hi) {
-        const u32 s = atomicAdd(out, 1u);
-        if (s < cap) out[1 + s] = base + i;
-      }
+      if (top <= target_hi) otedama_dev::hit_publish(sink, base + i, 0u);
     } else {
       echo_round(T, lo, W, 512u + 16u * 9u);
       u64 o[8];
@@ -418,22 +417,24 @@ int x11_device_cus() {
 }  // namespace x11k
 
 hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                              uint32_t* out, uint32_t cap, hipStream_t s) {
+                              const HitSink* sink, hipStream_t s) {
   using namespace x11k;
+  X11Abort ab;
+  if (sink) ab = X11Abort{sink->abort, sink->epoch};
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
   // bank-private AES table (64 KiB): 2 resident blocks of 512 per CU, grid-stride over the batch
   const u32 aes_want = (n + kAesBlock - 1) / kAesBlock, aes_cap = (u32)x11_device_cus() * 2 * 4;
   const dim3 aes_grid(aes_want < aes_cap ? aes_want : aes_cap), aes_block(kAesBlock);
   switch (stage) {
-    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n); break;
+    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n, ab); break;
     case kX11Simd: {
       const dim3 g8((8ull * n + kBlock - 1) / kBlock);
-      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n);
+      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n, ab);
       break;
     }
     case kX11Echo:
-      if (out) k_echo512_64<true><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, out, cap);
-      else k_echo512_64<false><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, nullptr, 0);
+      if (sink) k_echo512_64<true><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, *sink);
+      else k_echo512_64<false><<<aes_grid, aes_block, 0, s>>>(H, stride, n, base, p.target_hi, HitSink{});
       break;
     default: return hipErrorInvalidValue;
   }
@@ -441,21 +442,22 @@ hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint
 }
 
 hipError_t x11_launch_stage(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                            uint32_t* out, uint32_t cap, hipStream_t s) {
+                            const HitSink* sink, hipStream_t s) {
   if (stage < 0 || stage >= kX11Stages || n == 0 || stride < n || !H) return hipErrorInvalidValue;
-  if (stage <= kX11Cubehash) return x11_launch_stage_a(stage, p, base, H, stride, n, s);
-  return x11_launch_stage_b(stage, p, base, H, stride, n, out, cap, s);
+  if (stage <= kX11Cubehash) return x11_launch_stage_a(stage, p, base, H, stride, n,
+                                                       sink ? X11Abort{sink->abort, sink->epoch} : X11Abort{}, s);
+  return x11_launch_stage_b(stage, p, base, H, stride, n, sink, s);
 }
 
 // The whole chain over nonces base .. base + n - 1. H: 8 * stride u64 (stride >= n).
-// out != null: search mode (ECHO compares, H keeps the SIMD output); else H = digests.
+// sink != null: search mode (ECHO compares, H keeps the SIMD output); else H = digests.
 hipError_t x11_launch_chain(const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
-                            uint32_t* out, uint32_t cap, hipStream_t s) {
+                            const HitSink* sink, hipStream_t s) {
   // One launch per stage. Fusing the register-only middle (Skein..CubeHash) into one kernel measured
   // 1.3% slower than separate launches (its register union drops it to 4 waves/SIMD; the HBM round
   // trips it saves are hidden behind the VALU-bound stages anyway): profiles/r1/x11/NOTES.md.
   hipError_t e = hipSuccess;
-  for (int st = kX11Blake; e == hipSuccess && st <= kX11Echo; ++st) e = x11_launch_stage(st, p, base, H, stride, n, out, cap, s);
+  for (int st = kX11Blake; e == hipSuccess && st <= kX11Echo; ++st) e = x11_launch_stage(st, p, base, H, stride, n, sink, s);
   return e;
 }
 

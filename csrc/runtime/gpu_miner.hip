@@ -1,19 +1,36 @@
-// GpuMiner: one host thread per GPU driving double-buffered search batches on a
-// private HIP stream (short launches + pinned result buffers so a
-// job switch or a found share is never more than ~one batch away).
+// GpuMiner: one host thread per GPU driving search batches on a private HIP stream.
 //
-// Per batch: hipMemsetAsync(hit counter) -> search kernel -> hipMemcpyAsync of
-// the hit slots into pinned host memory -> event. While batch k runs on the GPU
-// the thread re-verifies batch k-1's candidates on the CPU (full 256-bit compare)
-// and queues shares tagged with the job epoch that produced them.
+// Share path: a kernel publishes each hit the moment it is found into a ring of HitRecords in host-coherent
+// pinned memory (record, system-scope fence, tag: otedama/hitsink.h). This thread polls the rings of the
+// batches in flight every ~100 us, re-verifies each candidate on the CPU (full 256-bit compare against the
+// job's current target) and pushes the share to the queue, whose eventfd wakes the control plane. A hit is
+// therefore on its way to the pool while the launch that found it is still running, instead of after the
+// batch (2^29 nonces, ~28 ms) and its copy-back.
+//
+// Job switches: new work (or a pause) opens a new launch epoch and writes it to an uncached device word on a
+// control stream (hipStreamWriteValue32). Every wave polls that word once per grid-stride trip, so batches of
+// the old epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first
+// batch of the new work starts right behind them. The switch time (set_job -> new batch running) is recorded.
+//
+// Device time: s_memrealtime (100 MHz) is mapped to CLOCK_MONOTONIC by a probe kernel at start-up (min round
+// trip of several probes) and re-checked every 10 s by a calibration thread on a stream of its own (a probe
+// that queued behind busy CUs is rejected by its round trip), so a share carries the kernel's own hit time.
+//
+// Parity: the reference's worker sends each share as it is found (internal/miner/worker.go:262-275) and picks
+// up new work between 1024-nonce batches (worker.go:231-248).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 
+#include "otedama/hitsink.h"
 #include "otedama/job.h"
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
@@ -22,16 +39,15 @@
 
 namespace otedama {
 
-hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, uint32_t* out,
-                                 uint32_t cap, int grid, hipStream_t stream);
-hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uint32_t* out, uint32_t cap,
+hipError_t launch_sha256d_search(const Sha256dParams& p, uint32_t base, uint64_t count, const HitSink& sink, int grid,
+                                 hipStream_t stream);
+hipError_t launch_sha256d_search_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, const HitSink& sink,
                                    int grid, hipStream_t stream);
 hipError_t launch_sha256d_search_v(const Sha256dParamsV& p, const Sha256dVariant* vars, uint32_t base, uint64_t count,
-                                   uint32_t* out, uint32_t cap, int grid, hipStream_t stream, int block = 256,
-                                   int chains = 1);
+                                   const HitSink& sink, int grid, hipStream_t stream, int block = 256, int chains = 1);
 
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
-                                int gap, uint32_t* out, uint32_t cap, int grid, hipStream_t stream);
+                                int gap, const HitSink& sink, int grid, hipStream_t stream);
 uint64_t scrypt_scratch_bytes(int grid, int gap);
 int gpu_cu_count(int device);
 
@@ -42,24 +58,54 @@ int gpu_cu_count(int device);
       throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " #call); \
   } while (0)
 
+}  // namespace otedama
+
+// Device clock probe: one lane stores the 64-bit 100 MHz real-time counter (vector store to host memory).
+__global__ void otd_rt_probe(uint64_t* out) {
+  if (threadIdx.x == 0) *out = __builtin_amdgcn_s_memrealtime();
+}
+
+namespace otedama {
+
 namespace {
 constexpr uint32_t kHitCap = 1024;
+constexpr int kInflight = 2;
+constexpr double kRtHz = 100e6;
+constexpr auto kIdlePoll = std::chrono::microseconds(100);
 
-struct Slot {
-  uint32_t* d_out = nullptr;
-  uint32_t* h_out = nullptr;
-  hipEvent_t start{}, done{};
-  bool busy = false;
-  std::shared_ptr<const JobTemplate> job;
-  uint64_t gen = 0;
-  uint64_t count = 0;  // nonces per variant
-  int nvar = 1;        // > 1: K-variant / version-parallel SHA-256d launch, hits carry the variant index
+// Header variants of one stripe group (up to 128 consecutive positions sharing block 2). Built once per
+// (work generation, group) and shared by every launch of the group (~1000 launches at 2^29 nonces each).
+struct Group {
+  uint64_t gen = ~0ull, k = ~0ull;
+  int nvar = 1;
+  bool use_v = false;
   uint8_t header[kSha256dV2Group][80];
   uint32_t version[kSha256dV2Group] = {0}, ntime[kSha256dV2Group] = {0};
   uint64_t en2[kSha256dV2Group] = {0};
-  Sha256dVariant* d_vars = nullptr;  // version-parallel kernel: per-lane variant table (device)
-  Sha256dVariant* h_vars = nullptr;  // pinned staging copy
-  TraceId range = 0;  // roctx: enqueue -> host verification of this batch
+  Sha256dParamsV v_params{};
+  Sha256dVariant v_table[kSha256dV2Group];
+};
+
+struct Batch {
+  bool busy = false;
+  std::shared_ptr<const JobTemplate> job;
+  std::shared_ptr<const Group> group;
+  uint64_t gen = 0;
+  uint32_t epoch = 0, tag = 0;
+  uint64_t count = 0;  // nonces per variant
+  int nvar = 1;
+  uint32_t consumed = 0;  // ring records already handled
+  double enq_host = 0;    // monotonic seconds at enqueue
+  uint32_t rt_enq = 0;    // device realtime (low 32 bits) estimated at enqueue
+  bool started = false;
+  hipEvent_t start{}, done{};
+  uint32_t* d_count = nullptr;  // candidate counter (device memory)
+  uint32_t* h_count = nullptr;  // pinned copy of the final count
+  HitRecord* ring = nullptr;    // host-coherent records (host pointer)
+  HitRecord* ring_dev = nullptr;  // the same records, device address
+  Sha256dVariant* d_vars = nullptr;
+  Sha256dVariant* h_vars = nullptr;
+  TraceId range = 0;
 };
 }  // namespace
 
@@ -98,37 +144,67 @@ void GpuMiner::stop() {
 void GpuMiner::loop() {
   trace_name_thread(("otedama-" + device_id_).c_str());
   OTD_HIP(hipSetDevice(device_));
-  hipStream_t stream = nullptr;
-  Slot slots[2];
-  // scrypt scratch (allocated lazily on the first scrypt job)
-  void* scratch = nullptr;
+  hipStream_t stream = nullptr, ctl = nullptr, cal = nullptr;
+  Batch slots[kInflight];
+  uint32_t* d_abort = nullptr;   // uncached device word: the newest launch epoch that must keep running
+  uint64_t* h_rt = nullptr;      // probe output (pinned, host-coherent)
+  uint64_t* d_rt = nullptr;      // its device address
+  std::thread cal_th;            // device-clock re-calibration
+  std::atomic<bool> cal_stop{false};
+  std::mutex cal_mu;
+  std::condition_variable cal_cv;
+  void* scratch = nullptr;       // scrypt pad, allocated on the first scrypt job
   void* xbuf = nullptr;
-  // X11 intermediate digests (8 u64 planes x batch), allocated on the first x11 job
-  uint64_t* x11_h = nullptr;
-  // Released on every exit, including a HIP error thrown mid-loop (device fault): in-flight
-  // batches are drained first so nothing is freed under a running kernel or copy.
+  uint64_t* x11_h = nullptr;     // X11 intermediate digests (8 u64 planes x batch)
+  // Released on every exit, including a HIP error thrown mid-loop (device fault): in-flight batches are drained
+  // first so nothing is freed under a running kernel or copy.
   struct Release {
     std::function<void()> f;
     ~Release() { f(); }
   } release{[&] {
+    if (cal_th.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(cal_mu);
+        cal_stop = true;
+      }
+      cal_cv.notify_all();
+      cal_th.join();
+    }
     if (stream) (void)hipStreamSynchronize(stream);
+    if (ctl) (void)hipStreamSynchronize(ctl);
+    if (cal) (void)hipStreamSynchronize(cal);
     for (auto& s : slots) {
-      if (s.d_out) (void)hipFree(s.d_out);
-      if (s.h_out) (void)hipHostFree(s.h_out);
+      if (s.d_count) (void)hipFree(s.d_count);
+      if (s.h_count) (void)hipHostFree(s.h_count);
+      if (s.ring) (void)hipHostFree(s.ring);
       if (s.start) (void)hipEventDestroy(s.start);
       if (s.done) (void)hipEventDestroy(s.done);
       if (s.d_vars) (void)hipFree(s.d_vars);
       if (s.h_vars) (void)hipHostFree(s.h_vars);
     }
+    if (d_abort) (void)hipFree(d_abort);
+    if (h_rt) (void)hipHostFree(h_rt);
     if (scratch) (void)hipFree(scratch);
     if (xbuf) (void)hipFree(xbuf);
     if (x11_h) (void)hipFree(x11_h);
     if (stream) (void)hipStreamDestroy(stream);
+    if (ctl) (void)hipStreamDestroy(ctl);
+    if (cal) (void)hipStreamDestroy(cal);
   }};
   OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  OTD_HIP(hipStreamCreateWithFlags(&ctl, hipStreamNonBlocking));
+  OTD_HIP(hipStreamCreateWithFlags(&cal, hipStreamNonBlocking));
+  OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
+  OTD_HIP(hipMemset(d_abort, 0, 256));
+  OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_rt), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  OTD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_rt), h_rt, 0));
   for (auto& s : slots) {
-    OTD_HIP(hipMalloc(&s.d_out, (1 + 2 * kHitCap) * sizeof(uint32_t)));
-    OTD_HIP(hipHostMalloc(&s.h_out, (1 + 2 * kHitCap) * sizeof(uint32_t), hipHostMallocDefault));
+    OTD_HIP(hipMalloc(&s.d_count, 64));
+    OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_count), 64, hipHostMallocDefault));
+    OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.ring), kHitCap * sizeof(HitRecord),
+                          hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(s.ring, 0, kHitCap * sizeof(HitRecord));
+    OTD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.ring_dev), s.ring, 0));
     OTD_HIP(hipEventCreate(&s.start));
     OTD_HIP(hipEventCreate(&s.done));
     if (sha_v_) {
@@ -136,242 +212,409 @@ void GpuMiner::loop() {
       OTD_HIP(hipHostMalloc(&s.h_vars, kSha256dV2Group * sizeof(Sha256dVariant), hipHostMallocDefault));
     }
   }
+  const int cus = gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256;
   // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
   // 13.6-14.0 for the per-lane kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md).
   const int scrypt_gap = kScryptCoop;
-  const int scrypt_grid = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
+  const int scrypt_grid = cus * 16;
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
   // X11: eleven stage kernels per batch over a 64 B/nonce digest buffer (512 MiB at 2^23).
   const uint32_t x11_batch = 1u << 23;
-  // K-variant SHA-256d kernel (K states per lane, 4-6 waves/SIMD): 16 blocks of 256 per CU
-  // (tools/bench_sha_k.py sweeps K and the grid; profiles/r2/).
-  grid_k_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 16;
-  // Version-parallel kernel (8-waves/SIMD build): 64 blocks of 256 per CU (tools/bench_sha_v.py, profiles/r2/sha_v).
-  grid_v_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 64;
-  // Two-chain kernel (4 waves/SIMD build): 128 blocks of 256 per CU (tools/bench_sha_v.py --chains2-bpc,
-  // profiles/r2/sha_v2).
-  grid_v2_ = (gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256) * 128;
-  // Host variant table of the current 64/128-variant group, rebuilt only when the group changes (once per 2^32
-  // nonces).
-  uint64_t v_table_gen = ~0ull, v_table_k = ~0ull;
-  int v_table_n = 0;
-  Sha256dParamsV v_params{};
-  Sha256dVariant v_table[kSha256dV2Group];
+  // K-variant SHA-256d kernel: 16 blocks of 256 per CU (tools/bench_sha_k.py, profiles/r2/).
+  grid_k_ = cus * 16;
+  // Version-parallel kernel (8-waves/SIMD build): 64 blocks of 256 per CU (profiles/r2/sha_v).
+  grid_v_ = cus * 64;
+  // Two-chain kernel (4 waves/SIMD build): 128 blocks of 256 per CU (profiles/r2/sha_v2).
+  grid_v2_ = cus * 128;
 
-  uint64_t cur_gen = ~0ull;
-  uint64_t k = 0;       // variant-stripe position
-  uint64_t nonce_off = 0;
-  int which = 0;
-
-  auto finish = [&](Slot& s) {
-    if (!s.busy) return;
-    OTD_HIP(hipEventSynchronize(s.done));
-    trace_stop(s.range);
-    float ms = 0;
-    hipEventElapsedTime(&ms, s.start, s.done);
-    const uint32_t n = s.h_out[0] < kHitCap ? s.h_out[0] : kHitCap;
-    TraceScope verify_scope("otd.verify_candidates");
-    uint64_t good = 0, bad = 0;
-    const bool multi = s.nvar > 1;
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t nonce = multi ? s.h_out[1 + 2 * i] : s.h_out[1 + i];
-      const uint32_t vi = multi ? s.h_out[2 + 2 * i] : 0u;
-      if (vi >= (uint32_t)s.nvar) { ++bad; continue; }
-      uint8_t hdr[80];
-      std::memcpy(hdr, s.header[vi], 80);
-      store_le32(hdr + 76, nonce);
-      ShareRecord r{};
-      if (!verify_share(s.job->algo, hdr, s.job->target, r.hash)) { ++bad; continue; }
-      r.epoch = s.job->epoch; r.job_id = s.job->job_id; r.channel_id = s.job->channel_id;
-      r.nonce = nonce; r.ntime = s.ntime[vi]; r.version = s.version[vi]; r.extranonce2 = s.en2[vi];
-      r.extranonce2_size = s.job->extranonce2_size; r.device_id = device_id_;
-      r.found_at = monotonic_seconds();
-      queue_.push(std::move(r));
-      ++good;
+  // ---- device clock -> host clock
+  std::atomic<double> rt_offset{0.0};  // host monotonic seconds at device realtime 0
+  double calib_rtt = 1e9;
+  // One probe: (host midpoint, device realtime) bracketed by the launch and the stream sync; the tightest
+  // bracket wins, and a later probe replaces it only when its round trip is within 2x of the best (50 us floor):
+  // that tracks clock drift without accepting a probe that waited for a CU behind the search waves.
+  auto probe = [&](hipStream_t on) {
+    __atomic_store_n(h_rt, 0ull, __ATOMIC_RELEASE);
+    const double t0 = monotonic_seconds();
+    hipLaunchKernelGGL(otd_rt_probe, dim3(1), dim3(64), 0, on, d_rt);
+    OTD_HIP(hipGetLastError());
+    OTD_HIP(hipStreamSynchronize(on));
+    const double t1 = monotonic_seconds();
+    const uint64_t rt = __atomic_load_n(h_rt, __ATOMIC_ACQUIRE);
+    if (rt && (t1 - t0) < std::max(2.0 * calib_rtt, 50e-6)) {
+      rt_offset.store(0.5 * (t0 + t1) - double(rt) / kRtHz);
+      calib_rtt = std::min(calib_rtt, t1 - t0);
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.clock_calib_rtt_us = (t1 - t0) * 1e6;
     }
-    std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.hashes += s.count * (uint64_t)s.nvar;
-    stats_.candidates += s.h_out[0];
-    stats_.shares += good;
-    stats_.rejected_candidates += bad;
-    stats_.busy_seconds += ms * 1e-3;
-    stats_.launches += 1;
-    if (multi) stats_.variant_launches += 1;
-    s.busy = false;
-    s.job.reset();
+  };
+  for (int t = 0; t < 8; ++t) probe(stream);
+  rt_offset_ = rt_offset.load();
+  cal_th = std::thread([&] {
+    try {
+      OTD_HIP(hipSetDevice(device_));
+      std::unique_lock<std::mutex> lk(cal_mu);
+      while (!cal_cv.wait_for(lk, std::chrono::seconds(10), [&] { return cal_stop.load(); })) {
+        lk.unlock();
+        for (int t = 0; t < 4 && !cal_stop.load(); ++t) probe(cal);
+        lk.lock();
+      }
+    } catch (const std::exception&) {
+      // a failing probe is a device fault the miner thread reports through its own launches
+    }
+  });
+  // The thread uses locals declared after `release`: join it before they go out of scope (on every exit path).
+  struct Joiner {
+    std::function<void()> f;
+    ~Joiner() { f(); }
+  } cal_join{[&] {
+    {
+      std::lock_guard<std::mutex> g(cal_mu);
+      cal_stop = true;
+    }
+    cal_cv.notify_all();
+    if (cal_th.joinable()) cal_th.join();
+  }};
+
+  std::shared_ptr<Group> group;  // current stripe group
+  uint64_t cur_gen = ~0ull;
+  uint64_t k = 0;  // variant-stripe position of the current group
+  uint64_t nonce_off = 0;
+  uint32_t epoch = 1, tag = 0;
+  uint64_t epoch_gen = ~0ull;  // work generation the current epoch was opened for (0 = paused)
+  bool switch_pending = false;
+  double switch_t0 = 0;
+  double rate_hpms = 0;  // hashes per ms of completed full batches (for aborted-batch accounting)
+  std::deque<int> fifo;  // in-flight slots, issue order
+
+  auto verify_push = [&](Batch& b, uint32_t nonce, uint32_t vi, uint32_t stamp, bool stamped,
+                         const std::shared_ptr<const JobTemplate>& cur, uint64_t cur_g, uint64_t* good,
+                         uint64_t* bad) {
+    if (vi >= (uint32_t)b.nvar) { ++*bad; return; }
+    uint8_t hdr[80];
+    std::memcpy(hdr, b.group->header[vi], 80);
+    store_le32(hdr + 76, nonce);
+    ShareRecord r{};
+    // the job's current target: a target-only update (same work generation) applies to batches in flight too
+    const uint8_t* target = (cur && cur_g == b.gen) ? cur->target : b.job->target;
+    if (!verify_share(b.job->algo, hdr, target, r.hash)) { ++*bad; return; }
+    r.epoch = b.job->epoch; r.job_id = b.job->job_id; r.channel_id = b.job->channel_id;
+    r.nonce = nonce; r.ntime = b.group->ntime[vi]; r.version = b.group->version[vi]; r.extranonce2 = b.group->en2[vi];
+    r.extranonce2_size = b.job->extranonce2_size; r.device_id = device_id_;
+    r.found_at = monotonic_seconds();
+    if (stamped) r.device_found_at = b.enq_host + double(int32_t(stamp - b.rt_enq)) / kRtHz;
+    queue_.push(std::move(r));
+    ++*good;
   };
 
-  while (running_.load()) {
-    uint64_t gen = 0;
-    auto job = current_job(&gen);
-    if (!job) {
-      finish(slots[which ^ 1]);
-      continue;
+  // Consume the published records of a batch; `final_n` = the batch's final count (after completion) or ~0u
+  // while it runs. Returns the number of records handled.
+  auto drain_ring = [&](Batch& b, uint32_t final_n, const std::shared_ptr<const JobTemplate>& cur,
+                        uint64_t cur_g) -> uint32_t {
+    const uint32_t limit = final_n == ~0u ? kHitCap : std::min(final_n, kHitCap);
+    uint64_t good = 0, bad = 0, lost = 0, handled = 0;
+    while (b.consumed < limit) {
+      HitRecord* r = b.ring + b.consumed;
+      const uint32_t tg = __atomic_load_n(&r->tag, __ATOMIC_ACQUIRE);
+      if (tg != b.tag) {
+        if (final_n == ~0u) break;  // not written yet
+        ++lost;                     // completed launch without its record: count and skip (should not happen)
+        ++b.consumed;
+        continue;
+      }
+      const uint32_t nonce = __atomic_load_n(&r->nonce, __ATOMIC_RELAXED);
+      const uint32_t vi = __atomic_load_n(&r->variant, __ATOMIC_RELAXED);
+      const uint32_t stamp = __atomic_load_n(&r->stamp, __ATOMIC_RELAXED);
+      verify_push(b, nonce, vi, stamp, true, cur, cur_g, &good, &bad);
+      ++b.consumed;
+      ++handled;
     }
-    if (gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
+    if (handled || lost) {
+      std::lock_guard<std::mutex> g(stats_mu_);
+      stats_.shares += good;
+      stats_.rejected_candidates += bad + lost;
+      if (final_n == ~0u) stats_.ring_hits += handled;
+    }
+    return uint32_t(handled);
+  };
+
+  auto finish = [&](Batch& b, const std::shared_ptr<const JobTemplate>& cur, uint64_t cur_g) {
+    trace_stop(b.range);
+    const uint32_t n = *b.h_count;
+    drain_ring(b, n, cur, cur_g);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, b.start, b.done);
+    const uint64_t full = b.count * uint64_t(b.nvar);
+    const bool aborted = int32_t(epoch - b.epoch) > 0;  // a newer epoch was opened after this batch
+    uint64_t done_hashes = full;
+    if (aborted && rate_hpms > 0) done_hashes = std::min<uint64_t>(full, uint64_t(rate_hpms * double(ms)));
+    if (!aborted && ms > 0) rate_hpms = rate_hpms > 0 ? 0.8 * rate_hpms + 0.2 * (double(full) / ms) : double(full) / ms;
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.hashes += done_hashes;
+    stats_.candidates += n;
+    stats_.busy_seconds += ms * 1e-3;
+    stats_.launches += 1;
+    if (aborted) stats_.aborted_launches += 1;
+    if (b.nvar > 1) stats_.variant_launches += 1;
+    b.busy = false;
+    b.job.reset();
+    b.group.reset();
+  };
+
+  auto build_group = [&](const std::shared_ptr<const JobTemplate>& job, uint64_t gen) {
+    auto gp = std::make_shared<Group>();
+    gp->gen = gen;
+    gp->k = k;
+    gp->nvar = 1;
     const uint64_t v = job->variant_start + k * job->variant_stride;
-    if (v >= job->variant_space()) {  // stripe exhausted; wait for fresh work
-      finish(slots[which ^ 1]);
-      std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      continue;
-    }
-    Slot& s = slots[which];
-    finish(s);  // slot reuse: make sure its previous batch is consumed
-    s.job = job;
-    s.gen = gen;
-    s.nvar = 1;
-    job->variant_header(v, s.header[0], &s.version[0], &s.ntime[0], &s.en2[0]);
-    bool use_v = false;
-    if (job->algo == Algo::kSha256d && sha_v_) {
-      // 128 (two-chain kernel) or 64 consecutive stripe positions with a common block 2 -> one or two variants per
-      // lane of the version-parallel kernel. A group is all-or-nothing (a shorter run takes the next layout down,
-      // ending at the K path below) and depends only on (job, k), so every launch of a group uses the same kernel
-      // and W3/nonce space.
-      const int want = sha_v2_ ? kSha256dV2Group : kSha256dVGroup;
+    job->variant_header(v, gp->header[0], &gp->version[0], &gp->ntime[0], &gp->en2[0]);
+    if (job->algo == Algo::kSha256d && (sha_v_ || sha_k_ > 1)) {
+      // Consecutive stripe positions whose headers differ only in block 1 (version rolling) share block 2: up to
+      // 128 (two-chain version-parallel kernel), 64 (one chain) or K (per-lane K-variant kernel). A group is
+      // all-or-nothing per layout and depends only on (work, k), so all its launches use one kernel.
+      const int want = sha_v2_ ? kSha256dV2Group : sha_v_ ? kSha256dVGroup : sha_k_;
       int kv = 1;
       while (kv < want) {
         const uint64_t vk = job->variant_start + (k + kv) * job->variant_stride;
         if (vk >= job->variant_space()) break;
-        job->variant_header(vk, s.header[kv], &s.version[kv], &s.ntime[kv], &s.en2[kv]);
-        if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
+        job->variant_header(vk, gp->header[kv], &gp->version[kv], &gp->ntime[kv], &gp->en2[kv]);
+        if (std::memcmp(gp->header[kv] + 64, gp->header[0] + 64, 12) != 0) break;
         ++kv;
       }
-      if (kv >= kSha256dV2Group && sha_v2_) {
-        use_v = true;
-        s.nvar = kSha256dV2Group;
-      } else if (kv >= kSha256dVGroup) {
-        use_v = true;
-        s.nvar = kSha256dVGroup;
+      if (sha_v2_ && kv >= kSha256dV2Group) {
+        gp->use_v = true;
+        gp->nvar = kSha256dV2Group;
+      } else if (sha_v_ && kv >= kSha256dVGroup) {
+        gp->use_v = true;
+        gp->nvar = kSha256dVGroup;
+      } else if (sha_k_ > 1) {
+        gp->nvar = sha256d_k_floor(std::min(kv, sha_k_));  // kernels exist for K in {2,3,4,6,8,12,16}
+      }
+      if (gp->use_v) {
+        const uint8_t* hs[kSha256dV2Group];
+        for (int j = 0; j < gp->nvar; ++j) hs[j] = gp->header[j];
+        if (!sha256d_prepare_v(hs, gp->nvar, job->target, &gp->v_params, gp->v_table))
+          throw std::runtime_error("sha256d_prepare_v");
+        gp->v_params.occupancy8 = gp->nvar == kSha256dV2Group ? 0 : 1;
       }
     }
-    if (!use_v && job->algo == Algo::kSha256d && sha_k_ > 1) {
-      // Group the next stripe positions whose headers differ only in block 1 (version rolling): they share
-      // the block-2 message schedule in sha256d_search_k. Stops at the first one that differs in 64..75.
-      int kv = 1;
-      while (kv < sha_k_) {
-        const uint64_t vk = job->variant_start + (k + kv) * job->variant_stride;
-        if (vk >= job->variant_space()) break;
-        job->variant_header(vk, s.header[kv], &s.version[kv], &s.ntime[kv], &s.en2[kv]);
-        if (std::memcmp(s.header[kv] + 64, s.header[0] + 64, 12) != 0) break;
-        ++kv;
-      }
-      s.nvar = sha256d_k_floor(kv);  // kernels exist for K in {2,3,4,6,8,12,16}
-    }
+    return gp;
+  };
+
+  auto enqueue = [&](Batch& s, const std::shared_ptr<const JobTemplate>& job, uint64_t gen) {
+    if (!group || group->gen != gen || group->k != k) group = build_group(job, gen);
+    s.job = job;
+    s.group = group;
+    s.gen = gen;
+    s.nvar = group->nvar;
+    s.epoch = epoch;
+    s.tag = ++tag == 0 ? ++tag : tag;
+    s.consumed = 0;
+    s.started = false;
     s.range = trace_start(job->algo == Algo::kScrypt ? "otd.scrypt.batch"
                           : job->algo == Algo::kX11  ? "otd.x11.batch"
                                                      : "otd.sha256d.batch");
-    OTD_HIP(hipMemsetAsync(s.d_out, 0, sizeof(uint32_t), stream));
+    HitSink sink;
+    sink.out = s.d_count;
+    sink.ring = s.ring_dev;
+    sink.abort = d_abort;
+    sink.cap = kHitCap;
+    sink.tag = s.tag;
+    sink.epoch = s.epoch;
+    sink.words = 2;
+    OTD_HIP(hipMemsetAsync(s.d_count, 0, 64, stream));
     OTD_HIP(hipEventRecord(s.start, stream));
+    s.enq_host = monotonic_seconds();
+    rt_offset_ = rt_offset.load();
+    s.rt_enq = uint32_t(uint64_t((s.enq_host - rt_offset_) * kRtHz));
     if (job->algo == Algo::kScrypt) {
       if (!scratch) {
         OTD_HIP(hipMalloc(&scratch, scrypt_scratch_bytes(scrypt_grid, scrypt_gap)));
         OTD_HIP(hipMalloc(&xbuf, uint64_t(scrypt_batch) * 128));
       }
       ScryptParams p;
-      scrypt_prepare(s.header[0], job->target, &p);
+      scrypt_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = remaining < scrypt_batch ? remaining : scrypt_batch;
-      OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, s.d_out,
-                                   kHitCap, scrypt_grid, stream));
+      OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, sink,
+                                   scrypt_grid, stream));
     } else if (job->algo == Algo::kX11) {
       if (!x11_h) OTD_HIP(hipMalloc(&x11_h, uint64_t(x11_batch) * 64));
       X11Params p;
-      x11_prepare(s.header[0], job->target, &p);
+      x11_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = remaining < x11_batch ? remaining : x11_batch;
-      OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), s.d_out, kHitCap, stream));
-    } else if (use_v) {
-      const bool two = s.nvar == kSha256dV2Group;
-      if (v_table_gen != gen || v_table_k != k || v_table_n != s.nvar) {
-        const uint8_t* hs[kSha256dV2Group];
-        for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
-        if (!sha256d_prepare_v(hs, s.nvar, job->target, &v_params, v_table))
-          throw std::runtime_error("sha256d_prepare_v");
-        v_params.occupancy8 = two ? 0 : 1;  // two chains: the 4-waves/SIMD build; one chain: the 8-wave build
-        v_table_gen = gen;
-        v_table_k = k;
-        v_table_n = s.nvar;
-      }
+      OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), &sink, stream));
+    } else if (group->use_v) {
+      const bool two = group->nvar == kSha256dV2Group;
+      Sha256dParamsV vp = group->v_params;
       // The table is cached per (work, group) but a target-only update (SV2 SetTarget, V1 set_difficulty) keeps
-      // the work generation: the share filter must follow the job's current target on every launch.
-      v_params.target_hi = load_le32(job->target + 28);
-      const size_t table_bytes = size_t(s.nvar) * sizeof(Sha256dVariant);
-      std::memcpy(s.h_vars, v_table, table_bytes);
+      // the work generation: the share filter follows the job's current target on every launch.
+      vp.target_hi = load_le32(job->target + 28);
+      const size_t table_bytes = size_t(group->nvar) * sizeof(Sha256dVariant);
+      std::memcpy(s.h_vars, group->v_table, table_bytes);
       OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, table_bytes, hipMemcpyHostToDevice, stream));
       // W3 (big-endian nonce word) windows tile [0, 2^32) exactly like the nonce windows of the other kernels;
       // the kernel reports nonce = bswap(W3). Launch duration stays batch_ hashes.
-      s.count = batch_ >= uint64_t(s.nvar) ? batch_ / uint64_t(s.nvar) : 1;  // powers of two: still tiles 2^32
-      OTD_HIP(launch_sha256d_search_v(v_params, s.d_vars, uint32_t(nonce_off), s.count, s.d_out, kHitCap,
-                                      two ? grid_v2_ : grid_v_, stream, 256, two ? 2 : 1));
-    } else if (s.nvar > 1) {
+      s.count = batch_ >= uint64_t(group->nvar) ? batch_ / uint64_t(group->nvar) : 1;
+      OTD_HIP(launch_sha256d_search_v(vp, s.d_vars, uint32_t(nonce_off), s.count, sink, two ? grid_v2_ : grid_v_,
+                                      stream, 256, two ? 2 : 1));
+    } else if (group->nvar > 1) {
       Sha256dParamsK p;
       const uint8_t* hs[kSha256dMaxK];
-      for (int j = 0; j < s.nvar; ++j) hs[j] = s.header[j];
-      if (!sha256d_prepare_k(hs, s.nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
-      // Keep one launch's duration (job-switch latency) about independent of K: nonces per
-      // variant = batch / (largest power of two <= K); batch is a power of two that tiles 2^32, so this
-      // still tiles it.
+      for (int j = 0; j < group->nvar; ++j) hs[j] = group->header[j];
+      if (!sha256d_prepare_k(hs, group->nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
+      // Keep one launch's duration about independent of K: nonces per variant = batch / (largest power of two
+      // <= K); batch is a power of two that tiles 2^32, so this still tiles it.
       uint64_t div = 1;
-      while (div * 2 <= (uint64_t)s.nvar && div * 2 <= batch_) div *= 2;
+      while (div * 2 <= (uint64_t)group->nvar && div * 2 <= batch_) div *= 2;
       s.count = batch_ / div;
-      OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_k_, stream));
+      OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, sink, grid_k_, stream));
     } else {
       Sha256dParams p;
-      sha256d_prepare(s.header[0], job->target, &p);
+      sha256d_prepare(group->header[0], job->target, &p);
       s.count = batch_;
-      OTD_HIP(launch_sha256d_search(p, uint32_t(nonce_off), s.count, s.d_out, kHitCap, grid_, stream));
+      OTD_HIP(launch_sha256d_search(p, uint32_t(nonce_off), s.count, sink, grid_, stream));
     }
-    OTD_HIP(hipMemcpyAsync(s.h_out, s.d_out, (1 + (s.nvar > 1 ? 2 : 1) * kHitCap) * sizeof(uint32_t),
-                           hipMemcpyDeviceToHost, stream));
+    OTD_HIP(hipMemcpyAsync(s.h_count, s.d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     OTD_HIP(hipEventRecord(s.done, stream));
     s.busy = true;
     nonce_off += s.count;
-    if (nonce_off >= (1ull << 32)) { nonce_off = 0; k += (uint64_t)s.nvar; }
-    which ^= 1;
-    finish(slots[which]);  // consume the previous batch while this one runs
+    const uint64_t group_n = uint64_t(group->nvar);
+    if (nonce_off >= (1ull << 32)) { nonce_off = 0; k += group_n; }
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.variant_gen = gen;
+    stats_.variant_next = job->variant_start + (nonce_off == 0 ? k : k + group_n) * job->variant_stride;
+  };
+
+  while (running_.load()) {
+    uint64_t gen = 0;
+    double set_at = 0;
+    auto job = peek_job(&gen, &set_at);
+    bool progressed = false;
+    // New work or a pause opens a new launch epoch; batches of older epochs stop at their next abort poll.
+    const uint64_t want_gen = job ? gen : 0;
+    if (want_gen != epoch_gen) {
+      epoch_gen = want_gen;
+      ++epoch;
+      if (!fifo.empty()) OTD_HIP(hipStreamWriteValue32(ctl, d_abort, epoch, 0));
+      if (job) { switch_pending = true; switch_t0 = set_at; }
+    }
+    if (job && gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
+    // 1) hits of the batches in flight, oldest first
+    for (int i : fifo) progressed |= drain_ring(slots[i], ~0u, job, gen) > 0;
+    // 2) retire completed batches in issue order
+    while (!fifo.empty()) {
+      Batch& b = slots[fifo.front()];
+      const hipError_t q = hipEventQuery(b.done);
+      if (q == hipErrorNotReady) break;
+      OTD_HIP(q);
+      if (!b.started) b.started = true;
+      finish(b, job, gen);
+      fifo.pop_front();
+      progressed = true;
+    }
+    // 3) job-switch time: set_job -> the first batch of the new epoch running on the device
+    if (switch_pending) {
+      for (int i : fifo) {
+        Batch& b = slots[i];
+        if (b.epoch != epoch) continue;
+        const hipError_t q = hipEventQuery(b.start);
+        if (q == hipErrorNotReady) break;
+        OTD_HIP(q);
+        b.started = true;
+        const double ms = (monotonic_seconds() - switch_t0) * 1e3;
+        switch_pending = false;
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.job_switches += 1;
+        stats_.last_job_switch_ms = ms;
+        stats_.job_switch_ms.push_back(ms);
+        if (stats_.job_switch_ms.size() > 64) stats_.job_switch_ms.erase(stats_.job_switch_ms.begin());
+        break;
+      }
+    }
+    // 4) keep kInflight batches queued
+    while (job && (int)fifo.size() < kInflight) {
+      const uint64_t v = job->variant_start + k * job->variant_stride;
+      if (v >= job->variant_space()) break;  // stripe exhausted: wait for fresh work
+      int free_slot = -1;
+      for (int i = 0; i < kInflight; ++i)
+        if (!slots[i].busy) { free_slot = i; break; }
+      if (free_slot < 0) break;
+      enqueue(slots[free_slot], job, gen);
+      fifo.push_back(free_slot);
+      progressed = true;
+    }
+    if (!progressed) {
+      if (!job && fifo.empty()) {
+        uint64_t g2 = 0;
+        (void)current_job(&g2);  // waits (<= 10 ms) for work instead of spinning
+      } else {
+        std::this_thread::sleep_for(kIdlePoll);
+      }
+    }
   }
-  finish(slots[0]);
-  finish(slots[1]);
+  // drain: let the batches in flight finish (abort them first: the miner is stopping)
+  if (!fifo.empty()) {
+    ++epoch;
+    (void)hipStreamWriteValue32(ctl, d_abort, epoch, 0);
+  }
+  uint64_t gen = 0;
+  auto job = peek_job(&gen, nullptr);
+  while (!fifo.empty()) {
+    Batch& b = slots[fifo.front()];
+    OTD_HIP(hipEventSynchronize(b.done));
+    finish(b, job, gen);
+    fifo.pop_front();
+  }
 }
 
 // ------------------------------------------------------------- direct launches
 // Synchronous-free launch API for the Python ops layer (torch-owned buffers and
-// streams): pointers and the stream arrive as integers.
+// streams): pointers and the stream arrive as integers. Hits go to the legacy
+// device-memory slots after out[0]; no abort word.
+
+static HitSink ops_sink(uintptr_t out, uint32_t cap, uint32_t words) {
+  HitSink s;
+  s.out = reinterpret_cast<uint32_t*>(out);
+  s.cap = cap;
+  s.words = words;
+  return s;
+}
 
 void py_launch_sha256d(const Sha256dParams& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                        uintptr_t stream) {
-  OTD_HIP(launch_sha256d_search(p, base, count, reinterpret_cast<uint32_t*>(out), cap, grid,
-                                reinterpret_cast<hipStream_t>(stream)));
+  OTD_HIP(launch_sha256d_search(p, base, count, ops_sink(out, cap, 1), grid, reinterpret_cast<hipStream_t>(stream)));
 }
 
 void py_launch_sha256d_k(const Sha256dParamsK& p, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap, int grid,
                          uintptr_t stream) {
-  OTD_HIP(launch_sha256d_search_k(p, base, count, reinterpret_cast<uint32_t*>(out), cap, grid,
-                                  reinterpret_cast<hipStream_t>(stream)));
+  OTD_HIP(launch_sha256d_search_k(p, base, count, ops_sink(out, cap, 2), grid, reinterpret_cast<hipStream_t>(stream)));
 }
 
 void py_launch_sha256d_v(const Sha256dParamsV& p, uintptr_t vars, uint32_t base, uint64_t count, uintptr_t out,
                          uint32_t cap, int grid, uintptr_t stream, int block, int chains) {
   OTD_HIP(launch_sha256d_search_v(p, reinterpret_cast<const Sha256dVariant*>(vars), base, count,
-                                  reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream),
-                                  block, chains));
+                                  ops_sink(out, cap, 2), grid, reinterpret_cast<hipStream_t>(stream), block, chains));
 }
 
 void py_launch_scrypt(const ScryptParams& p, uint32_t base, uint32_t count, uintptr_t xbuf, uintptr_t scratch, int gap,
                       uintptr_t out, uint32_t cap, int grid, uintptr_t stream) {
   OTD_HIP(launch_scrypt_search(p, base, count, reinterpret_cast<void*>(xbuf), reinterpret_cast<void*>(scratch), gap,
-                               reinterpret_cast<uint32_t*>(out), cap, grid, reinterpret_cast<hipStream_t>(stream)));
+                               ops_sink(out, cap, 1), grid, reinterpret_cast<hipStream_t>(stream)));
 }
 
 void py_launch_x11_stage(const X11Params& p, int stage, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n,
                          uintptr_t out, uint32_t cap, uintptr_t stream) {
-  OTD_HIP(x11_launch_stage(stage, p, base, reinterpret_cast<uint64_t*>(H), stride, n, reinterpret_cast<uint32_t*>(out),
-                           cap, reinterpret_cast<hipStream_t>(stream)));
+  const HitSink s = ops_sink(out, cap, 1);
+  OTD_HIP(x11_launch_stage(stage, p, base, reinterpret_cast<uint64_t*>(H), stride, n, out ? &s : nullptr,
+                           reinterpret_cast<hipStream_t>(stream)));
 }
 
 void py_launch_x11(const X11Params& p, uint32_t base, uintptr_t H, uint32_t stride, uint32_t n, uintptr_t out,
                    uint32_t cap, uintptr_t stream) {
-  OTD_HIP(x11_launch_chain(p, base, reinterpret_cast<uint64_t*>(H), stride, n, reinterpret_cast<uint32_t*>(out), cap,
+  const HitSink s = ops_sink(out, cap, 1);
+  OTD_HIP(x11_launch_chain(p, base, reinterpret_cast<uint64_t*>(H), stride, n, out ? &s : nullptr,
                            reinterpret_cast<hipStream_t>(stream)));
 }
 

@@ -1,9 +1,13 @@
 // Host side of the mining runtime: job variants, share verification, the share
 // queue, the CPU miner and the CPU scrypt reference.
 #include <immintrin.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cstring>
+#include <stdexcept>
 
 #include "otedama/job.h"
 #include "otedama/runtime.h"
@@ -165,13 +169,28 @@ bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32
 
 // -------------------------------------------------------------- share queue
 
+ShareQueue::ShareQueue(size_t cap) : cap_(cap) {
+  efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (efd_ < 0) throw std::runtime_error(std::string("eventfd: ") + std::strerror(errno));
+}
+
+ShareQueue::~ShareQueue() {
+  if (efd_ >= 0) close(efd_);
+}
+
 bool ShareQueue::push(ShareRecord&& s) {
-  std::lock_guard<std::mutex> g(mu_);
-  if (q_.size() >= cap_) {
-    dropped_.fetch_add(1);
-    return false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (q_.size() >= cap_) {
+      dropped_.fetch_add(1);
+      return false;
+    }
+    q_.push_back(std::move(s));
   }
-  q_.push_back(std::move(s));
+  // Wake the consumer. The counter saturates harmlessly (EAGAIN at 2^64-2): readers drain the whole queue.
+  const uint64_t one = 1;
+  ssize_t rc;
+  do rc = write(efd_, &one, sizeof one); while (rc < 0 && errno == EINTR);
   return true;
 }
 
@@ -208,6 +227,7 @@ static bool same_work(const JobTemplate& a, const JobTemplate& b) {
 void MinerBase::set_job(std::shared_ptr<const JobTemplate> job) {
   {
     std::lock_guard<std::mutex> g(job_mu_);
+    if (job && (!job_ || !(last_work_ && same_work(*last_work_, *job)))) job_set_at_ = monotonic_seconds();
     if (job && !(last_work_ && same_work(*last_work_, *job))) ++job_gen_;
     if (job) last_work_ = job;
     job_ = std::move(job);
@@ -221,6 +241,13 @@ std::shared_ptr<const JobTemplate> MinerBase::current_job(uint64_t* gen) {
     job_cv_.wait_for(g, std::chrono::milliseconds(10));
   }
   if (gen) *gen = job_gen_;
+  return job_;
+}
+
+std::shared_ptr<const JobTemplate> MinerBase::peek_job(uint64_t* gen, double* set_at) {
+  std::lock_guard<std::mutex> g(job_mu_);
+  if (gen) *gen = job_gen_;
+  if (set_at) *set_at = job_set_at_;
   return job_;
 }
 
@@ -370,6 +397,8 @@ void CpuMiner::loop(int /*tid*/) {
       queue_.push(std::move(s));
     }
     std::lock_guard<std::mutex> g(stats_mu_);
+    if (stats_.variant_gen != gen) { stats_.variant_gen = gen; stats_.variant_next = 0; }
+    if (v + job->variant_stride > stats_.variant_next) stats_.variant_next = v + job->variant_stride;
     stats_.hashes += kChunk;
     stats_.candidates += hits.size();
     stats_.shares += hits.size();

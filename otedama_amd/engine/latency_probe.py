@@ -1,38 +1,83 @@
-"""End-to-end share-latency probe (BASELINE metric "p50 share latency").
+"""End-to-end share-latency and job-switch probes (BASELINE metric "p50 share latency").
 
-Runs the real engine on one GPU against the in-process local pool over a
-loopback Stratum V2 connection for a few seconds and reports:
-  * submit -> accept quantiles (the reference's definition:
-    otedama_submit_latency_milliseconds, internal/engine/run.go:813-821), and
-  * hit -> accept quantiles: from the moment the host runtime verified the
-    kernel's candidate to the pool's SubmitSharesSuccess (native share queue +
-    asyncio submit + pool-side re-hash / validation).
+Share latency: the real engine mines on one GPU (default 2^29-nonce batches) against the local validating pool
+running in a SEPARATE process (``otedama pool``), over loopback Stratum V2. Reported quantiles:
+  * submit -> accept (the reference's definition: otedama_submit_latency_milliseconds,
+    internal/engine/run.go:813-821);
+  * device hit -> accept: from the kernel's own hit time (s_memrealtime stamped in the hit record, mapped to the
+    host clock) through the host-coherent hit ring, CPU re-verification, the share queue's eventfd, the asyncio
+    submit, the pool process's re-hash / validation and its SubmitSharesSuccess;
+  * host verify -> accept (the part after the miner thread picked the hit up).
 The reference never published a number for this.
+
+Job switch: the native GpuMiner is handed new work every few hundred ms; each switch is timed from set_job() to
+the first batch of the new work running on the device (obsolete batches stop at the device abort word).
 """
 from __future__ import annotations
 
 import asyncio
-
-from otedama_amd import hal
-from otedama_amd.config import Config, MiningConfig, PoolConfig
-from otedama_amd.engine.run import Engine, Options
-from otedama_amd.pool.server import PoolOptions, PoolServer
-from otedama_amd.provider import StaticRateSource
+import os
+import signal
+import statistics
+import subprocess
+import sys
+import time
 
 PROBE_ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-async def _probe(device_index: int, seconds: float, algorithm: str, shares_per_sec: float, batch_nonces: int,
-                 expected_hashrate: float) -> dict:
+def spawn_pool(algorithm: str, difficulty: float, timeout: float = 120.0) -> tuple[subprocess.Popen, str]:
+    """Start ``otedama pool`` in its own process on an ephemeral loopback port; returns (process, sv2 address)."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "otedama_amd", "pool", "--algorithms", algorithm, "--listen-sv2", "127.0.0.1:0",
+           "--listen-v1=", "--difficulty", repr(difficulty), "--retarget-seconds", "3600", "--share-seconds", "1",
+           "--job-interval", "3600", "--block-interval", "3600", "--payout-address", PROBE_ADDR]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
+    deadline = time.monotonic() + timeout
+    seen = []
+    while time.monotonic() < deadline:
+        line = proc.stdout.readline()
+        if not line:
+            break
+        seen.append(line)
+        if "listening sv2=" in line:
+            addr = line.split("listening sv2=", 1)[1].split()[0]
+            return proc, addr
+    proc.kill()
+    raise RuntimeError("pool process did not start: " + "".join(seen[-5:]))
+
+
+def stop_pool(proc: subprocess.Popen) -> dict:
+    """SIGTERM the pool; it prints its stats as one JSON line per algorithm on the way out."""
+    import json
+
+    proc.send_signal(signal.SIGTERM)
+    try:
+        out, _ = proc.communicate(timeout=30)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        out, _ = proc.communicate()
+    for line in reversed((out or "").splitlines()):
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                pass
+    return {}
+
+
+async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, batch_nonces: int) -> dict:
+    from otedama_amd import hal
+    from otedama_amd.config import Config, MiningConfig, PoolConfig
+    from otedama_amd.engine.run import Engine, Options
+    from otedama_amd.provider import StaticRateSource
+
     devs = [d for d in hal.HIPDriver().enumerate() if d.index == device_index]
     if not devs:
         raise RuntimeError(f"no HIP device {device_index}")
-    hashes_per_diff1 = 2.0 ** 16 if algorithm == "scrypt" else 2.0 ** 32  # scrypt pools: diff1 = 0xFFFF << 224
-    diff = expected_hashrate / (shares_per_sec * hashes_per_diff1)
-    pool = PoolServer(PoolOptions(algorithm=algorithm, initial_difficulty=diff, retarget_seconds=3600,
-                                  payout_address=PROBE_ADDR, listen_v1=""))
-    await pool.start()
-    cfg = Config(bitcoin_address=PROBE_ADDR, pools=[PoolConfig(url=f"stratum+v2://{pool.addr_sv2}")],
+    cfg = Config(bitcoin_address=PROBE_ADDR, pools=[PoolConfig(url=f"stratum+v2://{addr}")],
                  mining=MiningConfig(algorithm=algorithm, batch_nonces=batch_nonces))
     eng = Engine(Options(config=cfg, devices=devs, rate_fetcher=StaticRateSource(95000), stats_interval=1.0))
     task = asyncio.ensure_future(eng.run())
@@ -42,19 +87,69 @@ async def _probe(device_index: int, seconds: float, algorithm: str, shares_per_s
         await task
     except (asyncio.CancelledError, Exception):  # noqa: BLE001
         pass
-    await pool.stop()
-    lat, pipe = eng.latency, eng.pipeline_latency
+    return {"eng": eng}
+
+
+def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm: str = "sha256d",
+                          shares_per_sec: float = 40.0, batch_nonces: int = 1 << 29,
+                          expected_hashrate: float = 19e9) -> dict:
+    hashes_per_diff1 = 2.0 ** 16 if algorithm == "scrypt" else 2.0 ** 32  # scrypt pools: diff1 = 0xFFFF << 224
+    diff = expected_hashrate / (shares_per_sec * hashes_per_diff1)
+    proc, addr = spawn_pool(algorithm, diff)
+    try:
+        eng = asyncio.run(_probe(device_index, seconds, algorithm, addr, batch_nonces))["eng"]
+    finally:
+        pool = stop_pool(proc)
+    lat, pipe, dev = eng.latency, eng.pipeline_latency, eng.device_latency
     return {
         "p50_ms": lat.quantile(0.5), "p95_ms": lat.quantile(0.95), "p99_ms": lat.quantile(0.99),
+        "device_hit_to_accept_p50_ms": dev.quantile(0.5), "device_hit_to_accept_p95_ms": dev.quantile(0.95),
+        "device_hit_to_accept_p99_ms": dev.quantile(0.99),
         "hit_to_accept_p50_ms": pipe.quantile(0.5), "hit_to_accept_p95_ms": pipe.quantile(0.95),
         "accepted": eng.m.shares_accepted.value(), "rejected": eng.m.shares_rejected.value(),
-        "pool_accepted": pool.accepted, "pool_rejected": pool.rejected, "share_difficulty": diff,
-        "batch_nonces": batch_nonces, "seconds": seconds, "protocol": "stratum-v2 (loopback)",
+        "pool_accepted": pool.get("accepted"), "pool_rejected": pool.get("rejected"), "share_difficulty": diff,
+        "batch_nonces": batch_nonces, "seconds": seconds,
+        "protocol": "stratum-v2 over loopback TCP; pool in a separate process (otedama pool)",
         "engine_hashrate": eng.current_hashrate,
     }
 
 
-def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm: str = "sha256d",
-                          shares_per_sec: float = 40.0, batch_nonces: int = 1 << 27,
-                          expected_hashrate: float = 16e9) -> dict:
-    return asyncio.run(_probe(device_index, seconds, algorithm, shares_per_sec, batch_nonces, expected_hashrate))
+def _switch_job(seed: int, algorithm: str) -> dict:
+    import hashlib
+
+    from otedama_amd.models.algorithms import ALGORITHMS
+    from otedama_amd.models.header import int_to_hash
+
+    h = hashlib.sha256(f"otedama-switch-{algorithm}-{seed}".encode()).digest()
+    header = (0x20000000).to_bytes(4, "little") + h + hashlib.sha256(h).digest() + \
+        (1_700_000_000).to_bytes(4, "little") + (0x1703A30C).to_bytes(4, "little") + bytes(4)
+    return {"header": header, "target": int_to_hash(ALGORITHMS[algorithm].diff1), "job_id": f"s{seed}",
+            "epoch": seed + 1, "algo": algorithm, "version_mask": 0x1FFFE000}
+
+
+def measure_job_switch(device_index: int = 0, algorithm: str = "sha256d", switches: int = 8,
+                       dwell: float | None = None, batch_nonces: int = 1 << 29) -> dict:
+    """Hand the native miner new work ``switches`` times and report set_job -> new batch running."""
+    from otedama_amd.ops.native import require_native
+
+    N = require_native()
+    cus = N.gpu_cu_count(device_index) or 256
+    dwell = dwell if dwell is not None else (0.6 if algorithm == "scrypt" else 0.25)
+    m = N.GpuMiner(device_index, f"gpu-{device_index}", batch_nonces=batch_nonces, grid=cus * 6, queue_cap=4096,
+                   sha_variants=128)
+    m.start()
+    try:
+        m.set_job(_switch_job(0, algorithm))
+        time.sleep(max(dwell, 2.0 if algorithm == "scrypt" else 0.5))  # first job: allocations, warm-up
+        for i in range(1, switches + 1):
+            m.set_job(_switch_job(i, algorithm))
+            time.sleep(dwell)
+        st = m.stats()
+    finally:
+        m.stop()
+    samples = list(st["job_switch_ms"])[1:]  # drop the cold first job
+    if st["faulted"]:
+        raise RuntimeError(st["error"])
+    return {"p50_ms": statistics.median(samples) if samples else None, "max_ms": max(samples) if samples else None,
+            "samples_ms": samples, "aborted_launches": st["aborted_launches"], "batch_nonces": batch_nonces,
+            "definition": "set_job(new work) -> first batch of the new work running on the GPU"}

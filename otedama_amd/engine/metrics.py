@@ -66,6 +66,14 @@ class EngineMetrics:
         self.submit_latency_p50 = G("otedama_submit_latency_milliseconds", lat_help, {"quantile": "0.5"})
         self.submit_latency_p95 = G("otedama_submit_latency_milliseconds", lat_help, {"quantile": "0.95"})
         self.submit_latency_p99 = G("otedama_submit_latency_milliseconds", lat_help, {"quantile": "0.99"})
+        hit_help = ("Device hit -> pool accept latency: from the kernel's own hit time (s_memrealtime mapped to the "
+                    "host clock) to the pool's acceptance.")
+        self.hit_latency_p50 = G("otedama_share_hit_to_accept_milliseconds", hit_help, {"quantile": "0.5"})
+        self.hit_latency_p95 = G("otedama_share_hit_to_accept_milliseconds", hit_help, {"quantile": "0.95"})
+        self.hit_latency_p99 = G("otedama_share_hit_to_accept_milliseconds", hit_help, {"quantile": "0.99"})
+        self.job_switch_ms = G("otedama_job_switch_milliseconds",
+                               "Most recent work switch on a GPU: new work handed to the device -> the first batch "
+                               "of it running (obsolete batches stop at the device abort word). Max over devices.")
         self.share_acceptance_rate = G("otedama_share_acceptance_rate",
                                        "Accepted shares / total judged shares (1.0 = all accepted).")
         self.shares_unaccounted = G("otedama_shares_unaccounted",

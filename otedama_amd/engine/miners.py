@@ -185,6 +185,10 @@ class MinerSet:
             out.extend(m.native.poll(max_per_device))
         return out
 
+    def share_fds(self) -> list[int]:
+        """eventfds that turn readable when a device queues a share (native ShareQueue / device process)."""
+        return [m.native.share_fd() for m in self.miners if hasattr(m.native, "share_fd")]
+
     def device_stats(self) -> dict[str, dict]:
         out = {}
         for m in self.miners:

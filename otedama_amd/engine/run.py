@@ -27,6 +27,7 @@ rebalance the rest.
 from __future__ import annotations
 
 import asyncio
+import os
 import sys
 import time
 from dataclasses import dataclass
@@ -62,7 +63,8 @@ RECONNECT_BACKOFF_INITIAL = 1.0
 RECONNECT_BACKOFF_MAX = 64.0
 STREAM_STALE_TIMEOUT = 180.0
 DEFAULT_HYSTERESIS = 0.05
-SHARE_POLL_INTERVAL = 0.005
+SHARE_POLL_INTERVAL = 0.005  # share-queue poll for miner sets without wake-up fds (test fakes)
+SHARE_WAKE_FALLBACK = 0.25   # with eventfds: safety re-poll interval (a missed wake-up costs at most this)
 SUBMIT_KEYS_CAP = 1024  # unacked-submit map bound (internal/engine/run.go:726)
 
 
@@ -138,6 +140,7 @@ class Engine:
         self.curtailed = False
         self.latency = LatencyTracker(256)           # submit -> accept (reference semantics)
         self.pipeline_latency = LatencyTracker(4096)  # host-verified hit -> accept
+        self.device_latency = LatencyTracker(4096)    # the kernel's hit (device clock) -> accept
         self.hash_window = HashrateWindow()
         self.current_hashrate = 0.0
         self.device_hashrates: dict[str, float] = {}
@@ -206,6 +209,8 @@ class Engine:
             "submit_tasks_inflight": len(self._submit_tasks),
             "latency_ms": {"p50": self.latency.quantile(0.5), "p95": self.latency.quantile(0.95),
                            "p99": self.latency.quantile(0.99)},
+            "hit_to_accept_ms": {"p50": self.device_latency.quantile(0.5), "p95": self.device_latency.quantile(0.95),
+                                 "p99": self.device_latency.quantile(0.99)},
             "process": {"threads": _th.active_count(),
                         "max_rss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0},
         }
@@ -571,10 +576,36 @@ class Engine:
             self.log("info", f"engine: job {job.job_id} version=0x{job.version:08X} active")
 
     async def _share_pump(self, session) -> None:
+        """Drain the miners' share queues. Native queues signal an eventfd on every push (loop.add_reader), so a
+        share is picked up within one event-loop turn of being queued instead of a polling interval."""
+        loop = asyncio.get_running_loop()
+        wake = asyncio.Event()
+        fds = list(self.miners.share_fds()) if hasattr(self.miners, "share_fds") else []
+        for fd in fds:
+            loop.add_reader(fd, _ack_eventfd, fd, wake)
+        try:
+            await self._share_pump_loop(session, wake, bool(fds))
+        finally:
+            for fd in fds:
+                try:
+                    loop.remove_reader(fd)
+                except (ValueError, OSError):
+                    pass
+
+    async def _share_pump_loop(self, session, wake: asyncio.Event, has_fds: bool) -> None:
         while True:
             shares = self.miners.poll(256)  # native queue drain; releases the GIL, never blocks
             if not shares:
-                await asyncio.sleep(SHARE_POLL_INTERVAL)
+                wake.clear()
+                shares = self.miners.poll(256)  # re-check after clearing: a push in between is not lost
+            if not shares:
+                if has_fds:
+                    try:
+                        await asyncio.wait_for(wake.wait(), SHARE_WAKE_FALLBACK)
+                    except asyncio.TimeoutError:
+                        pass
+                else:
+                    await asyncio.sleep(SHARE_POLL_INTERVAL)
                 continue
             for s in shares:
                 self.m.shares_found.inc()
@@ -588,11 +619,13 @@ class Engine:
                     continue
                 self._submitted.add(key)
                 sub = ShareSubmission(s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
-                t = asyncio.ensure_future(self._submit(session, sub, s.get("found_at", 0.0)))
+                t = asyncio.ensure_future(self._submit(session, sub, s.get("found_at", 0.0),
+                                                       s.get("device_found_at", 0.0)))
                 self._submit_tasks.add(t)
                 t.add_done_callback(self._submit_tasks.discard)
 
-    async def _submit(self, session, sub: ShareSubmission, found_at: float = 0.0) -> None:
+    async def _submit(self, session, sub: ShareSubmission, found_at: float = 0.0,
+                      device_found_at: float = 0.0) -> None:
         self.m.shares_submitted.inc()
         trace_mark("otd.share.submit")
         try:
@@ -604,8 +637,11 @@ class Engine:
         if res.accepted:
             self.m.shares_accepted.inc()
             self.latency.record(res.latency_ms)
-            if found_at > 0:  # device verify -> pool accept (native queue + submit + pool validation)
-                self.pipeline_latency.record((time.monotonic() - found_at) * 1e3)
+            now = time.monotonic()
+            if found_at > 0:  # host verify -> pool accept (native queue + submit + pool validation)
+                self.pipeline_latency.record((now - found_at) * 1e3)
+            if device_found_at > 0:  # the kernel's hit (s_memrealtime on the host clock) -> pool accept
+                self.device_latency.record((now - device_found_at) * 1e3)
             self.log("info", f"engine: share accepted job={sub.job_id} nonce=0x{sub.nonce:08X} "
                              f"({res.latency_ms:.1f} ms)")
         else:
@@ -667,6 +703,13 @@ class Engine:
         if judged >= 20 and acc_rate < 0.97:
             self.log("warn", f"engine: share acceptance {acc_rate * 100:.1f}% ({self.m.shares_accepted.value()}/"
                              f"{judged}) — check the reject-reason breakdown")
+        if self.device_latency.quantile(0.5) > 0:
+            self.m.hit_latency_p50.set(self.device_latency.quantile(0.5))
+            self.m.hit_latency_p95.set(self.device_latency.quantile(0.95))
+            self.m.hit_latency_p99.set(self.device_latency.quantile(0.99))
+        switches = [float(st.get("last_job_switch_ms", 0.0) or 0.0) for st in dstats.values()]
+        if switches:
+            self.m.job_switch_ms.set(max(switches))
         p95 = self.latency.quantile(0.95)
         if p95 > 0:
             p50, p99 = self.latency.quantile(0.5), self.latency.quantile(0.99)
@@ -696,6 +739,15 @@ class Engine:
                 threads = max(int(st.get("threads", 1) or 1), 1)
                 self.m.set_device_busy(dev, min(max((busy - prev[0]) / (dt * threads), 0.0), 1.0))
             self.m.add_device_launches(dev, launches - prev[2])
+
+
+def _ack_eventfd(fd: int, wake: asyncio.Event) -> None:
+    """add_reader callback: reset the native queue's eventfd and wake the share pump."""
+    try:
+        os.read(fd, 8)
+    except (BlockingIOError, InterruptedError):
+        pass
+    wake.set()
 
 
 def update_stream(streams: dict[str, arb.Stream], q) -> str:

@@ -1,0 +1,155 @@
+"""Native GPU runtime on a real MI355X: in-kernel hit publication, the device abort word, target-only updates.
+
+* Hits reach the host while the launch that found them is still running (host-coherent ring polled by the
+  miner thread), each carrying the kernel's own s_memrealtime stamp mapped to the host clock.
+* New work moves the device abort word: the running batch stops within a grid-stride trip and the switch
+  (set_job -> first batch of the new work running) is timed.
+* A target-only update (same work, SV2 SetTarget / V1 set_difficulty) reaches the share filter at the next launch
+  of the cached variant group (the version-parallel path used to keep the old target for the group).
+Every share is re-hashed on the CPU (hashlib) against the header it claims.
+"""
+import hashlib
+import os
+import struct
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _native():
+    from otedama_amd.ops.native import require_native
+
+    return require_native()
+
+
+def _check_share(hdr: bytes, s: dict, target_int: int, algo: str = "sha256d") -> None:
+    h80 = bytearray(hdr)
+    struct.pack_into("<I", h80, 0, s["version"])
+    struct.pack_into("<I", h80, 76, s["nonce"])
+    if algo == "scrypt":
+        d = hashlib.scrypt(bytes(h80), salt=bytes(h80), n=1024, r=1, p=1, dklen=32)
+    else:
+        d = hashlib.sha256(hashlib.sha256(bytes(h80)).digest()).digest()
+    assert d == s["hash"] and int.from_bytes(d, "little") <= target_int
+
+
+def _job(hdr, target_int, epoch, job_id, **kw):
+    from otedama_amd.models.header import int_to_hash
+
+    return dict({"header": hdr, "target": int_to_hash(target_int), "epoch": epoch, "job_id": job_id,
+                 "version_mask": 0x1FFFE000}, **kw)
+
+
+def test_hits_arrive_while_the_launch_runs():
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    target = (1 << 232) - 1  # ~256 hits per 2^32-hash launch
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32)  # one launch = 2^32 hashes (~0.22 s)
+    m.set_job(_job(hdr, target, 7, "j7"))
+    m.start()
+    try:
+        deadline = time.monotonic() + 10
+        first = []
+        while time.monotonic() < deadline and not first:
+            first = m.poll(256)
+            time.sleep(0.0005)
+        st_first = m.stats()
+        time.sleep(0.6)
+        rest = m.poll(4096)
+    finally:
+        m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert first, st
+    assert st_first["launches"] == 0, st_first  # delivered before any batch completed
+    assert st["ring_hits"] > 0
+    for s in first + rest:
+        _check_share(hdr, s, target)
+        assert s["epoch"] == 7 and s["job_id"] == "j7"
+        # device clock mapped to the host clock: the hit precedes its verification by well under a launch
+        assert 0 < s["device_found_at"] <= s["found_at"] + 0.002, s
+        assert s["found_at"] - s["device_found_at"] < 0.05, s
+    assert st["clock_calib_rtt_us"] > 0
+
+
+def test_new_work_aborts_the_running_batch():
+    N = _native()
+    hdr_a, hdr_b = os.urandom(76) + bytes(4), os.urandom(76) + bytes(4)
+    target = (1 << 236) - 1
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32)  # ~0.22 s launches: a switch without abort waits for two
+    m.set_job(_job(hdr_a, target, 1, "a"))
+    m.start()
+    try:
+        time.sleep(0.5)
+        m.poll(4096)
+        m.set_job(_job(hdr_b, target, 2, "b"))
+        time.sleep(0.05)
+        st_switch = m.stats()
+        time.sleep(0.4)
+        shares = m.poll(4096)
+    finally:
+        m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st_switch["job_switches"] >= 2, st_switch  # the first job and the switch to b
+    assert st_switch["last_job_switch_ms"] < 20.0, st_switch
+    assert st["aborted_launches"] >= 1, st
+    b = [s for s in shares if s["job_id"] == "b"]
+    assert b
+    for s in shares:
+        _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target)
+
+
+def test_target_only_update_reaches_the_running_group():
+    """Same work, easier target, partway through a 128-variant group: shares at the new target appear within a
+    couple of 2^29-nonce launches (the version-parallel variant table stays cached; its target must not)."""
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    hard, easy = (1 << 190) - 1, (1 << 234) - 1
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 29)
+    m.set_job(_job(hdr, hard, 1, "t"))
+    m.start()
+    try:
+        time.sleep(0.4)
+        assert m.poll(256) == []
+        t0 = time.monotonic()
+        m.set_job(_job(hdr, easy, 2, "t"))
+        shares = []
+        while time.monotonic() - t0 < 2.0 and not shares:
+            shares = m.poll(256)
+            time.sleep(0.001)
+        dt = time.monotonic() - t0
+        st = m.stats()
+    finally:
+        m.stop()
+    assert not st["faulted"], st
+    assert shares, st
+    assert dt < 0.2, dt
+    assert st["job_switches"] == 1  # a target-only update is not new work: no abort, no cursor reset
+    for s in shares:
+        _check_share(hdr, s, easy)
+        assert s["epoch"] == 2
+
+
+def test_scrypt_switch_stops_the_romix_batch():
+    N = _native()
+    hdr_a, hdr_b = os.urandom(76) + bytes(4), os.urandom(76) + bytes(4)
+    target = (1 << 244) - 1  # ~256 hits per 1 Mi-hash batch
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 29)
+    m.set_job(_job(hdr_a, target, 1, "a", algo="scrypt"))
+    m.start()
+    try:
+        time.sleep(2.5)  # 128 GiB scratch allocation + first batches
+        m.set_job(_job(hdr_b, target, 2, "b", algo="scrypt"))
+        time.sleep(0.5)
+        shares = m.poll(4096)
+    finally:
+        m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st  # <= about half a ROMix
+    assert st["aborted_launches"] >= 1
+    for s in shares[:40]:
+        _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target, "scrypt")
