@@ -124,7 +124,7 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["faulted"] = s.faulted;
   d["error"] = s.error;
   d["variant_next"] = s.variant_next;
-  d["variant_gen"] = s.variant_gen;
+  d["variant_epoch"] = s.variant_epoch;
   d["job_switches"] = s.job_switches;
   d["last_job_switch_ms"] = s.last_job_switch_ms;
   d["job_switch_ms"] = s.job_switch_ms;

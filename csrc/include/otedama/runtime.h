@@ -78,10 +78,11 @@ struct MinerStats {
   double busy_seconds = 0;           // device (or thread) time spent hashing
   bool faulted = false;              // the device thread died on a HIP error
   std::string error;
-  // Search-space cursor: first variant index of this device's stripe not yet started, for the work generation
-  // `variant_gen` (a re-split after a device / rank loss starts past every cursor so nothing is searched twice).
+  // Search-space cursor: first variant index of this device's stripe not yet started, and the control-plane epoch
+  // of the job it belongs to (a re-split after a device / rank loss starts past every cursor of the current work
+  // so nothing is searched twice).
   uint64_t variant_next = 0;
-  uint64_t variant_gen = 0;
+  uint64_t variant_epoch = 0;
   // Job switches (GPU): set_job() of new work -> the first batch of that work running on the device, in ms.
   uint64_t job_switches = 0;
   double last_job_switch_ms = 0;

@@ -483,7 +483,7 @@ void GpuMiner::loop() {
     const uint64_t group_n = uint64_t(group->nvar);
     if (nonce_off >= (1ull << 32)) { nonce_off = 0; k += group_n; }
     std::lock_guard<std::mutex> g(stats_mu_);
-    stats_.variant_gen = gen;
+    stats_.variant_epoch = job->epoch;
     stats_.variant_next = job->variant_start + (nonce_off == 0 ? k : k + group_n) * job->variant_stride;
   };
 

@@ -397,7 +397,7 @@ void CpuMiner::loop(int /*tid*/) {
       queue_.push(std::move(s));
     }
     std::lock_guard<std::mutex> g(stats_mu_);
-    if (stats_.variant_gen != gen) { stats_.variant_gen = gen; stats_.variant_next = 0; }
+    if (stats_.variant_epoch != job->epoch) { stats_.variant_epoch = job->epoch; stats_.variant_next = 0; }
     if (v + job->variant_stride > stats_.variant_next) stats_.variant_next = v + job->variant_stride;
     stats_.hashes += kChunk;
     stats_.candidates += hits.size();

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import importlib
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -28,7 +29,10 @@ def load(build_if_missing: bool = True):
         # two HSA runtimes in one process cannot both enumerate the GPU.
         # A host without /dev/kfd has no GPU for either runtime to enumerate, so a CPU-only process skips the
         # ~2 s torch import (startup to first hash stays well under the reference's 1 s budget).
-        if os.path.exists("/dev/kfd") or os.environ.get("OTEDAMA_IMPORT_TORCH_FIRST") == "1":
+        # A device process (engine/devproc.py) never imports torch (OTEDAMA_NO_TORCH=1): the extension then binds
+        # to /opt/rocm's runtime alone, and start-up skips torch's ~1-2 s import.
+        no_torch = os.environ.get("OTEDAMA_NO_TORCH") == "1" and "torch" not in sys.modules
+        if not no_torch and (os.path.exists("/dev/kfd") or os.environ.get("OTEDAMA_IMPORT_TORCH_FIRST") == "1"):
             try:
                 import torch  # noqa: F401
             except ImportError:
