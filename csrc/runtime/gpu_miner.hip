@@ -86,6 +86,17 @@ struct Group {
   Sha256dVariant v_table[kSha256dV2Group];
 };
 
+// A published hit handed to the verifier thread (scrypt), with everything needed to rebuild its header.
+struct Candidate {
+  std::shared_ptr<const JobTemplate> job;
+  std::shared_ptr<const Group> group;
+  uint64_t gen;
+  uint32_t nonce, vi, stamp;
+  double enq_host;
+  uint32_t rt_enq;
+  int nvar;
+};
+
 struct Batch {
   bool busy = false;
   std::shared_ptr<const JobTemplate> job;
@@ -286,8 +297,31 @@ void GpuMiner::loop() {
   double switch_t0 = 0;
   double rate_hpms = 0;  // hashes per ms of completed full batches (for aborted-batch accounting)
   std::deque<int> fifo;  // in-flight slots, issue order
+  std::deque<Candidate> vq;  // scrypt candidates awaiting host verification
+  std::mutex vq_mu;
+  std::condition_variable vq_cv;
+  bool vq_stop = false;
+  std::thread verifier;
 
-  auto verify_push = [&](Batch& b, uint32_t nonce, uint32_t vi, uint32_t stamp, bool stamped,
+  // New work or a pause opens a new launch epoch and moves the device abort word: batches of older epochs stop at
+  // their next poll. Called at the top of every loop trip and between hit verifications (a burst of scrypt hits
+  // costs ~1 ms of CPU each and must not delay a switch).
+  auto check_epoch = [&](uint64_t* gen_out) {
+    uint64_t gen = 0;
+    double set_at = 0;
+    auto job = peek_job(&gen, &set_at);
+    const uint64_t want_gen = job ? gen : 0;
+    if (want_gen != epoch_gen) {
+      epoch_gen = want_gen;
+      ++epoch;
+      if (!fifo.empty()) OTD_HIP(hipStreamWriteValue32(ctl, d_abort, epoch, 0));
+      if (job) { switch_pending = true; switch_t0 = set_at; }
+    }
+    if (gen_out) *gen_out = gen;
+    return job;
+  };
+
+  auto verify_push = [&](const Candidate& b, uint32_t nonce, uint32_t vi, uint32_t stamp, bool stamped,
                          const std::shared_ptr<const JobTemplate>& cur, uint64_t cur_g, uint64_t* good,
                          uint64_t* bad) {
     if (vi >= (uint32_t)b.nvar) { ++*bad; return; }
@@ -307,6 +341,38 @@ void GpuMiner::loop() {
     ++*good;
   };
 
+  verifier = std::thread([&] {
+    std::unique_lock<std::mutex> lk(vq_mu);
+    for (;;) {
+      vq_cv.wait(lk, [&] { return vq_stop || !vq.empty(); });
+      if (vq.empty()) return;  // stopping and drained
+      Candidate c = std::move(vq.front());
+      vq.pop_front();
+      lk.unlock();
+      uint64_t good = 0, bad = 0, g = 0;
+      auto cur = peek_job(&g, nullptr);
+      verify_push(c, c.nonce, c.vi, c.stamp, true, cur, g, &good, &bad);
+      {
+        std::lock_guard<std::mutex> sg(stats_mu_);
+        stats_.shares += good;
+        stats_.rejected_candidates += bad;
+      }
+      lk.lock();
+    }
+  });
+  struct VerifierJoin {
+    std::function<void()> f;
+    ~VerifierJoin() { f(); }
+  } verifier_join{[&] {
+    {
+      std::lock_guard<std::mutex> g(vq_mu);
+      vq_stop = true;
+      if (!running_.load() && vq.size() > 64) vq.resize(64);  // shutting down: bound the work left (~1 ms each)
+    }
+    vq_cv.notify_all();
+    if (verifier.joinable()) verifier.join();
+  }};
+
   // Consume the published records of a batch; `final_n` = the batch's final count (after completion) or ~0u
   // while it runs. Returns the number of records handled.
   auto drain_ring = [&](Batch& b, uint32_t final_n, const std::shared_ptr<const JobTemplate>& cur,
@@ -325,7 +391,16 @@ void GpuMiner::loop() {
       const uint32_t nonce = __atomic_load_n(&r->nonce, __ATOMIC_RELAXED);
       const uint32_t vi = __atomic_load_n(&r->variant, __ATOMIC_RELAXED);
       const uint32_t stamp = __atomic_load_n(&r->stamp, __ATOMIC_RELAXED);
-      verify_push(b, nonce, vi, stamp, true, cur, cur_g, &good, &bad);
+      if (b.job->algo == Algo::kScrypt) {
+        // host scrypt costs ~1 ms per candidate: verified on the verifier thread so a burst of candidates never
+        // holds up a job switch or the next launch
+        std::lock_guard<std::mutex> g(vq_mu);
+        vq.push_back(Candidate{b.job, b.group, b.gen, nonce, vi, stamp, b.enq_host, b.rt_enq, b.nvar});
+        vq_cv.notify_one();
+      } else {
+        verify_push(Candidate{b.job, b.group, b.gen, 0, 0, 0, b.enq_host, b.rt_enq, b.nvar}, nonce, vi, stamp, true,
+                    cur, cur_g, &good, &bad);
+      }
       ++b.consumed;
       ++handled;
     }
@@ -489,17 +564,8 @@ void GpuMiner::loop() {
 
   while (running_.load()) {
     uint64_t gen = 0;
-    double set_at = 0;
-    auto job = peek_job(&gen, &set_at);
+    auto job = check_epoch(&gen);
     bool progressed = false;
-    // New work or a pause opens a new launch epoch; batches of older epochs stop at their next abort poll.
-    const uint64_t want_gen = job ? gen : 0;
-    if (want_gen != epoch_gen) {
-      epoch_gen = want_gen;
-      ++epoch;
-      if (!fifo.empty()) OTD_HIP(hipStreamWriteValue32(ctl, d_abort, epoch, 0));
-      if (job) { switch_pending = true; switch_t0 = set_at; }
-    }
     if (job && gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
     // 1) hits of the batches in flight, oldest first
     for (int i : fifo) progressed |= drain_ring(slots[i], ~0u, job, gen) > 0;

@@ -9,14 +9,21 @@ variant stripe) and drains the native share queues.
 Reference defect fixed: every device gets a disjoint slice of the search space
 instead of the identical Work (engine/run.go:1294-1296).
 
+Isolation (``isolation="process"``, the default for GPUs in ``otedama run``):
+every device runs in a child process of its own (engine/devproc.py), so a
+kernel fault that aborts a process takes one device down, not the node.
+
 Device faults (the reference has no GPU path and a dead worker
-goroutine just stops contributing): a GpuMiner whose host thread died on a HIP
-error is retired by ``retire_faulted()`` and the rank's variant class is
-re-split among the surviving devices (parallel/partition.py). The new stripes
-take effect with the next *new* work: switching stripes mid-job would restart
-the survivors' cursors over variants they already searched and re-submit
-duplicate shares. Per-device stalls (a live device with work whose hash counter
-stopped moving for ``stall_samples`` ticks) are reported by ``stalled()``.
+goroutine just stops contributing): a device whose miner died (HIP error in its
+host thread, or its process exited) is retired and the rank's variant class is
+re-split among the survivors AT ONCE, starting past the high-water mark of every
+device's cursor on the current work (the native miners report the next variant
+they have not started, tagged with the job epoch), so the dead device's residue
+class keeps being searched and nothing is searched twice. A dead device process
+is replaced after a backoff (1 s doubling to 64 s, internal/engine/run.go:56-63);
+when the fresh process reports in, the stripes are re-split again to include it.
+Per-device stalls (a live device with work whose hash counter stopped moving for
+``stall_samples`` ticks) are reported by ``stalled()``.
 """
 from __future__ import annotations
 
@@ -30,6 +37,13 @@ from otedama_amd.parallel.partition import stripe_for
 
 # Template keys that do not change the search space (same as the native same_work()).
 _NOT_WORK = frozenset({"target", "job_id", "epoch", "channel_id", "variant_start", "variant_stride"})
+RESPAWN_BACKOFF_INITIAL = 1.0
+RESPAWN_BACKOFF_MAX = 64.0
+RESPAWN_HEALTHY_RESET = 60.0  # a process that ran this long resets its backoff
+# Re-split margin in variant groups: a device may start one more 128-variant group between its last cursor report
+# and the re-split, so the new base clears every reported cursor by two groups of the old stride.
+RESPLIT_GROUPS = 2
+GROUP = 128
 
 
 def _work_key(t: dict | None):
@@ -48,6 +62,8 @@ class DeviceMiner:
     hashrate: float = 0.0
     idle_samples: int = 0  # consecutive stats ticks with work but no hash progress
     extra: dict = field(default_factory=dict)
+    backoff: float = RESPAWN_BACKOFF_INITIAL
+    respawn_timer: threading.Timer | None = None
 
     @property
     def id(self) -> str:
@@ -57,28 +73,53 @@ class DeviceMiner:
 class MinerSet:
     def __init__(self, devices: list, algorithm: str = "sha256d", batch_nonces: int = 1 << 29,
                  cpu_threads: int = 0, rank: int = 0, world_size: int = 1, log=None, queue_cap: int = 4096,
-                 stall_samples: int = 3, sha_variants: int = 128):
+                 stall_samples: int = 3, sha_variants: int = 128, isolation: str = "thread"):
+        if isolation not in ("thread", "process"):
+            raise ValueError("isolation must be 'thread' or 'process'")
         N = require_native()
+        self.N = N
         self.algorithm = algorithm
+        self.isolation = isolation
         self.log = log or (lambda level, msg: None)
         self.miners: list[DeviceMiner] = []
+        self._lock = threading.RLock()
+        self._stopped = False
         gpus = [d for d in devices if d.identity().family == Family.GPU and d.index >= 0
                 and d.capabilities().supports(algorithm)]
         for d in gpus:
             cus = int(d.extra.get("cus", 256))
-            m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6, queue_cap=queue_cap,
-                           sha_variants=sha_variants)
+            if isolation == "process":
+                from otedama_amd.engine.devproc import DeviceProcess
+
+                m = DeviceProcess(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6,
+                                  queue_cap=queue_cap, sha_variants=sha_variants, log=self.log,
+                                  on_exit=self._on_process_exit, on_ready=self._on_process_ready)
+            else:
+                m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6, queue_cap=queue_cap,
+                               sha_variants=sha_variants)
             self.miners.append(DeviceMiner(d, m))
         cpus = [d for d in devices if d.identity().family == Family.CPU]
         if cpus and algorithm == "sha256d" and (cpu_threads > 0 or not gpus):
-            threads = cpu_threads or cpus[0].threads
-            self.miners.append(DeviceMiner(cpus[0], N.CpuMiner(threads, cpus[0].identity().id, queue_cap),
-                                           extra={"threads": max(int(threads or 1), 1)}))
+            if isolation == "process":
+                # one process per CPU device (production has one, cpu-0; tests model several devices this way)
+                from otedama_amd.engine.devproc import DeviceProcess
+
+                for d in cpus:
+                    threads = max(int(cpu_threads or d.threads or 1), 1)
+                    m = DeviceProcess(-1, d.identity().id, queue_cap=queue_cap, cpu_threads=threads, log=self.log,
+                                      on_exit=self._on_process_exit, on_ready=self._on_process_ready)
+                    self.miners.append(DeviceMiner(d, m, extra={"threads": threads}))
+            else:
+                threads = cpu_threads or cpus[0].threads
+                self.miners.append(DeviceMiner(cpus[0], N.CpuMiner(threads, cpus[0].identity().id, queue_cap),
+                                               extra={"threads": max(int(threads or 1), 1)}))
         self.rank, self.world_size = rank, world_size
         self.stall_samples = max(1, stall_samples)
         self._restripe_pending = False
+        self._variant_base = 0   # local re-split offset on top of the template's (node-level) variant_base
+        self._work_epoch0 = 0    # first epoch of the current work (cursor reports older than this are ignored)
+        self.resplits = 0
         self._restripe()
-        self._lock = threading.Lock()
         self._epoch = 0
         self._template: dict | None = None
         self._t_last = time.monotonic()
@@ -102,8 +143,21 @@ class MinerSet:
             m.native.start()
 
     def stop(self) -> None:
+        with self._lock:
+            self._stopped = True
+            for m in self.miners:
+                if m.respawn_timer is not None:
+                    m.respawn_timer.cancel()
         for m in self.miners:
             m.native.stop()
+
+    def set_rank(self, rank: int, world_size: int) -> None:
+        """Node re-formed (parallel/node.py): this rank's residue class changed. Takes effect with the next
+        set_job (the node leader re-sends the job, with a fresh variant_base, right after a re-form)."""
+        with self._lock:
+            self.rank, self.world_size = rank, world_size
+            self._variant_base = 0
+            self._restripe()
 
     def set_job(self, template: dict | None, epoch: int | None = None) -> int:
         """Hand a job template to every non-paused device; returns the new epoch.
@@ -112,10 +166,14 @@ class MinerSet:
         with self._lock:
             self._epoch = epoch if epoch is not None else self._epoch + 1
             new = dict(template) if template is not None else None
-            if self._restripe_pending and new is not None and _work_key(new) != _work_key(self._template):
-                self._restripe()
-                self._restripe_pending = False
-                self.log("info", f"miners: variant stripes re-split over {len(self.live())} live device(s)")
+            if new is not None and _work_key(new) != _work_key(self._template):
+                # new work: cursors restart, the local re-split offset is void
+                self._work_epoch0 = self._epoch
+                self._variant_base = 0
+                if self._restripe_pending:
+                    self._restripe()
+                    self._restripe_pending = False
+                    self.log("info", f"miners: variant stripes re-split over {len(self.live())} live device(s)")
             self._template = new
             for m in self.miners:
                 self._apply(m)
@@ -128,20 +186,115 @@ class MinerSet:
             m.native.set_job(None)
             return
         t = dict(self._template)
+        node_base = int(t.pop("variant_base", 0) or 0)
         t["epoch"] = self._epoch
-        t["variant_start"] = m.stripe_index
+        t["variant_start"] = node_base + self._variant_base + m.stripe_index
         t["variant_stride"] = m.stripe_stride
         m.native.set_job(t)
 
     def live(self) -> list[DeviceMiner]:
         return [m for m in self.miners if not m.retired]
 
-    def retire_faulted(self) -> list[tuple[str, str]]:
-        """Retire devices whose native thread died; returns the newly retired ``(id, error)``.
+    # ------------------------------------------------------------------ faults and re-splits
+    def high_water(self) -> int:
+        """Highest 'next unstarted variant' reported by any device (live or dead) for the current work."""
+        hw = 0
+        for m in self.miners:
+            try:
+                st = m.native.stats()
+            except Exception:  # noqa: BLE001
+                continue
+            if int(st.get("variant_epoch", -1)) >= self._work_epoch0 > 0:
+                hw = max(hw, int(st.get("variant_next", 0)))
+        return hw
 
-        The survivors take over the retired stripes at the next new work (see module doc)."""
+    def _resplit_now(self, why: str) -> None:
+        """Re-split this rank's class over the live devices past every cursor of the current work, and re-issue
+        the work at once (caller holds the lock). Falls back to a re-split at the next new work when the jump
+        does not fit in the job's variant space."""
+        live = self.live()
+        old = [(m.stripe_index, m.stripe_stride) for m in self.miners]
+        old_stride = max((st for _, st in old), default=1)
+        self._restripe()
+        if self._template is None or not live:
+            self._restripe_pending = False
+            return
+        t = self._template
+        node_base = int(t.get("variant_base", 0) or 0)
+        hw = self.high_water()
+        base = max(hw - node_base, 0) + RESPLIT_GROUPS * GROUP * old_stride
+        probe = {k: v for k, v in t.items() if k != "variant_base"}
+        try:
+            space = int(self.N.variant_space(probe))
+        except Exception:  # noqa: BLE001 - a template the native side cannot parse: keep the deferred path
+            space = 0
+        if node_base + base + self.stripe_total > space:
+            for m, (i, st) in zip(self.miners, old):  # keep the running stripes until the next new work
+                m.stripe_index, m.stripe_stride = i, st
+            self._restripe_pending = True
+            self.log("warn", f"miners: {why}; variant space exhausted for an immediate re-split, the "
+                             f"{len(live)} live device(s) take the new stripes with the next work")
+            return
+        self._variant_base = base
+        self._restripe_pending = False
+        self.resplits += 1
+        for m in self.miners:
+            self._apply(m)
+        self.log("info", f"miners: {why}; {len(live)} live device(s) re-split from variant {node_base + base}")
+
+    def _on_process_exit(self, dp) -> None:
+        """A device process died (reader thread): retire its device, re-split, schedule a fresh process."""
+        with self._lock:
+            if self._stopped:
+                return
+            for m in self.miners:
+                if m.native is dp and not m.retired:
+                    m.retired = True
+                    m.hashrate = 0.0
+                    self._resplit_now(f"device {m.id} lost ({dp.error})")
+                    self._schedule_respawn(m)
+
+    def _schedule_respawn(self, m: DeviceMiner) -> None:
+        if m.respawn_timer is not None:
+            m.respawn_timer.cancel()
+        ready_at = getattr(m.native, "ready_at", 0.0)
+        if ready_at and time.monotonic() - ready_at >= RESPAWN_HEALTHY_RESET:
+            m.backoff = RESPAWN_BACKOFF_INITIAL
+        delay = m.backoff
+        m.backoff = min(m.backoff * 2, RESPAWN_BACKOFF_MAX)
+        m.respawn_timer = threading.Timer(delay, self._respawn, args=(m,))
+        m.respawn_timer.daemon = True
+        m.respawn_timer.start()
+        self.log("info", f"miners: restarting {m.id} in {delay:.0f}s")
+
+    def _respawn(self, m: DeviceMiner) -> None:
+        with self._lock:
+            if self._stopped or not m.retired:
+                return
+        try:
+            m.native.restart()
+        except Exception as exc:  # noqa: BLE001
+            self.log("error", f"miners: restart of {m.id} failed: {exc}")
+            with self._lock:
+                self._schedule_respawn(m)
+
+    def _on_process_ready(self, dp) -> None:
+        """A (re)spawned device process is mining: bring its device back into the stripe plan."""
+        with self._lock:
+            if self._stopped:
+                return
+            for m in self.miners:
+                if m.native is dp and m.retired:
+                    m.retired = False
+                    m.idle_samples = 0
+                    self._resplit_now(f"device {m.id} back (process restart {dp.restarts})")
+
+    def retire_faulted(self) -> list[tuple[str, str]]:
+        """Retire devices whose native thread died; returns the newly retired ``(id, error)``. The survivors take
+        over the retired stripes at once (see module doc); a device process is also restarted."""
         out = []
         with self._lock:
+            newly = []
             for m in self.miners:
                 if m.retired:
                     continue
@@ -149,13 +302,20 @@ class MinerSet:
                 if st["faulted"]:
                     m.retired = True
                     m.hashrate = 0.0
-                    m.native.stop()
+                    if not hasattr(m.native, "restart"):
+                        m.native.stop()
                     out.append((m.id, st["error"]))
+                    newly.append(m)
             if out:
-                self._restripe_pending = True
                 live = len(self.live())
                 for dev, err in out:
                     self.log("error", f"miners: device {dev} faulted ({err}); retired, {live} device(s) left")
+                self._resplit_now(", ".join(f"device {d} faulted" for d, _ in out))
+                for m in newly:
+                    if hasattr(m.native, "restart"):
+                        if getattr(m.native, "alive", False):
+                            m.native.kill()  # a faulted context is unusable: replace the process
+                        self._schedule_respawn(m)
         return out
 
     def stalled(self) -> list[str]:

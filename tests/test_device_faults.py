@@ -1,8 +1,10 @@
 """GPU-fault handling and per-device stall detection.
 
 A faulted device is retired and its rank's variant class (parallel/partition.py) is re-split among
-the survivors at the next NEW work, never mid-job (that would re-search variants and re-submit
-duplicates). A live device with work whose hash counter stops is reported as stalled."""
+the survivors at once, starting past the high-water mark of every device's cursor on the current work
+(never re-searching a variant, so no duplicate shares); when that jump does not fit in the job's
+variant space the re-split waits for the next NEW work. A live device with work whose hash counter
+stops is reported as stalled."""
 from types import SimpleNamespace
 
 import pytest
@@ -15,6 +17,7 @@ from otedama_amd.parallel.partition import stripe_for
 class FakeNative:
     def __init__(self):
         self.jobs, self.hashes, self.fault, self.stopped = [], 0, "", False
+        self.cursor = (0, 0)  # (variant_next, variant_epoch) as the native miners report them
 
     def start(self):
         pass
@@ -30,7 +33,7 @@ class FakeNative:
 
     def stats(self):
         return {"hashes": self.hashes, "shares": 0, "dropped": 0, "faulted": bool(self.fault), "error": self.fault,
-                "candidates": 0, "launches": 0}
+                "candidates": 0, "launches": 0, "variant_next": self.cursor[0], "variant_epoch": self.cursor[1]}
 
 
 def _dev(name):
@@ -38,14 +41,17 @@ def _dev(name):
 
 
 def _set(n, rank=0, world=1, log=None):
+    from otedama_amd.ops.native import require_native
+
     ms = MinerSet.__new__(MinerSet)
     ms.algorithm, ms.log = "sha256d", log or (lambda lvl, msg: None)
+    ms.N, ms._variant_base, ms._work_epoch0, ms.resplits, ms._stopped = require_native(), 0, 0, 0, False
     ms.miners = [DeviceMiner(_dev(f"gpu{i}"), FakeNative()) for i in range(n)]
     ms.rank, ms.world_size, ms.stall_samples, ms._restripe_pending = rank, world, 3, False
     ms._restripe()
     import threading
     import time
-    ms._lock, ms._epoch, ms._template, ms._t_last = threading.Lock(), 0, None, time.monotonic()
+    ms._lock, ms._epoch, ms._template, ms._t_last = threading.RLock(), 0, None, time.monotonic()
     return ms
 
 
@@ -75,6 +81,7 @@ def _tmpl(prev=b"\x01", target="ff" * 32, job="j1"):
 
 
 def test_faulted_device_retired_and_stripe_resplit_on_next_new_work():
+    """A template whose variant space cannot take the jump (here: not even parseable) defers the re-split."""
     logs = []
     ms = _set(3, log=lambda lvl, msg: logs.append((lvl, msg)))
     ms.set_job(_tmpl())
@@ -128,3 +135,39 @@ def test_engine_metrics_track_device_health():
     m.devices_faulted.set(1)
     assert m.devices_active.value() == 7 and m.devices_faulted.value() == 1
     assert miners_mod._work_key(_tmpl(target="00" * 32)) == miners_mod._work_key(_tmpl())
+
+
+def _real_tmpl(prev=b"\x01", target=b"\xff" * 32, job="j1", mask=0x1FFFE000):
+    return {"algo": "sha256d", "header": (prev * 80)[:80], "target": target, "job_id": job, "version_mask": mask}
+
+
+def test_fault_resplits_at_once_past_every_cursor():
+    """Real template (2^16 BIP320 variants): the survivors get the whole class immediately, starting past the
+    highest cursor any device reported (dead one included) plus two 128-variant groups of the old stride."""
+    ms = _set(3)
+    ep = ms.set_job(_real_tmpl())
+    assert [(j["variant_start"], j["variant_stride"]) for j in (m.native.jobs[-1] for m in ms.miners)] == \
+        [(0, 3), (1, 3), (2, 3)]
+    # cursors: gpu0 started variants 0,3 (next 6); gpu1 up to 7 (next 10, then died); gpu2 next 5
+    ms.miners[0].native.cursor, ms.miners[1].native.cursor, ms.miners[2].native.cursor = (6, ep), (10, ep), (5, ep)
+    ms.miners[1].native.fault = "device process killed by signal 9"
+    assert [d for d, _ in ms.retire_faulted()] == ["gpu1"]
+    base = 10 + 2 * 128 * 3
+    survivors = [m.native.jobs[-1] for m in (ms.miners[0], ms.miners[2])]
+    assert [(j["variant_start"], j["variant_stride"]) for j in survivors] == [(base, 2), (base + 1, 2)]
+    assert ms.resplits == 1
+    # the dead device's residue class (1 mod 3) is covered going forward, and nothing below base repeats
+    covered = sorted(v for j in survivors for v in range(j["variant_start"], base + 600, j["variant_stride"]))
+    assert covered == list(range(base, base + 600))
+    # cursors of an older job epoch are ignored: new work restarts from 0
+    ms.miners[0].native.cursor = (9000, ep)
+    ep2 = ms.set_job(_real_tmpl(prev=b"\x02", job="j2"))
+    assert ep2 > ep and [m.native.jobs[-1]["variant_start"] for m in (ms.miners[0], ms.miners[2])] == [0, 1]
+
+
+def test_node_variant_base_adds_to_the_local_resplit():
+    ms = _set(2, rank=1, world=4)
+    ms.set_job(dict(_real_tmpl(), variant_base=4096))
+    assert [(m.native.jobs[-1]["variant_start"], m.native.jobs[-1]["variant_stride"]) for m in ms.miners] == \
+        [(4096 + 1, 8), (4096 + 5, 8)]
+    assert "variant_base" not in ms.miners[0].native.jobs[-1]

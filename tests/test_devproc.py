@@ -1,0 +1,104 @@
+"""One process per device (engine/devproc.py) on the CPU: the same parent/child protocol, re-split and respawn
+path as the GPU processes, with native CpuMiner children (a dead device must not stop the
+node). A child is SIGKILLed mid-job: within ~2 s the survivors are re-striped past every cursor so the dead
+device's residue class keeps being searched, verified shares keep flowing, a fresh process replaces the dead one
+and rejoins the stripe plan, and nothing hangs."""
+import os
+import signal
+import time
+
+import pytest
+
+from otedama_amd import hal
+from otedama_amd.engine.miners import MinerSet
+from otedama_amd.models.header import int_to_hash, sha256d
+
+
+def _devs(n):
+    return [hal.SimpleDevice(hal.Identity(f"cpu-{i}", hal.Family.CPU, "t", "cpu"),
+                             hal.Capabilities(sha256d=True, general_compute=True), threads=1) for i in range(n)]
+
+
+def _job():
+    hdr = bytes([1, 0, 0, 0]) + bytes(range(32)) + bytes(range(32, 64)) + (1700000000).to_bytes(4, "little") + \
+        bytes.fromhex("ffff001d") + bytes(4)
+    return {"header": hdr, "target": int_to_hash(1 << 241), "job_id": "job-A", "algo": "sha256d",
+            "version_mask": 0x1FFFE000}
+
+
+def _verify(s):
+    hdr = bytearray(_job()["header"])
+    hdr[0:4] = int(s["version"]).to_bytes(4, "little")
+    hdr[76:80] = int(s["nonce"]).to_bytes(4, "little")
+    return int.from_bytes(sha256d(bytes(hdr)), "little") <= 1 << 241
+
+
+def _wait(pred, timeout):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if pred():
+            return True
+        time.sleep(0.02)
+    return pred()
+
+
+def test_sigkilled_device_process_is_resplit_and_replaced():
+    logs = []
+    ms = MinerSet(_devs(4), "sha256d", isolation="process", log=lambda lvl, msg: logs.append((lvl, msg)))
+    ms.start()
+    shares = []
+    try:
+        assert _wait(lambda: all(m.native.ready_at > 0 for m in ms.miners), 60), logs
+        ep = ms.set_job(_job())
+        assert _wait(lambda: len({s["device_id"] for s in (shares.extend(ms.poll(256)) or shares)}) == 4, 60)
+        victim = ms.miners[2]
+        old_pid = victim.native.pid
+        # cursors are reported at 2 Hz; wait for one with the current epoch
+        assert _wait(lambda: victim.native.stats().get("variant_epoch", 0) >= ep, 5)
+        hw_before = ms.high_water()
+        t_kill = time.monotonic()
+        os.kill(old_pid, signal.SIGKILL)
+        assert _wait(lambda: victim.retired and ms.resplits >= 1, 2.0), logs
+        t_resplit = time.monotonic() - t_kill
+        assert t_resplit < 2.0
+        # survivors: stride 3, starting past every cursor (the dead device's class is covered from there on)
+        jobs = [m.native._job for m in ms.miners if m is not victim]
+        starts = sorted(j["variant_start"] for j in jobs)
+        assert all(j["variant_stride"] == 3 for j in jobs)
+        assert starts == [starts[0], starts[0] + 1, starts[0] + 2] and starts[0] > hw_before
+        assert victim.native.stats()["faulted"]
+        # verified shares keep flowing from the survivors
+        n0 = len(shares)
+        assert _wait(lambda: len(shares.extend(ms.poll(256)) or shares) >= n0 + 6, 20)
+        # the replacement process (backoff 1 s) reports in and is re-striped back in
+        assert _wait(lambda: not victim.retired, 20), logs
+        assert victim.native.pid != old_pid and victim.native.restarts == 1
+        assert _wait(lambda: ms.resplits >= 2, 5)
+        jobs = [m.native._job for m in ms.miners]
+        assert all(j["variant_stride"] == 4 for j in jobs)
+        n1 = len(shares)
+        assert _wait(lambda: any(s["device_id"] == "cpu-2" for s in (shares.extend(ms.poll(256)) or shares)[n1:]), 30)
+    finally:
+        t0 = time.monotonic()
+        ms.stop()
+        assert time.monotonic() - t0 < 15  # nothing hangs
+    assert shares and all(_verify(s) for s in shares)
+    assert all(s["job_id"] == "job-A" for s in shares)
+    assert any("lost" in m for _, m in logs) and any("back" in m for _, m in logs)
+
+
+def test_device_process_startup_and_counters_survive_restart():
+    ms = MinerSet(_devs(1), "sha256d", isolation="process")
+    ms.start()
+    try:
+        dp = ms.miners[0].native
+        assert _wait(lambda: dp.ready_at > 0, 60)
+        assert 0 < dp.startup_seconds < 30
+        ms.set_job(_job())
+        assert _wait(lambda: dp.stats()["hashes"] > 0, 20)
+        h = dp.stats()["hashes"]
+        dp.kill(signal.SIGKILL)
+        assert _wait(lambda: not ms.miners[0].retired and dp.restarts == 1 and dp.alive, 20)
+        assert dp.stats()["hashes"] >= h  # cumulative across the restart
+    finally:
+        ms.stop()

@@ -136,7 +136,7 @@ def test_target_only_update_reaches_the_running_group():
 def test_scrypt_switch_stops_the_romix_batch():
     N = _native()
     hdr_a, hdr_b = os.urandom(76) + bytes(4), os.urandom(76) + bytes(4)
-    target = (1 << 244) - 1  # ~256 hits per 1 Mi-hash batch
+    target = (1 << 240) - 1  # ~16 hits per 1 Mi-hash batch
     m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 29)
     m.set_job(_job(hdr_a, target, 1, "a", algo="scrypt"))
     m.start()
@@ -149,7 +149,7 @@ def test_scrypt_switch_stops_the_romix_batch():
         m.stop()
     st = m.stats()
     assert not st["faulted"], st
-    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st  # <= about half a ROMix
+    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st  # polls at every quarter of the ROMix
     assert st["aborted_launches"] >= 1
     for s in shares[:40]:
         _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target, "scrypt")

@@ -3,7 +3,7 @@
 # smoke and the N=1 bench (hashrates must hold within noise of profiles/r3/a_first).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/${R3_TAG:-r3c}
+O=gpurun_out/${R3_TAG:-r3d}
 mkdir -p $O
 export TMPDIR=/tmp
 export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
