@@ -12,6 +12,7 @@ from otedama_amd.cli.main import EXIT_OK, EXIT_USAGE
 SHELLS = ("bash", "zsh", "fish")
 COMMANDS = {
     "run": "Start mining on MI355X GPUs / CPU",
+    "node": "Run one rank per GPU (fault-tolerant RCCL node)",
     "pool": "Run the local Stratum pool",
     "bench": "Measure hash rates",
     "devices": "List mining devices",

@@ -32,6 +32,7 @@ Usage:
 
 Commands:
   run        Start mining (gfx950 GPUs + CPU) against the configured pools.
+  node       Run one rank per GPU under a fault-tolerant supervisor (RCCL node).
   pool       Run the local Stratum V1/V2 pool (share validation, vardiff).
   bench      Measure hash rates (sha256d / scrypt, CPU and GPU).
   devices    List detected mining devices.
@@ -237,7 +238,7 @@ def cmd_version(args, stdout, stderr) -> int:
 
 
 # ------------------------------------------------------------------ dispatcher
-COMMANDS = ("run", "pool", "bench", "devices", "version", "config", "service", "doctor", "completion", "help")
+COMMANDS = ("run", "node", "pool", "bench", "devices", "version", "config", "service", "doctor", "completion", "help")
 
 
 def run(args: list[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr) -> int:
@@ -249,6 +250,10 @@ def run(args: list[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stder
         from otedama_amd.cli.run_cmd import cmd_run
 
         return cmd_run(rest, stdout, stderr)
+    if cmd == "node":
+        from otedama_amd.cli.node_cmd import cmd_node
+
+        return cmd_node(rest, stdout, stderr)
     if cmd == "pool":
         from otedama_amd.cli.pool_cmd import cmd_pool
 

@@ -100,16 +100,23 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         return EXIT_OK
     node = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # torchrun node mode: one rank per GPU; rank 0 is the pool-facing engine
-        from otedama_amd.parallel.comm import NodeComm, init_from_env
+        # node mode (otedama node / torchrun): one rank per GPU; rank 0 is the pool-facing engine. A rank the
+        # supervisor restarted after a loss joins the running node instead of forming it.
+        from otedama_amd.parallel.comm import NodeComm, init_from_env, join_from_env
 
-        info = init_from_env()
+        joining = os.environ.get("OTEDAMA_NODE_JOIN") == "1"
+        if joining and int(os.environ.get("RANK", "0")) == 0:
+            stderr.write("otedama run: rank 0 cannot join a node (it forms it)\n")
+            return EXIT_CONFIG
+        info = join_from_env() if joining else init_from_env()
         # the rank's HIP ordinal (init_from_env maps local ranks onto the visible GPUs; on an 8-GPU node it is the
         # local rank, on a 1-GPU rehearsal over gloo every rank shares GPU 0)
         cfg.mining.gpus = str(info.device.index if info.device.type == "cuda" else info.local_rank)
-        cfg.mining.cpu_threads = 0  # equal device count per rank keeps the stripes disjoint
-        if info.rank > 0:
-            return _run_node_worker(cfg, info, NodeComm(info), stdout)
+        # equal device count per rank keeps the stripes disjoint: the rank's GPU, or (a CPU-only rehearsal node over
+        # gloo) one CPU miner per rank
+        cfg.mining.cpu_threads = 0 if info.device.type == "cuda" else max(1, cfg.mining.cpu_threads)
+        if info.orig_rank > 0:
+            return _run_node_worker(cfg, info, NodeComm(info), stdout, joining)
         node = NodeComm(info)
         no_tui = True
     logln("info", i18n.STARTUP_READY)
@@ -127,22 +134,26 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
             shutdown(node.info)
 
 
-def _run_node_worker(cfg, info, comm, stdout) -> int:
-    """Ranks > 0 of a torchrun node: mine rank 0's jobs on the local GPU until rank 0 stops."""
+def _run_node_worker(cfg, info, comm, stdout, joining: bool = False) -> int:
+    """Ranks > 0 of a node: mine rank 0's jobs on the local GPU until rank 0 stops."""
     from otedama_amd import hal
     from otedama_amd.engine.miners import MinerSet
     from otedama_amd.parallel.comm import shutdown
     from otedama_amd.parallel.node import NodeWorker
 
-    devs = hal.Detector(hal.default_registry(0)).detect()
-    gpu = info.device.index if info.device.type == "cuda" else info.local_rank
-    devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == gpu]
-    local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0, rank=info.rank,
-                     world_size=info.world_size, sha_variants=cfg.mining.sha_variants)
-    stdout.write(f"[info] node: rank {info.rank}/{info.world_size} mining on GPU {gpu} "
-                 f"({len(local)} device(s))\n")
+    on_gpu = info.device.type == "cuda"
+    devs = hal.Detector(hal.default_registry(cfg.mining.cpu_threads)).detect()
+    gpu = info.device.index if on_gpu else info.local_rank
+    if on_gpu:
+        devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == gpu]
+    else:  # CPU-only rehearsal node: this rank's CPU miner
+        devs = [d for d in devs if d.identity().family == hal.Family.CPU]
+    local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0 if on_gpu else cfg.mining.cpu_threads,
+                     rank=max(info.rank, 0), world_size=max(info.world_size, 1), sha_variants=cfg.mining.sha_variants)
+    stdout.write(f"[info] node: rank {info.orig_rank} {'joining' if joining else f'of {info.world_size}'} mining on "
+                 f"GPU {gpu} ({len(local)} device(s))\n")
     try:
-        NodeWorker(local, comm).run()
+        NodeWorker(local, comm, log=lambda lvl, msg: stdout.write(f"[{lvl}] {msg}\n"), joining=joining).run()
     finally:
         shutdown(info)
     return EXIT_OK

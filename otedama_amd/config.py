@@ -72,6 +72,8 @@ class MiningConfig:
     ntime_roll: int = 0
     sha_variants: int = 128             # SHA-256d header variants per GPU launch: 128 / 64 (version-parallel, two or
                                         # one per lane), 1..16 (K variants per lane; 1 = single midstate)
+    isolation: str = "process"          # GPUs: "process" = one device process per GPU (a GPU fault stops one device,
+                                        # the engine stays GPU-free); "thread" = every GPU's miner in this process
 
 
 @dataclass
@@ -156,6 +158,8 @@ class Config:
             issues.append("mining.batch_nonces must be in [65536, 2^32]")
         if self.mining.sha_variants not in (64, 128) and not 1 <= self.mining.sha_variants <= 16:
             issues.append(f"mining.sha_variants {self.mining.sha_variants} must be 128, 64 or 1..16")
+        if self.mining.isolation not in ("process", "thread"):
+            issues.append(f"mining.isolation {self.mining.isolation!r} must be process or thread")
         if self.pool_server.initial_difficulty <= 0:
             issues.append("pool_server.initial_difficulty must be > 0")
         if self.pool_server.target_share_seconds <= 0:

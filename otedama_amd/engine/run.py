@@ -236,8 +236,12 @@ class Engine:
                 self.log("info", f"engine: device {d.identity()} caps={d.capabilities()}")
             node = self.opts.node_comm
             world = node.info.world_size if node is not None else 1
+            # one process per GPU unless this process is already one rank of a node (a rank owns one GPU)
+            gpus = any(d.identity().family == hal.Family.GPU for d in self.devices)
+            isolation = "process" if (cfg.mining.isolation == "process" and gpus and node is None) else "thread"
             self.miners = MinerSet(self.devices, self.algorithm.name, cfg.mining.batch_nonces, cfg.mining.cpu_threads,
-                                   rank=0, world_size=world, log=self.log, sha_variants=cfg.mining.sha_variants)
+                                   rank=0, world_size=world, log=self.log, sha_variants=cfg.mining.sha_variants,
+                                   isolation=isolation)
             if node is not None and world > 1:
                 from otedama_amd.parallel.node import NodeMinerSet
 
@@ -273,7 +277,9 @@ class Engine:
                 self.opts.on_ready(False)
 
     def _detect_devices(self) -> list:
-        reg = hal.default_registry(self.cfg.mining.cpu_threads)
+        # device processes open their GPUs themselves: name them from the KFD topology without a HIP runtime here
+        gpu_free = self.cfg.mining.isolation == "process" and self.opts.node_comm is None
+        reg = hal.default_registry(self.cfg.mining.cpu_threads, gpu_free=gpu_free)
         devs = hal.Detector(reg, lambda drv, msg, err: self.log("warn", f"hal: {drv}: {msg}: {err}")).detect()
         sel = self.cfg.mining.gpus.strip().lower()
         if sel == "none":

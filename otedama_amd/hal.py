@@ -151,6 +151,70 @@ class HIPDriver:
         return out
 
 
+KFD_TOPOLOGY_PATH = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_props(path: str) -> dict[str, int]:
+    out = {}
+    for line in _read(path).splitlines():
+        k, _, v = line.partition(" ")
+        try:
+            out[k] = int(v)
+        except ValueError:
+            pass
+    return out
+
+
+def _visible(n: int) -> list[int]:
+    """HIP ordinals after HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (integer lists)."""
+    idx = list(range(n))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is None:
+            continue
+        sel = [int(x) for x in v.split(",") if x.strip().lstrip("-").isdigit()]
+        idx = [idx[i] for i in sel if 0 <= i < len(idx)] if v.strip() else []
+    return idx
+
+
+class KFDDriver:
+    """GPU devices from the KFD topology in sysfs, in HIP ordinal order, WITHOUT initialising a HIP runtime.
+
+    Used when every device runs in its own process (engine/devproc.py): the engine process never opens the GPU,
+    so the devices it hands out can only be named here and are opened by their own processes."""
+
+    def __init__(self, base_path: str | None = None):
+        self.base_path = base_path or KFD_TOPOLOGY_PATH
+
+    def name(self) -> str:
+        return "hip"
+
+    def enumerate(self) -> list:
+        try:
+            nodes = sorted((int(d) for d in os.listdir(self.base_path) if d.isdigit()))
+        except OSError:
+            nodes = []
+        if not nodes and self.base_path == KFD_TOPOLOGY_PATH and os.path.exists("/dev/kfd"):
+            return HIPDriver().enumerate()  # sysfs topology not readable here: ask the runtime after all
+        gpus = []
+        for n in nodes:
+            p = _kfd_props(os.path.join(self.base_path, str(n), "properties"))
+            if p.get("simd_count", 0) <= 0 or not p.get("gfx_target_version"):
+                continue  # a CPU node
+            v = p["gfx_target_version"]
+            arch = f"gfx{v // 10000}{(v // 100) % 100:x}{v % 100:x}"
+            cus = p["simd_count"] // max(p.get("simd_per_cu", 4), 1)
+            gpus.append((arch, cus))
+        out = []
+        for i, k in enumerate(_visible(len(gpus))):
+            arch, cus = gpus[k]
+            caps = KERNEL_ISAS.get(arch, Capabilities(general_compute=True))
+            model = "AMD Instinct MI355X" if arch == "gfx950" else f"AMD GPU ({arch})"
+            out.append(SimpleDevice(Identity(f"gpu-{i}", Family.GPU, "AMD", f"{model} {cus}CU {arch}"), caps,
+                                    index=i, extra={"arch": arch, "cus": cus, "source": "kfd"}))
+        return out
+
+
 DRM_BASE_PATH = "/sys/class/drm"
 
 
@@ -288,10 +352,12 @@ class Detector:
         return out
 
 
-def default_registry(cpu_threads: int = 0, include_drm: bool = True) -> Registry:
+def default_registry(cpu_threads: int = 0, include_drm: bool = True, gpu_free: bool = False) -> Registry:
+    """``gpu_free``: enumerate GPUs from the KFD topology instead of the HIP runtime (the process stays GPU-free;
+    its devices run in device processes)."""
     r = Registry()
     r.register(CPUDriver(cpu_threads))
-    r.register(HIPDriver())
+    r.register(KFDDriver() if gpu_free else HIPDriver())
     if include_drm:
         r.register(GPULinuxDriver(skip_vendors=("0x1002",)))  # AMD GPUs come from the HIP driver
     return r

@@ -16,12 +16,21 @@ collectives run on a dedicated comm stream so they overlap the search kernels
 running on the miners' own HIP streams. ``run_async`` is the overlapped form
 (nothing on the compute stream waits for the collective; bench.py double-buffers
 the hit slots it gathers), ``_run`` the blocking one for results read at once.
+
+Fault tolerance (parallel/node.py): the rendezvous TCPStore is created here (or
+joined, when a GPU-free supervisor or torchrun's agent hosts it) and kept in
+``DistInfo.store`` for the node's control plane and heartbeats; the process
+group has a bounded timeout and lives under a per-generation store prefix, so
+``NodeComm.reform`` can abort a group that lost a rank and form the next one
+from the survivors. ``bounded`` collectives never wait past a deadline.
 """
 from __future__ import annotations
 
+import datetime
 import json
 import os
-from dataclasses import dataclass
+import time
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -32,17 +41,46 @@ SHARE_WORDS = 9  # epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_
 COUNTER_WORDS = 4  # hashes, shares, dropped, faulted
 
 
+PG_TIMEOUT_S = float(os.environ.get("OTEDAMA_PG_TIMEOUT", "30"))
+
+
+class CollectiveTimeout(RuntimeError):
+    """A bounded collective did not finish in time (a peer is dead or stuck)."""
+
+
 @dataclass
 class DistInfo:
-    rank: int = 0
+    rank: int = 0            # rank in the current process group
     world_size: int = 1
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    orig_rank: int = -1      # launcher-assigned identity (RANK at start); stable across re-forms
+    generation: int = 0      # process-group generation (store prefix otd-g<gen>)
+    members: list = field(default_factory=list)  # orig ranks of the current group, in group-rank order
+    store: object = None     # the rendezvous TCPStore (node control plane)
+
+    def __post_init__(self):
+        if self.orig_rank < 0:
+            self.orig_rank = self.rank
+        if not self.members:
+            self.members = list(range(self.world_size))
 
     @property
     def is_primary(self) -> bool:
         return self.rank == 0
+
+
+def _connect_store(rank: int, world: int):
+    """The rendezvous store: joined when a supervisor (OTEDAMA_STORE_HOSTED=1) or torchrun's agent hosts it, else
+    hosted by rank 0."""
+    addr = os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("MASTER_PORT", "29500"))
+    hosted = os.environ.get("OTEDAMA_STORE_HOSTED") == "1" or os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+    master = rank == 0 and not hosted
+    kw = {"multi_tenant": True} if master else {}  # as torch's own env:// rendezvous hosts it
+    return dist.TCPStore(addr, port, world_size=None if hosted else world, is_master=master,
+                         timeout=datetime.timedelta(seconds=max(PG_TIMEOUT_S, 60.0)), wait_for_workers=False, **kw)
 
 
 def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> DistInfo:
@@ -65,11 +103,35 @@ def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> Di
         return DistInfo(rank, 1, local, "none", device)
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # RCCL: no watchdog that tears the process down on a peer's death; node.py aborts and re-forms instead
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+    store = None
     if not dist.is_initialized():
+        store = _connect_store(rank, world)
         kw = {"device_id": device} if backend == "nccl" else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
-    return DistInfo(rank, world, local, backend, device)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                store=dist.PrefixStore("otd-g0", store),
+                                timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
+    return DistInfo(rank, world, local, backend, device, store=store)
+
+
+def join_from_env(backend: str | None = None, use_gpu: bool | None = None) -> DistInfo:
+    """A replacement rank (the supervisor re-spawned a dead one): connect to the store only; the node leader adds
+    it to the next process-group generation (parallel/node.py)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    backend = backend or os.environ.get("OTEDAMA_DIST_BACKEND") or None
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    ordinal = local % max(1, torch.cuda.device_count()) if (use_gpu and backend == "gloo") else local
+    device = torch.device(f"cuda:{ordinal}") if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+    store = _connect_store(rank, world)
+    return DistInfo(-1, 0, local, backend or ("nccl" if use_gpu else "gloo"), device, orig_rank=rank,
+                    generation=-1, members=[], store=store)
 
 
 def barrier(info: DistInfo) -> None:
@@ -86,18 +148,84 @@ def shutdown(info: DistInfo) -> None:
 
 
 class NodeComm:
-    """R1/R2/R3 over torch.distributed with preallocated fixed-size buffers."""
+    """R1/R2/R3 over torch.distributed with preallocated fixed-size buffers.
 
-    def __init__(self, info: DistInfo):
+    ``bounded=True`` (the node): every collective is issued async and polled against ``deadline`` seconds; a
+    collective that fails or times out raises (CollectiveTimeout / RuntimeError) instead of blocking forever."""
+
+    def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0):
         self.info = info
+        self.bounded = bounded
+        self.deadline = deadline
+        self.collectives = 0  # device collectives issued by this rank (node tick accounting)
         dev = info.device
         self._job = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8, device=dev)
         self._slots = torch.zeros(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
-        self._gathered = torch.zeros(info.world_size, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
         self._counters = torch.zeros(COUNTER_WORDS, dtype=torch.int64, device=dev)
-        self._counter_rows = torch.zeros(info.world_size, COUNTER_WORDS, dtype=torch.int64, device=dev)
         self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+        self._alloc_world(max(info.world_size, 1))
         self.stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+
+    def _alloc_world(self, world: int) -> None:
+        dev = self.info.device
+        self._gathered = torch.zeros(world, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
+        self._counter_rows = torch.zeros(world, COUNTER_WORDS, dtype=torch.int64, device=dev)
+
+    # ---------------------------------------------------------------- group generations
+    def abort(self) -> None:
+        """Drop the current process group without waiting on it (a peer died)."""
+        if not dist.is_initialized():
+            return
+        try:
+            if self.info.backend == "nccl":
+                from torch.distributed.distributed_c10d import _abort_process_group
+
+                _abort_process_group()
+            else:
+                dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 - the group is unusable either way
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def reform(self, members: list[int], generation: int) -> None:
+        """Leave the current group and form generation ``generation`` of the given orig ranks (this one included):
+        group rank = position in ``members``. Every member calls this with the same arguments."""
+        info = self.info
+        if info.orig_rank not in members:
+            raise ValueError(f"rank {info.orig_rank} is not a member of generation {generation}")
+        self.abort()
+        rank, world = members.index(info.orig_rank), len(members)
+        if world > 1:
+            kw = {"device_id": info.device} if info.backend == "nccl" else {}
+            dist.init_process_group(backend=info.backend, rank=rank, world_size=world,
+                                    store=dist.PrefixStore(f"otd-g{generation}", info.store),
+                                    timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
+        info.rank, info.world_size, info.generation, info.members = rank, world, generation, list(members)
+        self._alloc_world(world)
+
+    def _collect(self, start) -> None:
+        """Run one collective. ``start(async_op)`` issues it; bounded mode polls the Work against the deadline."""
+        self.collectives += 1
+        if not self.bounded:
+            self._run(lambda: start(False))
+            return
+        if self.stream is not None:
+            cur = torch.cuda.current_stream(self.info.device)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                work = start(True)
+        else:
+            work = start(True)
+        end = time.monotonic() + self.deadline
+        while not work.is_completed():
+            if time.monotonic() > end:
+                raise CollectiveTimeout(f"collective did not finish in {self.deadline:.1f} s")
+            time.sleep(0.0002)
+        work.wait()  # re-raises a failed collective (gloo: a peer's connection closed)
+        if self.stream is not None:
+            self.stream.synchronize()
 
     # ---------------------------------------------------------------- R1
     def broadcast_job(self, job: dict | None) -> dict | None:
@@ -111,7 +239,7 @@ class NodeComm:
             host[: len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
             self._job.copy_(host)
         if self.info.world_size > 1:
-            self._run(lambda: dist.broadcast(self._job, src=0))
+            self._collect(lambda a: dist.broadcast(self._job, src=0, async_op=a))
         host = self._job.cpu().numpy().tobytes()
         n = int.from_bytes(host[:4], "little")
         if n == 0:
@@ -132,7 +260,8 @@ class NodeComm:
             ], dtype=torch.int64)
         self._slots.copy_(host)
         if self.info.world_size > 1:
-            self._run(lambda: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots))
+            self._collect(lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
+                                                                async_op=a))
         else:
             self._gathered[0].copy_(self._slots)
         out = []
@@ -146,6 +275,7 @@ class NodeComm:
                     "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
                     "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
                     "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6,
+                    "orig_rank": self.info.members[r] if r < len(self.info.members) else r,
                 })
         return out
 
@@ -153,7 +283,7 @@ class NodeComm:
     def allreduce_counters(self, hashes: int, shares: int = 0, dropped: int = 0, faults: int = 0) -> tuple:
         self._counters.copy_(torch.tensor([hashes, shares, dropped, faults], dtype=torch.int64))
         if self.info.world_size > 1:
-            self._run(lambda: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM))
+            self._collect(lambda a: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM, async_op=a))
         return tuple(int(x) for x in self._counters.cpu().tolist())
 
     def gather_counters(self, values: list[int]) -> list[list[int]]:
@@ -161,7 +291,8 @@ class NodeComm:
         mine = torch.tensor(list(values)[:COUNTER_WORDS] + [0] * (COUNTER_WORDS - len(values)), dtype=torch.int64)
         self._counters.copy_(mine)
         if self.info.world_size > 1:
-            self._run(lambda: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters))
+            self._collect(lambda a: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters,
+                                                                async_op=a))
         else:
             self._counter_rows[0].copy_(self._counters)
         return self._counter_rows.cpu().tolist()
@@ -171,13 +302,13 @@ class NodeComm:
         if self.info.is_primary:
             self._ctl.copy_(torch.tensor(list(words)[:4] + [0] * (4 - len(words)), dtype=torch.int64))
         if self.info.world_size > 1:
-            self._run(lambda: dist.broadcast(self._ctl, src=0))
+            self._collect(lambda a: dist.broadcast(self._ctl, src=0, async_op=a))
         return self._ctl.cpu().tolist()
 
     def allreduce_max(self, value: float) -> float:
         t = torch.tensor([value], dtype=torch.float64, device=self.info.device)
         if self.info.world_size > 1:
-            self._run(lambda: dist.all_reduce(t, op=dist.ReduceOp.MAX))
+            self._collect(lambda a: dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=a))
         return float(t.item())
 
     def _run(self, fn) -> None:

@@ -101,3 +101,80 @@ def run_ranks(cmd: Sequence[str], world: int, port: int | None = None, env: dict
         _stop_all(procs, grace=5.0)
         for sig, h in prev.items():
             signal.signal(sig, h)
+
+
+def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env: dict | None = None,
+                   respawn: bool = True, backoff_initial: float = 1.0, backoff_max: float = 64.0, log=None,
+                   stop_event=None) -> int:
+    """Run a fault-tolerant node: ``world`` ranks of ``cmd`` around a rendezvous TCPStore hosted HERE (this
+    process is GPU-free and outlives any rank).
+
+    A follower (rank > 0) that exits is marked ``otd/dead/<r>`` in the store (the leader re-forms the process
+    group without it within one liveness check, parallel/node.py) and, with ``respawn``, restarted after a backoff
+    (1 s doubling to 64 s, internal/engine/run.go:56-63) as a joiner that the leader re-admits. Rank 0 is the
+    pool session: when it exits the node stops and its exit code is returned."""
+    import datetime
+
+    import torch.distributed as dist
+
+    log = log or (lambda msg: print(f"[node] {msg}", file=sys.stderr, flush=True))
+    port = port or free_port()
+    store = dist.TCPStore(MASTER_ADDR, port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    procs: dict[int, subprocess.Popen] = {}
+    backoff = {r: backoff_initial for r in range(world)}
+    respawn_at: dict[int, float] = {}
+    started: dict[int, float] = {}
+
+    def spawn(r: int, join: bool) -> None:
+        extra = {"OTEDAMA_STORE_HOSTED": "1"}
+        if join:
+            extra["OTEDAMA_NODE_JOIN"] = "1"
+        procs[r] = subprocess.Popen(list(cmd), env=rank_env(r, world, port, env, **extra))
+        started[r] = time.monotonic()
+
+    prev = {}
+
+    def forward(sig, _frame):
+        _stop_all(list(procs.values()), grace=10.0)
+        sys.exit(128 + sig)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            prev[sig] = signal.signal(sig, forward)
+        except ValueError:
+            pass
+    try:
+        for r in range(world):
+            spawn(r, join=False)
+        while True:
+            if stop_event is not None and stop_event.is_set():
+                return 0
+            rc0 = procs[0].poll()
+            if rc0 is not None:
+                log(f"rank 0 exited with code {rc0}; stopping the node")
+                return rc0
+            now = time.monotonic()
+            for r in range(1, world):
+                p = procs.get(r)
+                if p is not None and p.poll() is not None:
+                    log(f"rank {r} exited with code {p.returncode}")
+                    store.set(f"otd/dead/{r}", str(p.returncode))
+                    del procs[r]
+                    if now - started.get(r, now) > 60.0:
+                        backoff[r] = backoff_initial  # it had been healthy: start the backoff over
+                    if respawn:
+                        respawn_at[r] = now + backoff[r]
+                        log(f"rank {r}: restarting in {backoff[r]:.0f}s")
+                        backoff[r] = min(backoff[r] * 2, backoff_max)
+                if r not in procs and r in respawn_at and now >= respawn_at[r]:
+                    del respawn_at[r]
+                    try:
+                        store.delete_key(f"otd/dead/{r}")
+                    except Exception:  # noqa: BLE001
+                        pass
+                    spawn(r, join=True)
+            time.sleep(0.05)
+    finally:
+        _stop_all(list(procs.values()), grace=10.0)
+        for sig, h in prev.items():
+            signal.signal(sig, h)

@@ -102,3 +102,25 @@ def test_device_process_startup_and_counters_survive_restart():
         assert dp.stats()["hashes"] >= h  # cumulative across the restart
     finally:
         ms.stop()
+
+
+def test_kfd_topology_enumeration_without_a_runtime(tmp_path, monkeypatch):
+    """The engine names GPUs from the KFD topology (no HIP runtime in the parent); CPU nodes are skipped, the
+    arch comes from gfx_target_version, CUs from simd_count / simd_per_cu, and *_VISIBLE_DEVICES re-numbers."""
+    nodes = {0: "cpu_cores_count 64\nsimd_count 0\ngfx_target_version 0\n",
+             1: "simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n",
+             2: "simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n",
+             3: "simd_count 440\nsimd_per_cu 4\ngfx_target_version 90010\n"}
+    for n, text in nodes.items():
+        d = tmp_path / str(n)
+        d.mkdir()
+        (d / "properties").write_text(text)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    devs = hal.KFDDriver(str(tmp_path)).enumerate()
+    assert [(d.identity().id, d.index, d.extra["arch"], d.extra["cus"]) for d in devs] == \
+        [("gpu-0", 0, "gfx950", 256), ("gpu-1", 1, "gfx950", 256), ("gpu-2", 2, "gfx90a", 110)]
+    assert devs[0].capabilities().sha256d and not devs[2].capabilities().sha256d
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
+    devs = hal.KFDDriver(str(tmp_path)).enumerate()
+    assert [(d.index, d.extra["arch"]) for d in devs] == [(0, "gfx950"), (1, "gfx90a")]

@@ -1,0 +1,145 @@
+"""Node rank loss on CPU (gloo): the same op log / heartbeat / re-form code as the RCCL node (parallel/node.py).
+
+World 4 and 8: one rank is SIGKILLed mid-job. Within ~2 s the leader re-forms the process group with the
+survivors and re-broadcasts the job with a variant base past every reported cursor, so the dead rank's residue
+class is covered by the survivors; verified shares keep flowing; every process exits (nothing hangs). A
+replacement process started by the supervisor is re-admitted by the next re-form. In steady state with no shares
+and no job churn a rank issues at most about one device collective per second."""
+import datetime
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+import torch.distributed as dist
+
+from otedama_amd.models.header import sha256d
+from otedama_amd.parallel.launch import free_port, rank_env
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "tests", "_node_rank.py")
+
+
+def _job_header():
+    return bytes([1, 0, 0, 0]) + bytes(range(32)) + bytes(range(32, 64)) + (1700000000).to_bytes(4, "little") + \
+        bytes.fromhex("ffff001d") + bytes(4)
+
+
+def _spawn(world, out, mode, port, store_hosted=True, rank=None, join=False):
+    ranks = range(world) if rank is None else [rank]
+    procs = {}
+    for r in ranks:
+        extra = {"OTEDAMA_STORE_HOSTED": "1" if store_hosted else "0", "OTEDAMA_PG_TIMEOUT": "20"}
+        if join:
+            extra["OTEDAMA_NODE_JOIN"] = "1"
+        env = rank_env(r, world, port, **extra)
+        env["PYTHONPATH"] = ROOT
+        procs[r] = subprocess.Popen([sys.executable, SCRIPT, str(out), mode], env=env, cwd=ROOT,
+                                    stdout=subprocess.DEVNULL, stderr=open(os.path.join(out, f"err{r}.txt"), "w"))
+    return procs
+
+
+def _wait_file(path, timeout, procs):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        if os.path.exists(path):
+            return True
+        if procs[0].poll() is not None:
+            return False
+        time.sleep(0.05)
+    return False
+
+
+def _finish(procs, timeout=60):
+    end = time.monotonic() + timeout
+    codes = {}
+    for r, p in procs.items():
+        try:
+            codes[r] = p.wait(timeout=max(1, end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            codes[r] = "hung"
+    return codes
+
+
+def _verify(s):
+    hdr = bytearray(_job_header())
+    hdr[0:4] = int(s["version"]).to_bytes(4, "little")
+    hdr[76:80] = int(s["nonce"]).to_bytes(4, "little")
+    return int.from_bytes(sha256d(bytes(hdr)), "little") <= (1 << 236) - 1
+
+
+@pytest.mark.parametrize("world,victim,mark_dead", [(4, 2, True), (8, 5, True), (4, 3, False)])
+def test_rank_loss_reforms_and_keeps_mining(tmp_path, world, victim, mark_dead):
+    port = free_port()
+    store = dist.TCPStore("127.0.0.1", port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    procs = _spawn(world, tmp_path, "kill", port)
+    try:
+        assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
+        procs[victim].send_signal(signal.SIGKILL)
+        t_kill = time.time()
+        if mark_dead:  # what the supervisor does when a child exits
+            store.set(f"otd/dead/{victim}", "1")
+        with open(tmp_path / "killed.json", "w") as f:
+            json.dump({"rank": victim, "t": t_kill}, f)
+        codes = _finish({r: p for r, p in procs.items() if r != victim})
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
+    assert all(c == 0 for c in codes.values()), (codes, open(tmp_path / "err0.txt").read()[-3000:])
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert res["phase1_devices"] == sorted(["cpu-0"] + [f"rank{r}" for r in range(1, world)])
+    assert res["reform_after_s"] is not None, res["logs"]
+    # supervisor-marked: detected at the next liveness check (~0.1-0.3 s on an idle host; the bound leaves room for
+    # 8 busy ranks sharing the test host's CPUs); unmarked: heartbeat timeout (2 s) or a failed collective
+    assert res["reform_after_s"] < (3.0 if mark_dead else 4.5), res["reform_after_s"]
+    assert res["lost"] == [victim]
+    members, base = res["members"], res["base"]
+    assert members == [r for r in range(world) if r != victim]
+    # the survivors' stripes {base + i + (world-1) k} cover every residue class, the dead rank's included, and the
+    # shares they find after the re-form come from exactly those stripes
+    assert res["post"], res["logs"]
+    for s in res["post"]:
+        orig = int(s["dev"][4:])
+        assert ((s["version"] >> 13) & 0xFFFF) == base + members.index(orig), (s, base, members)
+    assert all(_verify(s) for s in res["shares"])
+    assert len({s["dev"] for s in res["post"]}) >= min(2, world - 2)
+
+
+def test_replacement_rank_rejoins(tmp_path):
+    world, victim = 4, 1
+    port = free_port()
+    store = dist.TCPStore("127.0.0.1", port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    procs = _spawn(world, tmp_path, "rejoin", port)
+    try:
+        assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
+        procs[victim].send_signal(signal.SIGKILL)
+        store.set(f"otd/dead/{victim}", "1")
+        with open(tmp_path / "killed.json", "w") as f:
+            json.dump({"rank": victim, "t": time.time()}, f)
+        time.sleep(1.5)
+        store.delete_key(f"otd/dead/{victim}")
+        procs[victim] = _spawn(world, tmp_path, "rejoin", port, rank=victim, join=True)[victim]
+        codes = _finish(procs)
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert codes[0] == 0, (codes, res.get("logs"))
+    assert res["members_after_rejoin"] == [0, 1, 2, 3], res["logs"]
+    assert res["victim_shares_after_rejoin"], res["logs"]
+
+
+def test_quiet_node_issues_about_one_collective_per_second(tmp_path):
+    world = 4
+    port = free_port()
+    procs = _spawn(world, tmp_path, "quiet", port, store_hosted=False)
+    codes = _finish(procs, timeout=120)
+    assert all(c == 0 for c in codes.values()), codes
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert res["collectives_per_s"] <= 1.0, res

@@ -60,14 +60,17 @@ def _worker(rank: int, port: int, out_path: str, world: int = WORLD) -> None:
         if min(per_rank) >= 3 and len(shares) >= 2 * world:
             break
         time.sleep(0.02)
+    end = time.monotonic() + 10  # remote counters arrive with the 2 Hz heartbeats (and R3 every stats interval)
+    while time.monotonic() < end and not all(node.device_stats()[f"rank{r}"]["hashes"] > 0 for r in range(1, world)):
+        time.sleep(0.05)
     node.update_hashrates()
     stats = node.device_stats()
     total = node.total_hashes()
     # pause the remote rank, wait for its counter to freeze
     node.pause_device("rank1", True)
-    time.sleep(0.3)
+    time.sleep(1.2)  # the pause reaches rank 1 (R1) and its counter reaches rank 0 (2 Hz heartbeat)
     h1 = node.device_stats()["rank1"]["hashes"]
-    time.sleep(0.3)
+    time.sleep(1.2)
     h2 = node.device_stats()["rank1"]["hashes"]
     node.stop()
     shutdown(info)
