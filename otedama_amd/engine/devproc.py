@@ -102,6 +102,7 @@ class DeviceProcess:
         self.ready_at = 0.0
         self.spawned_at = 0.0
         self.startup_seconds = 0.0       # spawn -> child reported its miner running
+        self.first_hash_wall = 0.0       # wall clock of the child's first completed batch
 
     # ------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -201,6 +202,7 @@ class DeviceProcess:
         st["process_restarts"] = self.restarts
         st["pid"] = self.pid
         st["startup_seconds"] = self.startup_seconds
+        st["first_hash_wall"] = self.first_hash_wall
         return st
 
     # ------------------------------------------------------------- plumbing
@@ -236,6 +238,8 @@ class DeviceProcess:
                 elif op == "stats":
                     with self._lock:
                         self._child = m["st"]
+                elif op == "first_hash":
+                    self.first_hash_wall = float(m.get("wall", 0.0))
                 elif op == "ready":
                     self.ready_at = time.monotonic()
                     self.startup_seconds = self.ready_at - self.spawned_at
@@ -289,10 +293,13 @@ def _child(argv: list[str]) -> int:
     poller.register(efd, select.POLLIN)
     fr = _Framer()
     next_stats = 0.0
+    first_hash = False  # until the first batch completes: poll fast and report it at once (start-up timing)
     rc = 0
     try:
         while True:
             timeout = max(0.0, next_stats - time.monotonic())
+            if not first_hash:
+                timeout = min(timeout, 0.005)
             for fd, _ev in poller.poll(timeout * 1e3):
                 if fd == efd:
                     try:
@@ -311,6 +318,10 @@ def _child(argv: list[str]) -> int:
                         m.set_job(msg.get("t"))
                     elif msg.get("op") == "stop":
                         return 0
+            if not first_hash and m.stats()["hashes"] > 0:
+                first_hash = True
+                _send(sock, {"op": "first_hash", "wall": time.time()})
+                next_stats = 0.0
             if time.monotonic() >= next_stats:
                 st = m.stats()
                 _send(sock, {"op": "stats", "st": st})

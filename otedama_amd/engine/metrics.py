@@ -122,8 +122,12 @@ class EngineMetrics:
         self.stale_skipped = C("otedama_shares_stale_skipped_total",
                                "Shares found for a job the pool already invalidated (not submitted).")
         self.node_collective_seconds = G("otedama_node_collective_seconds",
-                                         "Multi-GPU node: wall time of the last R1/R2/R3 collective tick on rank 0 "
-                                         "(0 outside node mode).")
+                                         "Multi-GPU node: median wall time of rank 0's node ops (R1 job broadcast, R2 "
+                                         "share gather, R3 counters, re-forms); 0 outside node mode.")
+        self.node_collective_p99 = G("otedama_node_collective_p99_seconds",
+                                     "Multi-GPU node: 99th-percentile wall time of rank 0's node ops.")
+        self.node_collectives = G("otedama_node_device_collectives",
+                                  "Multi-GPU node: device collectives (RCCL) issued by rank 0 since start.")
         self.node_ranks = G("otedama_node_ranks", "Multi-GPU node: ranks (one per GPU) in the torchrun job; 1 when "
                                                   "running standalone.")
         self.node_ranks.set(1)

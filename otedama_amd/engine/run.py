@@ -203,10 +203,15 @@ class Engine:
         return {
             "epoch": ms.epoch if ms is not None else 0,
             "devices": devs,
-            "node": None if link is None else {"rank": link.rank, "world": link.world, "tick_s": link.tick,
-                                               "counter_rows": link.rows,
-                                               "error": str(link.error) if link.error else None},
+            "node": None if link is None else {
+                "rank": link.rank, "world": link.world, "tick_s": link.tick, "counter_rows": link.rows,
+                "generation": link.comm.info.generation, "members": list(link.comm.info.members),
+                "lost_ranks": list(getattr(ms, "lost_ranks", [])), "device_collectives": link.comm.collectives,
+                "ops": link.ops_run, "reforms": link.reforms,
+                "op_p50_s": link.tick_quantile(0.5), "op_p99_s": link.tick_quantile(0.99),
+                "error": str(link.error) if link.error else None},
             "submit_tasks_inflight": len(self._submit_tasks),
+            "startup": self._startup(),
             "latency_ms": {"p50": self.latency.quantile(0.5), "p95": self.latency.quantile(0.95),
                            "p99": self.latency.quantile(0.99)},
             "hit_to_accept_ms": {"p50": self.device_latency.quantile(0.5), "p95": self.device_latency.quantile(0.95),
@@ -214,6 +219,29 @@ class Engine:
             "process": {"threads": _th.active_count(),
                         "max_rss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0},
         }
+
+    def _startup(self) -> dict:
+        """Process start -> first completed GPU batch, per device (device processes report their first hash), and
+        this process's resident set (BENCHMARKS.md:105-129 reports <1 s to hashing and 25 MB)."""
+        out = {}
+        try:
+            import psutil
+
+            p = psutil.Process()
+            t0 = p.create_time()
+            out["rss_mib"] = p.memory_info().rss / 2**20
+            kids = p.children(recursive=True)
+            out["children_rss_mib"] = sum(k.memory_info().rss for k in kids) / 2**20
+        except Exception:  # noqa: BLE001 - psutil missing or a child gone
+            t0 = 0.0
+        ms = self.miners
+        firsts = {}
+        for m in getattr(ms, "miners", []) or []:
+            wall = float(getattr(m.native, "first_hash_wall", 0.0) or 0.0)
+            if wall and t0:
+                firsts[m.id] = wall - t0
+        out["first_hash_after_start_s"] = firsts
+        return out
 
     def device_list(self) -> list[dict]:
         return [{"id": d.identity().id, "family": d.identity().family.value, "vendor": d.identity().vendor,
@@ -685,7 +713,9 @@ class Engine:
         link = getattr(self.miners, "link", None)
         if link is not None:
             self.m.node_ranks.set(link.world)
-            self.m.node_collective_seconds.set(getattr(link, "last_tick_seconds", 0.0))
+            self.m.node_collective_seconds.set(link.tick_quantile(0.5))
+            self.m.node_collective_p99.set(link.tick_quantile(0.99))
+            self.m.node_collectives.set(link.comm.collectives)
         self.m.devices_faulted.set(sum(1 for s in dstats.values() if s["faulted"]))
         self.m.devices_stalled.set(len(stalled_devs))
         self.m.devices_active.set(len(self.miners.live()) - len(stalled_devs))

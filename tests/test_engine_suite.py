@@ -13,6 +13,7 @@ miners), so every branch is deterministic. Reference behaviour (file:line in /ro
   * reconnect loop: pool-fast, address-slow, backoff 1..64 s, fatal  run.go:343-521
 """
 import asyncio
+from types import SimpleNamespace
 import io
 import re
 
@@ -1394,10 +1395,15 @@ def test_tick_stats_publishes_device_busy_ratio_and_launches():
 def test_tick_stats_publishes_node_collective_tick():
     class Link:
         world = 8
-        last_tick_seconds = 0.0004
+        comm = SimpleNamespace(collectives=12)
+
+        def tick_quantile(self, q):
+            return 0.0004 if q == 0.5 else 0.002
+
     clock = Clock()
     eng, _ = make_engine(clock=clock)
     assert eng.m.node_ranks.value() == 1
     eng.miners.link = Link()
     tick(eng, clock, 1, 1)
     assert eng.m.node_ranks.value() == 8 and eng.m.node_collective_seconds.value() == pytest.approx(0.0004)
+    assert eng.m.node_collective_p99.value() == pytest.approx(0.002) and eng.m.node_collectives.value() == 12

@@ -1,0 +1,135 @@
+"""GPU-box rehearsal of the production entry points on one MI355X.
+
+1. ``otedama run`` (one device process per GPU, the engine GPU-free) against ``otedama pool`` in another process:
+   process start -> first completed GPU batch, resident set of the engine and of the device process, hashrate.
+2. ``otedama node --gpus 2`` with ``OTEDAMA_DIST_BACKEND=gloo``: two ranks sharing the one GPU, the same op-log /
+   heartbeat control plane as the RCCL node: node hashrate vs 1., and the device collectives per second.
+
+Prints one JSON line; every number is read from the running processes (/debug/stats, /api/v1/stats, psutil).
+Usage: python tools/gpu_node_rehearsal.py [--seconds 25]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _get(url: str):
+    with urllib.request.urlopen(url, timeout=5) as r:
+        return json.loads(r.read())
+
+
+def _wait(pred, timeout, step=0.02):
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        try:
+            v = pred()
+            if v:
+                return v
+        except Exception:  # noqa: BLE001 - the HTTP server is not up yet
+            pass
+        time.sleep(step)
+    return None
+
+
+def _hashes(http: str) -> int:
+    st = _get(f"http://{http}/debug/stats")
+    return sum(int(d.get("hashes", 0)) for d in st["devices"].values())
+
+
+def _measure(cmd: list[str], http: str, env: dict, seconds: float, log_path: str) -> dict:
+    t_spawn = time.time()
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(log_path, "w"), stderr=subprocess.STDOUT)
+    out: dict = {}
+    try:
+        first = _wait(lambda: _hashes(http) > 0 and time.time(), 120)
+        out["spawn_to_first_hash_s"] = (first - t_spawn) if first else None
+        st = _wait(lambda: _get(f"http://{http}/debug/stats"), 10)
+        out["startup"] = (st or {}).get("startup")
+        time.sleep(5.0)  # past the first job's start-up transients
+        h0, t0 = _hashes(http), time.monotonic()
+        time.sleep(seconds)
+        h1, t1 = _hashes(http), time.monotonic()
+        out["hashrate"] = (h1 - h0) / (t1 - t0)
+        dbg = _get(f"http://{http}/debug/stats")
+        out["node"] = dbg.get("node")
+        out["startup"] = dbg.get("startup") or out["startup"]
+        try:
+            import psutil
+
+            pp = psutil.Process(p.pid)
+            out["rss_mib"] = {str(c.pid): round(c.memory_info().rss / 2**20, 1)
+                              for c in [pp, *pp.children(recursive=True)]}
+        except Exception as exc:  # noqa: BLE001
+            out["rss_mib"] = str(exc)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        try:
+            out["exit_code"] = p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out["exit_code"] = "killed"
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=20.0)
+    ap.add_argument("--out-dir", default=os.path.join(ROOT, "gpurun_out", "node_rehearsal"))
+    a = ap.parse_args()
+    os.makedirs(a.out_dir, exist_ok=True)
+    from otedama_amd.engine.latency_probe import PROBE_ADDR
+    from otedama_amd.parallel.launch import free_port
+
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    pool_http = f"127.0.0.1:{free_port()}"
+    pool = subprocess.Popen([sys.executable, "-m", "otedama_amd", "pool", "--algorithms", "sha256d",
+                             "--listen-sv2", "127.0.0.1:0", "--listen-v1=", "--difficulty", "4",
+                             "--share-seconds", "1000", "--retarget-seconds", "3600", "--job-interval", "3600",
+                             "--block-interval", "3600", "--http-addr", pool_http, "--payout-address", PROBE_ADDR],
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
+    addr = None
+    for _ in range(400):
+        line = pool.stdout.readline()
+        if "listening sv2=" in line:
+            addr = line.split("listening sv2=", 1)[1].split()[0]
+            break
+    if not addr:
+        print(json.dumps({"error": "pool did not start"}))
+        return 1
+    cfg = os.path.join(a.out_dir, "config.yaml")
+    with open(cfg, "w") as f:
+        f.write(f"bitcoin_address: {PROBE_ADDR}\npools:\n  - url: stratum+v2://{addr}\n")
+    res = {}
+    try:
+        http1 = f"127.0.0.1:{free_port()}"
+        res["run"] = _measure([sys.executable, "-m", "otedama_amd", "run", "--config", cfg, "--no-tui",
+                               "--http-addr", http1], http1, env, a.seconds, os.path.join(a.out_dir, "run.log"))
+        http2 = f"127.0.0.1:{free_port()}"
+        res["node_gloo_2ranks_shared_gpu"] = _measure(
+            [sys.executable, "-m", "otedama_amd", "node", "--gpus", "2", "--config", cfg, "--no-tui", "--http-addr",
+             http2], http2, dict(env, OTEDAMA_DIST_BACKEND="gloo"), a.seconds, os.path.join(a.out_dir, "node.log"))
+        r, n = res["run"].get("hashrate"), res["node_gloo_2ranks_shared_gpu"].get("hashrate")
+        res["node_vs_run"] = (n / r) if r and n else None
+        res["pool"] = _get(f"http://{pool_http}/api/v1/pool")
+    finally:
+        pool.send_signal(signal.SIGTERM)
+        try:
+            pool.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            pool.kill()
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
