@@ -1,4 +1,4 @@
-// GpuMiner: one host thread per GPU driving search batches on a private HIP stream.
+// GpuMiner: one host thread per GPU driving search batches on private HIP streams.
 //
 // Share path: a kernel publishes each hit the moment it is found into a ring of HitRecords in host-coherent
 // pinned memory (record, system-scope fence, tag: otedama/hitsink.h). This thread polls the rings of the
@@ -11,6 +11,10 @@
 // control stream (hipStreamWriteValue32). Every wave polls that word once per grid-stride trip, so batches of
 // the old epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first
 // batch of the new work starts right behind them. The switch time (set_job -> new batch running) is recorded.
+//
+// Launch overlap: the two batches in flight sit on two streams (one per slot), so the next SHA-256d batch's waves
+// fill the CUs that the running batch's tail leaves idle; without it a 2^29-nonce launch (28 ms) lost ~2.5% to its
+// tail (profiles/r3/e_rehearsal). scrypt / X11 batches share their scratch buffers and are chained with an event.
 //
 // Device time: s_memrealtime (100 MHz) is mapped to CLOCK_MONOTONIC by a probe kernel at start-up (min round
 // trip of several probes) and re-checked every 10 s by a calibration thread on a stream of its own (a probe
@@ -109,6 +113,7 @@ struct Batch {
   double enq_host = 0;    // monotonic seconds at enqueue
   uint32_t rt_enq = 0;    // device realtime (low 32 bits) estimated at enqueue
   bool started = false;
+  hipStream_t stream = nullptr;  // this slot's stream
   hipEvent_t start{}, done{};
   uint32_t* d_count = nullptr;  // candidate counter (device memory)
   uint32_t* h_count = nullptr;  // pinned copy of the final count
@@ -155,7 +160,7 @@ void GpuMiner::stop() {
 void GpuMiner::loop() {
   trace_name_thread(("otedama-" + device_id_).c_str());
   OTD_HIP(hipSetDevice(device_));
-  hipStream_t stream = nullptr, ctl = nullptr, cal = nullptr;
+  hipStream_t ctl = nullptr, cal = nullptr;
   Batch slots[kInflight];
   uint32_t* d_abort = nullptr;   // uncached device word: the newest launch epoch that must keep running
   uint64_t* h_rt = nullptr;      // probe output (pinned, host-coherent)
@@ -181,7 +186,8 @@ void GpuMiner::loop() {
       cal_cv.notify_all();
       cal_th.join();
     }
-    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& s : slots)
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (ctl) (void)hipStreamSynchronize(ctl);
     if (cal) (void)hipStreamSynchronize(cal);
     for (auto& s : slots) {
@@ -198,11 +204,12 @@ void GpuMiner::loop() {
     if (scratch) (void)hipFree(scratch);
     if (xbuf) (void)hipFree(xbuf);
     if (x11_h) (void)hipFree(x11_h);
-    if (stream) (void)hipStreamDestroy(stream);
+    for (auto& s : slots)
+      if (s.stream) (void)hipStreamDestroy(s.stream);
     if (ctl) (void)hipStreamDestroy(ctl);
     if (cal) (void)hipStreamDestroy(cal);
   }};
-  OTD_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  for (auto& s : slots) OTD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   OTD_HIP(hipStreamCreateWithFlags(&ctl, hipStreamNonBlocking));
   OTD_HIP(hipStreamCreateWithFlags(&cal, hipStreamNonBlocking));
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
@@ -259,7 +266,7 @@ void GpuMiner::loop() {
       stats_.clock_calib_rtt_us = (t1 - t0) * 1e6;
     }
   };
-  for (int t = 0; t < 8; ++t) probe(stream);
+  for (int t = 0; t < 8; ++t) probe(slots[0].stream);
   rt_offset_ = rt_offset.load();
   cal_th = std::thread([&] {
     try {
@@ -476,7 +483,8 @@ void GpuMiner::loop() {
     return gp;
   };
 
-  auto enqueue = [&](Batch& s, const std::shared_ptr<const JobTemplate>& job, uint64_t gen) {
+  auto enqueue = [&](Batch& s, const std::shared_ptr<const JobTemplate>& job, uint64_t gen, const Batch* prev) {
+    hipStream_t stream = s.stream;
     if (!group || group->gen != gen || group->k != k) group = build_group(job, gen);
     s.job = job;
     s.group = group;
@@ -497,6 +505,8 @@ void GpuMiner::loop() {
     sink.tag = s.tag;
     sink.epoch = s.epoch;
     sink.words = 2;
+    // scrypt pad / X11 digests are shared by the batches: chain them; SHA-256d batches overlap freely
+    if (prev && prev->busy && job->algo != Algo::kSha256d) OTD_HIP(hipStreamWaitEvent(stream, prev->done, 0));
     OTD_HIP(hipMemsetAsync(s.d_count, 0, 64, stream));
     OTD_HIP(hipEventRecord(s.start, stream));
     s.enq_host = monotonic_seconds();
@@ -569,15 +579,15 @@ void GpuMiner::loop() {
     if (job && gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
     // 1) hits of the batches in flight, oldest first
     for (int i : fifo) progressed |= drain_ring(slots[i], ~0u, job, gen) > 0;
-    // 2) retire completed batches in issue order
-    while (!fifo.empty()) {
-      Batch& b = slots[fifo.front()];
+    // 2) retire completed batches (the two streams may complete out of issue order)
+    for (auto it = fifo.begin(); it != fifo.end();) {
+      Batch& b = slots[*it];
       const hipError_t q = hipEventQuery(b.done);
-      if (q == hipErrorNotReady) break;
+      if (q == hipErrorNotReady) { ++it; continue; }
       OTD_HIP(q);
       if (!b.started) b.started = true;
       finish(b, job, gen);
-      fifo.pop_front();
+      it = fifo.erase(it);
       progressed = true;
     }
     // 3) job-switch time: set_job -> the first batch of the new epoch running on the device
@@ -607,7 +617,7 @@ void GpuMiner::loop() {
       for (int i = 0; i < kInflight; ++i)
         if (!slots[i].busy) { free_slot = i; break; }
       if (free_slot < 0) break;
-      enqueue(slots[free_slot], job, gen);
+      enqueue(slots[free_slot], job, gen, fifo.empty() ? nullptr : &slots[fifo.back()]);
       fifo.push_back(free_slot);
       progressed = true;
     }

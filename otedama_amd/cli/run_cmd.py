@@ -99,6 +99,10 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         stdout.write("dry-run: configuration is valid; would start run\n")
         return EXIT_OK
     node = None
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and cfg.mining.isolation == "process":
+        # the GPUs belong to device processes: this process never touches them, so it loads the native host
+        # code without torch (start-up and RSS; ops/native.py)
+        os.environ.setdefault("OTEDAMA_NO_TORCH", "1")
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # node mode (otedama node / torchrun): one rank per GPU; rank 0 is the pool-facing engine. A rank the
         # supervisor restarted after a loss joins the running node instead of forming it.

@@ -103,6 +103,7 @@ class DeviceProcess:
         self.spawned_at = 0.0
         self.startup_seconds = 0.0       # spawn -> child reported its miner running
         self.first_hash_wall = 0.0       # wall clock of the child's first completed batch
+        self.child_timing: dict = {}     # wall clock: child main(), native module loaded, first batch done
 
     # ------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -203,6 +204,7 @@ class DeviceProcess:
         st["pid"] = self.pid
         st["startup_seconds"] = self.startup_seconds
         st["first_hash_wall"] = self.first_hash_wall
+        st["child_timing"] = dict(self.child_timing)
         return st
 
     # ------------------------------------------------------------- plumbing
@@ -240,6 +242,8 @@ class DeviceProcess:
                         self._child = m["st"]
                 elif op == "first_hash":
                     self.first_hash_wall = float(m.get("wall", 0.0))
+                    self.child_timing = {"main": m.get("t_main", 0.0), "native_loaded": m.get("t_native", 0.0),
+                                         "first_hash": self.first_hash_wall}
                 elif op == "ready":
                     self.ready_at = time.monotonic()
                     self.startup_seconds = self.ready_at - self.spawned_at
@@ -275,11 +279,13 @@ def _child(argv: list[str]) -> int:
     ap.add_argument("--sha-variants", type=int, default=128)
     ap.add_argument("--cpu-threads", type=int, default=0, help="> 0: a native CpuMiner instead of a GPU (tests)")
     a = ap.parse_args(argv)
+    t_main = time.time()
     os.environ["OTEDAMA_NO_TORCH"] = "1"
     sock = socket.socket(fileno=a.fd)
     from otedama_amd.ops.native import require_native
 
     N = require_native()
+    t_native = time.time()
     if a.cpu_threads > 0:
         m = N.CpuMiner(a.cpu_threads, a.id, a.queue_cap)
     else:
@@ -320,7 +326,7 @@ def _child(argv: list[str]) -> int:
                         return 0
             if not first_hash and m.stats()["hashes"] > 0:
                 first_hash = True
-                _send(sock, {"op": "first_hash", "wall": time.time()})
+                _send(sock, {"op": "first_hash", "wall": time.time(), "t_main": t_main, "t_native": t_native})
                 next_stats = 0.0
             if time.monotonic() >= next_stats:
                 st = m.stats()

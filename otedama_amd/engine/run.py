@@ -235,12 +235,15 @@ class Engine:
         except Exception:  # noqa: BLE001 - psutil missing or a child gone
             t0 = 0.0
         ms = self.miners
-        firsts = {}
+        firsts, phases = {}, {}
         for m in getattr(ms, "miners", []) or []:
             wall = float(getattr(m.native, "first_hash_wall", 0.0) or 0.0)
             if wall and t0:
                 firsts[m.id] = wall - t0
+                ct = getattr(m.native, "child_timing", {}) or {}
+                phases[m.id] = {k: (v - t0) if v else None for k, v in ct.items()}
         out["first_hash_after_start_s"] = firsts
+        out["device_process_phases_s"] = phases  # seconds after engine start: child main, native loaded, 1st batch
         return out
 
     def device_list(self) -> list[dict]:
