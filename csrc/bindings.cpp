@@ -391,7 +391,7 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<GpuMiner, MinerBase, std::shared_ptr<GpuMiner>>(m, "GpuMiner")
       .def(py::init<int, std::string, uint64_t, int, size_t, int>(), py::arg("device"), py::arg("device_id"),
-           py::arg("batch_nonces") = (1ull << 29), py::arg("grid") = 2048, py::arg("queue_cap") = 1024,
+           py::arg("batch_nonces") = (1ull << 32), py::arg("grid") = 2048, py::arg("queue_cap") = 1024,
            py::arg("sha_variants") = 128);
   py::class_<CpuMiner, MinerBase, std::shared_ptr<CpuMiner>>(m, "CpuMiner")
       .def(py::init<int, std::string, size_t>(), py::arg("threads"), py::arg("device_id") = "cpu-0",

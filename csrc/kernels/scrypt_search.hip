@@ -306,32 +306,21 @@ __device__ __forceinline__ void coop_consume(uint32_t X[32], uint4* __restrict__
   }
 }
 
-// The abort word (otedama/hitsink.h) is polled at every quarter of the ROMix (a wave's hash takes ~32 ms): an
-// obsolete batch stops within ~8 ms of hashing instead of finishing two launches. The polls sit between
-// straight-line halves of each BlockMix loop; polling inside the loops made the allocator reload spilled values
-// every iteration (64-VGPR budget). Returns false when aborted.
+// The abort word (otedama/hitsink.h) is polled before each ROMix phase (a wave's hash takes ~32 ms, its phases
+// ~16 ms each): an obsolete batch stops within half a hash instead of finishing two launches. Polling inside the
+// BlockMix loops made the allocator reload spilled values every iteration (64-VGPR budget), and splitting each
+// loop in two for quarter polls cost 0.9% of ROMix time (four loop bodies in the instruction cache instead of
+// two, profiles/r3/f_regressions). Returns false when aborted.
 template <int LCPOL>
 __device__ __forceinline__ bool scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
                                                   uint32_t lane, const otedama::HitSink& sink) {
   if (abort_newer(abort_peek(sink), sink.epoch)) return false;
-  for (uint32_t i = 0; i < 512; ++i) {
+  for (uint32_t i = 0; i < 1024; ++i) {
     coop_store_entry(X, rs, tile, lane, i);
     blockmix(X);
   }
   if (abort_newer(abort_peek(sink), sink.epoch)) return false;
-  for (uint32_t i = 512; i < 1024; ++i) {
-    coop_store_entry(X, rs, tile, lane, i);
-    blockmix(X);
-  }
-  if (abort_newer(abort_peek(sink), sink.epoch)) return false;
-  for (int i = 0; i < 512; ++i) {
-    coop_v4u R[4];
-    coop_issue<LCPOL>(X, rs, tile, lane, R);
-    coop_consume(X, tile, lane, R);
-    blockmix(X);
-  }
-  if (abort_newer(abort_peek(sink), sink.epoch)) return false;
-  for (int i = 0; i < 512; ++i) {
+  for (int i = 0; i < 1024; ++i) {
     coop_v4u R[4];
     coop_issue<LCPOL>(X, rs, tile, lane, R);
     coop_consume(X, tile, lane, R);

@@ -157,8 +157,10 @@ enum X11Stage : int {
 // Stage 0 writes H from the header + nonces; stages 1..10 transform H in place.
 // Stage 10 with `out` != null compares against the target and appends nonces
 // instead of writing H (search mode).
-// Abort word of the batch (otedama/hitsink.h): every stage kernel stops early once the host moved it past `epoch`
-// (whole-launch kernels check once per wave, grid-stride kernels once per trip); word == nullptr: never.
+// Abort word of the batch (otedama/hitsink.h), polled by the first stage (BLAKE skips its digests) and the last
+// (ECHO publishes nothing) once the host moved it past `epoch`; word == nullptr: never. The nine stages between
+// run a superseded batch to its end (~18 ms): polling in them cost 1-7% per stage (CubeHash +6.8%, Keccak +4%,
+// profiles/r3/f_regressions) for a job-switch saving the SHA-256d / scrypt paths do not need from X11.
 struct X11Abort {
   const uint32_t* word = nullptr;
   uint32_t epoch = 0;

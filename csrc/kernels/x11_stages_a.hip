@@ -220,13 +220,11 @@ __device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
   }
 }
 
-__global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n,
-                                                                                                     X11Abort ab) {
+__global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ u64 T[kGroestlPrivQwords];
   groestl_priv_fill(T);
   const u32 lo = groestl_laneoff();
   for (u32 i = blockIdx.x * kGroestlBlock + threadIdx.x; i < n; i += gridDim.x * kGroestlBlock) {
-    if (x11_stop(ab)) return;  // after the table fill: no block barrier follows
     u64 m[16], p[16], q[16];
     load_hash(Hb, stride, i, m);
     m[8] = 0x80;
@@ -636,10 +634,9 @@ __device__ __forceinline__ void cubehash512_64(u64 h[8]) {
 
 // One kernel per stage: each stage runs at its own register budget / occupancy.
 #define X11_STAGE_KERNEL(NAME, FN)                                                          \
-  __global__ __launch_bounds__(kBlock) void NAME(u64* __restrict__ Hb, u32 stride, u32 n,   \
-                                                  X11Abort ab) {                            \
+  __global__ __launch_bounds__(kBlock) void NAME(u64* __restrict__ Hb, u32 stride, u32 n) { \
     const u32 i = blockIdx.x * kBlock + threadIdx.x;                                        \
-    if (i >= n || x11_stop(ab)) return;                                                     \
+    if (i >= n) return;                                                                     \
     u64 h[8];                                                                               \
     load_hash(Hb, stride, i, h);                                                            \
     FN(h);                                                                                  \
@@ -669,17 +666,17 @@ hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
   switch (stage) {
     case kX11Blake: k_blake512_80<<<grid, block, 0, s>>>(p, base, H, stride, n, ab); break;
-    case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
+    case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     case kX11Groestl: {
       const u32 want = (n + kGroestlBlock - 1) / kGroestlBlock, cap = (u32)x11_device_cus() * 2 * 4;
-      k_groestl512_64<<<dim3(want < cap ? want : cap), dim3(kGroestlBlock), 0, s>>>(H, stride, n, ab);
+      k_groestl512_64<<<dim3(want < cap ? want : cap), dim3(kGroestlBlock), 0, s>>>(H, stride, n);
       break;
     }
-    case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
-    case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
-    case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
-    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
-    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n, ab); break;
+    case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -33,12 +33,11 @@ __device__ __forceinline__ void shavite_F(const u32* T, u32 lo, u32 x[4], const 
   aes_round(T, lo, x[0], x[1], x[2], x[3]);
 }
 
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
-    if (x11_stop(ab)) return;  // after the table fill: no block barrier follows
   u64 h[8];
   load_hash(Hb, stride, i, h);
   // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
@@ -222,7 +221,7 @@ constexpr int kSimdBlock = 256;
 constexpr u32 kSimdLds = 624;
 
 // Eight lanes per hash: launch with 8 * n threads.
-__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ __attribute__((aligned(16))) u32 L[kSimdLds];
   for (u32 t = threadIdx.x; t < kSimdLds; t += kSimdBlock) {
     u32 v = 0;
@@ -242,7 +241,7 @@ __global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb,
   __syncthreads();
   const u32 t = blockIdx.x * kSimdBlock + threadIdx.x;
   const u32 i = t >> 3, j = t & 7;
-  if (i >= n || x11_stop(ab)) return;  // whole 8-lane groups exit together (the abort word is wave-uniform)
+  if (i >= n) return;  // whole 8-lane groups exit together
   u64 h[8];
   load_hash(Hb, stride, i, h);
   u32 xw[16];
@@ -419,17 +418,15 @@ int x11_device_cus() {
 hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
                               const HitSink* sink, hipStream_t s) {
   using namespace x11k;
-  X11Abort ab;
-  if (sink) ab = X11Abort{sink->abort, sink->epoch};
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
   // bank-private AES table (64 KiB): 2 resident blocks of 512 per CU, grid-stride over the batch
   const u32 aes_want = (n + kAesBlock - 1) / kAesBlock, aes_cap = (u32)x11_device_cus() * 2 * 4;
   const dim3 aes_grid(aes_want < aes_cap ? aes_want : aes_cap), aes_block(kAesBlock);
   switch (stage) {
-    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n, ab); break;
+    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n); break;
     case kX11Simd: {
       const dim3 g8((8ull * n + kBlock - 1) / kBlock);
-      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n, ab);
+      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n);
       break;
     }
     case kX11Echo:

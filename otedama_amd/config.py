@@ -67,7 +67,9 @@ class MiningConfig:
     algorithm: str = "sha256d"          # sha256d | scrypt | x11
     gpus: str = "all"                   # "all", "none", or comma list of device indices
     cpu_threads: int = 0                # 0 = CPU miner only when no GPU is present
-    batch_nonces: int = 1 << 29         # per-launch nonce batch (share latency vs launch overhead)
+    batch_nonces: int = 1 << 32         # hashes per launch (SHA-256d): hits leave the GPU as they are found and new
+                                        # work aborts a running launch, so only the launch tail / per-wave set-up cost
+                                        # depends on it (2^32: ~0.22 s launches)
     version_rolling: bool = True        # BIP320 (negotiated with the pool)
     ntime_roll: int = 0
     sha_variants: int = 128             # SHA-256d header variants per GPU launch: 128 / 64 (version-parallel, two or

@@ -74,7 +74,7 @@ class _Framer:
 class DeviceProcess:
     """Parent-side handle with the native miner's interface (start/stop/set_job/poll/stats/share_fd)."""
 
-    def __init__(self, device_index: int, device_id: str, batch_nonces: int = 1 << 29, grid: int = 1536,
+    def __init__(self, device_index: int, device_id: str, batch_nonces: int = 1 << 32, grid: int = 1536,
                  queue_cap: int = 4096, sha_variants: int = 128, cpu_threads: int = 0, log=None,
                  on_exit=None, on_ready=None, env: dict | None = None):
         self.device_index = device_index
@@ -102,7 +102,7 @@ class DeviceProcess:
         self.ready_at = 0.0
         self.spawned_at = 0.0
         self.startup_seconds = 0.0       # spawn -> child reported its miner running
-        self.first_hash_wall = 0.0       # wall clock of the child's first completed batch
+        self.first_hash_wall = 0.0       # wall clock when the child's first batch was running
         self.child_timing: dict = {}     # wall clock: child main(), native module loaded, first batch done
 
     # ------------------------------------------------------------- lifecycle
@@ -273,7 +273,7 @@ def _child(argv: list[str]) -> int:
     ap.add_argument("--fd", type=int, required=True)
     ap.add_argument("--device", type=int, required=True)
     ap.add_argument("--id", required=True)
-    ap.add_argument("--batch", type=int, default=1 << 29)
+    ap.add_argument("--batch", type=int, default=1 << 32)
     ap.add_argument("--grid", type=int, default=1536)
     ap.add_argument("--queue-cap", type=int, default=4096)
     ap.add_argument("--sha-variants", type=int, default=128)
@@ -299,7 +299,7 @@ def _child(argv: list[str]) -> int:
     poller.register(efd, select.POLLIN)
     fr = _Framer()
     next_stats = 0.0
-    first_hash = False  # until the first batch completes: poll fast and report it at once (start-up timing)
+    first_hash = False  # until the first batch is running: poll fast and report it at once (start-up timing)
     rc = 0
     try:
         while True:
@@ -324,7 +324,8 @@ def _child(argv: list[str]) -> int:
                         m.set_job(msg.get("t"))
                     elif msg.get("op") == "stop":
                         return 0
-            if not first_hash and m.stats()["hashes"] > 0:
+            if not first_hash and (m.stats()["job_switches"] > 0 or m.stats()["hashes"] > 0):
+                # hashing has begun: the first batch of the first job is running on the device (CPU: counted)
                 first_hash = True
                 _send(sock, {"op": "first_hash", "wall": time.time(), "t_main": t_main, "t_native": t_native})
                 next_stats = 0.0

@@ -1,6 +1,6 @@
 """End-to-end share-latency and job-switch probes (BASELINE metric "p50 share latency").
 
-Share latency: the real engine mines on one GPU (default 2^29-nonce batches) against the local validating pool
+Share latency: the real engine mines on one GPU (default 2^32-hash launches) against the local validating pool
 running in a SEPARATE process (``otedama pool``), over loopback Stratum V2. Reported quantiles:
   * submit -> accept (the reference's definition: otedama_submit_latency_milliseconds,
     internal/engine/run.go:813-821);
@@ -91,7 +91,7 @@ async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, b
 
 
 def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm: str = "sha256d",
-                          shares_per_sec: float = 40.0, batch_nonces: int = 1 << 29,
+                          shares_per_sec: float = 40.0, batch_nonces: int = 1 << 32,
                           expected_hashrate: float = 19e9) -> dict:
     hashes_per_diff1 = 2.0 ** 16 if algorithm == "scrypt" else 2.0 ** 32  # scrypt pools: diff1 = 0xFFFF << 224
     diff = expected_hashrate / (shares_per_sec * hashes_per_diff1)
@@ -128,7 +128,7 @@ def _switch_job(seed: int, algorithm: str) -> dict:
 
 
 def measure_job_switch(device_index: int = 0, algorithm: str = "sha256d", switches: int = 8,
-                       dwell: float | None = None, batch_nonces: int = 1 << 29) -> dict:
+                       dwell: float | None = None, batch_nonces: int = 1 << 32) -> dict:
     """Hand the native miner new work ``switches`` times and report set_job -> new batch running."""
     from otedama_amd.ops.native import require_native
 

@@ -71,7 +71,7 @@ class DeviceMiner:
 
 
 class MinerSet:
-    def __init__(self, devices: list, algorithm: str = "sha256d", batch_nonces: int = 1 << 29,
+    def __init__(self, devices: list, algorithm: str = "sha256d", batch_nonces: int = 1 << 32,
                  cpu_threads: int = 0, rank: int = 0, world_size: int = 1, log=None, queue_cap: int = 4096,
                  stall_samples: int = 3, sha_variants: int = 128, isolation: str = "thread"):
         if isolation not in ("thread", "process"):
