@@ -274,14 +274,52 @@ def _add(p1, p2):
     return x3, (lam * (x1 - x3) - y1) % P
 
 
+def _jdouble(p1):
+    x, y, z = p1
+    if y == 0:
+        return 0, 1, 0
+    ysq = y * y % P
+    s = 4 * x * ysq % P
+    m = 3 * x * x % P  # a = 0
+    nx = (m * m - 2 * s) % P
+    return nx, (m * (s - nx) - 8 * ysq * ysq) % P, 2 * y * z % P
+
+
+def _jadd_affine(p1, x2, y2):
+    """Jacobian + affine (mixed addition); the infinity point is z = 0."""
+    x1, y1, z1 = p1
+    if z1 == 0:
+        return x2, y2, 1
+    z1z1 = z1 * z1 % P
+    u2 = x2 * z1z1 % P
+    s2 = y2 * z1 * z1z1 % P
+    h = (u2 - x1) % P
+    r = (s2 - y1) % P
+    if h == 0:
+        return _jdouble(p1) if r == 0 else (0, 1, 0)
+    hh = h * h % P
+    hhh = h * hh % P
+    v = x1 * hh % P
+    nx = (r * r - hhh - 2 * v) % P
+    return nx, (r * (v - nx) - y1 * hhh) % P, z1 * h % P
+
+
 def point_mul(pt, k: int):
-    r = None
-    while k:
-        if k & 1:
-            r = _add(r, pt)
-        pt = _add(pt, pt)
-        k >>= 1
-    return r
+    """k·pt in Jacobian coordinates (one field inversion at the end instead of one per step)."""
+    if pt is None or k % N == 0:
+        return None
+    x2, y2 = pt
+    acc = (0, 1, 0)
+    for bit in bin(k)[2:]:
+        acc = _jdouble(acc)
+        if bit == "1":
+            acc = _jadd_affine(acc, x2, y2)
+    x, y, z = acc
+    if z == 0:
+        return None
+    zi = pow(z, -1, P)
+    zi2 = zi * zi % P
+    return x * zi2 % P, y * zi2 * zi % P
 
 
 def lift_x(x: int):

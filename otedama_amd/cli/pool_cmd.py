@@ -67,6 +67,7 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs.string("http-addr", "", "Address for /metrics /healthz /api/v1/{pool,workers,blocks} (empty disables).")
     fs.string("dialect", "reference", "SV2 wire dialect: reference | spec.")
     fs.bool("sv2-noise", False, "Encrypt SV2 connections with Noise NX (miners pin the printed authority key).")
+    fs.string("noise-suite", "", "Noise suites accepted: empty = both, ellswift (current SV2) or legacy.")
     fs.string("noise-authority-key", "", "Hex secp256k1 secret signing the Noise certificate (empty = fresh per run).")
     fs.float("duration", 0.0, "Stop after this many seconds (0 = run until signalled).")
     fs.string("config", "", "Path to the YAML config file (default: $OTEDAMA_CONFIG or ~/.config/otedama/config.yaml).")
@@ -86,6 +87,9 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         if err:
             stderr.write(f"pool: payout address invalid: {err}\n")
             return EXIT_CONFIG
+    if fs["noise-suite"] not in ("", "ellswift", "legacy"):
+        stderr.write("pool: --noise-suite must be ellswift or legacy (empty accepts both)\n")
+        return EXIT_CONFIG
     if fs["noise-authority-key"]:
         from otedama_amd.btccrypto import N as CURVE_ORDER
 
@@ -119,7 +123,7 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
                            target_share_seconds=fs["share-seconds"], retarget_seconds=fs["retarget-seconds"],
                            block_interval=fs["block-interval"], job_interval=fs["job-interval"],
                            journal_path=journal or ":memory:", payout_scheme=fs["payout-scheme"],
-                           dialect=fs["dialect"], noise=fs["sv2-noise"],
+                           dialect=fs["dialect"], noise=fs["sv2-noise"], noise_suite=fs["noise-suite"],
                            coinbase_message=fs.values.get("coinbase-message", PoolOptions.coinbase_message),
                            noise_authority_secret=int(fs["noise-authority-key"] or "0", 16))
 

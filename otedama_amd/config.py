@@ -55,6 +55,8 @@ class PoolConfig:
     sv2_extended_channel: bool = False  # SV2 only: extended channel (miner-side extranonce rolling)
     noise: bool = False                 # SV2 only: Noise NX encryption (spec §4); implied by pool_pubkey
     pool_pubkey: str = ""               # SV2 only: pinned authority key (64 hex chars, x-only secp256k1)
+    noise_suite: str = "ellswift"       # SV2 Noise: "ellswift" (Noise_NX_Secp256k1+EllSwift_ChaChaPoly_SHA256, the
+                                        # current spec) or "legacy" (32-byte x-only keys, rounds 1-2 wire format)
 
 
 @dataclass
@@ -141,6 +143,8 @@ class Config:
                     issues.append(f"pools[{i}].url invalid: {err}")
             if (p.noise or p.pool_pubkey) and p.url and not p.url.startswith(("stratum+v2://", "stratum+v2tls://")):
                 issues.append(f"pools[{i}]: noise / pool_pubkey apply to stratum+v2 URLs only")
+            if p.noise_suite not in ("ellswift", "legacy"):
+                issues.append(f"pools[{i}].noise_suite {p.noise_suite!r} is not one of ellswift, legacy")
             if p.pool_pubkey and not _is_xonly_hex(p.pool_pubkey):
                 issues.append(f"pools[{i}].pool_pubkey must be 64 hex characters (x-only secp256k1 key)")
             if p.payout_scheme not in PAYOUT_SCHEMES:

@@ -558,7 +558,8 @@ class Engine:
                             nominal_hashrate=self.current_hashrate,
                             extended_channel=bool(pc.sv2_extended_channel) if pc is not None else False,
                             noise=bool(pc.noise) if pc is not None else False,
-                            pool_pubkey=bytes.fromhex(pc.pool_pubkey) if pc is not None and pc.pool_pubkey else b"")
+                            pool_pubkey=bytes.fromhex(pc.pool_pubkey) if pc is not None and pc.pool_pubkey else b"",
+                            noise_suite=pc.noise_suite if pc is not None else "ellswift")
         session = await self._dial(url, creds)
         self._session = session
         self.connected = True

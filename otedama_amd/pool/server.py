@@ -72,6 +72,7 @@ class PoolOptions:
     noise: bool = False
     noise_authority_secret: int = 0
     noise_cert_seconds: int = 365 * 86400
+    noise_suite: str = ""  # "" = accept both suites (by message 1's length); "ellswift" | "legacy" = only that one
 
 
 @dataclass
@@ -436,7 +437,8 @@ class PoolServer:
             from otedama_amd.stratum import noise
 
             try:
-                reader, writer = await noise.server_handshake(reader, writer, self._noise_static, self._noise_cert)
+                reader, writer = await noise.server_handshake(reader, writer, self._noise_static, self._noise_cert,
+                                                              suite=self.opts.noise_suite or None)
             except (noise.NoiseError, asyncio.IncompleteReadError, asyncio.TimeoutError, ConnectionError, OSError):
                 writer.close()
                 self.reject_reasons["noise-handshake"] = self.reject_reasons.get("noise-handshake", 0) + 1

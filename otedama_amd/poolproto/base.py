@@ -179,6 +179,7 @@ class Credentials:
     nominal_hashrate: float = 0.0
     extended_channel: bool = False   # SV2: open an extended channel and roll extranonce under the pool's prefix
     noise: bool = False              # SV2: Noise NX channel encryption (implied by a pinned pool_pubkey)
+    noise_suite: str = "ellswift"    # SV2 Noise suite: "ellswift" (BIP324 encodings, current spec) | "legacy"
 
 
 class Session(abc.ABC):

@@ -293,7 +293,8 @@ async def noise_connect(reader, writer, creds: Credentials, timeout: float, log=
     from otedama_amd.stratum import noise
 
     try:
-        er, ew, payload, static = await noise.client_handshake(reader, writer, timeout=timeout)
+        er, ew, payload, static = await noise.client_handshake(reader, writer, timeout=timeout,
+                                                               suite=creds.noise_suite or noise.DEFAULT_SUITE)
     except (noise.NoiseError, asyncio.IncompleteReadError, asyncio.TimeoutError) as exc:
         writer.close()
         raise HandshakeFailed(f"noise handshake: {exc}") from exc

@@ -1,4 +1,14 @@
-"""Noise_NX_secp256k1_ChaChaPoly_SHA256 for Stratum V2 (both roles) + encrypted streams.
+"""Noise NX for Stratum V2 (both roles) + encrypted streams, in two suites.
+
+  * ``ellswift`` (default): ``Noise_NX_Secp256k1+EllSwift_ChaChaPoly_SHA256``, the current SV2 suite. Every public
+    key on the wire is a 64-byte BIP324 ElligatorSwift encoding (stratum/ellswift.py) and each DH is BIP324's
+    x-only ``v2_ecdh`` (tagged hash of initiator encoding ‖ responder encoding ‖ shared x). Message 1 is 64 bytes,
+    message 2 is 64 + (64+16) + (payload+16) = 234 bytes with the 74-byte SignatureNoiseMessage.
+    Parity UNPINNED: no SV2/BIP324 test vectors are reachable offline; tests pin round trips and both-sides
+    agreement (tests/test_ellswift.py).
+  * ``legacy``: ``Noise_NX_secp256k1_ChaChaPoly_SHA256`` with 32-byte even-y x-only keys and raw x-coordinate DH
+    (round 1-2 wire format, kept for peers that speak it).
+The responder tells the suites apart by message 1's length (32 vs 64 bytes); the initiator picks one.
 
 Parity: internal/stratum/noise.go (and noise_pool.go)
   * HandshakeState / CipherState (ChaChaPoly, nonce = 0^4 ‖ LE64(n)) .. noise.go:50-90
@@ -25,9 +35,13 @@ import os
 import struct
 
 from otedama_amd import btccrypto as ec
+from otedama_amd.stratum import ellswift
 from otedama_amd.utils import aead
 
-PROTOCOL_NAME = b"Noise_NX_secp256k1_ChaChaPoly_SHA256"
+PROTOCOL_NAME = b"Noise_NX_secp256k1_ChaChaPoly_SHA256"          # legacy suite
+PROTOCOL_NAME_ELLSWIFT = b"Noise_NX_Secp256k1+EllSwift_ChaChaPoly_SHA256"
+SUITES = ("ellswift", "legacy")
+DEFAULT_SUITE = "ellswift"
 MAX_FRAME = 65535
 KEY_LEN = 32
 TAG = aead.TAG_BYTES
@@ -123,18 +137,45 @@ class SymmetricState:
 
 
 # ------------------------------------------------------------------ handshake
-class Initiator:
-    """Client side: -> e ; <- e, ee, s, es, payload."""
+def _suite(suite: str) -> str:
+    if suite not in SUITES:
+        raise NoiseError(f"noise: unknown suite {suite!r} (want one of {', '.join(SUITES)})")
+    return suite
 
-    def __init__(self, expected_static: bytes | None = None, prologue: bytes = b""):
-        self.ss = SymmetricState()
+
+def _ell_keypair(priv: int | None = None) -> tuple[int, bytes]:
+    while priv is None or not 0 < priv < ec.N:
+        priv = int.from_bytes(os.urandom(32), "big")
+    return priv, ellswift.create(priv)
+
+
+def _ell_xonly(enc: bytes) -> bytes:
+    return ellswift.decode(enc).to_bytes(32, "big")
+
+
+class Initiator:
+    """Client side: -> e ; <- e, ee, s, es, payload.
+
+    ``remote_static`` is the responder's 32-byte x-only static key in both suites (what certificates sign and what
+    ``expected_static`` pins); ``remote_static_wire`` is the key as it was sent (64-byte ElligatorSwift or 32)."""
+
+    def __init__(self, expected_static: bytes | None = None, prologue: bytes = b"", suite: str = DEFAULT_SUITE):
+        self.suite = _suite(suite)
+        self.klen = 64 if suite == "ellswift" else 32
+        self.ss = SymmetricState(PROTOCOL_NAME_ELLSWIFT if suite == "ellswift" else PROTOCOL_NAME)
         self.ss.mix_hash(prologue)
-        self.e, self.e_pub = keypair()
+        self.e, self.e_pub = _ell_keypair() if suite == "ellswift" else keypair()
         self.expected_static = expected_static
         self.remote_static = b""
+        self.remote_static_wire = b""
         self.payload = b""
         self.send: CipherState | None = None
         self.recv: CipherState | None = None
+
+    def _dh(self, priv: int, theirs: bytes, ours: bytes) -> bytes:
+        if self.suite == "ellswift":
+            return ellswift.xdh(priv, theirs, ours, initiating=True)
+        return dh(priv, theirs)
 
     def write_message1(self) -> bytes:
         self.ss.mix_hash(self.e_pub)
@@ -142,17 +183,19 @@ class Initiator:
         return self.e_pub
 
     def read_message2(self, msg: bytes) -> bytes:
-        if len(msg) < 32 + 32 + TAG + TAG:
+        k = self.klen
+        if len(msg) < k + k + TAG + TAG:
             raise NoiseError(f"noise: message2 too short ({len(msg)} bytes)")
-        re = msg[:32]
+        re = msg[:k]
         self.ss.mix_hash(re)
-        self.ss.mix_key(dh(self.e, re))                      # ee
-        rs = self.ss.decrypt_and_hash(msg[32:32 + 32 + TAG])  # s
-        if self.expected_static is not None and not hmac.compare_digest(rs, self.expected_static):
+        self.ss.mix_key(self._dh(self.e, re, self.e_pub))     # ee
+        rs = self.ss.decrypt_and_hash(msg[k:k + k + TAG])     # s
+        rs_x = _ell_xonly(rs) if self.suite == "ellswift" else rs
+        if self.expected_static is not None and not hmac.compare_digest(rs_x, self.expected_static):
             raise NoiseError("noise: responder static key does not match the pinned key")
-        self.ss.mix_key(dh(self.e, rs))                      # es
-        self.payload = self.ss.decrypt_and_hash(msg[32 + 32 + TAG:])
-        self.remote_static = rs
+        self.ss.mix_key(self._dh(self.e, rs, self.e_pub))     # es
+        self.payload = self.ss.decrypt_and_hash(msg[k + k + TAG:])
+        self.remote_static, self.remote_static_wire = rs_x, rs
         self.send, self.recv = self.ss.split()
         return self.payload
 
@@ -162,28 +205,45 @@ class Initiator:
 
 
 class Responder:
-    """Pool side, holding the long-term static key."""
+    """Pool side, holding the long-term static key. ``suite=None`` accepts either suite, chosen by the length of
+    message 1 (64 bytes: ElligatorSwift, 32: legacy); a fixed suite refuses the other."""
 
-    def __init__(self, static_priv: int, prologue: bytes = b""):
-        self.ss = SymmetricState()
-        self.ss.mix_hash(prologue)
-        self.s, self.s_pub = keypair(static_priv)
+    def __init__(self, static_priv: int, prologue: bytes = b"", suite: str | None = None):
+        self.suite = _suite(suite) if suite is not None else None
+        self.prologue = prologue
+        self.static_priv = static_priv
+        self.s_xonly = keypair(static_priv)[1]  # what pins and certificates name, in both suites
         self.send: CipherState | None = None
         self.recv: CipherState | None = None
+        self.ss: SymmetricState | None = None
+
+    def _dh(self, priv: int, theirs: bytes, ours: bytes) -> bytes:
+        if self.suite == "ellswift":
+            return ellswift.xdh(priv, theirs, ours, initiating=False)
+        return dh(priv, theirs)
 
     def read_message1(self, msg: bytes) -> None:
-        if len(msg) != 32:
-            raise NoiseError(f"noise: message1 must be 32 bytes, got {len(msg)}")
+        by_len = {64: "ellswift", 32: "legacy"}.get(len(msg))
+        if by_len is None or (self.suite is not None and by_len != self.suite):
+            want = {"ellswift": "64", "legacy": "32"}.get(self.suite or "", "32 or 64")
+            raise NoiseError(f"noise: message1 must be {want} bytes, got {len(msg)}")
+        self.suite = by_len
+        self.ss = SymmetricState(PROTOCOL_NAME_ELLSWIFT if by_len == "ellswift" else PROTOCOL_NAME)
+        self.ss.mix_hash(self.prologue)
+        if by_len == "ellswift":
+            self.s, self.s_pub = _ell_keypair(self.static_priv)
+        else:
+            self.s, self.s_pub = keypair(self.static_priv)
         self.re = msg
         self.ss.mix_hash(msg)
         self.ss.mix_hash(b"")
 
     def write_message2(self, payload: bytes = b"") -> bytes:
-        e, e_pub = keypair()
+        e, e_pub = _ell_keypair() if self.suite == "ellswift" else keypair()
         self.ss.mix_hash(e_pub)
-        self.ss.mix_key(dh(e, self.re))           # ee
+        self.ss.mix_key(self._dh(e, self.re, e_pub))           # ee
         enc_s = self.ss.encrypt_and_hash(self.s_pub)
-        self.ss.mix_key(dh(self.s, self.re))      # es
+        self.ss.mix_key(self._dh(self.s, self.re, self.s_pub))  # es
         enc_p = self.ss.encrypt_and_hash(payload)
         r, i = self.ss.split()
         self.send, self.recv = i, r               # responder sends with k2, receives with k1
@@ -265,9 +325,10 @@ async def _read_hs(reader: asyncio.StreamReader) -> bytes:
     return await reader.readexactly(n)
 
 
-async def client_handshake(reader, writer, expected_static: bytes | None = None, timeout: float = 10.0):
-    """Runs NX as initiator; returns (EncryptedReader, EncryptedWriter, server_payload, server_static)."""
-    hs = Initiator(expected_static)
+async def client_handshake(reader, writer, expected_static: bytes | None = None, timeout: float = 10.0,
+                           suite: str = DEFAULT_SUITE):
+    """Runs NX as initiator; returns (EncryptedReader, EncryptedWriter, server_payload, server_static x-only)."""
+    hs = Initiator(expected_static, suite=suite)
     m1 = hs.write_message1()
     writer.write(struct.pack("<H", len(m1)) + m1)
     await writer.drain()
@@ -275,9 +336,10 @@ async def client_handshake(reader, writer, expected_static: bytes | None = None,
     return EncryptedReader(reader, hs.recv), EncryptedWriter(writer, hs.send), payload, hs.remote_static
 
 
-async def server_handshake(reader, writer, static_priv: int, payload: bytes = b"", timeout: float = 10.0):
-    """Runs NX as responder; returns (EncryptedReader, EncryptedWriter)."""
-    hs = Responder(static_priv)
+async def server_handshake(reader, writer, static_priv: int, payload: bytes = b"", timeout: float = 10.0,
+                           suite: str | None = None):
+    """Runs NX as responder (either suite unless ``suite`` fixes one); returns (EncryptedReader, EncryptedWriter)."""
+    hs = Responder(static_priv, suite=suite)
     hs.read_message1(await asyncio.wait_for(_read_hs(reader), timeout))
     m2 = hs.write_message2(payload)
     writer.write(struct.pack("<H", len(m2)) + m2)

@@ -161,7 +161,10 @@ def test_config_pool_noise_fields_validate():
     good = "ab" * 32
     C.Config(bitcoin_address=ADDR, pools=[C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey=good)]).validate()
     C.Config(bitcoin_address=ADDR, pools=[C.PoolConfig(url="stratum+v2tls://p:3336", noise=True)]).validate()
-    for bad in (C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey="xyz"),
+    C.Config(bitcoin_address=ADDR, pools=[C.PoolConfig(url="stratum+v2://p:3336", noise=True,
+                                                       noise_suite="legacy")]).validate()
+    for bad in (C.PoolConfig(url="stratum+v2://p:3336", noise=True, noise_suite="p256"),
+                C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey="xyz"),
                 C.PoolConfig(url="stratum+v2://p:3336", pool_pubkey="ab" * 31),
                 C.PoolConfig(url="stratum+tcp://p:3333", noise=True)):
         with pytest.raises(C.ConfigError):

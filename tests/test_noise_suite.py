@@ -141,30 +141,33 @@ def test_empty_key_is_passthrough():
 
 
 # ------------------------------------------------------------------ handshake state machine
-def test_initiator_message1_and_transport_before_completion():
-    hs = N.Initiator()
+@pytest.mark.parametrize("suite,klen", [("ellswift", 64), ("legacy", 32)])
+def test_initiator_message1_and_transport_before_completion(suite, klen):
+    hs = N.Initiator(suite=suite)
     m1 = hs.write_message1()
-    assert len(m1) == 32 and m1 == hs.e_pub
+    assert len(m1) == klen and m1 == hs.e_pub
     assert hs.send is None and hs.recv is None  # no transport ciphers before message 2
 
 
-def test_read_message2_too_short():
-    hs = N.Initiator()
+@pytest.mark.parametrize("suite,klen", [("ellswift", 64), ("legacy", 32)])
+def test_read_message2_too_short(suite, klen):
+    hs = N.Initiator(suite=suite)
     hs.write_message1()
     with pytest.raises(N.NoiseError, match="too short"):
-        hs.read_message2(b"\x00" * (32 + 32 + 2 * N.TAG - 1))
+        hs.read_message2(b"\x00" * (klen + klen + 2 * N.TAG - 1))
 
 
-def test_message1_must_be_32_bytes():
+def test_message1_must_be_32_or_64_bytes():
     r = N.Responder(12345)
-    for n in (0, 31, 33, 65):
+    for n in (0, 31, 33, 63, 65):
         with pytest.raises(N.NoiseError):
             r.read_message1(b"\x02" * n)
 
 
 def test_message2_with_invalid_ephemeral_key():
+    """Legacy suite: x >= p is no curve point. (EllSwift has no invalid encodings: every 64 bytes decode.)"""
     r = N.Responder(12345)
-    i = N.Initiator()
+    i = N.Initiator(suite="legacy")
     r.read_message1(i.write_message1())
     m2 = bytearray(r.write_message2(b"p"))
     m2[:32] = b"\xff" * 32  # x >= p: not on the curve
@@ -172,12 +175,13 @@ def test_message2_with_invalid_ephemeral_key():
         i.read_message2(bytes(m2))
 
 
-def test_completed_handshake_transport_keys_cross_over():
+@pytest.mark.parametrize("suite", N.SUITES)
+def test_completed_handshake_transport_keys_cross_over(suite):
     r = N.Responder(987654321)
-    i = N.Initiator(expected_static=r.s_pub)
+    i = N.Initiator(expected_static=r.s_xonly, suite=suite)
     r.read_message1(i.write_message1())
     assert i.read_message2(r.write_message2(b"cert")) == b"cert"
-    assert i.handshake_hash == r.handshake_hash and i.remote_static == r.s_pub
+    assert i.handshake_hash == r.handshake_hash and i.remote_static == r.s_xonly
     assert i.send.k == r.recv.k and i.recv.k == r.send.k and i.send.k != i.recv.k
     assert r.recv.decrypt(b"", i.send.encrypt(b"", b"up")) == b"up"
     assert i.recv.decrypt(b"", r.send.encrypt(b"", b"down")) == b"down"

@@ -219,6 +219,12 @@ def test_sv2_over_noise_with_pinned_authority():
         assert any("not authenticated" in m for _, m in logs)
         await asyncio.wait_for(s2.jobs.get(), 5)
         await s2.close()
+        # the legacy 32-byte-key suite still authenticates against the same listener (it accepts both)
+        s3 = await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}",
+                                   Credentials(user=ADDR, pool_pubkey=pool.noise_authority_pub, noise_suite="legacy"))
+        assert isinstance(s3.reader, noise.EncryptedReader)
+        await asyncio.wait_for(s3.jobs.get(), 5)
+        await s3.close()
         # a plaintext client against a Noise listener fails the handshake instead of hanging
         with pytest.raises(Exception):
             await V2Dialer().dial(f"stratum+v2://{pool.addr_sv2}", Credentials(user=ADDR), timeout=2.0)
