@@ -66,6 +66,8 @@ class V2Session(Session):
         self.extranonce_prefix = b""
         self.extended = False          # extended channel: jobs carry the coinbase, submits carry our extranonce
         self.extranonce_size = 0
+        self._extranonce_total = 0     # prefix + miner part: fixed for the channel (spec §5.3.9)
+        self._prefix_epoch = 0         # bumped by SetExtranoncePrefix; tags the job ids handed to the miner
         self._jobs: dict[int, M.NewMiningJob] = {}
         self._active: M.NewMiningJob | None = None
         self._active_ntime = 0
@@ -138,6 +140,7 @@ class V2Session(Session):
                 raise HandshakeFailed(f"extended channel: unsupported extranonce size {resp.extranonce_size}")
             self.extended = True
             self.extranonce_prefix, self.extranonce_size = resp.extranonce_prefix, resp.extranonce_size
+            self._extranonce_total = len(resp.extranonce_prefix) + resp.extranonce_size
         else:
             self.extranonce_prefix = resp.extranonce
 
@@ -156,10 +159,15 @@ class V2Session(Session):
             await self._teardown()
 
     # ---------------------------------------------------------- state machine
+    def _job_id(self, pool_job_id: int) -> str:
+        """Job id as handed to the miner: the pool's id, tagged with the extranonce-prefix epoch once the pool has
+        replaced the prefix, so a share found under the old prefix is recognised at submit time."""
+        return str(pool_job_id) if self._prefix_epoch == 0 else f"{pool_job_id}~{self._prefix_epoch}"
+
     def _start_job(self, j, ntime: int) -> None:
         self._active, self._active_ntime = j, ntime
         if isinstance(j, M.NewExtendedMiningJob):  # coinbase + merkle path: the miner builds the root per extranonce
-            job = Job(job_id=str(j.job_id), version=j.version, prev_hash=self._prev_hash, merkle_root=None,
+            job = Job(job_id=self._job_id(j.job_id), version=j.version, prev_hash=self._prev_hash, merkle_root=None,
                       ntime=ntime, nbits=self._nbits, clean_jobs=True, target=self.share_target,
                       version_mask=self.version_mask if j.version_rolling_allowed else 0, channel_id=self.channel_id,
                       coinb1=j.coinbase_prefix, coinb2=j.coinbase_suffix, extranonce1=self.extranonce_prefix,
@@ -211,12 +219,25 @@ class V2Session(Session):
             if ent is not None and not ent[0].done():
                 ent[0].set_result(ShareResult(False, msg.error, latency_ms=(time.perf_counter() - ent[1]) * 1e3))
         elif isinstance(msg, M.SetExtranoncePrefix):
-            # spec §5.3.9: a new prefix for this channel's extranonce space. On an extended channel the active job
-            # is re-issued (clean) so the miner rebuilds every coinbase under the new prefix; a standard channel's
-            # merkle roots come from the pool and change with its next job.
+            # spec §5.3.9: a new prefix for this channel's extranonce space. The channel's total extranonce length
+            # is fixed, so the miner's rollable part is what the new prefix leaves. On an extended channel the active
+            # job is re-issued (clean) under a new prefix epoch: the miner rebuilds every coinbase under the new
+            # prefix and shares found under the old one are dropped at submit instead of being sent to be rejected.
+            # A standard channel's merkle roots come from the pool and change with its next job.
             if msg.channel_id == self.channel_id:
-                self.extranonce_prefix = bytes(msg.extranonce_prefix)
-                self.log("info", "engine: extranonce prefix updated by pool")
+                prefix = bytes(msg.extranonce_prefix)
+                if self.extended:
+                    size = self._extranonce_total - len(prefix)
+                    if not 0 < size <= 8:
+                        self.log("error", f"engine: SetExtranoncePrefix leaves {size} extranonce bytes "
+                                          f"(prefix {len(prefix)} of {self._extranonce_total}); closing the session")
+                        asyncio.ensure_future(self.close())
+                        return
+                    self.extranonce_size = size
+                self.extranonce_prefix = prefix
+                self._prefix_epoch += 1
+                self.log("info", f"engine: extranonce prefix updated by pool ({len(prefix)} bytes, "
+                                 f"{self.extranonce_size} rollable)")
                 if self.extended and self._active is not None and self._have_prev:
                     self._start_job(self._active, self._active_ntime)
         elif isinstance(msg, M.Reconnect):
@@ -228,10 +249,13 @@ class V2Session(Session):
     async def submit(self, sub: ShareSubmission, timeout: float = 30.0) -> ShareResult:
         if self._closed:
             raise PoolProtoError("stratumv2: session closed")
+        jid, _, ep = str(sub.job_id).partition("~")
         try:
-            job_id = int(sub.job_id)
+            job_id, epoch = int(jid), int(ep or 0)
         except ValueError:
             return ShareResult(False, f"stale-job (unknown job id {sub.job_id!r})")
+        if self.extended and epoch != self._prefix_epoch:
+            return ShareResult(False, "stale-prefix (found under a replaced extranonce prefix; not submitted)")
         self._seq = (self._seq + 1) & 0xFFFFFFFF
         seq = self._seq
         fut = asyncio.get_running_loop().create_future()

@@ -367,9 +367,38 @@ def test_set_extranonce_prefix_reissues_the_extended_job():
         first = await _next_job(s)
         again = await _next_job(s)
         assert first.extranonce1 == b"\x09\x09"
-        assert again.job_id == "3" and again.clean_jobs and again.extranonce1 == b"\x0a\x0b\x0c"
+        # total extranonce = 2 + 4 = 6 bytes; a 3-byte prefix leaves 3 rollable, and the re-issued job carries the
+        # new prefix epoch in its id so a share found under the old prefix is dropped instead of being rejected
+        assert again.job_id == "3~1" and again.clean_jobs and again.extranonce1 == b"\x0a\x0b\x0c"
+        assert again.extranonce2_size == 3 and s.extranonce_size == 3
         assert s.extranonce_prefix == b"\x0a\x0b\x0c" and s.jobs.empty()
+        n_sent = len(pool.got)
+        r = await s.submit(B.ShareSubmission(first.job_id, 1, 10, 0x20000000, b"\xaa\xbb\xcc\xdd"))
+        assert not r.accepted and "stale-prefix" in r.reason
+        await asyncio.sleep(0.05)
+        assert len(pool.got) == n_sent  # nothing went to the pool
         await s.close()
+        await pool.stop()
+    run(go())
+
+
+def test_set_extranonce_prefix_leaving_no_rollable_bytes_closes_the_session():
+    async def script(pool):
+        await pool.send(M.NewExtendedMiningJob(7, 3, False, 0, 0x20000000, True, [ROOT], b"\x01" * 10, b"\x02" * 10))
+        await pool.send(M.SetNewPrevHash(7, 3, PREV, 10, 0x1d00ffff))
+        await asyncio.sleep(0.1)
+        await pool.send(M.SetExtranoncePrefix(7, b"\x0a" * 6))  # 6 of 6 bytes: nothing left to roll
+        await asyncio.sleep(0.5)
+
+    async def go():
+        pool = Pool(open_reply=M.OpenExtendedMiningChannelSuccess(1, 7, T1, 4, b"\x09\x09"), script=script)
+        s = await _dial(pool, extended_channel=True)
+        await _next_job(s)
+        for _ in range(50):
+            if s.closed:
+                break
+            await asyncio.sleep(0.02)
+        assert s.closed and s.extranonce_prefix == b"\x09\x09"
         await pool.stop()
     run(go())
 
