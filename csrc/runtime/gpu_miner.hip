@@ -159,7 +159,17 @@ void GpuMiner::stop() {
 
 void GpuMiner::loop() {
   trace_name_thread(("otedama-" + device_id_).c_str());
+  double t_phase = monotonic_seconds();
+  const double t_loop = t_phase;
+  auto phase = [&](const char* name) {
+    const double now = monotonic_seconds();
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.startup_ms.emplace_back(name, (now - t_phase) * 1e3);
+    t_phase = now;
+  };
   OTD_HIP(hipSetDevice(device_));
+  OTD_HIP(hipFree(nullptr));  // force runtime / context creation here so the phase below is honest
+  phase("hip_set_device");
   hipStream_t ctl = nullptr, cal = nullptr;
   Batch slots[kInflight];
   uint32_t* d_abort = nullptr;   // uncached device word: the newest launch epoch that must keep running
@@ -230,6 +240,7 @@ void GpuMiner::loop() {
       OTD_HIP(hipHostMalloc(&s.h_vars, kSha256dV2Group * sizeof(Sha256dVariant), hipHostMallocDefault));
     }
   }
+  phase("buffers");
   const int cus = gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256;
   // Lane-cooperative full-line ROMix (gap 1, nt pad traffic, 16 blocks/CU = 128 GiB of HBM): ~16.75 MH/s vs
   // 13.6-14.0 for the per-lane kernels at gap 1/2 (profiles/r1/scrypt_romix_ab.md).
@@ -268,6 +279,8 @@ void GpuMiner::loop() {
   };
   for (int t = 0; t < 8; ++t) probe(slots[0].stream);
   rt_offset_ = rt_offset.load();
+  phase("clock_calibration");
+  bool first_switch = true;
   cal_th = std::thread([&] {
     try {
       OTD_HIP(hipSetDevice(device_));
@@ -336,10 +349,11 @@ void GpuMiner::loop() {
     std::memcpy(hdr, b.group->header[vi], 80);
     store_le32(hdr + 76, nonce);
     ShareRecord r{};
-    // the job's current target: a target-only update (same work generation) applies to batches in flight too
-    const uint8_t* target = (cur && cur_g == b.gen) ? cur->target : b.job->target;
-    if (!verify_share(b.job->algo, hdr, target, r.hash)) { ++*bad; return; }
-    r.epoch = b.job->epoch; r.job_id = b.job->job_id; r.channel_id = b.job->channel_id;
+    // A target-only update (same work generation) applies to batches in flight too: their hits are checked
+    // against, and reported under, the current template (its target and control-plane epoch).
+    const JobTemplate* tj = (cur && cur_g == b.gen) ? cur.get() : b.job.get();
+    if (!verify_share(b.job->algo, hdr, tj->target, r.hash)) { ++*bad; return; }
+    r.epoch = tj->epoch; r.job_id = tj->job_id; r.channel_id = tj->channel_id;
     r.nonce = nonce; r.ntime = b.group->ntime[vi]; r.version = b.group->version[vi]; r.extranonce2 = b.group->en2[vi];
     r.extranonce2_size = b.job->extranonce2_size; r.device_id = device_id_;
     r.found_at = monotonic_seconds();
@@ -602,6 +616,13 @@ void GpuMiner::loop() {
         const double ms = (monotonic_seconds() - switch_t0) * 1e3;
         switch_pending = false;
         std::lock_guard<std::mutex> g(stats_mu_);
+        if (first_switch) {
+          first_switch = false;
+          double before = 0;  // the phases above, so the wait is what is left of loop start -> set_job
+          for (const auto& kv : stats_.startup_ms) before += kv.second;
+          stats_.startup_ms.emplace_back("wait_first_job", std::max(0.0, (switch_t0 - t_loop) * 1e3 - before));
+          stats_.startup_ms.emplace_back("first_batch", ms);
+        }
         stats_.job_switches += 1;
         stats_.last_job_switch_ms = ms;
         stats_.job_switch_ms.push_back(ms);

@@ -104,6 +104,7 @@ class DeviceProcess:
         self.startup_seconds = 0.0       # spawn -> child reported its miner running
         self.first_hash_wall = 0.0       # wall clock when the child's first batch was running
         self.child_timing: dict = {}     # wall clock: child main(), native module loaded, first batch done
+        self.native_startup_ms: dict = {}  # the native miner thread's own phases (hip_set_device, buffers, ...)
 
     # ------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -205,6 +206,7 @@ class DeviceProcess:
         st["startup_seconds"] = self.startup_seconds
         st["first_hash_wall"] = self.first_hash_wall
         st["child_timing"] = dict(self.child_timing)
+        st["native_startup_ms"] = dict(self.native_startup_ms)
         return st
 
     # ------------------------------------------------------------- plumbing
@@ -243,7 +245,9 @@ class DeviceProcess:
                 elif op == "first_hash":
                     self.first_hash_wall = float(m.get("wall", 0.0))
                     self.child_timing = {"main": m.get("t_main", 0.0), "native_loaded": m.get("t_native", 0.0),
+                                         "miner_started": m.get("t_started", 0.0), "first_job": m.get("t_job", 0.0),
                                          "first_hash": self.first_hash_wall}
+                    self.native_startup_ms = dict(m.get("native_ms") or {})
                 elif op == "ready":
                     self.ready_at = time.monotonic()
                     self.startup_seconds = self.ready_at - self.spawned_at
@@ -292,6 +296,8 @@ def _child(argv: list[str]) -> int:
         m = N.GpuMiner(a.device, a.id, batch_nonces=a.batch, grid=a.grid, queue_cap=a.queue_cap,
                        sha_variants=a.sha_variants)
     m.start()
+    t_started = time.time()
+    t_job = 0.0
     _send(sock, {"op": "ready", "pid": os.getpid()})
     efd = m.share_fd()
     poller = select.poll()
@@ -322,12 +328,15 @@ def _child(argv: list[str]) -> int:
                 for msg in fr.feed(data):
                     if msg.get("op") == "job":
                         m.set_job(msg.get("t"))
+                        t_job = t_job or time.time()
                     elif msg.get("op") == "stop":
                         return 0
             if not first_hash and (m.stats()["job_switches"] > 0 or m.stats()["hashes"] > 0):
                 # hashing has begun: the first batch of the first job is running on the device (CPU: counted)
                 first_hash = True
-                _send(sock, {"op": "first_hash", "wall": time.time(), "t_main": t_main, "t_native": t_native})
+                _send(sock, {"op": "first_hash", "wall": time.time(), "t_main": t_main, "t_native": t_native,
+                             "t_started": t_started, "t_job": t_job,
+                             "native_ms": dict(m.stats().get("startup_ms", {}))})
                 next_stats = 0.0
             if time.monotonic() >= next_stats:
                 st = m.stats()

@@ -235,15 +235,23 @@ class Engine:
         except Exception:  # noqa: BLE001 - psutil missing or a child gone
             t0 = 0.0
         ms = self.miners
-        firsts, phases = {}, {}
+        firsts, phases, native = {}, {}, {}
         for m in getattr(ms, "miners", []) or []:
             wall = float(getattr(m.native, "first_hash_wall", 0.0) or 0.0)
             if wall and t0:
                 firsts[m.id] = wall - t0
                 ct = getattr(m.native, "child_timing", {}) or {}
                 phases[m.id] = {k: (v - t0) if v else None for k, v in ct.items()}
+            try:
+                nat = m.native.stats().get("native_startup_ms") or m.native.stats().get("startup_ms")
+            except Exception:  # noqa: BLE001 - a miner without stats
+                nat = None
+            if nat:
+                native[m.id] = dict(nat)
         out["first_hash_after_start_s"] = firsts
-        out["device_process_phases_s"] = phases  # seconds after engine start: child main, native loaded, 1st batch
+        # seconds after engine start: child main, native loaded, miner started, first job in, first batch running
+        out["device_process_phases_s"] = phases
+        out["native_phases_ms"] = native  # inside the device thread: hip_set_device, buffers, clock_calibration, ...
         return out
 
     def device_list(self) -> list[dict]:

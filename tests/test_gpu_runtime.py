@@ -153,3 +153,27 @@ def test_scrypt_switch_stops_the_romix_batch():
     assert st["aborted_launches"] >= 1
     for s in shares[:40]:
         _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target, "scrypt")
+
+
+def test_startup_phases_are_recorded():
+    """The device thread times its own start-up (start -> first GPU hash): HIP context, buffers,
+    clock calibration, the wait for the first job and the first batch (set_job -> running, incl. code-object load)."""
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    t0 = time.monotonic()
+    m = N.GpuMiner(0, "gpu-0")
+    m.start()
+    try:
+        m.set_job(_job(hdr, (1 << 190) - 1, 1, "t"))
+        while time.monotonic() - t0 < 20 and m.stats()["job_switches"] < 1:
+            time.sleep(0.002)
+        wall = time.monotonic() - t0
+        st = m.stats()
+    finally:
+        m.stop()
+    assert not st["faulted"], st
+    ph = st["startup_ms"]
+    print("startup phases ms:", {k: round(v, 2) for k, v in ph.items()}, "construct->first batch s:", round(wall, 3))
+    assert list(ph) == ["hip_set_device", "buffers", "clock_calibration", "wait_first_job", "first_batch"]
+    assert all(v >= 0 for v in ph.values())
+    assert sum(ph.values()) <= wall * 1e3 + 50
