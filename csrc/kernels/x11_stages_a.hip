@@ -361,19 +361,26 @@ __device__ __forceinline__ void jh_round(u32 x[8][4], const u32* c) {
   }
 }
 
-__device__ __forceinline__ void jh_E8(u32 x[8][4]) {
+// BC: the 42 x 8 round constants. The kernel stages them in LDS so each round's eight words arrive in VGPRs by
+// ds_read (no VALU): from the scalar cache they needed a v_mov per word (8 per round, 5.5% of JH's VALU), and an
+// SGPR operand would put v_bitop3 in the slow issue class (profiles/r1/x11/NOTES.md).
+__device__ __forceinline__ void jh_E8(u32 x[8][4], const u32 (*BC)[8]) {
   for (int r = 0; r < 42; r += 7) {
-    jh_round<0>(x, x11t::JH_BC[r + 0]);
-    jh_round<1>(x, x11t::JH_BC[r + 1]);
-    jh_round<2>(x, x11t::JH_BC[r + 2]);
-    jh_round<3>(x, x11t::JH_BC[r + 3]);
-    jh_round<4>(x, x11t::JH_BC[r + 4]);
-    jh_round<5>(x, x11t::JH_BC[r + 5]);
-    jh_round<6>(x, x11t::JH_BC[r + 6]);
+    jh_round<0>(x, BC[r + 0]);
+    jh_round<1>(x, BC[r + 1]);
+    jh_round<2>(x, BC[r + 2]);
+    jh_round<3>(x, BC[r + 3]);
+    jh_round<4>(x, BC[r + 4]);
+    jh_round<5>(x, BC[r + 5]);
+    jh_round<6>(x, BC[r + 6]);
   }
 }
 
-__device__ __forceinline__ void jh512_64(u64 h[8]) {
+// kReload: re-read the message words from H for the second injection instead of keeping them live across E8
+// (16 fewer VGPRs; variant measured by tools/x11_variants.hip).
+template <bool kReload = false>
+__device__ __forceinline__ void jh512_64(u64 h[8], const u32 (*BC)[8], const u64* __restrict__ Hb = nullptr,
+                                         u32 stride = 0, u32 i = 0) {
   u32 m[16];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { m[2 * k] = lo32(h[k]); m[2 * k + 1] = hi32(h[k]); }
@@ -382,13 +389,19 @@ __device__ __forceinline__ void jh512_64(u64 h[8]) {
   for (int k = 0; k < 32; ++k) x[k / 4][k % 4] = x11t::JH_IV[k];
 #pragma unroll
   for (int k = 0; k < 16; ++k) x[k / 4][k % 4] ^= m[k];
-  jh_E8(x);
+  jh_E8(x, BC);
+  if (kReload) {
+    u64 r[8];
+    load_hash(Hb, stride, i, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { m[2 * k] = lo32(r[k]); m[2 * k + 1] = hi32(r[k]); }
+  }
 #pragma unroll
   for (int k = 0; k < 16; ++k) x[4 + k / 4][k % 4] ^= m[k];
   // padding block: 0x80, zeros, 128-bit big-endian bit length (512)
   x[0][0] ^= 0x80u;
   x[3][3] ^= 0x00020000u;
-  jh_E8(x);
+  jh_E8(x, BC);
   x[4][0] ^= 0x80u;
   x[7][3] ^= 0x00020000u;
 #pragma unroll
@@ -644,11 +657,51 @@ __device__ __forceinline__ void cubehash512_64(u64 h[8]) {
   }
 X11_STAGE_KERNEL(k_bmw512_64, bmw512_64)
 X11_STAGE_KERNEL(k_skein512_64, skein512_64)
-X11_STAGE_KERNEL(k_jh512_64, jh512_64)
 X11_STAGE_KERNEL(k_keccak512_64, keccak512_64)
 X11_STAGE_KERNEL(k_luffa512_64, luffa512_64)
 X11_STAGE_KERNEL(k_cubehash512_64, cubehash512_64)
 #undef X11_STAGE_KERNEL
+
+__device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u32 n, bool reload) {
+  __shared__ __attribute__((aligned(16))) u32 BC[42][8];
+  for (u32 t = threadIdx.x; t < 42 * 8; t += kBlock) BC[t / 8][t % 8] = x11t::JH_BC[t / 8][t % 8];
+  __syncthreads();
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  if (reload) jh512_64<true>(h, BC, Hb, stride, i);
+  else jh512_64(h, BC);
+  store_hash(Hb, stride, i, h);
+}
+// LDS constants, message re-read, 7 waves/SIMD (72 VGPRs, 44 B of spills outside the round loops): 1.93 ms per
+// 2^23 vs 1.97 for the scalar-cache constants at 7 waves and 2.00 for LDS constants at 5 waves
+// (tools/x11_variants.hip, profiles/r3/h_jh/).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, true);
+}
+#ifdef OTEDAMA_X11_VARIANTS
+// Alternatives timed by tools/x11_variants.hip (not built into the extension).
+__global__ __launch_bounds__(kBlock) void k_jh512_64_sgpr(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;  // round constants through the scalar cache + v_mov
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  jh512_64(h, x11t::JH_BC);
+  store_hash(Hb, stride, i, h);
+}
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64_w7(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, false);
+}
+__global__ __launch_bounds__(kBlock) void k_jh512_64_reload(u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, true);
+}
+__global__ __launch_bounds__(kBlock) void k_jh512_64_lds(u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, false);
+}
+#endif
 
 __global__ __launch_bounds__(kBlock) void k_blake512_80(X11Params p, u32 base, u64* __restrict__ H, u32 stride, u32 n,
                                                        X11Abort ab) {

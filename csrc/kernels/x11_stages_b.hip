@@ -33,13 +33,50 @@ __device__ __forceinline__ void shavite_F(const u32* T, u32 lo, u32 x[4], const 
   aes_round(T, lo, x[0], x[1], x[2], x[3]);
 }
 
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  __shared__ u32 T[kAesPrivWords];
-  aes_priv_fill(T);
-  const u32 lo = aes_laneoff();
-  for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
-  u64 h[8];
-  load_hash(Hb, stride, i, h);
+// Key schedule, odd rounds: the AES-based step on the rolling 32-word window. The counter {512, 0, 0, 0} enters at
+// rounds 1, 5, 9, 13 (kInj 0..3), right after the word group that the spec mixes it into.
+template <int kInj>
+__device__ __forceinline__ void shavite_rk_odd(const u32* T, u32 lo, u32 rk[32]) {
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    u32 t0 = rk[4 * g + 1], t1 = rk[4 * g + 2], t2 = rk[4 * g + 3], t3 = rk[4 * g];
+    aes_round(T, lo, t0, t1, t2, t3);
+    const int p = g ? 4 * g - 4 : 28;
+    rk[4 * g] = t0 ^ rk[p];
+    rk[4 * g + 1] = t1 ^ rk[p + 1];
+    rk[4 * g + 2] = t2 ^ rk[p + 2];
+    rk[4 * g + 3] = t3 ^ rk[p + 3];
+    if (kInj == 0 && g == 0) { rk[0] ^= 512u; rk[3] = ~rk[3]; }
+    if (kInj == 1 && g == 1) { rk[7] ^= ~512u; }
+    if (kInj == 2 && g == 7) { rk[30] ^= 512u; rk[31] = ~rk[31]; }
+    if (kInj == 3 && g == 6) { rk[25] ^= 512u; rk[27] = ~rk[27]; }
+  }
+}
+// Key schedule, even rounds: rk[i] = rk[i - 32] ^ rk[i - 7] on the window.
+__device__ __forceinline__ void shavite_rk_even(u32 rk[32]) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) rk[k] ^= k >= 7 ? rk[k - 7] : rk[k + 25];
+}
+// One round on the state (a, b, c, d): a ^= F(b, rk[0..15]), c ^= F(d, rk[16..31]); the next round's state is
+// (d, a, b, c), which the caller realises by passing the arrays in that order (no register moves).
+__device__ __forceinline__ void shavite_round(const u32* T, u32 lo, const u32 rk[32], u32 a[4], const u32 b[4],
+                                              u32 c[4], const u32 d[4]) {
+  u32 x[4] = {b[0], b[1], b[2], b[3]};
+  shavite_F(T, lo, x, rk);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] ^= x[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = d[k];
+  shavite_F(T, lo, x, rk + 16);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c[k] ^= x[k];
+}
+
+// 14 rounds: round 0, three trips of rounds 4t+1 .. 4t+4 (odd, even, odd, even: the state rotation closes after
+// four rounds, so the rolled loop carries no register moves), round 13. The one-round rolled loop it replaces spent
+// ~85 v_mov per round on the rotation and the schedule window (18% of SHAvite's VALU; tools/x11_variants.hip).
+template <bool kLegacy>
+__device__ __forceinline__ void shavite512_64(const u32* T, u32 lo, u64 h[8]) {
   // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
   u32 rk[32];
 #pragma unroll
@@ -54,40 +91,48 @@ __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4)
   for (int k = 0; k < 4; ++k) {
     A[k] = kShaviteIv[k]; B[k] = kShaviteIv[4 + k]; C[k] = kShaviteIv[8 + k]; D[k] = kShaviteIv[12 + k];
   }
-  // counter = {512, 0, 0, 0}
+  if (kLegacy) {
+    // counter = {512, 0, 0, 0}
 #pragma unroll 1
-  for (int r = 0; r < 14; ++r) {
-    if (r & 1) {
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        u32 t0 = rk[4 * g + 1], t1 = rk[4 * g + 2], t2 = rk[4 * g + 3], t3 = rk[4 * g];
-        aes_round(T, lo, t0, t1, t2, t3);
-        const int p = g ? 4 * g - 4 : 28;
-        rk[4 * g] = t0 ^ rk[p];
-        rk[4 * g + 1] = t1 ^ rk[p + 1];
-        rk[4 * g + 2] = t2 ^ rk[p + 2];
-        rk[4 * g + 3] = t3 ^ rk[p + 3];
-        if (g == 0 && r == 1) { rk[0] ^= 512u; rk[3] = ~rk[3]; }
-        if (g == 1 && r == 5) { rk[7] ^= ~512u; }
-        if (g == 7 && r == 9) { rk[30] ^= 512u; rk[31] = ~rk[31]; }
-        if (g == 6 && r == 13) { rk[25] ^= 512u; rk[27] = ~rk[27]; }
+    for (int r = 0; r < 14; ++r) {
+      if (r & 1) {
+        if (r == 1) shavite_rk_odd<0>(T, lo, rk);
+        else if (r == 5) shavite_rk_odd<1>(T, lo, rk);
+        else if (r == 9) shavite_rk_odd<2>(T, lo, rk);
+        else if (r == 13) shavite_rk_odd<3>(T, lo, rk);
+        else shavite_rk_odd<-1>(T, lo, rk);
+      } else if (r) {
+        shavite_rk_even(rk);
       }
-    } else if (r) {
+      shavite_round(T, lo, rk, A, B, C, D);
 #pragma unroll
-      for (int k = 0; k < 32; ++k) rk[k] ^= k >= 7 ? rk[k - 7] : rk[k + 25];
+      for (int k = 0; k < 4; ++k) {
+        const u32 t = D[k];
+        D[k] = C[k]; C[k] = B[k]; B[k] = A[k]; A[k] = t;
+      }
     }
-    u32 x[4] = {B[0], B[1], B[2], B[3]};
-    shavite_F(T, lo, x, rk);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) A[k] ^= x[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = D[k];
-    shavite_F(T, lo, x, rk + 16);
+  } else {
+    shavite_round(T, lo, rk, A, B, C, D);  // round 0: the message block itself
+#pragma unroll 1
+    for (int t = 0; t < 3; ++t) {
+      if (t == 0) shavite_rk_odd<0>(T, lo, rk);
+      else if (t == 1) shavite_rk_odd<1>(T, lo, rk);
+      else shavite_rk_odd<2>(T, lo, rk);
+      shavite_round(T, lo, rk, D, A, B, C);
+      shavite_rk_even(rk);
+      shavite_round(T, lo, rk, C, D, A, B);
+      shavite_rk_odd<-1>(T, lo, rk);
+      shavite_round(T, lo, rk, B, C, D, A);
+      shavite_rk_even(rk);
+      shavite_round(T, lo, rk, A, B, C, D);
+    }
+    shavite_rk_odd<3>(T, lo, rk);
+    shavite_round(T, lo, rk, D, A, B, C);
+    // the state after round 13 is (C, D, A, B) in the spec's order
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      C[k] ^= x[k];
-      const u32 t = D[k];
-      D[k] = C[k]; C[k] = B[k]; B[k] = A[k]; A[k] = t;
+      const u32 a = C[k], b = D[k];
+      C[k] = A[k]; D[k] = B[k]; A[k] = a; B[k] = b;
     }
   }
 #pragma unroll
@@ -97,9 +142,30 @@ __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4)
     h[4 + k] = mk64(kShaviteIv[8 + 2 * k] ^ C[2 * k], kShaviteIv[9 + 2 * k] ^ C[2 * k + 1]);
     h[6 + k] = mk64(kShaviteIv[12 + 2 * k] ^ D[2 * k], kShaviteIv[13 + 2 * k] ^ D[2 * k + 1]);
   }
-  store_hash(Hb, stride, i, h);
+}
+
+template <bool kLegacy>
+__device__ __forceinline__ void shavite_stage(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u32 T[kAesPrivWords];
+  aes_priv_fill(T);
+  const u32 lo = aes_laneoff();
+  for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
+    u64 h[8];
+    load_hash(Hb, stride, i, h);
+    shavite512_64<kLegacy>(T, lo, h);
+    store_hash(Hb, stride, i, h);
   }
 }
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  shavite_stage<false>(Hb, stride, n);
+}
+#ifdef OTEDAMA_X11_VARIANTS
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64_rolled(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  shavite_stage<true>(Hb, stride, n);
+}
+#endif
 
 // ------------------------------------------------------------------ SIMD-512
 constexpr u32 kSimdIv[32] = {

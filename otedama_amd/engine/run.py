@@ -135,6 +135,7 @@ class Engine:
         self.registry.register_collector(runtime_collector())
         self.algorithm = get_algorithm(self.cfg.mining.algorithm)
         self.start_time = opts.clock.now()
+        self._marks: dict[str, float] = {}
         self.devices: list = []
         self.miners: MinerSet | None = None
         self.curtailed = False
@@ -252,6 +253,9 @@ class Engine:
         # seconds after engine start: child main, native loaded, miner started, first job in, first batch running
         out["device_process_phases_s"] = phases
         out["native_phases_ms"] = native  # inside the device thread: hip_set_device, buffers, clock_calibration, ...
+        # this process: run() entered, devices named, miners (device processes) started, pool dial / connected,
+        # first job handed to the devices; seconds after process start
+        out["engine_phases_s"] = {k: (v - t0) for k, v in self._marks.items()} if t0 else {}
         return out
 
     def device_list(self) -> list[dict]:
@@ -259,8 +263,13 @@ class Engine:
                  "model": d.identity().model, "capabilities": d.capabilities().__dict__} for d in self.devices]
 
     # ---------------------------------------------------------------- run
+    def _mark(self, name: str) -> None:
+        """Wall time of the first occurrence of a start-up event (engine_phases_s in /debug/stats)."""
+        self._marks.setdefault(name, time.time())
+
     async def run(self) -> None:
         cfg = self.cfg
+        self._mark("run")
         self.m.uptime.set(0)
         self.m.start_time.set(self.start_time)
         if cfg.power_watts > 0 and cfg.electricity_price_per_kwh > 0:
@@ -271,6 +280,7 @@ class Engine:
             self.devices = self.opts.devices if self.opts.devices is not None else await asyncio.to_thread(
                 self._detect_devices)
             self.log("info", f"engine: detected {len(self.devices)} device(s)")
+            self._mark("devices_detected")
             for d in self.devices:
                 self.log("info", f"engine: device {d.identity()} caps={d.capabilities()}")
             node = self.opts.node_comm
@@ -289,6 +299,7 @@ class Engine:
             if len(self.miners) == 0:
                 raise RuntimeError(f"engine: no device can mine {self.algorithm.name}")
             self.miners.start()
+            self._mark("miners_started")
             if self._rate_fetcher is None:
                 from otedama_amd.rates import Fetcher
 
@@ -568,7 +579,9 @@ class Engine:
                             noise=bool(pc.noise) if pc is not None else False,
                             pool_pubkey=bytes.fromhex(pc.pool_pubkey) if pc is not None and pc.pool_pubkey else b"",
                             noise_suite=pc.noise_suite if pc is not None else "ellswift")
+        self._mark("pool_dial")
         session = await self._dial(url, creds)
+        self._mark("pool_connected")
         self._session = session
         self.connected = True
         self.m.pool_connection_state.set(2)
@@ -619,6 +632,7 @@ class Engine:
                 self.log("debug", f"engine: job {job.job_id} ignored (curtailed)")
                 continue
             self.miners.set_job(job.template())
+            self._mark("first_job_to_devices")
             self.log("info", f"engine: job {job.job_id} version=0x{job.version:08X} active")
 
     async def _share_pump(self, session) -> None:

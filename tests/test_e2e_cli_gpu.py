@@ -153,7 +153,7 @@ def test_cli_node_mode_two_ranks_share_one_gpu(tmp_path):
                 if acc >= 10 and rank1 >= 2:
                     break
             assert acc >= 10 and rank1 >= 2, body + "".join(lines[-40:])
-            assert any("node: rank 1/2 mining on GPU 0 (1 device(s))" in x for x in lines), "".join(lines[-40:])
+            assert any("node: rank 1 of 2 mining on GPU 0 (1 device(s))" in x for x in lines), "".join(lines[-40:])
             assert pool.m_accepted.value() >= acc
         finally:
             os.killpg(proc.pid, signal.SIGTERM)
