@@ -361,9 +361,8 @@ __device__ __forceinline__ void jh_round(u32 x[8][4], const u32* c) {
   }
 }
 
-// BC: the 42 x 8 round constants. The kernel stages them in LDS so each round's eight words arrive in VGPRs by
-// ds_read (no VALU): from the scalar cache they needed a v_mov per word (8 per round, 5.5% of JH's VALU), and an
-// SGPR operand would put v_bitop3 in the slow issue class (profiles/r1/x11/NOTES.md).
+// BC: the 42 x 8 round constants (x11t::JH_BC, or an LDS copy in the variants of tools/x11_variants.hip). An SGPR
+// operand would put v_bitop3 in the slow issue class (profiles/r1/x11/NOTES.md), so each word is moved to a VGPR.
 __device__ __forceinline__ void jh_E8(u32 x[8][4], const u32 (*BC)[8]) {
   for (int r = 0; r < 42; r += 7) {
     jh_round<0>(x, BC[r + 0]);
@@ -662,6 +661,7 @@ X11_STAGE_KERNEL(k_luffa512_64, luffa512_64)
 X11_STAGE_KERNEL(k_cubehash512_64, cubehash512_64)
 #undef X11_STAGE_KERNEL
 
+#ifdef OTEDAMA_X11_VARIANTS
 __device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u32 n, bool reload) {
   __shared__ __attribute__((aligned(16))) u32 BC[42][8];
   for (u32 t = threadIdx.x; t < 42 * 8; t += kBlock) BC[t / 8][t % 8] = x11t::JH_BC[t / 8][t % 8];
@@ -674,28 +674,26 @@ __device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u
   else jh512_64(h, BC);
   store_hash(Hb, stride, i, h);
 }
-// LDS constants, message re-read, 7 waves/SIMD (72 VGPRs, 44 B of spills outside the round loops): 1.93 ms per
-// 2^23 vs 1.97 for the scalar-cache constants at 7 waves and 2.00 for LDS constants at 5 waves
-// (tools/x11_variants.hip, profiles/r3/h_jh/).
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
-  jh_stage_lds(Hb, stride, n, true);
-}
-#ifdef OTEDAMA_X11_VARIANTS
-// Alternatives timed by tools/x11_variants.hip (not built into the extension).
-__global__ __launch_bounds__(kBlock) void k_jh512_64_sgpr(u64* __restrict__ Hb, u32 stride, u32 n) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;  // round constants through the scalar cache + v_mov
+#endif
+// Round constants through the scalar cache (one v_mov per word into a VGPR operand: 672 per hash, 5.5% of JH's
+// VALU). Staging them in LDS removes every v_mov but measured the same (1.90-1.97 vs 1.92-1.94 ms per 2^23 at
+// 7 waves, 2.00 at 5 waves: tools/x11_variants.hip, profiles/r3/h_jh/), so the simpler kernel stays.
+__global__ __launch_bounds__(kBlock) void k_jh512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   u64 h[8];
   load_hash(Hb, stride, i, h);
   jh512_64(h, x11t::JH_BC);
   store_hash(Hb, stride, i, h);
 }
+#ifdef OTEDAMA_X11_VARIANTS
+// Alternatives timed by tools/x11_variants.hip (not built into the extension).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64_w7(
     u64* __restrict__ Hb, u32 stride, u32 n) {
   jh_stage_lds(Hb, stride, n, false);
 }
-__global__ __launch_bounds__(kBlock) void k_jh512_64_reload(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64_reload_w7(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
   jh_stage_lds(Hb, stride, n, true);
 }
 __global__ __launch_bounds__(kBlock) void k_jh512_64_lds(u64* __restrict__ Hb, u32 stride, u32 n) {

@@ -220,8 +220,14 @@ void GpuMiner::loop() {
     if (cal) (void)hipStreamDestroy(cal);
   }};
   for (auto& s : slots) OTD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-  OTD_HIP(hipStreamCreateWithFlags(&ctl, hipStreamNonBlocking));
-  OTD_HIP(hipStreamCreateWithFlags(&cal, hipStreamNonBlocking));
+  // The abort-word writes and the clock probes must never queue behind a search kernel: HIP multiplexes streams of
+  // one priority onto GPU_MAX_HW_QUEUES (4) hardware queues, and with two search streams plus torch's in the same
+  // process a control stream can land on a busy queue, where its write waits for a whole 2^32-hash launch (the
+  // job switch grew from 0.3 ms to ~110 ms). High-priority streams come from a separate queue pool.
+  int prio_lo = 0, prio_hi = 0;
+  OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  OTD_HIP(hipStreamCreateWithPriority(&ctl, hipStreamNonBlocking, prio_hi));
+  OTD_HIP(hipStreamCreateWithPriority(&cal, hipStreamNonBlocking, prio_hi));
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
   OTD_HIP(hipMemset(d_abort, 0, 256));
   OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_rt), 64, hipHostMallocCoherent | hipHostMallocMapped));

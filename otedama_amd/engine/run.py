@@ -125,6 +125,20 @@ def mask_addr(a: str) -> str:
     return a if len(a) <= 12 else a[:6] + "…" + a[-4:]
 
 
+
+def _process_start_wall() -> float:
+    """Wall-clock time this process started, to ~10 ms: its start in clock ticks after boot (/proc/self/stat
+    field 22) against the uptime now (/proc/uptime); 0.0 where /proc is unavailable."""
+    try:
+        with open("/proc/self/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        with open("/proc/uptime") as f:
+            uptime = float(f.read().split()[0])
+        started = int(fields[19]) / os.sysconf("SC_CLK_TCK")
+        return time.time() - (uptime - started)
+    except (OSError, ValueError, IndexError):
+        return 0.0
+
 class Engine:
     def __init__(self, opts: Options):
         self.opts = opts
@@ -225,16 +239,17 @@ class Engine:
         """Process start -> first completed GPU batch, per device (device processes report their first hash), and
         this process's resident set (BENCHMARKS.md:105-129 reports <1 s to hashing and 25 MB)."""
         out = {}
+        t0 = _process_start_wall()
         try:
             import psutil
 
             p = psutil.Process()
-            t0 = p.create_time()
+            t0 = t0 or p.create_time()  # psutil's is only as precise as the boot time (whole seconds)
             out["rss_mib"] = p.memory_info().rss / 2**20
             kids = p.children(recursive=True)
             out["children_rss_mib"] = sum(k.memory_info().rss for k in kids) / 2**20
         except Exception:  # noqa: BLE001 - psutil missing or a child gone
-            t0 = 0.0
+            pass
         ms = self.miners
         firsts, phases, native = {}, {}, {}
         for m in getattr(ms, "miners", []) or []:
@@ -582,6 +597,8 @@ class Engine:
         self._mark("pool_dial")
         session = await self._dial(url, creds)
         self._mark("pool_connected")
+        for k, v in (getattr(session, "dial_timing", None) or {}).items():
+            self._marks.setdefault(f"pool_{k}", v)
         self._session = session
         self.connected = True
         self.m.pool_connection_state.set(2)

@@ -54,6 +54,13 @@ def load(build_if_missing: bool = True):
         return None
 
 
+def loaded():
+    """The native module if this process already imported it, else None. Never imports: the extension links the HIP
+    runtime (libamdhip64, libhsa-runtime64, comgr), ~1.4 s to page in on a cold GPU host, which a GPU-free engine
+    (device processes own the GPUs) must not pay for an optional fast path."""
+    return _mod if _mod is not None else sys.modules.get("otedama_amd._native")
+
+
 def available() -> bool:
     return load() is not None
 

@@ -127,14 +127,15 @@ class PoolServer:
         # share-hash workers for slow PoW (scrypt); sized to the host, never more than 8 threads
         self._hash_pool = concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1),
                                                                 thread_name_prefix="otedama-pool-hash")
-        # hashlib.scrypt holds the GIL; the native C++ scrypt releases it, so the workers run in parallel
+        # hashlib.scrypt holds the GIL; the native C++ scrypt releases it, so the workers run in parallel. The pool
+        # loads the extension once at start (native SV2 frame splitting and AEAD for every connection too) rather
+        # than on its first connection.
         self._slow_hash = self.algo.hash
-        if self.algo.name == "scrypt":
-            from otedama_amd.ops.native import load
+        from otedama_amd.ops.native import load
 
-            n = load(build_if_missing=False)
-            if n is not None:
-                self._slow_hash = n.scrypt_1024_1_1
+        n = load(build_if_missing=False)
+        if n is not None and self.algo.name == "scrypt":
+            self._slow_hash = n.scrypt_1024_1_1
         self.block: BlockTemplate | None = None
         self.jobs: "OrderedDict[str, PoolJob]" = OrderedDict()
         self._job_counter = 0

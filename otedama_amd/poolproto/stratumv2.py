@@ -80,6 +80,7 @@ class V2Session(Session):
         self._write_lock = asyncio.Lock()
         self._task: asyncio.Task | None = None
         self.last_job_received_at = 0.0
+        self.dial_timing: dict[str, float] = {}
         self.log = lambda level, msg: None
 
     @property
@@ -345,18 +346,23 @@ class V2Dialer(Dialer):
                    log=None) -> Session:
         rest = strip_scheme(url)
         host, port = split_host_port(rest, 3336)
+        timing = {"dial": time.time()}  # wall clock of each connection step (engine start-up phases)
         if self.dial_fn is not None:
             reader, writer = await self.dial_fn(host, port)
         else:
             reader, writer = await tls.open_connection(host, port, self.use_tls, creds.tls_root_cas_pem or None,
                                                        timeout)
+        timing["tcp"] = time.time()
         if creds.noise or creds.pool_pubkey:
             reader, writer = await noise_connect(reader, writer, creds, timeout, log)
+            timing["noise"] = time.time()
         s = V2Session(reader, writer, creds, self.protocol, f"{host}:{port}", self.dialect, algorithm)
+        s.dial_timing = timing
         if log is not None:
             s.log = log
         try:
             await asyncio.wait_for(s.handshake(), timeout + 30)
+            timing["channel_open"] = time.time()
         except BaseException:
             await s.close()
             raise

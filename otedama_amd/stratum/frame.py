@@ -161,9 +161,11 @@ def _scan_py(buf, max_frame_size: int):
 
 
 def _scanner():
-    from otedama_amd.ops.native import load
+    """The native splitter when the extension is already in this process (the pool server loads it at start),
+    else the Python one: a miner engine reads a few frames a second and must not load the HIP runtime for them."""
+    from otedama_amd.ops.native import loaded
 
-    mod = load(build_if_missing=False)
+    mod = loaded()
     return mod.sv2_scan if mod is not None and hasattr(mod, "sv2_scan") else _scan_py
 
 

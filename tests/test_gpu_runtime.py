@@ -141,7 +141,10 @@ def test_scrypt_switch_stops_the_romix_batch():
     m.set_job(_job(hdr_a, target, 1, "a", algo="scrypt"))
     m.start()
     try:
-        time.sleep(2.5)  # 128 GiB scratch allocation + first batches
+        t0 = time.monotonic()
+        while m.stats()["job_switches"] < 1 and time.monotonic() - t0 < 30:  # 128 GiB scratch + first batch
+            time.sleep(0.01)
+        time.sleep(0.3)
         m.set_job(_job(hdr_b, target, 2, "b", algo="scrypt"))
         time.sleep(0.5)
         shares = m.poll(4096)
@@ -149,7 +152,9 @@ def test_scrypt_switch_stops_the_romix_batch():
         m.stop()
     st = m.stats()
     assert not st["faulted"], st
-    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st  # polls at every quarter of the ROMix
+    print("scrypt switch ms:", st["job_switch_ms"])
+    # polls at both ROMix phase boundaries: a running wave stops within one phase (~15 ms)
+    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st
     assert st["aborted_launches"] >= 1
     for s in shares[:40]:
         _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target, "scrypt")
@@ -177,3 +182,22 @@ def test_startup_phases_are_recorded():
     assert list(ph) == ["hip_set_device", "buffers", "clock_calibration", "wait_first_job", "first_batch"]
     assert all(v >= 0 for v in ph.values())
     assert sum(ph.values()) <= wall * 1e3 + 50
+
+
+def test_job_switch_with_other_streams_in_the_process():
+    """The abort-word write must not queue behind a search kernel when the process holds more HIP streams than the
+    runtime has hardware queues (torch's streams plus the miner's two search streams): bench.py measured ~110 ms
+    switches at 2^32-hash launches before the control stream got a high-priority queue of its own."""
+    import torch
+
+    from otedama_amd.engine.latency_probe import measure_job_switch
+
+    extra = [torch.cuda.Stream() for _ in range(6)]
+    for s in extra:  # give each stream a queue (first use) and keep them alive
+        with torch.cuda.stream(s):
+            torch.ones(1, device="cuda").add_(1)
+    torch.cuda.synchronize()
+    res = measure_job_switch(0, "sha256d", switches=6, batch_nonces=1 << 32)
+    print("job switch at 2^32:", res)
+    assert res["p50_ms"] is not None and res["p50_ms"] < 20.0, res
+    assert res["max_ms"] < 50.0, res

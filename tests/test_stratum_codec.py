@@ -374,3 +374,15 @@ def test_frame_reader_raises_a_buffered_bad_header_without_waiting_for_more_data
             await asyncio.wait_for(fr.read_frame(), 1.0)
 
     asyncio.run(go())
+
+
+def test_frame_scanner_does_not_load_the_hip_runtime():
+    """A GPU-free engine must not page in the extension (and with it libamdhip64) to split a few SV2 frames a
+    second: on a cold GPU host that cost ~1.4 s before the first job (profiles/r3/j_startup)."""
+    import subprocess
+    import sys
+
+    code = ("import sys; from otedama_amd.stratum.frame import FrameScanner; "
+            "FrameScanner().feed(b''); print('otedama_amd._native' in sys.modules)")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.stdout.strip() == "False", out.stdout + out.stderr
