@@ -75,7 +75,6 @@ __device__ __forceinline__ void shavite_round(const u32* T, u32 lo, const u32 rk
 // 14 rounds: round 0, three trips of rounds 4t+1 .. 4t+4 (odd, even, odd, even: the state rotation closes after
 // four rounds, so the rolled loop carries no register moves), round 13. The one-round rolled loop it replaces spent
 // ~85 v_mov per round on the rotation and the schedule window (18% of SHAvite's VALU; tools/x11_variants.hip).
-template <bool kLegacy>
 __device__ __forceinline__ void shavite512_64(const u32* T, u32 lo, u64 h[8]) {
   // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
   u32 rk[32];
@@ -91,49 +90,27 @@ __device__ __forceinline__ void shavite512_64(const u32* T, u32 lo, u64 h[8]) {
   for (int k = 0; k < 4; ++k) {
     A[k] = kShaviteIv[k]; B[k] = kShaviteIv[4 + k]; C[k] = kShaviteIv[8 + k]; D[k] = kShaviteIv[12 + k];
   }
-  if (kLegacy) {
-    // counter = {512, 0, 0, 0}
+  shavite_round(T, lo, rk, A, B, C, D);  // round 0: the message block itself
 #pragma unroll 1
-    for (int r = 0; r < 14; ++r) {
-      if (r & 1) {
-        if (r == 1) shavite_rk_odd<0>(T, lo, rk);
-        else if (r == 5) shavite_rk_odd<1>(T, lo, rk);
-        else if (r == 9) shavite_rk_odd<2>(T, lo, rk);
-        else if (r == 13) shavite_rk_odd<3>(T, lo, rk);
-        else shavite_rk_odd<-1>(T, lo, rk);
-      } else if (r) {
-        shavite_rk_even(rk);
-      }
-      shavite_round(T, lo, rk, A, B, C, D);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const u32 t = D[k];
-        D[k] = C[k]; C[k] = B[k]; B[k] = A[k]; A[k] = t;
-      }
-    }
-  } else {
-    shavite_round(T, lo, rk, A, B, C, D);  // round 0: the message block itself
-#pragma unroll 1
-    for (int t = 0; t < 3; ++t) {
-      if (t == 0) shavite_rk_odd<0>(T, lo, rk);
-      else if (t == 1) shavite_rk_odd<1>(T, lo, rk);
-      else shavite_rk_odd<2>(T, lo, rk);
-      shavite_round(T, lo, rk, D, A, B, C);
-      shavite_rk_even(rk);
-      shavite_round(T, lo, rk, C, D, A, B);
-      shavite_rk_odd<-1>(T, lo, rk);
-      shavite_round(T, lo, rk, B, C, D, A);
-      shavite_rk_even(rk);
-      shavite_round(T, lo, rk, A, B, C, D);
-    }
-    shavite_rk_odd<3>(T, lo, rk);
+  for (int t = 0; t < 3; ++t) {
+    if (t == 0) shavite_rk_odd<0>(T, lo, rk);
+    else if (t == 1) shavite_rk_odd<1>(T, lo, rk);
+    else shavite_rk_odd<2>(T, lo, rk);
     shavite_round(T, lo, rk, D, A, B, C);
-    // the state after round 13 is (C, D, A, B) in the spec's order
+    shavite_rk_even(rk);
+    shavite_round(T, lo, rk, C, D, A, B);
+    shavite_rk_odd<-1>(T, lo, rk);
+    shavite_round(T, lo, rk, B, C, D, A);
+    shavite_rk_even(rk);
+    shavite_round(T, lo, rk, A, B, C, D);
+  }
+  shavite_rk_odd<3>(T, lo, rk);
+  shavite_round(T, lo, rk, D, A, B, C);
+  // the state after round 13 is (C, D, A, B) in the spec's order
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u32 a = C[k], b = D[k];
-      C[k] = A[k]; D[k] = B[k]; A[k] = a; B[k] = b;
-    }
+  for (int k = 0; k < 4; ++k) {
+    const u32 a = C[k], b = D[k];
+    C[k] = A[k]; D[k] = B[k]; A[k] = a; B[k] = b;
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -144,26 +121,86 @@ __device__ __forceinline__ void shavite512_64(const u32* T, u32 lo, u64 h[8]) {
   }
 }
 
-template <bool kLegacy>
-__device__ __forceinline__ void shavite_stage(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
     u64 h[8];
     load_hash(Hb, stride, i, h);
-    shavite512_64<kLegacy>(T, lo, h);
+    shavite512_64(T, lo, h);
     store_hash(Hb, stride, i, h);
   }
 }
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
-  shavite_stage<false>(Hb, stride, n);
-}
 #ifdef OTEDAMA_X11_VARIANTS
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64_rolled(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
-  shavite_stage<true>(Hb, stride, n);
+// The round-2 kernel, verbatim (one round per trip of a rolled loop), timed by tools/x11_variants.hip.
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64_r2(u64* __restrict__ Hb, u32 stride, u32 n) {
+  __shared__ u32 T[kAesPrivWords];
+  aes_priv_fill(T);
+  const u32 lo = aes_laneoff();
+  for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  // Rolling 32-word window of the 448-word key schedule; block 0 is the padded message.
+  u32 rk[32];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { rk[2 * k] = lo32(h[k]); rk[2 * k + 1] = hi32(h[k]); }
+  rk[16] = 0x80u;
+#pragma unroll
+  for (int k = 17; k < 32; ++k) rk[k] = 0;
+  rk[27] = 0x02000000u;  // 512-bit length at bytes 110..113
+  rk[31] = 0x02000000u;  // digest size 512 at bytes 126..127
+  u32 A[4], B[4], C[4], D[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    A[k] = kShaviteIv[k]; B[k] = kShaviteIv[4 + k]; C[k] = kShaviteIv[8 + k]; D[k] = kShaviteIv[12 + k];
+  }
+  // counter = {512, 0, 0, 0}
+#pragma unroll 1
+  for (int r = 0; r < 14; ++r) {
+    if (r & 1) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        u32 t0 = rk[4 * g + 1], t1 = rk[4 * g + 2], t2 = rk[4 * g + 3], t3 = rk[4 * g];
+        aes_round(T, lo, t0, t1, t2, t3);
+        const int p = g ? 4 * g - 4 : 28;
+        rk[4 * g] = t0 ^ rk[p];
+        rk[4 * g + 1] = t1 ^ rk[p + 1];
+        rk[4 * g + 2] = t2 ^ rk[p + 2];
+        rk[4 * g + 3] = t3 ^ rk[p + 3];
+        if (g == 0 && r == 1) { rk[0] ^= 512u; rk[3] = ~rk[3]; }
+        if (g == 1 && r == 5) { rk[7] ^= ~512u; }
+        if (g == 7 && r == 9) { rk[30] ^= 512u; rk[31] = ~rk[31]; }
+        if (g == 6 && r == 13) { rk[25] ^= 512u; rk[27] = ~rk[27]; }
+      }
+    } else if (r) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) rk[k] ^= k >= 7 ? rk[k - 7] : rk[k + 25];
+    }
+    u32 x[4] = {B[0], B[1], B[2], B[3]};
+    shavite_F(T, lo, x, rk);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) A[k] ^= x[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = D[k];
+    shavite_F(T, lo, x, rk + 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      C[k] ^= x[k];
+      const u32 t = D[k];
+      D[k] = C[k]; C[k] = B[k]; B[k] = A[k]; A[k] = t;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    h[k] = mk64(kShaviteIv[2 * k] ^ A[2 * k], kShaviteIv[2 * k + 1] ^ A[2 * k + 1]);
+    h[2 + k] = mk64(kShaviteIv[4 + 2 * k] ^ B[2 * k], kShaviteIv[5 + 2 * k] ^ B[2 * k + 1]);
+    h[4 + k] = mk64(kShaviteIv[8 + 2 * k] ^ C[2 * k], kShaviteIv[9 + 2 * k] ^ C[2 * k + 1]);
+    h[6 + k] = mk64(kShaviteIv[12 + 2 * k] ^ D[2 * k], kShaviteIv[13 + 2 * k] ^ D[2 * k + 1]);
+  }
+  store_hash(Hb, stride, i, h);
+  }
 }
 #endif
 

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
                              {"jh_lds_reload_w7", k_jh512_64_reload_w7, false, 0},
                              {"jh_lds", k_jh512_64_lds, false, 0},
                              {"shavite_4round_trips (production)", k_shavite512_64, true, 1},
-                             {"shavite_rolled", k_shavite512_64_rolled, true, 1}};
+                             {"shavite_r2 (round-2 kernel)", k_shavite512_64_r2, true, 1}};
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   auto launch = [&](const Variant& v, u64* buf) {
