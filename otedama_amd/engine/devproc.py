@@ -152,10 +152,14 @@ class DeviceProcess:
             except OSError:
                 pass
 
-    def restart(self) -> None:
-        """Replace a dead child with a fresh process (the current job is re-sent once it is up)."""
+    def restart(self, replay_job: bool = True) -> None:
+        """Replace a dead child with a fresh process. ``replay_job``: re-send the last job at once; a MinerSet passes
+        False and applies a fresh stripe when the process reports ready, because replaying the dead process's
+        stripe would search its nonces a second time."""
         if self.alive:
             return
+        if not replay_job:
+            self._job = None
         with self._lock:
             for k in _CUMULATIVE:
                 self._base[k] += self._child.get(k, 0)

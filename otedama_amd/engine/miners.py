@@ -272,7 +272,7 @@ class MinerSet:
             if self._stopped or not m.retired:
                 return
         try:
-            m.native.restart()
+            m.native.restart(replay_job=False)  # its stripe is re-assigned past every cursor once it is ready
         except Exception as exc:  # noqa: BLE001
             self.log("error", f"miners: restart of {m.id} failed: {exc}")
             with self._lock:

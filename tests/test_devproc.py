@@ -84,6 +84,8 @@ def test_sigkilled_device_process_is_resplit_and_replaced():
         assert time.monotonic() - t0 < 15  # nothing hangs
     assert shares and all(_verify(s) for s in shares)
     assert all(s["job_id"] == "job-A" for s in shares)
+    # nothing searched twice: the replacement starts on a fresh stripe, not the dead process's old one
+    assert len({(s["version"], s["nonce"]) for s in shares}) == len(shares)
     assert any("lost" in m for _, m in logs) and any("back" in m for _, m in logs)
 
 

@@ -46,6 +46,23 @@ def _hashes(http: str) -> int:
     return sum(int(d.get("hashes", 0)) for d in st["devices"].values())
 
 
+def _rss_top(pid: int, n: int = 8) -> list:
+    """The process's largest resident mappings (MiB, path or [anon]) from /proc/<pid>/smaps."""
+    sizes: dict[str, float] = {}
+    name = "?"
+    try:
+        with open(f"/proc/{pid}/smaps") as f:
+            for line in f:
+                parts = line.split()
+                if parts and "-" in parts[0] and len(parts) >= 5:
+                    name = parts[5] if len(parts) >= 6 else "[anon]"
+                elif parts and parts[0] == "Rss:":
+                    sizes[name] = sizes.get(name, 0.0) + int(parts[1]) / 1024
+    except OSError as exc:
+        return [str(exc)]
+    return [(k, round(v, 1)) for k, v in sorted(sizes.items(), key=lambda kv: -kv[1])[:n]]
+
+
 def _measure(cmd: list[str], http: str, env: dict, seconds: float, log_path: str) -> dict:
     t_spawn = time.time()
     p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(log_path, "w"), stderr=subprocess.STDOUT)
@@ -69,6 +86,7 @@ def _measure(cmd: list[str], http: str, env: dict, seconds: float, log_path: str
             pp = psutil.Process(p.pid)
             out["rss_mib"] = {str(c.pid): round(c.memory_info().rss / 2**20, 1)
                               for c in [pp, *pp.children(recursive=True)]}
+            out["rss_top_mappings"] = {str(c.pid): _rss_top(c.pid) for c in [pp, *pp.children(recursive=True)]}
         except Exception as exc:  # noqa: BLE001
             out["rss_mib"] = str(exc)
     finally:
