@@ -295,3 +295,38 @@ def test_encode_frame_rejects_oversize_plaintext():
         N.encode_frame(tx, b"\x00" * (N.MAX_FRAME - N.TAG + 1))
     assert tx.n == 0  # the refused frame did not consume a nonce
     assert len(N.encode_frame(N.CipherState(b"\x42" * 32), b"\x00" * (N.MAX_FRAME - N.TAG))) == 2 + N.MAX_FRAME
+
+
+def test_libcrypto_aead_matches_the_native_binding():
+    """The ctypes libcrypto binding (used by a GPU-free engine that must not load the extension) and the native
+    extension's binding produce identical ciphertexts and tags and reject the same tampering."""
+    import os
+
+    from otedama_amd.ops.native import require_native
+    from otedama_amd.utils import aead
+
+    lc = aead.libcrypto()
+    if lc is None:
+        pytest.skip("libcrypto not loadable")
+    nat = require_native()
+    for kind in (aead.AES256GCM, aead.CHACHA20POLY1305):
+        for n in (0, 1, 31, 1000):
+            key, nonce, pt, ad = os.urandom(32), os.urandom(12), os.urandom(n), os.urandom(n % 7)
+            a = lc.seal(kind, key, nonce, pt, ad)
+            assert a == nat.aead_seal(kind, key, nonce, pt, ad)
+            assert lc.open_(kind, key, nonce, a, ad) == pt == nat.aead_open(kind, key, nonce, a, ad)
+            bad = bytearray(a)
+            bad[-1] ^= 1
+            assert lc.open_(kind, key, nonce, bytes(bad), ad) is None
+            assert lc.open_(kind, key, nonce, a, ad + b"x") is None
+
+
+def test_aead_does_not_load_the_extension():
+    import subprocess
+    import sys
+
+    code = ("import sys; from otedama_amd.utils import aead; c = aead.seal(aead.CHACHA20POLY1305, bytes(32), "
+            "bytes(12), b'hi'); assert aead.open_(aead.CHACHA20POLY1305, bytes(32), bytes(12), c) == b'hi'; "
+            "print('otedama_amd._native' in sys.modules)")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert out.stdout.strip() == "False", out.stdout + out.stderr
