@@ -135,6 +135,9 @@ py::dict stats_to_dict(const MinerStats& s) {
     py::dict ph;
     for (const auto& kv : s.startup_ms) ph[py::str(kv.first)] = kv.second;
     d["startup_ms"] = ph;
+    py::dict rs;
+    for (const auto& kv : s.startup_rss_mb) rs[py::str(kv.first)] = kv.second;
+    d["startup_rss_mb"] = rs;
   }
   return d;
 }

@@ -93,6 +93,7 @@ struct MinerStats {
   // Start-up phases of the device thread, in order, each a duration in ms (GPU: hip_set_device, buffers,
   // clock_calibration, wait_first_job, first_batch = first job's set_job -> its first batch running).
   std::vector<std::pair<std::string, double>> startup_ms;
+  std::vector<std::pair<std::string, double>> startup_rss_mb;  // process resident set after each phase (MiB)
 };
 
 // Full-target re-verification of a candidate (host SHA-256d / scrypt).

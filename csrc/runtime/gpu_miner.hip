@@ -27,12 +27,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <unistd.h>
 
 #include "otedama/hitsink.h"
 #include "otedama/job.h"
@@ -54,6 +56,16 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
                                 int gap, const HitSink& sink, int grid, hipStream_t stream);
 uint64_t scrypt_scratch_bytes(int grid, int gap);
 int gpu_cu_count(int device);
+
+// Resident set of this process in MiB (/proc/self/statm), for the start-up phase record.
+static double resident_mb() {
+  FILE* f = std::fopen("/proc/self/statm", "r");
+  if (!f) return 0;
+  unsigned long size = 0, res = 0;
+  const int n = std::fscanf(f, "%lu %lu", &size, &res);
+  std::fclose(f);
+  return n == 2 ? double(res) * double(sysconf(_SC_PAGESIZE)) / (1024.0 * 1024.0) : 0;
+}
 
 #define OTD_HIP(call)                                                                              \
   do {                                                                                             \
@@ -165,6 +177,7 @@ void GpuMiner::loop() {
     const double now = monotonic_seconds();
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.startup_ms.emplace_back(name, (now - t_phase) * 1e3);
+    stats_.startup_rss_mb.emplace_back(name, resident_mb());
     t_phase = now;
   };
   OTD_HIP(hipSetDevice(device_));
@@ -228,10 +241,12 @@ void GpuMiner::loop() {
   OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   OTD_HIP(hipStreamCreateWithPriority(&ctl, hipStreamNonBlocking, prio_hi));
   OTD_HIP(hipStreamCreateWithPriority(&cal, hipStreamNonBlocking, prio_hi));
+  phase("streams");
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
   OTD_HIP(hipMemset(d_abort, 0, 256));
   OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_rt), 64, hipHostMallocCoherent | hipHostMallocMapped));
   OTD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_rt), h_rt, 0));
+  phase("control_words");
   for (auto& s : slots) {
     OTD_HIP(hipMalloc(&s.d_count, 64));
     OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_count), 64, hipHostMallocDefault));

@@ -161,8 +161,9 @@ def test_scrypt_switch_stops_the_romix_batch():
 
 
 def test_startup_phases_are_recorded():
-    """The device thread times its own start-up (start -> first GPU hash): HIP context, buffers,
-    clock calibration, the wait for the first job and the first batch (set_job -> running, incl. code-object load)."""
+    """The device thread times its own start-up (start -> first GPU hash): HIP context, streams,
+    control words, buffers, clock calibration, the wait for the first job and the first batch (set_job -> running,
+    incl. code-object load), with the resident set after each."""
     N = _native()
     hdr = os.urandom(76) + bytes(4)
     t0 = time.monotonic()
@@ -179,7 +180,10 @@ def test_startup_phases_are_recorded():
     assert not st["faulted"], st
     ph = st["startup_ms"]
     print("startup phases ms:", {k: round(v, 2) for k, v in ph.items()}, "construct->first batch s:", round(wall, 3))
-    assert list(ph) == ["hip_set_device", "buffers", "clock_calibration", "wait_first_job", "first_batch"]
+    assert list(ph) == ["hip_set_device", "streams", "control_words", "buffers", "clock_calibration",
+                        "wait_first_job", "first_batch"]
+    print("resident MiB after each phase:", st["startup_rss_mb"])
+    assert list(st["startup_rss_mb"])[:5] == list(ph)[:5]
     assert all(v >= 0 for v in ph.values())
     assert sum(ph.values()) <= wall * 1e3 + 50
 
