@@ -70,13 +70,26 @@ class DeviceMiner:
         return self.device.identity().id
 
 
+def variant_space(t: dict) -> int:
+    """Number of header variants of a template: 2^popcount(version_mask) x extranonce2 values x (ntime_roll + 1),
+    saturating at 2^64 - 1 (csrc/runtime/miner_common.cpp JobTemplate::variant_space)."""
+    cap = (1 << 64) - 1
+    e2 = 1
+    if t.get("coinb1") is not None and int(t.get("extranonce2_size", 0) or 0) > 0:
+        size = int(t["extranonce2_size"])
+        e2 = cap if size >= 8 else 1 << (8 * size)
+    v = 1 << bin(int(t.get("version_mask", 0) or 0) & 0xFFFFFFFF).count("1")
+    return min(e2 * v * (int(t.get("ntime_roll", 0) or 0) + 1), cap)
+
+
 class MinerSet:
     def __init__(self, devices: list, algorithm: str = "sha256d", batch_nonces: int = 1 << 32,
                  cpu_threads: int = 0, rank: int = 0, world_size: int = 1, log=None, queue_cap: int = 4096,
                  stall_samples: int = 3, sha_variants: int = 128, isolation: str = "thread"):
         if isolation not in ("thread", "process"):
             raise ValueError("isolation must be 'thread' or 'process'")
-        N = require_native()
+        # with every device in its own process this process never needs the extension (or the HIP runtime it links)
+        N = require_native() if isolation == "thread" else None
         self.N = N
         self.algorithm = algorithm
         self.isolation = isolation
@@ -225,7 +238,7 @@ class MinerSet:
         base = max(hw - node_base, 0) + RESPLIT_GROUPS * GROUP * old_stride
         probe = {k: v for k, v in t.items() if k != "variant_base"}
         try:
-            space = int(self.N.variant_space(probe))
+            space = int(self.N.variant_space(probe)) if self.N is not None else variant_space(probe)
         except Exception:  # noqa: BLE001 - a template the native side cannot parse: keep the deferred path
             space = 0
         if node_base + base + self.stripe_total > space:

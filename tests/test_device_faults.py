@@ -171,3 +171,20 @@ def test_node_variant_base_adds_to_the_local_resplit():
     assert [(m.native.jobs[-1]["variant_start"], m.native.jobs[-1]["variant_stride"]) for m in ms.miners] == \
         [(4096 + 1, 8), (4096 + 5, 8)]
     assert "variant_base" not in ms.miners[0].native.jobs[-1]
+
+
+def test_python_variant_space_matches_native():
+    from otedama_amd.engine.miners import variant_space
+    from otedama_amd.ops.native import require_native
+
+    N = require_native()
+    base = {"header": bytes(80), "target": bytes(32), "algo": "sha256d"}
+    cases = [{}, {"version_mask": 0x1FFFE000}, {"version_mask": 0xFFFFFFFF}, {"ntime_roll": 7},
+             {"version_mask": 0x1FFFE000, "ntime_roll": 3},
+             {"coinb1": b"a", "coinb2": b"b", "extranonce1": b"e", "extranonce2_size": 4, "merkle_branches": []},
+             {"coinb1": b"a", "coinb2": b"b", "extranonce1": b"e", "extranonce2_size": 8, "merkle_branches": [],
+              "version_mask": 0x1FFFE000},
+             {"coinb1": b"a", "coinb2": b"b", "extranonce1": b"e", "extranonce2_size": 0, "merkle_branches": []}]
+    for c in cases:
+        t = dict(base, **c)
+        assert variant_space(t) == N.variant_space(t), c

@@ -126,3 +126,23 @@ def test_kfd_topology_enumeration_without_a_runtime(tmp_path, monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,2")
     devs = hal.KFDDriver(str(tmp_path)).enumerate()
     assert [(d.index, d.extra["arch"]) for d in devs] == [(0, "gfx950"), (1, "gfx90a")]
+
+
+def test_process_isolation_engine_side_does_not_load_the_extension():
+    """The engine of a GPU node hands every GPU to a device process: building its MinerSet must not import the
+    native extension (which links the HIP runtime; ~1 GB of RSS once a GPU context exists)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys\n"
+        "from otedama_amd import hal\n"
+        "from otedama_amd.engine.miners import MinerSet, variant_space\n"
+        "gpu = hal.SimpleDevice(hal.Identity('gpu-0', hal.Family.GPU, 'AMD', 'AMD Instinct MI355X 256CU gfx950'),\n"
+        "                       hal.KERNEL_ISAS['gfx950'], index=0, extra={'arch': 'gfx950', 'cus': 256})\n"
+        "ms = MinerSet([gpu], 'sha256d', isolation='process')\n"
+        "assert len(ms.miners) == 1 and variant_space({'version_mask': 0x1FFFE000}) == 65536\n"
+        "print('otedama_amd._native' in sys.modules)\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                         env=dict(os.environ, OTEDAMA_NO_TORCH="1"))
+    assert out.stdout.strip() == "False", out.stdout + out.stderr
