@@ -187,6 +187,7 @@ class NodeMinerSet:
         self._gen_started = time.monotonic()
         self.capacity = comm.info.world_size       # orig ranks 0..capacity-1 may exist
         self._rows_by_orig: dict[int, list[int]] = {}
+        self.row_times: dict[int, float] = {}  # wall time at which each remote rank's counter row was produced
         self._prev_rows: dict[int, list[int]] = {}
         self._rates: dict[str, float] = {}
         self._t_last = time.monotonic()
@@ -305,7 +306,7 @@ class NodeMinerSet:
             lost = r in self.lost_ranks
             d[f"rank{r}"] = {"hashes": row[0], "shares": row[1], "dropped": row[2], "faulted": bool(row[3]) or lost,
                              "error": "rank lost" if lost else ("remote device fault" if row[3] else ""),
-                             "candidates": 0, "launches": 0}
+                             "candidates": 0, "launches": 0, "counted_at": self.row_times.get(r, 0.0)}
         return d
 
     def total_hashes(self) -> int:
@@ -388,6 +389,7 @@ class NodeMinerSet:
             if r in members and now - hb["t"] <= self.hb_timeout:
                 self._rows_by_orig[r] = [int(hb.get("hashes", 0)), int(hb.get("shares", 0)),
                                          int(hb.get("dropped", 0)), int(hb.get("faulted", 0))]
+                self.row_times[r] = float(hb["t"])
         dead = []
         grace = time.monotonic() - self._gen_started < self.hb_timeout  # members of a new generation get one
         for r in members[1:]:                                           # timeout to (re)start heartbeating

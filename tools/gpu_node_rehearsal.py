@@ -46,6 +46,23 @@ def _hashes(http: str) -> int:
     return sum(int(d.get("hashes", 0)) for d in st["devices"].values())
 
 
+def _sample(http: str) -> dict:
+    """{device: (hashes, when counted)}: a remote rank's counters carry the time its heartbeat was written, so the
+    rate over a window is exact instead of off by up to one heartbeat period at each end."""
+    now = time.time()
+    st = _get(f"http://{http}/debug/stats")
+    return {k: (int(d.get("hashes", 0)), float(d.get("counted_at") or now)) for k, d in st["devices"].items()}
+
+
+def _rate(a: dict, b: dict) -> float:
+    total = 0.0
+    for k, (h1, t1) in b.items():
+        h0, t0 = a.get(k, (0, t1))
+        if t1 > t0:
+            total += (h1 - h0) / (t1 - t0)
+    return total
+
+
 def _rss_top(pid: int, n: int = 8) -> list:
     """The process's largest resident mappings (MiB, path or [anon]) from /proc/<pid>/smaps."""
     sizes: dict[str, float] = {}
@@ -73,10 +90,9 @@ def _measure(cmd: list[str], http: str, env: dict, seconds: float, log_path: str
         st = _wait(lambda: _get(f"http://{http}/debug/stats"), 10)
         out["startup"] = (st or {}).get("startup")
         time.sleep(5.0)  # past the first job's start-up transients
-        h0, t0 = _hashes(http), time.monotonic()
+        s0 = _sample(http)
         time.sleep(seconds)
-        h1, t1 = _hashes(http), time.monotonic()
-        out["hashrate"] = (h1 - h0) / (t1 - t0)
+        out["hashrate"] = _rate(s0, _sample(http))
         dbg = _get(f"http://{http}/debug/stats")
         out["node"] = dbg.get("node")
         out["startup"] = dbg.get("startup") or out["startup"]
