@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -212,7 +213,7 @@ void GpuMiner::loop() {
     for (auto& s : slots)
       if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (ctl) (void)hipStreamSynchronize(ctl);
-    if (cal) (void)hipStreamSynchronize(cal);
+    if (cal && cal != ctl) (void)hipStreamSynchronize(cal);
     for (auto& s : slots) {
       if (s.d_count) (void)hipFree(s.d_count);
       if (s.h_count) (void)hipHostFree(s.h_count);
@@ -228,19 +229,28 @@ void GpuMiner::loop() {
     if (xbuf) (void)hipFree(xbuf);
     if (x11_h) (void)hipFree(x11_h);
     for (auto& s : slots)
-      if (s.stream) (void)hipStreamDestroy(s.stream);
+      if (s.stream && (&s == &slots[0] || s.stream != slots[0].stream)) (void)hipStreamDestroy(s.stream);
     if (ctl) (void)hipStreamDestroy(ctl);
-    if (cal) (void)hipStreamDestroy(cal);
+    if (cal && cal != ctl) (void)hipStreamDestroy(cal);
   }};
-  for (auto& s : slots) OTD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  // Search streams: one per in-flight batch, so a launch's tail overlaps the next launch's first waves; with
+  // OTEDAMA_SEARCH_STREAMS=1 the batches share one stream (one hardware queue less, ~190 MB of host memory).
+  const char* ss_env = std::getenv("OTEDAMA_SEARCH_STREAMS");
+  const bool one_stream = ss_env && std::atoi(ss_env) == 1;
+  for (int i = 0; i < kInflight; ++i) {
+    if (one_stream && i > 0) slots[i].stream = slots[0].stream;
+    else OTD_HIP(hipStreamCreateWithFlags(&slots[i].stream, hipStreamNonBlocking));
+  }
   // The abort-word writes and the clock probes must never queue behind a search kernel: HIP multiplexes streams of
   // one priority onto GPU_MAX_HW_QUEUES (4) hardware queues, and with two search streams plus torch's in the same
   // process a control stream can land on a busy queue, where its write waits for a whole 2^32-hash launch (the
-  // job switch grew from 0.3 ms to ~110 ms). High-priority streams come from a separate queue pool.
+  // job switch grew from 0.3 ms to ~110 ms). High-priority streams come from a separate queue pool. The probes share
+  // the control stream: every hardware queue costs ~190 MB of pinned host memory (tools/stream_rss.hip,
+  // profiles/r3/o_rss), so the miner holds three (two search, one control) instead of four.
   int prio_lo = 0, prio_hi = 0;
   OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   OTD_HIP(hipStreamCreateWithPriority(&ctl, hipStreamNonBlocking, prio_hi));
-  OTD_HIP(hipStreamCreateWithPriority(&cal, hipStreamNonBlocking, prio_hi));
+  cal = ctl;
   phase("streams");
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
   OTD_HIP(hipMemset(d_abort, 0, 256));

@@ -119,6 +119,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=20.0)
     ap.add_argument("--out-dir", default=os.path.join(ROOT, "gpurun_out", "node_rehearsal"))
+    ap.add_argument("--run-only", action="store_true", help="measure `otedama run` only (no node rehearsal)")
     a = ap.parse_args()
     os.makedirs(a.out_dir, exist_ok=True)
     from otedama_amd.engine.latency_probe import PROBE_ADDR
@@ -148,6 +149,9 @@ def main() -> int:
         http1 = f"127.0.0.1:{free_port()}"
         res["run"] = _measure([sys.executable, "-m", "otedama_amd", "run", "--config", cfg, "--no-tui",
                                "--http-addr", http1], http1, env, a.seconds, os.path.join(a.out_dir, "run.log"))
+        if a.run_only:
+            print(json.dumps(res))
+            return 0
         http2 = f"127.0.0.1:{free_port()}"
         res["node_gloo_2ranks_shared_gpu"] = _measure(
             [sys.executable, "-m", "otedama_amd", "node", "--gpus", "2", "--config", cfg, "--no-tui", "--http-addr",
