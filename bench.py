@@ -480,8 +480,10 @@ def run_rank(args) -> int:
     # job-switch time of the native miner for SHA-256d and scrypt (set_job -> first batch of the new work running).
     latency = None
     switch: dict = {}
+    startup = None
     if not args.no_latency and info.is_primary and not cpu:
-        from otedama_amd.engine.latency_probe import measure_job_switch, measure_share_latency
+        from otedama_amd.engine.latency_probe import (measure_device_startup, measure_job_switch,
+                                                      measure_share_latency)
 
         try:
             latency = measure_share_latency(device_index=dev.index or 0, seconds=6.0)
@@ -492,6 +494,10 @@ def run_rank(args) -> int:
                 switch[algo] = measure_job_switch(device_index=dev.index or 0, algorithm=algo)
             except Exception as exc:  # noqa: BLE001
                 switch[algo] = {"error": f"{type(exc).__name__}: {exc}"}
+        try:
+            startup = measure_device_startup(device_index=dev.index or 0)
+        except Exception as exc:  # noqa: BLE001
+            startup = {"error": f"{type(exc).__name__}: {exc}"}
 
     if info.is_primary:
         out = {
@@ -552,6 +558,8 @@ def run_rank(args) -> int:
             "share_latency": latency,
             "job_switch_ms": {a: v.get("p50_ms") for a, v in switch.items()} or None,
             "job_switch": switch or None,
+            "device_process_startup_s": (startup or {}).get("spawn_to_first_batch_s"),
+            "device_process_startup": startup,
         }
         print(json.dumps(out), flush=True)
     shutdown(info)

@@ -153,3 +153,36 @@ def measure_job_switch(device_index: int = 0, algorithm: str = "sha256d", switch
     return {"p50_ms": statistics.median(samples) if samples else None, "max_ms": max(samples) if samples else None,
             "samples_ms": samples, "aborted_launches": st["aborted_launches"], "batch_nonces": batch_nonces,
             "definition": "set_job(new work) -> first batch of the new work running on the GPU"}
+
+
+def measure_device_startup(device_index: int = 0, timeout: float = 60.0) -> dict:
+    """Start-up of one production device process (engine/devproc.py: torch-free, its own HIP context): process
+    spawn -> the first batch of a SHA-256d job running on the GPU, the child's phases, and its resident set."""
+    from otedama_amd import hal
+    from otedama_amd.engine.devproc import DeviceProcess
+
+    devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
+    cus = int(devs[0].extra.get("cus", 256)) if devs else 256
+    dp = DeviceProcess(device_index, f"gpu-{device_index}", grid=cus * 6)
+    dp.set_job(_switch_job(0, "sha256d"))  # sent as soon as the child is up
+    t0 = time.time()
+    dp.start()
+    try:
+        end = time.monotonic() + timeout
+        while time.monotonic() < end and not dp.first_hash_wall:
+            time.sleep(0.005)
+        if not dp.first_hash_wall:
+            raise RuntimeError(f"device process reported no running batch within {timeout:.0f} s")
+        rss = None
+        try:
+            import psutil
+
+            rss = round(psutil.Process(dp.pid).memory_info().rss / 2**20, 1)
+        except Exception:  # noqa: BLE001 - psutil missing / child gone
+            pass
+        return {"spawn_to_first_batch_s": dp.first_hash_wall - t0,
+                "child_phases_s": {k: (v - t0) if v else None for k, v in dp.child_timing.items()},
+                "native_phases_ms": dict(dp.native_startup_ms), "rss_mib": rss,
+                "definition": "Popen of the device process -> its first SHA-256d batch running on the GPU"}
+    finally:
+        dp.stop()

@@ -89,3 +89,13 @@ def test_sigkilled_gpu_device_process_restarts_and_resumes():
         ms.stop()
     assert all(_verify(job, s, target) for s in shares)
     assert len({(s["version"], s["nonce"]) for s in shares}) == len(shares)  # nothing searched twice
+
+
+def test_device_process_starts_hashing_within_a_second():
+    """process start -> first GPU hash under 1 s (a warm page cache; bench.py records it)."""
+    from otedama_amd.engine.latency_probe import measure_device_startup
+
+    res = measure_device_startup(0)
+    print("device process start-up:", res)
+    assert res["spawn_to_first_batch_s"] < 1.0, res
+    assert res["native_phases_ms"].get("first_batch") is not None, res
