@@ -71,3 +71,25 @@ def test_refuses_more_gpus_than_visible():
 def test_torchrun_world_size_must_match_gpus():
     res = _bench("--gpus", "2", "--cpu-rehearsal", env={"WORLD_SIZE": "3", "RANK": "0"})
     assert res.returncode == 2 and "WORLD_SIZE=3" in res.stderr
+
+
+def test_driver_torchrun_invocation():
+    """Exactly the driver's multi-GPU command line (torchrun, its agent TCPStore, 127.0.0.1), with the CPU
+    rehearsal in place of the GPUs: ranks join the agent's store, run R1/R2/R3, and rank 0 prints one JSON line."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2",
+                          "--steps", "2", "--warmup", "1", "--cpu-rehearsal"],
+                         capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["rccl_ranks_seen"] == [0, 1]
+    assert d["hits_duplicate"] == 0 and d["hits_verified"] == d["hits_found"]
