@@ -477,7 +477,7 @@ def run_rank(args) -> int:
 
     # ---------------------------------------------------------- share latency
     # End-to-end share latency against the local pool in a separate process (default 2^29-nonce batches), then the
-    # job-switch time of the native miner for SHA-256d and scrypt (set_job -> first batch of the new work running).
+    # job-switch time of the native miner for SHA-256d, scrypt and X11 (set_job -> first batch of the new work running).
     latency = None
     switch: dict = {}
     startup = None
@@ -489,7 +489,7 @@ def run_rank(args) -> int:
             latency = measure_share_latency(device_index=dev.index or 0, seconds=6.0)
         except Exception as exc:  # noqa: BLE001 - latency is auxiliary; never fail the headline
             latency = {"error": f"{type(exc).__name__}: {exc}"}
-        for algo in ("sha256d", "scrypt"):
+        for algo in ("sha256d", "scrypt", "x11"):
             try:
                 switch[algo] = measure_job_switch(device_index=dev.index or 0, algorithm=algo)
             except Exception as exc:  # noqa: BLE001
