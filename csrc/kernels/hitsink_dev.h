@@ -18,9 +18,21 @@ __device__ __forceinline__ uint32_t abort_peek(const uint32_t* word, uint32_t ep
 }
 __device__ __forceinline__ uint32_t abort_peek(const otedama::HitSink& s) { return abort_peek(s.abort, s.epoch); }
 
+// Split poll for loops: abort_issue starts the load and returns the raw (per-lane, equal) value; abort_seen, called
+// one trip later, makes it wave-uniform and compares. abort_peek's readfirstlane right after the load makes the
+// wave wait for an uncached system-scope load (~1-2 us) on every trip; split, the load's latency hides under the
+// trip (the SHA-256d kernels lost ~0.5% to that wait, profiles/r3/g_ab).
+__device__ __forceinline__ uint32_t abort_issue(const otedama::HitSink& s) {
+  if (s.abort == nullptr) return s.epoch;
+  return __hip_atomic_load(const_cast<uint32_t*>(s.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // True once the host has moved the abort word past this batch's epoch (serial-number compare: wrap-safe).
 __device__ __forceinline__ bool abort_newer(uint32_t word, uint32_t epoch) {
   return static_cast<int32_t>(word - epoch) > 0;
+}
+__device__ __forceinline__ bool abort_seen(uint32_t raw, uint32_t epoch) {
+  return abort_newer(__builtin_amdgcn_readfirstlane(raw), epoch);
 }
 
 // One candidate. Miner path: the record is written, fenced at system scope, then tagged, so a host thread

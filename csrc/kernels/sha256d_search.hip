@@ -90,11 +90,11 @@ extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search(
     const otedama::Sha256dParams p, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t ab = abort_peek(sink), trip = 0;
+  uint32_t ab = abort_issue(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
     if (++trip == kAbortTrips) {
-      if (abort_newer(ab, sink.epoch)) break;
-      ab = abort_peek(sink);
+      if (abort_seen(ab, sink.epoch)) break;
+      ab = abort_issue(sink);
       trip = 0;
     }
     const uint32_t nonce = base + static_cast<uint32_t>(off);
@@ -200,11 +200,11 @@ __global__ __launch_bounds__(256) void otd_sha256d_search_k(const otedama::Sha25
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
   constexpr uint32_t kTrips = kAbortTrips / K > 0 ? kAbortTrips / K : 1;
-  uint32_t ab = abort_peek(sink), trip = 0;
+  uint32_t ab = abort_issue(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
     if (++trip == kTrips) {
-      if (abort_newer(ab, sink.epoch)) break;
-      ab = abort_peek(sink);
+      if (abort_seen(ab, sink.epoch)) break;
+      ab = abort_issue(sink);
       trip = 0;
     }
     const uint32_t nonce = base + static_cast<uint32_t>(off);

@@ -81,10 +81,10 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
 
   // Abort poll, one per grid-stride iteration: the load for the next check is issued at the top of each trip and
   // only waited on at the next trip's top, so its latency hides under a whole iteration of hashing.
-  uint32_t ab = abort_peek(sink);
+  uint32_t ab = abort_issue(sink);
   for (uint64_t off = first; off < count; off += stride) {
-    if (abort_newer(ab, sink.epoch)) break;
-    ab = abort_peek(sink);
+    if (abort_seen(ab, sink.epoch)) break;
+    ab = abort_issue(sink);
     const uint32_t w3 = base + static_cast<uint32_t>(off);  // wave-uniform
     // ---- hash 1, block 2: rounds 3..63 (schedule on the scalar unit) ----
     uint32_t W[64];
@@ -161,10 +161,10 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
     for (int i = 0; i < 8; ++i) { mid[c][i] = v.mid[i]; st3[c][i] = v.st3[i]; }
     pre3[c] = v.pre3; t2_3[c] = v.t2_3;
   }
-  uint32_t ab = abort_peek(sink);  // as in otd_sha256d_search_v: one poll per trip, latency hidden by the trip
+  uint32_t ab = abort_issue(sink);  // as in otd_sha256d_search_v: one poll per trip, latency hidden by the trip
   for (uint64_t off = first; off < count; off += stride) {
-    if (abort_newer(ab, sink.epoch)) break;
-    ab = abort_peek(sink);
+    if (abort_seen(ab, sink.epoch)) break;
+    ab = abort_issue(sink);
     const uint32_t w3 = base + static_cast<uint32_t>(off);
     uint32_t W[64];
     W[0] = p.w0; W[1] = p.w1; W[2] = p.w2; W[3] = w3;

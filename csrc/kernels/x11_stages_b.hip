@@ -453,9 +453,10 @@ __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4)
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
-    if (otedama_dev::abort_newer(otedama_dev::abort_peek(sink), sink.epoch)) return;
+    const u32 ab = otedama_dev::abort_issue(sink);  // checked after the digest loads: one memory wait, not two
     u64 h[8];
     load_hash(Hb, stride, i, h);
+    if (otedama_dev::abort_seen(ab, sink.epoch)) return;
     u32 W[16][4];
 #pragma unroll
     for (int k = 0; k < 16; ++k)

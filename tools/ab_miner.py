@@ -1,0 +1,62 @@
+"""Interleaved A/B of the production GPU miner (native GpuMiner: launches, hit ring, abort word, verification)
+between two source trees on one GPU, each measurement a fresh process.
+
+python tools/ab_miner.py --a . --b ab_old [--rounds 3] [--seconds 10]
+Prints one JSON line: SHA-256d hashes/s per round for A and B and the median ratio A/B.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+CHILD = r'''
+import os, sys, time, json
+sys.path.insert(0, sys.argv[1])
+os.environ["OTEDAMA_NO_TORCH"] = "1"
+from otedama_amd.ops.native import require_native
+from otedama_amd.models.header import int_to_hash
+N = require_native()
+secs = float(sys.argv[2])
+m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32, grid=N.gpu_cu_count(0) * 6, queue_cap=4096, sha_variants=128)
+hdr = bytes(range(76)) + bytes(4)
+m.set_job({"header": hdr, "target": int_to_hash((1 << 224) - 1), "job_id": "ab", "epoch": 1, "algo": "sha256d",
+           "version_mask": 0x1FFFE000})
+m.start()
+time.sleep(3.0)
+h0, t0 = m.stats()["hashes"], time.monotonic()
+time.sleep(secs)
+h1, t1 = m.stats()["hashes"], time.monotonic()
+m.stop()
+print(json.dumps({"hps": (h1 - h0) / (t1 - t0)}))
+'''
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--a", default=".")
+    ap.add_argument("--b", default="ab_old")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    a = ap.parse_args()
+    res = {"a": [], "b": []}
+    for _ in range(a.rounds):
+        for key, tree in (("a", a.a), ("b", a.b)):
+            out = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(tree), str(a.seconds)],
+                                 capture_output=True, text=True, timeout=120)
+            line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+            if out.returncode != 0 or not line:
+                print(json.dumps({"error": key, "stderr": out.stderr[-2000:]}))
+                return 1
+            res[key].append(json.loads(line[0])["hps"])
+    res["median_a"], res["median_b"] = statistics.median(res["a"]), statistics.median(res["b"])
+    res["a_over_b"] = res["median_a"] / res["median_b"]
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
