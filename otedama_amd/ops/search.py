@@ -201,10 +201,16 @@ class Sha256dSearchV:
             stream.wait_stream(cur)  # prepare() uploaded the variant table on the current stream
         with torch.cuda.stream(stream):
             out[:1].zero_()
+        self.launch_into(prep, base, count, out, stream)
+        return SearchResultK(out, self.cap)
+
+    def launch_into(self, prep: PreparedV, base: int, count: int, out: torch.Tensor, stream) -> None:
+        """Append this range's hits to ``out`` on ``stream``, with no zeroing and no stream ordering: for pipelined
+        callers that zero ``out`` once and spread one window over several launches on alternating streams (hit
+        slots are claimed atomically, so concurrent launches may share one buffer)."""
         self.native.launch_sha256d_v(prep.params, prep.vars.data_ptr(), base & 0xFFFFFFFF, int(count),
                                      out.data_ptr(), self.cap, self.grid, stream.cuda_stream, self.occupancy8,
                                      self.block, self.chains)
-        return SearchResultK(out, self.cap)
 
     def search(self, headers: list[bytes], target32: bytes, base: int = 0, count: int = 1 << 32) -> list[tuple[int, int]]:
         r = self.launch(self.prepare(headers, target32), base, count)
