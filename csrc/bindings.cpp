@@ -131,6 +131,7 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["aborted_launches"] = s.aborted_launches;
   d["ring_hits"] = s.ring_hits;
   d["clock_calib_rtt_us"] = s.clock_calib_rtt_us;
+  d["hashes_done_at_s"] = s.hashes_done_at_s;
   {
     py::dict ph;
     for (const auto& kv : s.startup_ms) ph[py::str(kv.first)] = kv.second;

@@ -90,6 +90,9 @@ struct MinerStats {
   uint64_t aborted_launches = 0;      // batches stopped early by the device abort word
   uint64_t ring_hits = 0;             // hits consumed from the host-coherent ring while their launch was running
   double clock_calib_rtt_us = 0;      // round trip of the device-clock calibration that is in use
+  // Device-timeline time (s, from the miner's start) at which the batches counted in `hashes` had completed: a
+  // rate over two samples, (hashes1 - hashes0) / (done_at1 - done_at0), is exact instead of quantized by launches.
+  double hashes_done_at_s = 0;
   // Start-up phases of the device thread, in order, each a duration in ms (GPU: hip_set_device, buffers,
   // clock_calibration, wait_first_job, first_batch = first job's set_job -> its first batch running).
   std::vector<std::pair<std::string, double>> startup_ms;

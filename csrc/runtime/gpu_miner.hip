@@ -187,6 +187,7 @@ void GpuMiner::loop() {
   hipStream_t ctl = nullptr, cal = nullptr;
   Batch slots[kInflight];
   uint32_t* d_abort = nullptr;   // uncached device word: the newest launch epoch that must keep running
+  hipEvent_t ref_ev = nullptr;   // device-timeline origin of hashes_done_at_s
   uint64_t* h_rt = nullptr;      // probe output (pinned, host-coherent)
   uint64_t* d_rt = nullptr;      // its device address
   std::thread cal_th;            // device-clock re-calibration
@@ -224,6 +225,7 @@ void GpuMiner::loop() {
       if (s.h_vars) (void)hipHostFree(s.h_vars);
     }
     if (d_abort) (void)hipFree(d_abort);
+    if (ref_ev) (void)hipEventDestroy(ref_ev);
     if (h_rt) (void)hipHostFree(h_rt);
     if (scratch) (void)hipFree(scratch);
     if (xbuf) (void)hipFree(xbuf);
@@ -311,6 +313,8 @@ void GpuMiner::loop() {
   for (int t = 0; t < 8; ++t) probe(slots[0].stream);
   rt_offset_ = rt_offset.load();
   phase("clock_calibration");
+  OTD_HIP(hipEventCreate(&ref_ev));
+  OTD_HIP(hipEventRecord(ref_ev, ctl));
   bool first_switch = true;
   cal_th = std::thread([&] {
     try {
@@ -471,6 +475,8 @@ void GpuMiner::loop() {
     drain_ring(b, n, cur, cur_g);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, b.start, b.done);
+    float done_ms = 0;  // device-timeline completion of this batch, for exact-window hash rates
+    const bool have_done = hipEventElapsedTime(&done_ms, ref_ev, b.done) == hipSuccess;
     const uint64_t full = b.count * uint64_t(b.nvar);
     const bool aborted = int32_t(epoch - b.epoch) > 0;  // a newer epoch was opened after this batch
     uint64_t done_hashes = full;
@@ -478,6 +484,7 @@ void GpuMiner::loop() {
     if (!aborted && ms > 0) rate_hpms = rate_hpms > 0 ? 0.8 * rate_hpms + 0.2 * (double(full) / ms) : double(full) / ms;
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.hashes += done_hashes;
+    if (have_done) stats_.hashes_done_at_s = std::max(stats_.hashes_done_at_s, double(done_ms) * 1e-3);
     stats_.candidates += n;
     stats_.busy_seconds += ms * 1e-3;
     stats_.launches += 1;

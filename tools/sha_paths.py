@@ -50,9 +50,18 @@ def main() -> int:
                    "algo": "sha256d", "version_mask": 0x1FFFE000})
         m.start()
         time.sleep(2.0)
-        h0, t0 = m.stats()["hashes"], time.monotonic()
+
+        def edge():  # counter moves only when a launch retires: time the window between two moves
+            h = m.stats()["hashes"]
+            while True:
+                h2 = m.stats()["hashes"]
+                if h2 != h:
+                    return h2, time.monotonic()
+                time.sleep(0.0002)
+
+        h0, t0 = edge()
         time.sleep(seconds)
-        h1, t1 = m.stats()["hashes"], time.monotonic()
+        h1, t1 = edge()
         m.stop()
         return (h1 - h0) / (t1 - t0)
 
