@@ -21,7 +21,8 @@ __device__ __forceinline__ uint32_t abort_peek(const otedama::HitSink& s) { retu
 // Split poll for loops: abort_issue starts the load and returns the raw (per-lane, equal) value; abort_seen, called
 // one trip later, makes it wave-uniform and compares. abort_peek's readfirstlane right after the load makes the
 // wave wait for an uncached system-scope load (~1-2 us) on every trip; split, the load's latency hides under the
-// trip (the SHA-256d kernels lost ~0.5% to that wait, profiles/r3/g_ab).
+// trip. (With 4 waves per SIMD the other waves covered most of that wait: the production miner measures the same
+// with either form and the same as the tree before the abort word, within 0.2%, profiles/r3/u_miner_ab.)
 __device__ __forceinline__ uint32_t abort_issue(const otedama::HitSink& s) {
   if (s.abort == nullptr) return s.epoch;
   return __hip_atomic_load(const_cast<uint32_t*>(s.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
