@@ -77,10 +77,12 @@ class _Heartbeat:
         self.th.start()
 
     def payload(self) -> dict:
-        st = self.local.device_stats().values()
+        st = list(self.local.device_stats().values())
         return {"t": time.time(), "hw": self.local.high_water(), "ep": self.local.epoch,
                 "hashes": sum(s["hashes"] for s in st), "shares": sum(s["shares"] for s in st),
                 "dropped": sum(s["dropped"] for s in st), "faulted": sum(1 for s in st if s["faulted"]),
+                # device-timeline completion time of the counted hashes (one GPU per rank): exact rate windows
+                "done": st[0].get("hashes_done_at_s", 0.0) if len(st) == 1 else 0.0,
                 "pid": os.getpid()}
 
     def _loop(self):
@@ -188,6 +190,7 @@ class NodeMinerSet:
         self.capacity = comm.info.world_size       # orig ranks 0..capacity-1 may exist
         self._rows_by_orig: dict[int, list[int]] = {}
         self.row_times: dict[int, float] = {}  # wall time at which each remote rank's counter row was produced
+        self.row_done_at: dict[int, float] = {}  # device-timeline time its counted hashes had completed
         self._prev_rows: dict[int, list[int]] = {}
         self._rates: dict[str, float] = {}
         self._t_last = time.monotonic()
@@ -306,7 +309,8 @@ class NodeMinerSet:
             lost = r in self.lost_ranks
             d[f"rank{r}"] = {"hashes": row[0], "shares": row[1], "dropped": row[2], "faulted": bool(row[3]) or lost,
                              "error": "rank lost" if lost else ("remote device fault" if row[3] else ""),
-                             "candidates": 0, "launches": 0, "counted_at": self.row_times.get(r, 0.0)}
+                             "candidates": 0, "launches": 0, "counted_at": self.row_times.get(r, 0.0),
+                             "hashes_done_at_s": self.row_done_at.get(r, 0.0)}
         return d
 
     def total_hashes(self) -> int:
@@ -390,6 +394,7 @@ class NodeMinerSet:
                 self._rows_by_orig[r] = [int(hb.get("hashes", 0)), int(hb.get("shares", 0)),
                                          int(hb.get("dropped", 0)), int(hb.get("faulted", 0))]
                 self.row_times[r] = float(hb["t"])
+                self.row_done_at[r] = float(hb.get("done", 0.0) or 0.0)
         dead = []
         grace = time.monotonic() - self._gen_started < self.hb_timeout  # members of a new generation get one
         for r in members[1:]:                                           # timeout to (re)start heartbeating

@@ -51,7 +51,10 @@ def _sample(http: str) -> dict:
     rate over a window is exact instead of off by up to one heartbeat period at each end."""
     now = time.time()
     st = _get(f"http://{http}/debug/stats")
-    return {k: (int(d.get("hashes", 0)), float(d.get("counted_at") or now)) for k, d in st["devices"].items()}
+    # the device-timeline completion time of the counted launches makes the window exact (counter moves come in
+    # whole 2^32-hash launches); else when the counters were taken
+    return {k: (int(d.get("hashes", 0)), float(d.get("hashes_done_at_s") or d.get("counted_at") or now))
+            for k, d in st["devices"].items()}
 
 
 def _rate(a: dict, b: dict) -> float:
