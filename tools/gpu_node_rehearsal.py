@@ -83,6 +83,32 @@ def _rss_top(pid: int, n: int = 8) -> list:
     return [(k, round(v, 1)) for k, v in sorted(sizes.items(), key=lambda kv: -kv[1])[:n]]
 
 
+def _measure_pair(cmds: list[list[str]], https: list[str], env: dict, seconds: float, log_dir: str) -> dict:
+    """Two independent `otedama run` processes sharing the one GPU: the fair baseline for a 2-rank node on this
+    1-GPU box (two processes' hardware queues time-share the GPU either way); their rates are summed."""
+    procs = [subprocess.Popen(c, env=env, cwd=ROOT, stdout=open(os.path.join(log_dir, f"pair{i}.log"), "w"),
+                              stderr=subprocess.STDOUT) for i, c in enumerate(cmds)]
+    out: dict = {}
+    try:
+        for h in https:
+            _wait(lambda h=h: _hashes(h) > 0, 120)
+        time.sleep(5.0)
+        s0 = [_sample(h) for h in https]
+        time.sleep(seconds)
+        s1 = [_sample(h) for h in https]
+        out["hashrates"] = [_rate(a, b) for a, b in zip(s0, s1)]
+        out["hashrate"] = sum(out["hashrates"])
+    finally:
+        for p in procs:
+            p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return out
+
+
 def _measure(cmd: list[str], http: str, env: dict, seconds: float, log_path: str) -> dict:
     t_spawn = time.time()
     p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(log_path, "w"), stderr=subprocess.STDOUT)
@@ -161,6 +187,13 @@ def main() -> int:
              http2], http2, dict(env, OTEDAMA_DIST_BACKEND="gloo"), a.seconds, os.path.join(a.out_dir, "node.log"))
         r, n = res["run"].get("hashrate"), res["node_gloo_2ranks_shared_gpu"].get("hashrate")
         res["node_vs_run"] = (n / r) if r and n else None
+        https = [f"127.0.0.1:{free_port()}" for _ in range(2)]
+        res["two_runs_shared_gpu"] = _measure_pair(
+            [[sys.executable, "-m", "otedama_amd", "run", "--config", cfg, "--no-tui", "--http-addr", h] for h in https],
+            https, env, a.seconds, a.out_dir)
+        p2 = res["two_runs_shared_gpu"].get("hashrate")
+        # the control plane's own cost: node vs the same two processes sharing the GPU without it
+        res["node_vs_two_runs"] = (n / p2) if p2 and n else None
         res["pool"] = _get(f"http://{pool_http}/api/v1/pool")
     finally:
         pool.send_signal(signal.SIGTERM)
