@@ -59,6 +59,7 @@ class DeviceMiner:
     paused: bool = False
     retired: bool = False  # faulted and removed from the stripe plan
     last_hashes: int = 0
+    last_done_at: float = 0.0  # device-timeline completion time of last_hashes (GPU miners)
     hashrate: float = 0.0
     idle_samples: int = 0  # consecutive stats ticks with work but no hash progress
     extra: dict = field(default_factory=dict)
@@ -387,8 +388,19 @@ class MinerSet:
         rates = {}
         working = self._template is not None
         for m in self.miners:
-            h = m.native.stats()["hashes"]
-            m.hashrate = 0.0 if m.retired else max(h - m.last_hashes, 0) / dt
+            st = m.native.stats()
+            h = st["hashes"]
+            done = float(st.get("hashes_done_at_s", 0.0) or 0.0)
+            # GPU counters move in whole launches (2^32 hashes, ~0.22 s): over the device-timeline span between the
+            # counted completions the rate is exact; sampled against wall time it jitters by a launch per interval
+            span = done - m.last_done_at
+            if m.retired:
+                m.hashrate = 0.0
+            elif done > 0 and m.last_done_at > 0 and span > 0 and h > m.last_hashes:
+                m.hashrate = (h - m.last_hashes) / span
+            else:
+                m.hashrate = max(h - m.last_hashes, 0) / dt
+            m.last_done_at = done
             if working and not m.paused and not m.retired and h == m.last_hashes:
                 m.idle_samples += 1
                 if m.idle_samples == self.stall_samples:
