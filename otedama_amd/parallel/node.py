@@ -24,7 +24,9 @@ generation (store prefix otd-g<gen>) with the survivors, ranks renumbered, and t
 with a ``variant_base`` past every cursor the ranks reported, so the dead rank's residue class is searched by
 the survivors from there on and nothing is searched twice. A replacement process (supervisor respawn) asks to
 join and is added by the next re-form. Rank 0 is the pool session: its loss ends the node (the supervisor
-restarts it).
+restarts it). Over gloo (CPU hosts, tests) one limit remains: a rank blocked in a ring collective that the dead
+rank's neighbours abandoned gives up after its bounded deadline, but tearing that group down waits out gloo's own
+op timeout (OTEDAMA_PG_TIMEOUT), so that re-form can take that long; RCCL groups are aborted at once.
 
 ``NodeMinerSet`` (rank 0) has the MinerSet API the engine uses; ``NodeWorker`` (ranks > 0) follows the op log.
 """
