@@ -260,54 +260,63 @@ __device__ __forceinline__ void simd_ntt_column(const u32 X[16], const u32 S[16]
   }
 }
 
-// tA of lane j ^ PP inside the 8-lane group, by DPP (quad_perm for xor 1/2/3, row_half_mirror for
-// xor 7; xor 4/5/6 = xor 7 then xor 3/2/1). The compiler fuses the DPP mov into the consuming add.
-template <int PP>
+// tA of lane j ^ PP inside the 8-lane group. xor 1/2/3 by DPP quad_perm and xor 7 by DPP row_half_mirror: the
+// compiler fuses those into the consuming add. xor 4/5/6 have no single DPP pattern (as DPP they cost a
+// separate v_mov_dpp, 31 VALU per lane over the two compressions); ds_swizzle's bit-mask mode reads lane
+// (l & 0x1F) ^ PP on the LDS unit instead, off the VALU, issued as soon as tA exists.
+template <int PP, bool kSw = true>
 __device__ __forceinline__ u32 simd_xlane(u32 v) {
-  constexpr int q = PP == 1 || PP == 6 ? 0xB1 : PP == 2 || PP == 5 ? 0x4E : 0x1B;  // xor 1 / 2 / 3
-  if (PP >= 4) {
-    v = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // xor 7
-    if (PP == 7) return v;
+  if constexpr (!kSw && PP >= 4 && PP <= 6) {  // round-2 form (tools/x11_variants.hip): xor 7, then xor 3/2/1
+    v = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    constexpr int q = PP == 6 ? 0xB1 : PP == 5 ? 0x4E : 0x1B;
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);
+  } else if constexpr (PP >= 4 && PP <= 6) {
+    return (u32)__builtin_amdgcn_ds_swizzle((int)v, (PP << 10) | 0x1F);
+  } else if constexpr (PP == 7) {
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror: xor 7
+  } else {
+    constexpr int q = PP == 1 ? 0xB1 : PP == 2 ? 0x4E : 0x1B;  // quad_perm: xor 1 / 2 / 3
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);
   }
-  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, q, 0xF, 0xF, false);
 }
 
 // One Feistel step on state column j (this lane).
-template <bool kMaj, int R, int S, int PP>
+template <bool kMaj, int R, int S, int PP, bool kSw = true>
 __device__ __forceinline__ void simd_step(u32& s0, u32& s1, u32& s2, u32& s3, u32 w) {
   const u32 tA = rotl32(s0, R);
   const u32 f = kMaj ? bop3<0xE8>(s0, s1, s2) : bop3<0xCA>(s0, s1, s2);  // MAJ / IF
   const u32 tt = s3 + w + f;
-  s0 = rotl32(tt, S) + simd_xlane<PP>(tA);
+  s0 = rotl32(tt, S) + simd_xlane<PP, kSw>(tA);
   s3 = s2;
   s2 = s1;
   s1 = tA;
 }
 
-template <int RD>
+template <int RD, bool kSw = true>
 __device__ __forceinline__ void simd_round(u32& s0, u32& s1, u32& s2, u32& s3, const u32 w[8]) {
   constexpr int r0 = kSimdRS[RD][0], r1 = kSimdRS[RD][1], r2 = kSimdRS[RD][2], r3 = kSimdRS[RD][3];
-  simd_step<false, r0, r1, kSimdPP[(0 + RD) % 7]>(s0, s1, s2, s3, w[0]);
-  simd_step<false, r1, r2, kSimdPP[(1 + RD) % 7]>(s0, s1, s2, s3, w[1]);
-  simd_step<false, r2, r3, kSimdPP[(2 + RD) % 7]>(s0, s1, s2, s3, w[2]);
-  simd_step<false, r3, r0, kSimdPP[(3 + RD) % 7]>(s0, s1, s2, s3, w[3]);
-  simd_step<true, r0, r1, kSimdPP[(4 + RD) % 7]>(s0, s1, s2, s3, w[4]);
-  simd_step<true, r1, r2, kSimdPP[(5 + RD) % 7]>(s0, s1, s2, s3, w[5]);
-  simd_step<true, r2, r3, kSimdPP[(6 + RD) % 7]>(s0, s1, s2, s3, w[6]);
-  simd_step<true, r3, r0, kSimdPP[(7 + RD) % 7]>(s0, s1, s2, s3, w[7]);
+  simd_step<false, r0, r1, kSimdPP[(0 + RD) % 7], kSw>(s0, s1, s2, s3, w[0]);
+  simd_step<false, r1, r2, kSimdPP[(1 + RD) % 7], kSw>(s0, s1, s2, s3, w[1]);
+  simd_step<false, r2, r3, kSimdPP[(2 + RD) % 7], kSw>(s0, s1, s2, s3, w[2]);
+  simd_step<false, r3, r0, kSimdPP[(3 + RD) % 7], kSw>(s0, s1, s2, s3, w[3]);
+  simd_step<true, r0, r1, kSimdPP[(4 + RD) % 7], kSw>(s0, s1, s2, s3, w[4]);
+  simd_step<true, r1, r2, kSimdPP[(5 + RD) % 7], kSw>(s0, s1, s2, s3, w[5]);
+  simd_step<true, r2, r3, kSimdPP[(6 + RD) % 7], kSw>(s0, s1, s2, s3, w[6]);
+  simd_step<true, r3, r0, kSimdPP[(7 + RD) % 7], kSw>(s0, s1, s2, s3, w[7]);
 }
 
 // 32 message steps + 4 feed-forward steps; h0..h3 = chaining column, s0..s3 = h ^ block.
+template <bool kSw = true>
 __device__ __forceinline__ void simd_compress(u32& s0, u32& s1, u32& s2, u32& s3, u32 h0, u32 h1, u32 h2, u32 h3,
                                               const u32 W[32]) {
-  simd_round<0>(s0, s1, s2, s3, W);
-  simd_round<1>(s0, s1, s2, s3, W + 8);
-  simd_round<2>(s0, s1, s2, s3, W + 16);
-  simd_round<3>(s0, s1, s2, s3, W + 24);
-  simd_step<false, 4, 13, kSimdPP[4]>(s0, s1, s2, s3, h0);
-  simd_step<false, 13, 10, kSimdPP[5]>(s0, s1, s2, s3, h1);
-  simd_step<false, 10, 25, kSimdPP[6]>(s0, s1, s2, s3, h2);
-  simd_step<false, 25, 4, kSimdPP[0]>(s0, s1, s2, s3, h3);
+  simd_round<0, kSw>(s0, s1, s2, s3, W);
+  simd_round<1, kSw>(s0, s1, s2, s3, W + 8);
+  simd_round<2, kSw>(s0, s1, s2, s3, W + 16);
+  simd_round<3, kSw>(s0, s1, s2, s3, W + 24);
+  simd_step<false, 4, 13, kSimdPP[4], kSw>(s0, s1, s2, s3, h0);
+  simd_step<false, 13, 10, kSimdPP[5], kSw>(s0, s1, s2, s3, h1);
+  simd_step<false, 10, 25, kSimdPP[6], kSw>(s0, s1, s2, s3, h2);
+  simd_step<false, 25, 4, kSimdPP[0], kSw>(s0, s1, s2, s3, h3);
 }
 
 // W = (l * mm mod 2^16) | (h * mm mod 2^16) << 16: pack (l, h) as u16 halves (one v_perm), then one
@@ -324,7 +333,8 @@ constexpr int kSimdBlock = 256;
 constexpr u32 kSimdLds = 624;
 
 // Eight lanes per hash: launch with 8 * n threads.
-__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+template <bool kSw>
+__device__ __forceinline__ void simd_stage(u64* __restrict__ Hb, u32 stride, u32 n) {
   __shared__ __attribute__((aligned(16))) u32 L[kSimdLds];
   for (u32 t = threadIdx.x; t < kSimdLds; t += kSimdBlock) {
     u32 v = 0;
@@ -383,14 +393,14 @@ __global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb,
   const u32 m0 = Hw[((size_t)(j >> 1) * stride + i) * 2 + (j & 1)];
   const u32 m1 = Hw[((size_t)(4 + (j >> 1)) * stride + i) * 2 + (j & 1)];
   u32 s0 = iv0 ^ m0, s1 = iv1 ^ m1, s2 = iv2, s3 = iv3;
-  simd_compress(s0, s1, s2, s3, iv0, iv1, iv2, iv3, W);
+  simd_compress<kSw>(s0, s1, s2, s3, iv0, iv1, iv2, iv3, W);
   // Final block: the 512-bit length (word 0), expanded with the final tweak (constant W_F).
   const u32* wf = L + 288 + 36 * j;
 #pragma unroll
   for (int st = 0; st < 32; ++st) W[st] = wf[st];
   const u32 c0 = s0, c1 = s1, c2 = s2, c3 = s3;
   if (j == 0) s0 ^= 512u;
-  simd_compress(s0, s1, s2, s3, c0, c1, c2, c3, W);
+  simd_compress<kSw>(s0, s1, s2, s3, c0, c1, c2, c3, W);
   // Output words j (s0) and 8 + j (s1); even lanes pair with their odd neighbour (DPP xor 1).
   const u32 n0 = simd_xlane<1>(s0), n1 = simd_xlane<1>(s1);
   if ((j & 1) == 0) {
@@ -398,6 +408,15 @@ __global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb,
     __builtin_nontemporal_store(mk64(s1, n1), Hb + (size_t)(4 + (j >> 1)) * stride + i);
   }
 }
+
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+  simd_stage<true>(Hb, stride, n);
+}
+#ifdef OTEDAMA_X11_VARIANTS
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64_dpp(u64* __restrict__ Hb, u32 stride, u32 n) {
+  simd_stage<false>(Hb, stride, n);
+}
+#endif
 
 // ------------------------------------------------------------------ ECHO-512
 // GF(2^8) doubling of 4 packed bytes: the 0x1b reduction as one packed 16-bit multiply (full rate;

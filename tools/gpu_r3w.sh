@@ -2,7 +2,7 @@
 # Round 3: which runtime knob owns the ~190 MB of host memory per hardware queue (tools/stream_rss.hip).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/${R3_TAG:-r3w}
+O=gpurun_out/r3w
 mkdir -p $O
 true &&
 for kv in NONE=1 HIP_FORCE_DEV_KERNARG=1 GPU_STAGING_BUFFER_SIZE=1 GPU_PINNED_XFER_SIZE=1 HSA_ENABLE_SDMA=0 \

@@ -40,7 +40,8 @@ typedef void (*StageFn)(u64*, u32, u32);
 struct Variant {
   const char* name;
   StageFn fn;
-  bool aes;    // grid-stride AES-table kernel: 512-thread blocks, 8 per CU (x11_launch_stage_b)
+  int kind;    // 0: one lane per nonce; 1: grid-stride AES-table kernel (512-thread blocks, 8 per CU);
+               // 2: SIMD-512, eight lanes per nonce
   int group;   // variants of one stage share a group; outputs are compared with the group's first
 };
 
@@ -54,18 +55,22 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, src, words);
   CK(hipGetLastError());
   using namespace otedama::x11k;
-  std::vector<Variant> vs = {{"jh_sgpr (production)", k_jh512_64, false, 0},
-                             {"jh_lds_w7", k_jh512_64_w7, false, 0},
-                             {"jh_lds_reload_w7", k_jh512_64_reload_w7, false, 0},
-                             {"jh_lds", k_jh512_64_lds, false, 0},
-                             {"shavite_4round_trips (production)", k_shavite512_64, true, 1},
-                             {"shavite_r2 (round-2 kernel)", k_shavite512_64_r2, true, 1}};
+  std::vector<Variant> vs = {{"jh_sgpr (production)", k_jh512_64, 0, 0},
+                             {"jh_lds_w7", k_jh512_64_w7, 0, 0},
+                             {"jh_lds_reload_w7", k_jh512_64_reload_w7, 0, 0},
+                             {"jh_lds", k_jh512_64_lds, 0, 0},
+                             {"shavite_4round_trips (production)", k_shavite512_64, 1, 1},
+                             {"shavite_r2 (round-2 kernel)", k_shavite512_64_r2, 1, 1},
+                             {"simd_swizzle (production)", k_simd512_64, 2, 2},
+                             {"simd_dpp (round-2 lane exchange)", k_simd512_64_dpp, 2, 2}};
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   auto launch = [&](const Variant& v, u64* buf) {
-    if (v.aes) {
+    if (v.kind == 1) {
       const u32 want = (n + 511) / 512, cap = (u32)cus * 8;
       hipLaunchKernelGGL(v.fn, dim3(want < cap ? want : cap), dim3(512), 0, 0, buf, stride, n);
+    } else if (v.kind == 2) {
+      hipLaunchKernelGGL(v.fn, dim3(uint32_t((8ull * n + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0, buf, stride, n);
     } else {
       hipLaunchKernelGGL(v.fn, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, 0, buf, stride, n);
     }
