@@ -661,7 +661,6 @@ X11_STAGE_KERNEL(k_luffa512_64, luffa512_64)
 X11_STAGE_KERNEL(k_cubehash512_64, cubehash512_64)
 #undef X11_STAGE_KERNEL
 
-#ifdef OTEDAMA_X11_VARIANTS
 __device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u32 n, bool reload) {
   __shared__ __attribute__((aligned(16))) u32 BC[42][8];
   for (u32 t = threadIdx.x; t < 42 * 8; t += kBlock) BC[t / 8][t % 8] = x11t::JH_BC[t / 8][t % 8];
@@ -674,17 +673,14 @@ __device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u
   else jh512_64(h, BC);
   store_hash(Hb, stride, i, h);
 }
-#endif
-// Round constants through the scalar cache (one v_mov per word into a VGPR operand: 672 per hash, 5.5% of JH's
-// VALU). Staging them in LDS removes every v_mov but measured the same (1.90-1.97 vs 1.92-1.94 ms per 2^23 at
-// 7 waves, 2.00 at 5 waves: tools/x11_variants.hip, profiles/r3/h_jh/), so the simpler kernel stays.
-__global__ __launch_bounds__(kBlock) void k_jh512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  u64 h[8];
-  load_hash(Hb, stride, i, h);
-  jh512_64(h, x11t::JH_BC);
-  store_hash(Hb, stride, i, h);
+// Round constants staged in LDS so each round's eight words arrive in VGPRs by ds_read (from the scalar cache
+// they need one v_mov per word: 672 per hash, 5.5% of JH's VALU), the message re-read from H for the second
+// injection, 7 waves/SIMD (72 VGPRs, 44 B of spills outside the round loops). Same-run times per 2^23 against
+// the scalar-cache kernel in four sessions: -4.4%, -2.0%, -1.3%, +1.0% (tools/x11_variants.hip,
+// profiles/r3/h_jh, l_shavite, x_simd).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, true);
 }
 #ifdef OTEDAMA_X11_VARIANTS
 // Alternatives timed by tools/x11_variants.hip (not built into the extension).
@@ -692,9 +688,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     u64* __restrict__ Hb, u32 stride, u32 n) {
   jh_stage_lds(Hb, stride, n, false);
 }
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64_reload_w7(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
-  jh_stage_lds(Hb, stride, n, true);
+__global__ __launch_bounds__(kBlock) void k_jh512_64_sgpr(u64* __restrict__ Hb, u32 stride, u32 n) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;  // round constants through the scalar cache + v_mov
+  if (i >= n) return;
+  u64 h[8];
+  load_hash(Hb, stride, i, h);
+  jh512_64(h, x11t::JH_BC);
+  store_hash(Hb, stride, i, h);
 }
 __global__ __launch_bounds__(kBlock) void k_jh512_64_lds(u64* __restrict__ Hb, u32 stride, u32 n) {
   jh_stage_lds(Hb, stride, n, false);

@@ -55,9 +55,9 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, src, words);
   CK(hipGetLastError());
   using namespace otedama::x11k;
-  std::vector<Variant> vs = {{"jh_sgpr (production)", k_jh512_64, 0, 0},
+  std::vector<Variant> vs = {{"jh_lds_reload_w7 (production)", k_jh512_64, 0, 0},
+                             {"jh_sgpr", k_jh512_64_sgpr, 0, 0},
                              {"jh_lds_w7", k_jh512_64_w7, 0, 0},
-                             {"jh_lds_reload_w7", k_jh512_64_reload_w7, 0, 0},
                              {"jh_lds", k_jh512_64_lds, 0, 0},
                              {"shavite_4round_trips (production)", k_shavite512_64, 1, 1},
                              {"shavite_r2 (round-2 kernel)", k_shavite512_64_r2, 1, 1},
