@@ -3,7 +3,7 @@
 # and the production rehearsal (run vs 2-rank gloo node).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/${R3_TAG:-r3q}
+O=gpurun_out/${R3_TAG:-r3y}
 mkdir -p $O
 export TMPDIR=/tmp
 export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
