@@ -99,3 +99,15 @@ def test_device_process_starts_hashing_within_a_second():
     print("device process start-up:", res)
     assert res["spawn_to_first_batch_s"] < 1.0, res
     assert res["native_phases_ms"].get("first_batch") is not None, res
+
+
+def test_share_latency_pool_in_its_own_process():
+    """device hit -> pool accept p50 under 2 ms, with the pool in a separate process and the GPU in
+    a device process (the production layout)."""
+    from otedama_amd.engine.latency_probe import measure_share_latency
+
+    res = measure_share_latency(device_index=0, seconds=4.0)
+    print("share latency:", {k: v for k, v in res.items() if k.endswith("_ms") or k.startswith("pool_")})
+    assert res["accepted"] >= 5 and res["rejected"] == 0 and res["pool_rejected"] == 0, res
+    assert res["device_hit_to_accept_p50_ms"] is not None and res["device_hit_to_accept_p50_ms"] < 2.0, res
+    assert res["p50_ms"] < 2.0, res
