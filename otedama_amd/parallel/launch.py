@@ -133,10 +133,10 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
         started[r] = time.monotonic()
 
     prev = {}
+    stopping = []
 
-    def forward(sig, _frame):
-        _stop_all(list(procs.values()), grace=10.0)
-        sys.exit(128 + sig)
+    def forward(sig, _frame):  # a clean stop: every rank gets SIGTERM and shuts down like `otedama run` does
+        stopping.append(sig)
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         try:
@@ -147,6 +147,11 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
         for r in range(world):
             spawn(r, join=False)
         while True:
+            if stopping:
+                log(f"signal {stopping[0]}: stopping the node")
+                _stop_all(list(procs.values()), grace=30.0)
+                rc0 = procs[0].returncode if 0 in procs else None
+                return 0 if rc0 in (0, -signal.SIGTERM, 128 + signal.SIGTERM) else (rc0 or 0)
             if stop_event is not None and stop_event.is_set():
                 return 0
             rc0 = procs[0].poll()

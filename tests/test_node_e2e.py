@@ -87,7 +87,8 @@ def test_otedama_node_keeps_mining_through_a_rank_loss(tmp_path):
     finally:
         sup.send_signal(signal.SIGTERM)
         try:
-            sup.wait(timeout=40)
+            rc = sup.wait(timeout=40)
+            assert rc == 0, (rc, (tmp_path / "node.out").read_text()[-3000:])  # a clean stop, like `otedama run`
         except subprocess.TimeoutExpired:
             for c in psutil.Process(sup.pid).children(recursive=True):
                 c.kill()
