@@ -52,12 +52,22 @@ def main() -> int:
     ap.add_argument("--b", default="ab_old")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--env-a", default="", help="KEY=VALUE[,KEY=VALUE] for the A processes")
+    ap.add_argument("--env-b", default="", help="KEY=VALUE[,KEY=VALUE] for the B processes")
     a = ap.parse_args()
+
+    def env_of(spec: str) -> dict:
+        e = dict(os.environ)
+        for kv in filter(None, spec.split(",")):
+            k, _, v = kv.partition("=")
+            e[k] = v
+        return e
+
     res = {"a": [], "b": []}
     for _ in range(a.rounds):
-        for key, tree in (("a", a.a), ("b", a.b)):
+        for key, tree, spec in (("a", a.a, a.env_a), ("b", a.b, a.env_b)):
             out = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(tree), str(a.seconds)],
-                                 capture_output=True, text=True, timeout=120)
+                                 capture_output=True, text=True, timeout=120, env=env_of(spec))
             line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
             if out.returncode != 0 or not line:
                 print(json.dumps({"error": key, "stderr": out.stderr[-2000:]}))
