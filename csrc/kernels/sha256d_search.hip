@@ -85,16 +85,19 @@ __device__ __forceinline__ uint32_t sha256d_h7(const otedama::Sha256dParams& p, 
 // Nonces are header-order values (bytes 76..79 little-endian); the kernel feeds
 // W3 = bswap(nonce) (one v_perm per nonce) so base/count index the nonce itself.
 // A trip here is one hash per lane (~1 us per wave), so the abort word is polled every kAbortTrips trips.
+// This kernel polls with abort_peek (wave-uniform right after the load), not the split issue/seen form of the
+// multi-variant kernels: in one process on the MI355X the split form ran 1.8-2.2% slower here at every grid
+// (and peek matched no poll at all), at the same 51/50 VGPRs and 7 waves/SIMD (profiles/r3/ad_single).
 constexpr uint32_t kAbortTrips = 32;
 extern "C" __global__ __launch_bounds__(256) void otd_sha256d_search(
     const otedama::Sha256dParams p, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t ab = abort_issue(sink), trip = 0;
+  uint32_t ab = abort_peek(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
     if (++trip == kAbortTrips) {
-      if (abort_seen(ab, sink.epoch)) break;
-      ab = abort_issue(sink);
+      if (abort_newer(ab, sink.epoch)) break;
+      ab = abort_peek(sink);
       trip = 0;
     }
     const uint32_t nonce = base + static_cast<uint32_t>(off);

@@ -23,6 +23,8 @@ import subprocess
 import sys
 import time
 
+from otedama_amd.ops.tuning import sha256d_grid
+
 PROBE_ADDR = "bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq"
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -135,7 +137,7 @@ def measure_job_switch(device_index: int = 0, algorithm: str = "sha256d", switch
     N = require_native()
     cus = N.gpu_cu_count(device_index) or 256
     dwell = dwell if dwell is not None else (0.6 if algorithm == "scrypt" else 0.25)
-    m = N.GpuMiner(device_index, f"gpu-{device_index}", batch_nonces=batch_nonces, grid=cus * 6, queue_cap=4096,
+    m = N.GpuMiner(device_index, f"gpu-{device_index}", batch_nonces=batch_nonces, grid=sha256d_grid(cus), queue_cap=4096,
                    sha_variants=128)
     m.start()
     try:
@@ -163,7 +165,7 @@ def measure_device_startup(device_index: int = 0, timeout: float = 60.0) -> dict
 
     devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
     cus = int(devs[0].extra.get("cus", 256)) if devs else 256
-    dp = DeviceProcess(device_index, f"gpu-{device_index}", grid=cus * 6)
+    dp = DeviceProcess(device_index, f"gpu-{device_index}", grid=sha256d_grid(cus))
     dp.set_job(_switch_job(0, "sha256d"))  # sent as soon as the child is up
     t0 = time.time()
     dp.start()

@@ -33,6 +33,7 @@ from dataclasses import dataclass, field
 
 from otedama_amd.hal import Family, SimpleDevice
 from otedama_amd.ops.native import require_native
+from otedama_amd.ops.tuning import sha256d_grid
 from otedama_amd.parallel.partition import stripe_for
 
 # Template keys that do not change the search space (same as the native same_work()).
@@ -105,11 +106,11 @@ class MinerSet:
             if isolation == "process":
                 from otedama_amd.engine.devproc import DeviceProcess
 
-                m = DeviceProcess(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6,
+                m = DeviceProcess(d.index, d.identity().id, batch_nonces=batch_nonces, grid=sha256d_grid(cus),
                                   queue_cap=queue_cap, sha_variants=sha_variants, log=self.log,
                                   on_exit=self._on_process_exit, on_ready=self._on_process_ready)
             else:
-                m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=cus * 6, queue_cap=queue_cap,
+                m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=sha256d_grid(cus), queue_cap=queue_cap,
                                sha_variants=sha_variants)
             self.miners.append(DeviceMiner(d, m))
         cpus = [d for d in devices if d.identity().family == Family.CPU]

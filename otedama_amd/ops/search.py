@@ -21,19 +21,13 @@ import torch
 
 from otedama_amd.ops.native import require_native
 
-# Blocks of 256 lanes per CU that stay resident for the SHA-256d kernel
-# (SGPR-limited to 6 on gfx950: see csrc/kernels/sha256d_search.hip).
-SHA256D_BLOCKS_PER_CU = 6
-SHA256D_K_BLOCKS_PER_CU = 16  # K-variant kernel: K=8 121 VGPRs (4 waves/SIMD); 4/8/12/16 per CU: 18.05/18.48/18.72/18.80 GH/s
-# Version-parallel kernel, 8-waves/SIMD build: 64 blocks of 256 per CU (tools/bench_sha_v.py sweep, profiles/r2/sha_v:
-# 8/16/32/64/96/128 per CU -> 18.37/18.73/19.00/19.61/19.58/19.61 GH/s; more resident-block rounds keep the waves'
-# scalar/vector phases apart).
-SHA256D_V_BLOCKS_PER_CU = 64
-# Two-chain version-parallel kernel (two variants per lane), 4-waves/SIMD build: 128 blocks per CU (profiles/r2/sha_v2:
-# 16/32/64/128/256 per CU -> 19.12/19.29/19.32/19.36-19.40/19.37-19.42 GH/s, against 19.21-19.30 for the one-chain
-# kernel in the same runs).
-SHA256D_V2_BLOCKS_PER_CU = 128
-SCRYPT_BLOCKS_PER_CU = 16  # 128 GiB pad at gap 1 (grid sweep: 2048 16.4, 4096 16.75, 5120 16.95 MH/s)
+from otedama_amd.ops.tuning import (  # noqa: F401  (re-exported: launch geometry lives in the torch-free module)
+    SCRYPT_BLOCKS_PER_CU,
+    SHA256D_BLOCKS_PER_CU,
+    SHA256D_K_BLOCKS_PER_CU,
+    SHA256D_V2_BLOCKS_PER_CU,
+    SHA256D_V_BLOCKS_PER_CU,
+)
 
 
 def _device_index(device) -> int:

@@ -2,11 +2,12 @@
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Icsrc/kernels \
 //          -mllvm -pragma-unroll-threshold=1000000 tools/sha_single_ab.hip -o tools/bin/sha_single_ab
-// Run:   tools/bin/sha_single_ab [rounds] [grid]   -> one JSON line: GH/s per form (median of rounds), hit counts
+// Run:   tools/bin/sha_single_ab [rounds] [grid ...]   -> one JSON line per grid: GH/s per form (median of rounds)
 //
-// Forms: the production kernel (abort_issue / abort_seen), the previous form (abort_peek right after the load),
-// and no poll at all; each with no abort word (the ops path, bench.py's single-midstate pass) and with an
-// uncached abort word that never moves (the native miner). Every form must report the same hits.
+// Forms: the production kernel (abort_peek right after the load), the split form of the multi-variant kernels
+// (abort_issue / abort_seen; production here until profiles/r3/ad_single), and no poll at all; each with no abort
+// word (the ops path, bench.py's single-midstate pass) and with an uncached abort word that never moves (the
+// native miner). Every form must report the same hits.
 #include "../csrc/kernels/sha256d_search.hip"
 
 #include <algorithm>
@@ -31,15 +32,15 @@ using otedama_dev::abort_peek;
 using otedama_dev::abort_seen;
 using otedama_dev::hit_publish;
 
-__global__ __launch_bounds__(256) void ab_single_peek(const otedama::Sha256dParams p, uint32_t base, uint64_t count,
-                                                      const otedama::HitSink sink) {
+__global__ __launch_bounds__(256) void ab_single_split(const otedama::Sha256dParams p, uint32_t base, uint64_t count,
+                                                       const otedama::HitSink sink) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t stride = gridDim.x * blockDim.x;
-  uint32_t ab = abort_peek(sink), trip = 0;
+  uint32_t ab = abort_issue(sink), trip = 0;
   for (uint64_t off = tid; off < count; off += stride) {
     if (++trip == kAbortTrips) {
-      if (abort_newer(ab, sink.epoch)) break;
-      ab = abort_peek(sink);
+      if (abort_seen(ab, sink.epoch)) break;
+      ab = abort_issue(sink);
       trip = 0;
     }
     const uint32_t nonce = base + static_cast<uint32_t>(off);
@@ -63,7 +64,9 @@ using Kern = void (*)(const otedama::Sha256dParams, uint32_t, uint64_t, const ot
 
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 5;
-  const uint32_t grid = argc > 2 ? uint32_t(std::atoi(argv[2])) : 1536;  // ops/search.py default: 6 blocks per CU
+  std::vector<uint32_t> grids;
+  for (int i = 2; i < argc; ++i) grids.push_back(uint32_t(std::atoi(argv[i])));
+  if (grids.empty()) grids.push_back(1536);
   const uint64_t count = 1ull << 32;
   otedama::Sha256dParams p{};
   for (int i = 0; i < 8; ++i) p.mid[i] = 0x6a09e667u * (i + 3), p.st3[i] = 0x9e3779b9u * (i + 7);
@@ -86,14 +89,16 @@ int main(int argc, char** argv) {
     std::vector<double> gh;
     uint32_t hits = 0;
   };
-  std::vector<Form> forms = {{"prod_issue_seen", otd_sha256d_search, false, {}},
-                             {"prev_peek", ab_single_peek, false, {}},
+  std::vector<Form> forms = {{"prod_peek", otd_sha256d_search, false, {}},
+                             {"split_issue_seen", ab_single_split, false, {}},
                              {"no_poll", ab_single_nopoll, false, {}},
-                             {"prod_issue_seen+word", otd_sha256d_search, true, {}},
-                             {"prev_peek+word", ab_single_peek, true, {}}};
+                             {"prod_peek+word", otd_sha256d_search, true, {}},
+                             {"split_issue_seen+word", ab_single_split, true, {}}};
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  for (const uint32_t grid : grids) {
+  for (auto& f : forms) f.gh.clear(), f.hits = 0;
   for (auto& f : forms) {  // warm-up: load each code object once
     otedama::HitSink s;
     s.out = out, s.cap = cap, s.epoch = epoch, s.abort = f.word ? word : nullptr;
@@ -127,5 +132,7 @@ int main(int argc, char** argv) {
                 forms[i].hits == forms[0].hits ? "true" : "false");
   }
   std::printf("}}\n");
+  std::fflush(stdout);
+  }
   return 0;
 }
