@@ -89,6 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
     ap.add_argument("--x11-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
+    ap.add_argument("--seed", type=int, default=1,
+                    help="synthetic header seed: the hit count of a seed is one Poisson draw, repeated on every run")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="gloo + native CPU scanner instead of the GPU kernels (launcher / collective tests)")
@@ -193,7 +195,7 @@ def run_rank(args) -> int:
         if not cpu:
             torch.cuda.synchronize(dev)
 
-    job = comm.broadcast_job(synthetic_job() if info.is_primary else None)  # R1: the job blob, once
+    job = comm.broadcast_job(synthetic_job(args.seed) if info.is_primary else None)  # R1: the job blob, once
     if cpu:
         from otedama_amd.models.header import int_to_hash
 
@@ -559,6 +561,7 @@ def run_rank(args) -> int:
             "hits_outside_window": outside,
             "hits_expected": expected,
             "hits_z": z,
+            "hits_seed": args.seed,  # fixed synthetic headers: every run of this seed draws the same hits
             "hits_r2_gathered": r2_hits,
             "scrypt_hashes_per_sec": scrypt_hps,
             "scrypt": scrypt_info,

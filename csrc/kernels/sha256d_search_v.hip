@@ -140,7 +140,9 @@ template __global__ void otd_sha256d_search_v<8>(const otedama::Sha256dParamsV, 
 // scalar schedule, so the SALU work per hash drops NC-fold, and the independent round chains give each wave ILP at
 // lower occupancy. NC = 2: 111 VGPRs, 4 waves/SIMD (MINW = 5: 96 VGPRs, 5 waves); NC = 3: 157 VGPRs, 3 waves;
 // NC = 4: 203 VGPRs, 2 waves. p.groups counts groups of 64*NC variants.
-template <int NC, int MINW>
+// POLL picks the abort-poll form: 0 split issue/seen every trip (production), 1 abort_peek every trip, 2 none.
+// Only 0 is instantiated here; tools/sha_v_ab.hip instantiates the others for same-process A/B runs.
+template <int NC, int MINW, int POLL = 0>
 __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_vn(
     const otedama::Sha256dParamsV p, VarPtr vars, uint32_t base, uint64_t count, const otedama::HitSink sink) {
   const uint32_t wpb = blockDim.x >> 6;
@@ -161,10 +163,16 @@ __global__ __launch_bounds__(256, MINW > 0 ? MINW : 1) void otd_sha256d_search_v
     for (int i = 0; i < 8; ++i) { mid[c][i] = v.mid[i]; st3[c][i] = v.st3[i]; }
     pre3[c] = v.pre3; t2_3[c] = v.t2_3;
   }
-  uint32_t ab = abort_issue(sink);  // as in otd_sha256d_search_v: one poll per trip, latency hidden by the trip
+  // as in otd_sha256d_search_v: one poll per trip, latency hidden by the trip
+  uint32_t ab = POLL == 1 ? abort_peek(sink) : abort_issue(sink);
   for (uint64_t off = first; off < count; off += stride) {
-    if (abort_seen(ab, sink.epoch)) break;
-    ab = abort_issue(sink);
+    if constexpr (POLL == 0) {
+      if (abort_seen(ab, sink.epoch)) break;
+      ab = abort_issue(sink);
+    } else if constexpr (POLL == 1) {
+      if (abort_newer(ab, sink.epoch)) break;
+      ab = abort_peek(sink);
+    }
     const uint32_t w3 = base + static_cast<uint32_t>(off);
     uint32_t W[64];
     W[0] = p.w0; W[1] = p.w1; W[2] = p.w2; W[3] = w3;

@@ -5,8 +5,10 @@ size a grid. Values are blocks of 256 lanes per CU; every number cites the sweep
 from __future__ import annotations
 
 # Single-midstate kernel (51 VGPRs, 7 waves/SIMD resident): an oversubscribed grid-stride grid wins over a resident
-# one. profiles/r3/ae_single: 6/7/8/14/28/64 per CU -> 16.18/16.23/16.24/16.35/16.43/16.50 GH/s (peek poll).
-SHA256D_BLOCKS_PER_CU = 64
+# one, a little more with every doubling (peek poll, one process per sweep): 6/7/8/14/28/64 per CU ->
+# 16.18/16.23/16.24/16.35/16.43/16.50 GH/s (profiles/r3/ad_single/peek_prod), 32/64/128/256 per CU ->
+# 16.42/16.48/16.52/16.55 (profiles/r3/af_single). A 2^32-nonce launch still gives every lane 256 trips.
+SHA256D_BLOCKS_PER_CU = 256
 SHA256D_K_BLOCKS_PER_CU = 16  # K-variant kernel: K=8 121 VGPRs (4 waves/SIMD); 4/8/12/16 per CU: 18.05/18.48/18.72/18.80 GH/s
 # Version-parallel kernel, 8-waves/SIMD build: 64 blocks of 256 per CU (tools/bench_sha_v.py sweep, profiles/r2/sha_v:
 # 8/16/32/64/96/128 per CU -> 18.37/18.73/19.00/19.61/19.58/19.61 GH/s; more resident-block rounds keep the waves'
