@@ -98,7 +98,14 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+# The benchmark is not the fault-tolerant node: a rank that is slow to start (a cold first `import torch` on a fresh
+# node can take a minute) or busy re-verifying hits must not trip the node's 30 s collective bound. Set before
+# otedama_amd.parallel is imported (it reads the bound at import); spawned ranks inherit it.
+BENCH_PG_TIMEOUT_S = "600"
+
+
 def main(argv=None) -> int:
+    os.environ.setdefault("OTEDAMA_PG_TIMEOUT", BENCH_PG_TIMEOUT_S)
     args = parse_args(argv)
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)

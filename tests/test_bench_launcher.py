@@ -93,3 +93,19 @@ def test_driver_torchrun_invocation():
     d = _json(res)
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["rccl_ranks_seen"] == [0, 1]
     assert d["hits_duplicate"] == 0 and d["hits_verified"] == d["hits_found"]
+
+
+def test_bench_ranks_get_a_long_collective_bound(monkeypatch):
+    """The bench is not the fault-tolerant node: its ranks run with a 600 s collective bound (a cold rank start on
+    a fresh 8-GPU node must not trip the node's 30 s default), unless the caller set one."""
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+    finally:
+        sys.path.remove(ROOT)
+    monkeypatch.delenv("OTEDAMA_PG_TIMEOUT", raising=False)
+    assert bench.main(["--gpus", "0"]) == 2  # refused before any rank starts, after the bound is set
+    assert os.environ["OTEDAMA_PG_TIMEOUT"] == bench.BENCH_PG_TIMEOUT_S
+    monkeypatch.setenv("OTEDAMA_PG_TIMEOUT", "45")
+    bench.main(["--gpus", "0"])
+    assert os.environ["OTEDAMA_PG_TIMEOUT"] == "45"
