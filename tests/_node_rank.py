@@ -59,8 +59,9 @@ def main(out_dir: str, mode: str) -> int:
                 break
             time.sleep(0.02)
         res["phase1_devices"] = sorted({s["device_id"] for s in shares})
-        with open(os.path.join(out_dir, "phase1.json"), "w") as f:
+        with open(os.path.join(out_dir, "phase1.json.tmp"), "w") as f:
             json.dump({"n": len(shares)}, f)
+        os.replace(os.path.join(out_dir, "phase1.json.tmp"), os.path.join(out_dir, "phase1.json"))
         killed = os.path.join(out_dir, "killed.json")
         end = time.monotonic() + 60
         while not os.path.exists(killed) and time.monotonic() < end:

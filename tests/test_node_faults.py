@@ -42,6 +42,14 @@ def _spawn(world, out, mode, port, store_hosted=True, rank=None, join=False):
     return procs
 
 
+def _write_json(path, obj):
+    """Write-then-rename: a rank polling for the file never opens it empty (a plain open/dump raced the reader)."""
+    tmp = f"{path}.tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+
+
 def _wait_file(path, timeout, procs):
     end = time.monotonic() + timeout
     while time.monotonic() < end:
@@ -83,8 +91,7 @@ def test_rank_loss_reforms_and_keeps_mining(tmp_path, world, victim, mark_dead):
         t_kill = time.time()
         if mark_dead:  # what the supervisor does when a child exits
             store.set(f"otd/dead/{victim}", "1")
-        with open(tmp_path / "killed.json", "w") as f:
-            json.dump({"rank": victim, "t": t_kill}, f)
+        _write_json(tmp_path / "killed.json", {"rank": victim, "t": t_kill})
         codes = _finish({r: p for r, p in procs.items() if r != victim})
     finally:
         for p in procs.values():
@@ -124,8 +131,7 @@ def test_replacement_rank_rejoins(tmp_path):
         assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
         procs[victim].send_signal(signal.SIGKILL)
         store.set(f"otd/dead/{victim}", "1")
-        with open(tmp_path / "killed.json", "w") as f:
-            json.dump({"rank": victim, "t": time.time()}, f)
+        _write_json(tmp_path / "killed.json", {"rank": victim, "t": time.time()})
         time.sleep(1.5)
         store.delete_key(f"otd/dead/{victim}")
         procs[victim] = _spawn(world, tmp_path, "rejoin", port, rank=victim, join=True)[victim]
