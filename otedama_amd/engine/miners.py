@@ -62,6 +62,7 @@ class DeviceMiner:
     last_hashes: int = 0
     last_done_at: float = 0.0  # device-timeline completion time of last_hashes (GPU miners)
     hashrate: float = 0.0
+    exact: bool = False  # hashrate came from a device-timeline span (not a wall-clock sample) at the last tick
     idle_samples: int = 0  # consecutive stats ticks with work but no hash progress
     extra: dict = field(default_factory=dict)
     backoff: float = RESPAWN_BACKOFF_INITIAL
@@ -395,10 +396,12 @@ class MinerSet:
             # GPU counters move in whole launches (2^32 hashes, ~0.22 s): over the device-timeline span between the
             # counted completions the rate is exact; sampled against wall time it jitters by a launch per interval
             span = done - m.last_done_at
+            m.exact = False
             if m.retired:
                 m.hashrate = 0.0
             elif done > 0 and m.last_done_at > 0 and span > 0 and h > m.last_hashes:
                 m.hashrate = (h - m.last_hashes) / span
+                m.exact = True
             else:
                 m.hashrate = max(h - m.last_hashes, 0) / dt
             m.last_done_at = done
@@ -412,6 +415,16 @@ class MinerSet:
             m.last_hashes = h
             rates[m.id] = m.hashrate
         return rates
+
+    def exact_total(self) -> float | None:
+        """Sum of the device rates when every live miner's rate at the last tick came from a device-timeline span,
+        else None (the engine then keeps its wall-clock window). A wall-clock window over GPU counters that move a
+        whole launch (2^32 hashes) at a time, refreshed by a device process's heartbeats, misreads a short interval
+        by a launch or more (a 1 s window at 19.3 GH/s read 25.7)."""
+        live = [m for m in self.miners if not m.retired]
+        if not live or not all(m.exact for m in live):
+            return None
+        return sum(m.hashrate for m in live)
 
     def hashrate_of(self, device_id: str) -> float:
         for m in self.miners:

@@ -737,8 +737,12 @@ class Engine:
         now = self.opts.clock.now()
         total = self.miners.total_hashes()
         rate = self.hash_window.observe(total, now)
-        self.current_hashrate = rate
         self.device_hashrates = self.miners.update_hashrates()
+        exact = getattr(self.miners, "exact_total", None)
+        exact_rate = exact() if exact is not None else None
+        if exact_rate is not None:  # GPU miners: device-timeline spans, no launch quantization
+            rate = exact_rate
+        self.current_hashrate = rate
         for dev, r in self.device_hashrates.items():
             self.m.set_device_hashrate(dev, r)
         shares = self.m.shares_found.value()

@@ -17,6 +17,7 @@ from otedama_amd.parallel.partition import stripe_for
 class FakeNative:
     def __init__(self):
         self.jobs, self.hashes, self.fault, self.stopped = [], 0, "", False
+        self.done_at = 0.0  # device-timeline completion time of `hashes` (0: none reported)
         self.cursor = (0, 0)  # (variant_next, variant_epoch) as the native miners report them
 
     def start(self):
@@ -33,7 +34,8 @@ class FakeNative:
 
     def stats(self):
         return {"hashes": self.hashes, "shares": 0, "dropped": 0, "faulted": bool(self.fault), "error": self.fault,
-                "candidates": 0, "launches": 0, "variant_next": self.cursor[0], "variant_epoch": self.cursor[1]}
+                "candidates": 0, "launches": 0, "variant_next": self.cursor[0], "variant_epoch": self.cursor[1],
+                "hashes_done_at_s": self.done_at}
 
 
 def _dev(name):
@@ -188,3 +190,24 @@ def test_python_variant_space_matches_native():
     for c in cases:
         t = dict(base, **c)
         assert variant_space(t) == N.variant_space(t), c
+
+
+def test_total_hashrate_from_device_timeline_spans():
+    """GPU counters move a whole launch at a time: the node total is the sum of the exact device-timeline rates, not
+    a wall-clock sample (which read 25.7 GH/s for a 19.3 GH/s device over a 1 s window)."""
+    ms = _set(2)
+    ms.set_job(_tmpl())
+    ms.update_hashrates()
+    assert ms.exact_total() is None                     # no device-timeline completion yet: wall window
+    for m in ms.miners:                                 # first completions: still no span to divide by
+        m.native.hashes, m.native.done_at = 1 << 32, 10.0
+    ms.update_hashrates()
+    assert ms.exact_total() is None
+    ms.miners[0].native.hashes, ms.miners[0].native.done_at = 6 << 32, 11.0   # 5 launches in 1.0 device-s
+    ms.miners[1].native.hashes, ms.miners[1].native.done_at = 4 << 32, 11.5   # 3 launches in 1.5 device-s
+    ms.update_hashrates()
+    assert ms.exact_total() == pytest.approx((5 << 32) / 1.0 + (3 << 32) / 1.5)
+    ms.miners[1].retired = True                         # a retired device no longer counts
+    ms.miners[0].native.hashes, ms.miners[0].native.done_at = 7 << 32, 11.25
+    ms.update_hashrates()
+    assert ms.exact_total() == pytest.approx((1 << 32) / 0.25)
