@@ -194,6 +194,8 @@ class NodeMinerSet:
         self.row_times: dict[int, float] = {}  # wall time at which each remote rank's counter row was produced
         self.row_done_at: dict[int, float] = {}  # device-timeline time its counted hashes had completed
         self._prev_rows: dict[int, list[int]] = {}
+        self._prev_done: dict[int, float] = {}  # row_done_at of _prev_rows (device timeline of that rank's GPU)
+        self._exact: dict[int, bool] = {}  # the rank's last rate came from a device-timeline span
         self._rates: dict[str, float] = {}
         self._t_last = time.monotonic()
         self._remote_faults: dict[int, int] = {}
@@ -358,12 +360,27 @@ class NodeMinerSet:
         for r in range(1, self.capacity):
             row, prev = self._rows_by_orig.get(r, [0, 0, 0, 0]), self._prev_rows.get(r, [0, 0, 0, 0])
             rid = f"rank{r}"
-            rates[rid] = max(row[0] - prev[0], 0) / dt
+            # as MinerSet.update_hashrates: between two counted completions on the rank's own device timeline the
+            # rate is exact; a wall-clock sample of launch-sized counter steps jitters by a launch per interval
+            done, pdone = self.row_done_at.get(r, 0.0), self._prev_done.get(r, 0.0)
+            self._exact[r] = done > 0 and pdone > 0 and done > pdone and row[0] > prev[0]
+            rates[rid] = (row[0] - prev[0]) / (done - pdone) if self._exact[r] else max(row[0] - prev[0], 0) / dt
+            self._prev_done[r] = done
             idle = working and r in members and rid not in self._paused and row[0] == prev[0]
             self._remote_idle[r] = self._remote_idle.get(r, 0) + 1 if idle else 0
             self._prev_rows[r] = list(row)
         self._rates = rates
         return rates
+
+    def exact_total(self) -> float | None:
+        """Node total from device-timeline rates when the local miners and every member rank have one (see
+        MinerSet.exact_total), else None."""
+        local = self.local.exact_total()
+        members = set(self.comm.info.members)
+        remote = [r for r in range(1, self.capacity) if r in members]
+        if local is None or not all(self._exact.get(r, False) for r in remote):
+            return None
+        return local + sum(self._rates.get(f"rank{r}", 0.0) for r in remote)
 
     def hashrate_of(self, device_id: str) -> float:
         return self._rates.get(device_id, self.local.hashrate_of(device_id))

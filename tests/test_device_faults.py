@@ -5,6 +5,7 @@ the survivors at once, starting past the high-water mark of every device's curso
 (never re-searching a variant, so no duplicate shares); when that jump does not fit in the job's
 variant space the re-split waits for the next NEW work. A live device with work whose hash counter
 stops is reported as stalled."""
+import time
 from types import SimpleNamespace
 
 import pytest
@@ -211,3 +212,29 @@ def test_total_hashrate_from_device_timeline_spans():
     ms.miners[0].native.hashes, ms.miners[0].native.done_at = 7 << 32, 11.25
     ms.update_hashrates()
     assert ms.exact_total() == pytest.approx((1 << 32) / 0.25)
+
+
+def test_node_total_hashrate_from_each_ranks_device_timeline():
+    """The node leader's total: local device-timeline rates plus each member rank's rate over its heartbeat's
+    device-timeline completion span; a rank without one puts the node back on the wall-clock window."""
+    from otedama_amd.parallel.node import NodeMinerSet
+
+    local = _set(1)
+    local.set_job(_tmpl())
+    node = NodeMinerSet.__new__(NodeMinerSet)
+    node.local, node.capacity, node._blob, node._paused = local, 3, None, set()
+    node.comm = SimpleNamespace(info=SimpleNamespace(members=[0, 1, 2]))
+    node._rows_by_orig, node._prev_rows, node._prev_done, node._exact = {}, {}, {}, {}
+    node.row_done_at, node._rates, node._remote_idle, node._t_last = {}, {}, {}, time.monotonic()
+
+    def tick(local_h, local_t, rows):
+        local.miners[0].native.hashes, local.miners[0].native.done_at = local_h, local_t
+        for r, (h, t) in rows.items():
+            node._rows_by_orig[r], node.row_done_at[r] = [h, 0, 0, 0], t
+        node.update_hashrates()
+
+    tick(1 << 32, 1.0, {1: (1 << 32, 50.0), 2: (1 << 32, 7.0)})
+    tick(3 << 32, 1.5, {1: (4 << 32, 51.0), 2: (2 << 32, 7.5)})
+    assert node.exact_total() == pytest.approx((2 << 32) / 0.5 + (3 << 32) / 1.0 + (1 << 32) / 0.5)
+    tick(4 << 32, 1.75, {1: (5 << 32, 51.25), 2: (2 << 32, 7.5)})   # rank 2 counted nothing new
+    assert node.exact_total() is None
