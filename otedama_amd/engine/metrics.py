@@ -121,6 +121,9 @@ class EngineMetrics:
                                                   "difficulty x 2^32 / hashrate.")
         self.stale_skipped = C("otedama_shares_stale_skipped_total",
                                "Shares found for a job the pool already invalidated (not submitted).")
+        self.below_target_skipped = C("otedama_shares_below_target_skipped_total",
+                                      "Shares found under a share target the pool has since raised (SV2 SetTarget "
+                                      "re-issues the job; not submitted, the pool would reject them).")
         self.node_collective_seconds = G("otedama_node_collective_seconds",
                                          "Multi-GPU node: median wall time of rank 0's node ops (R1 job broadcast, R2 "
                                          "share gather, R3 counters, re-forms); 0 outside node mode.")

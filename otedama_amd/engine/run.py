@@ -167,6 +167,7 @@ class Engine:
         self.activity: dict[str, float] = {}
         self._active_job: Job | None = None
         self._valid_jobs: set[str] = set()
+        self._job_targets: dict[str, int | None] = {}  # job id -> its current share target (int, LE)
         self._submitted = BoundedSet(SUBMIT_KEYS_CAP)  # run.go:720-726: cap 1024, oldest half dropped
         self._session = None
         self._providers: list = []
@@ -621,6 +622,7 @@ class Engine:
             self.miners.pause_all()
             self._active_job = None
             self._valid_jobs.clear()
+            self._job_targets.clear()
 
     async def _notice_pump(self, session) -> None:
         while True:
@@ -634,14 +636,18 @@ class Engine:
             if job is None:
                 self._active_job = None
                 self._valid_jobs.clear()
+                self._job_targets.clear()
                 self.miners.pause_all()
                 continue
             if job.clean_jobs:
                 if job.job_id not in self._valid_jobs:
                     self._submitted.clear()
                 self._valid_jobs = {job.job_id}
+                self._job_targets = {k: v for k, v in self._job_targets.items() if k == job.job_id}
             else:
                 self._valid_jobs.add(job.job_id)
+            # the job's current share target: a target-only update (SV2 SetTarget) re-issues the same job id
+            self._job_targets[job.job_id] = int.from_bytes(job.target, "little") if job.target else None
             self._active_job = job
             publish_difficulty(self.m, session.suggested_difficulty(), self.current_hashrate,
                                float(2 ** 256) / self.algorithm.diff1)
@@ -689,6 +695,13 @@ class Engine:
                 self.m.inc_shares_found_for_device(s["device_id"])
                 if s["job_id"] not in self._valid_jobs:
                     self.m.stale_skipped.inc()
+                    continue
+                # Verified on the device's host thread against the target it had then; a share still queued when
+                # the pool raised the target would only be rejected as low-difficulty (the vardiff race right after
+                # connect), so it is dropped here instead.
+                tgt, h = self._job_targets.get(s["job_id"]), s.get("hash")
+                if tgt is not None and h and int.from_bytes(h, "little") > tgt:
+                    self.m.below_target_skipped.inc()
                     continue
                 en2 = extranonce2_bytes(s["extranonce2"], s["extranonce2_size"])
                 key = (s["job_id"], s["nonce"], s["ntime"], s["version"], en2)

@@ -167,9 +167,12 @@ def make_engine(cfg=None, **kw):
     return eng, logs
 
 
-def share(job_id="j1", nonce=1, ntime=0x60000000, version=0x20000004, dev="cpu-0", en2=0, en2_size=0):
-    return {"job_id": job_id, "nonce": nonce, "ntime": ntime, "version": version, "device_id": dev,
-            "extranonce2": en2, "extranonce2_size": en2_size, "found_at": 0.0}
+def share(job_id="j1", nonce=1, ntime=0x60000000, version=0x20000004, dev="cpu-0", en2=0, en2_size=0, digest=None):
+    s = {"job_id": job_id, "nonce": nonce, "ntime": ntime, "version": version, "device_id": dev,
+         "extranonce2": en2, "extranonce2_size": en2_size, "found_at": 0.0}
+    if digest is not None:
+        s["hash"] = digest
+    return s
 
 
 async def run_pump_until(coro, cond, timeout=2.0):
@@ -804,6 +807,24 @@ def test_share_pump_skips_stale_job_shares():
         await run_pump_until(eng._share_pump(sess), lambda: sess.submitted)
         assert [s.job_id for s in sess.submitted] == ["new"]
         assert eng.m.stale_skipped.value() == 1 and eng.m.shares_found.value() == 2
+    asyncio.run(go())
+
+
+def test_share_pump_drops_shares_below_a_raised_target():
+    """SV2 SetTarget re-issues the job with a higher difficulty: shares the device verified against the old target
+    and still queued would be rejected as low-difficulty, so they are dropped (counted) instead of submitted."""
+    async def go():
+        eng, _ = make_engine()
+        sess = FakeSession()
+        easy, hard = (1 << 250).to_bytes(32, "little"), (1 << 240).to_bytes(32, "little")
+        await sess.jobs.put(Job("j1", clean_jobs=True, target=easy))
+        await sess.jobs.put(Job("j1", clean_jobs=True, target=hard))   # the re-issue after SetTarget
+        await run_pump_until(eng._job_pump(sess), lambda: len(eng.miners.jobs) == 2)
+        weak, strong = (1 << 245).to_bytes(32, "little"), (1 << 230).to_bytes(32, "little")
+        eng.miners.queue = [share(nonce=1, digest=weak), share(nonce=2, digest=strong), share(nonce=3)]
+        await run_pump_until(eng._share_pump(sess), lambda: len(sess.submitted) == 2)
+        assert sorted(s.nonce for s in sess.submitted) == [2, 3]   # no hash (CPU-style share): not filtered
+        assert eng.m.below_target_skipped.value() == 1
     asyncio.run(go())
 
 

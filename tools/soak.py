@@ -2,7 +2,8 @@
 (a child process, native GPU miner) for a fixed time, with job refreshes and new blocks much more often than a
 real pool sends them. Samples /metrics and the miner's RSS every --every seconds and prints one JSON line per
 sample, then a summary line. Exits 1 if any share is rejected, a sample's hashrate falls below 90% of the
-median after warm-up, or the miner's RSS grows by more than --max-rss-growth-mb.
+median after warm-up, or the miner's RSS (the engine alone, and the engine with its device processes) grows by
+more than --max-rss-growth-mb.
 
 python tools/soak.py [--seconds 180] [--protocol sv2|v1] [--algorithm sha256d]
 """
@@ -41,6 +42,27 @@ def rss_mb(pid: int) -> float:
     except OSError:
         pass
     return 0.0
+
+
+def tree_rss_mb(pid: int) -> tuple[float, float]:
+    """(RSS of pid and all its descendants, RSS of the descendants): the engine keeps its GPUs in device processes."""
+    kids: dict[int, list[int]] = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat") as f:
+                ppid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, IndexError, ValueError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    todo, desc = list(kids.get(pid, [])), []
+    while todo:
+        c = todo.pop()
+        desc.append(c)
+        todo += kids.get(c, [])
+    child = sum(rss_mb(c) for c in desc)
+    return rss_mb(pid) + child, child
 
 
 def main() -> int:
@@ -117,6 +139,8 @@ def main() -> int:
                  "pool_accepted": pool.m_accepted.value(), "pool_rejected": pool.m_rejected.value(),
                  "blocks": pool.m_blocks.value() if hasattr(pool, "m_blocks") else None,
                  "rss_mb": round(rss_mb(proc.pid), 1)}
+            tree, child = tree_rss_mb(proc.pid)
+            s["tree_rss_mb"], s["device_procs_rss_mb"] = round(tree, 1), round(child, 1)
             samples.append(s)
             print(json.dumps(s), flush=True)
     finally:
@@ -139,9 +163,12 @@ def main() -> int:
                "accepted": last.get("accepted"), "rejected": last.get("rejected"),
                "pool_accepted": last.get("pool_accepted"), "pool_rejected": last.get("pool_rejected"),
                "blocks": last.get("blocks"), "rss_growth_mb": round((last.get("rss_mb") or 0.0) - rss0, 1),
+               "tree_rss_growth_mb": round((last.get("tree_rss_mb") or 0.0) - (steady[0].get("tree_rss_mb") or 0.0
+                                                                                if steady else 0.0), 1),
                "miner_exit_code": exit_code}
     ok = (rates and min(rates) >= 0.9 * med and not last.get("rejected") and not last.get("pool_rejected")
-          and summary["rss_growth_mb"] <= a.max_rss_growth_mb and exit_code == 0)
+          and summary["rss_growth_mb"] <= a.max_rss_growth_mb and summary["tree_rss_growth_mb"] <= a.max_rss_growth_mb
+          and exit_code == 0)
     summary["ok"] = bool(ok)
     print(json.dumps(summary), flush=True)
     return 0 if ok and rc == 0 else 1
