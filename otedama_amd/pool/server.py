@@ -111,6 +111,15 @@ class _Worker:
         self.accepted = 0
         self.rejected = 0
 
+    def retargeted(self, old: float) -> None:
+        """The worker's difficulty just moved away from `old`. Shares already in flight were found against some
+        difficulty of the last RETARGET_GRACE seconds: the grace honours the lowest of them, not only the one
+        before this retarget (vardiff ramps through several steps in its first second at a high share rate)."""
+        now = time.monotonic()
+        recent = now - self.retarget_at < RETARGET_GRACE
+        self.prev_difficulty = min(self.prev_difficulty, old) if recent else old
+        self.retarget_at = now
+
 
 class PoolServer:
     def __init__(self, opts: PoolOptions | None = None, registry: Registry | None = None, log=None):
@@ -388,7 +397,7 @@ class PoolServer:
         old = w.vd.difficulty
         new = self.vardiff.on_share(w.vd)
         if new is not None:
-            w.prev_difficulty, w.retarget_at = old, time.monotonic()
+            w.retargeted(old)
             self.journal.save_worker(w.name, new)
         return new
 
@@ -700,7 +709,7 @@ class _V2Conn:
             ent = self.channels.get(msg.channel_id)
             if ent is not None and msg.nominal_hashrate > 0:
                 w = ent[0]
-                w.prev_difficulty, w.retarget_at = w.vd.difficulty, time.monotonic()
+                w.retargeted(w.vd.difficulty)
                 w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
                 self._send(M.SetTarget(msg.channel_id, self.pool.share_target(w.vd.difficulty)))
         elif isinstance(msg, M.CloseChannel):

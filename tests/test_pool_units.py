@@ -218,3 +218,23 @@ def test_validate_recomputes_the_algorithm_hash(algo):
     v = p.validate(w, job.job_id, en, job.ntime, nonce + 1, job.version)  # a different nonce: its own hash
     assert v.hash == b"" or v.hash == get(algo).hash(p.header_for(job, en, job.version, job.ntime, nonce + 1))
     assert p.journal.counts()["accepted"] >= 1 and len(hdr) == 80
+
+
+def test_retarget_grace_honours_the_lowest_recent_difficulty(monkeypatch):
+    """Two retargets inside the grace window (the vardiff ramp right after connect): a share in flight from before
+    the first one still meets the grace difficulty, which is the lowest of the window, not only the last one."""
+    from otedama_amd.pool import server as srv
+    from otedama_amd.pool.vardiff import Vardiff, VardiffConfig
+
+    t = [100.0]
+    monkeypatch.setattr(srv.time, "monotonic", lambda: t[0])
+    w = srv._Worker("w", Vardiff(VardiffConfig()).new_state(2.0), 0)
+    w.retargeted(2.0)                  # 2 -> 4
+    w.vd.difficulty = 4.0
+    t[0] += 0.01
+    w.retargeted(4.0)                  # 4 -> 8, still inside the grace of the first step
+    w.vd.difficulty = 8.0
+    assert w.prev_difficulty == 2.0
+    t[0] += srv.RETARGET_GRACE + 1     # a retarget long after: the window starts again from the last difficulty
+    w.retargeted(8.0)
+    assert w.prev_difficulty == 8.0
