@@ -77,6 +77,9 @@ def main() -> int:
     ap.add_argument("--block-interval", type=float, default=45.0)
     ap.add_argument("--max-rss-growth-mb", type=float, default=64.0)
     ap.add_argument("--workdir", default="gpurun_out/soak")
+    ap.add_argument("--extended", action="store_true", help="SV2 extended channel (miner-side extranonce rolling)")
+    ap.add_argument("--noise", choices=("", "ellswift", "legacy"), default="",
+                    help="SV2 Noise NX with this suite, pinned to the pool's authority key")
     a = ap.parse_args()
 
     from otedama_amd.pool.server import PoolOptions, PoolServer
@@ -85,7 +88,7 @@ def main() -> int:
     work.mkdir(parents=True, exist_ok=True)
     pool = PoolServer(PoolOptions(algorithm=a.algorithm, initial_difficulty=a.difficulty, payout_address=ADDR,
                                   target_share_seconds=1.0, retarget_seconds=15.0, job_interval=a.job_interval,
-                                  block_interval=a.block_interval))
+                                  block_interval=a.block_interval, noise=bool(a.noise), noise_suite=a.noise))
     loop = asyncio.new_event_loop()
     ready = threading.Event()
 
@@ -101,7 +104,12 @@ def main() -> int:
         return 1
     url = f"stratum+v2://{pool.addr_sv2}" if a.protocol == "sv2" else f"stratum+tcp://{pool.addr_v1}"
     cfg = work / "config.yaml"
-    cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: {url}\nmining:\n  algorithm: {a.algorithm}\n")
+    extra = ""
+    if a.extended:
+        extra += "    sv2_extended_channel: true\n"
+    if a.noise:
+        extra += f"    noise_suite: {a.noise}\n    pool_pubkey: \"{pool.noise_authority_pub.hex()}\"\n"
+    cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: {url}\n{extra}mining:\n  algorithm: {a.algorithm}\n")
     env = dict(os.environ, HOME=str(work), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(work / "data"))
     log = open(work / "miner.log", "w")
     proc = subprocess.Popen([sys.executable, "-u", "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
@@ -159,6 +167,7 @@ def main() -> int:
     rss0 = steady[0]["rss_mb"] if steady else 0.0
     last = samples[-1] if samples else {}
     summary = {"summary": True, "seconds": a.seconds, "protocol": a.protocol, "algorithm": a.algorithm,
+               "extended_channel": a.extended, "noise": a.noise or None,
                "median_hashrate_ghs": med, "min_hashrate_ghs": min(rates) if rates else 0.0,
                "accepted": last.get("accepted"), "rejected": last.get("rejected"),
                "pool_accepted": last.get("pool_accepted"), "pool_rejected": last.get("pool_rejected"),
