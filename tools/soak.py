@@ -77,6 +77,10 @@ def main() -> int:
     ap.add_argument("--block-interval", type=float, default=45.0)
     ap.add_argument("--max-rss-growth-mb", type=float, default=64.0)
     ap.add_argument("--workdir", default="gpurun_out/soak")
+    ap.add_argument("--bounce-at", type=float, default=0.0,
+                    help="stop the pool this many seconds in, restart it on the same ports after --bounce-down s "
+                         "(the engine must reconnect and resume; samples within 20 s after it skip the rate check)")
+    ap.add_argument("--bounce-down", type=float, default=3.0)
     ap.add_argument("--extended", action="store_true", help="SV2 extended channel (miner-side extranonce rolling)")
     ap.add_argument("--noise", choices=("", "ellswift", "legacy"), default="",
                     help="SV2 Noise NX with this suite, pinned to the pool's authority key")
@@ -86,9 +90,16 @@ def main() -> int:
 
     work = Path(a.workdir)
     work.mkdir(parents=True, exist_ok=True)
-    pool = PoolServer(PoolOptions(algorithm=a.algorithm, initial_difficulty=a.difficulty, payout_address=ADDR,
-                                  target_share_seconds=1.0, retarget_seconds=15.0, job_interval=a.job_interval,
-                                  block_interval=a.block_interval, noise=bool(a.noise), noise_suite=a.noise))
+    if a.bounce_at and a.noise:
+        raise SystemExit("soak: --bounce-at with --noise is not supported (a restarted pool has a new authority key)")
+
+    def make_pool(sv2="127.0.0.1:0", v1="127.0.0.1:0"):
+        return PoolServer(PoolOptions(algorithm=a.algorithm, initial_difficulty=a.difficulty, payout_address=ADDR,
+                                      target_share_seconds=1.0, retarget_seconds=15.0, job_interval=a.job_interval,
+                                      block_interval=a.block_interval, noise=bool(a.noise), noise_suite=a.noise,
+                                      listen_sv2=sv2, listen_v1=v1))
+
+    pool = make_pool()
     loop = asyncio.new_event_loop()
     ready = threading.Event()
 
@@ -127,13 +138,34 @@ def main() -> int:
             http = m.group(1)
     threading.Thread(target=lambda: [log.write(x) for x in proc.stdout], daemon=True).start()
     samples, rc = [], 0
+    bounce = None
     try:
         if http is None:
             print(json.dumps({"error": "miner did not start", "log": str(work / "miner.log")}))
             return 1
         t0 = time.time()
+        base_acc = base_rej = 0.0  # pool counters of the pools before a bounce
         while time.time() - t0 < a.seconds:
             time.sleep(a.every)
+            if a.bounce_at and bounce is None and time.time() - t0 >= a.bounce_at:
+                acc_before = metric(urllib.request.urlopen(f"http://{http}/metrics", timeout=5).read().decode(),
+                                    "otedama_shares_total", '{status="accepted"}')
+                base_acc, base_rej = base_acc + pool.m_accepted.value(), base_rej + pool.m_rejected.value()
+                addrs = (pool.addr_sv2, pool.addr_v1)
+                asyncio.run_coroutine_threadsafe(pool.stop(), loop).result(30)
+                t_down = time.time()
+                time.sleep(a.bounce_down)
+                pool = make_pool(*addrs)
+                asyncio.run_coroutine_threadsafe(pool.start(), loop).result(30)
+                t_up = time.time()
+                first = None
+                while time.time() - t_up < 90 and first is None:
+                    time.sleep(0.2)
+                    if pool.m_accepted.value() > 0:
+                        first = time.time() - t_up
+                bounce = {"t": round(t_down - t0, 1), "down_s": round(t_up - t_down, 2), "accepted_before": acc_before,
+                          "first_accept_after_restart_s": round(first, 2) if first is not None else None}
+                print(json.dumps({"bounce": bounce}), flush=True)
             if proc.poll() is not None:
                 print(json.dumps({"error": f"miner exited with {proc.returncode}"}), flush=True)
                 return 1
@@ -144,7 +176,7 @@ def main() -> int:
                  "accepted": metric(body, "otedama_shares_total", '{status="accepted"}'),
                  "rejected": metric(body, "otedama_shares_total", '{status="rejected"}'),
                  "p50_submit_ms": metric(body, "otedama_submit_latency_milliseconds", '{quantile="0.5"}'),
-                 "pool_accepted": pool.m_accepted.value(), "pool_rejected": pool.m_rejected.value(),
+                 "pool_accepted": base_acc + pool.m_accepted.value(), "pool_rejected": base_rej + pool.m_rejected.value(),
                  "blocks": pool.m_blocks.value() if hasattr(pool, "m_blocks") else None,
                  "rss_mb": round(rss_mb(proc.pid), 1)}
             tree, child = tree_rss_mb(proc.pid)
@@ -161,13 +193,14 @@ def main() -> int:
         asyncio.run_coroutine_threadsafe(pool.stop(), loop).result(30)
         loop.call_soon_threadsafe(loop.stop)
         log.close()
-    steady = [s for s in samples if s["t"] >= a.warmup] or samples
+    steady = [s for s in samples if s["t"] >= a.warmup
+              and not (bounce is not None and bounce["t"] <= s["t"] <= bounce["t"] + a.bounce_down + 20.0)] or samples
     rates = [s["hashrate_ghs"] for s in steady]
     med = statistics.median(rates) if rates else 0.0
     rss0 = steady[0]["rss_mb"] if steady else 0.0
     last = samples[-1] if samples else {}
     summary = {"summary": True, "seconds": a.seconds, "protocol": a.protocol, "algorithm": a.algorithm,
-               "extended_channel": a.extended, "noise": a.noise or None,
+               "extended_channel": a.extended, "noise": a.noise or None, "bounce": bounce,
                "median_hashrate_ghs": med, "min_hashrate_ghs": min(rates) if rates else 0.0,
                "accepted": last.get("accepted"), "rejected": last.get("rejected"),
                "pool_accepted": last.get("pool_accepted"), "pool_rejected": last.get("pool_rejected"),
@@ -175,7 +208,7 @@ def main() -> int:
                "tree_rss_growth_mb": round((last.get("tree_rss_mb") or 0.0) - (steady[0].get("tree_rss_mb") or 0.0
                                                                                 if steady else 0.0), 1),
                "miner_exit_code": exit_code}
-    ok = (rates and min(rates) >= 0.9 * med and not last.get("rejected") and not last.get("pool_rejected")
+    ok = (rates and min(rates) >= 0.9 * med and (not a.bounce_at or (bounce or {}).get("first_accept_after_restart_s")) and not last.get("rejected") and not last.get("pool_rejected")
           and summary["rss_growth_mb"] <= a.max_rss_growth_mb and summary["tree_rss_growth_mb"] <= a.max_rss_growth_mb
           and exit_code == 0)
     summary["ok"] = bool(ok)
