@@ -257,7 +257,12 @@ class DeviceProcess:
                     self.startup_seconds = self.ready_at - self.spawned_at
                     if self.on_ready is not None:
                         self.on_ready(self)
-        # EOF: the child exited (or is exiting)
+        # EOF: the child exited (or is exiting). Its socket is closed here, not left to garbage collection once a
+        # restart replaces self._sock (a closed socket object makes a late _post raise OSError, which it ignores).
+        try:
+            sock.close()
+        except OSError:
+            pass
         try:
             rc = proc.wait(timeout=10)
         except subprocess.TimeoutExpired:

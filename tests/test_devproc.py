@@ -99,9 +99,11 @@ def test_device_process_startup_and_counters_survive_restart():
         ms.set_job(_job())
         assert _wait(lambda: dp.stats()["hashes"] > 0, 20)
         h = dp.stats()["hashes"]
+        fds = len(os.listdir("/proc/self/fd"))
         dp.kill(signal.SIGKILL)
         assert _wait(lambda: not ms.miners[0].retired and dp.restarts == 1 and dp.alive, 20)
         assert dp.stats()["hashes"] >= h  # cumulative across the restart
+        assert len(os.listdir("/proc/self/fd")) <= fds  # the dead child's socket was closed, the new one replaces it
     finally:
         ms.stop()
 
