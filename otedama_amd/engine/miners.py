@@ -63,6 +63,7 @@ class DeviceMiner:
     last_done_at: float = 0.0  # device-timeline completion time of last_hashes (GPU miners)
     hashrate: float = 0.0
     exact: bool = False  # hashrate came from a device-timeline span (not a wall-clock sample) at the last tick
+    timeline: bool = False  # the miner reports device-timeline completions (GPU); CPU counters move continuously
     idle_samples: int = 0  # consecutive stats ticks with work but no hash progress
     extra: dict = field(default_factory=dict)
     backoff: float = RESPAWN_BACKOFF_INITIAL
@@ -397,6 +398,7 @@ class MinerSet:
             # counted completions the rate is exact; sampled against wall time it jitters by a launch per interval
             span = done - m.last_done_at
             m.exact = False
+            m.timeline = done > 0
             if m.retired:
                 m.hashrate = 0.0
             elif done > 0 and m.last_done_at > 0 and span > 0 and h > m.last_hashes:
@@ -417,13 +419,14 @@ class MinerSet:
         return rates
 
     def exact_total(self) -> float | None:
-        """Sum of the device rates when every live miner's rate at the last tick came from a device-timeline span,
-        else None (the engine then keeps its wall-clock window). A wall-clock window over GPU counters that move a
+        """Sum of the device rates when every live GPU miner's rate at the last tick came from a device-timeline span
+        (CPU miners add their wall-clock rate), else None (the engine then keeps its wall-clock window). A wall-clock window over GPU counters that move a
         whole launch (2^32 hashes) at a time, refreshed by a device process's heartbeats, misreads a short interval
         by a launch or more (a 1 s window at 19.3 GH/s read 25.7)."""
         live = [m for m in self.miners if not m.retired]
-        if not live or not all(m.exact for m in live):
+        if not any(m.exact for m in live) or any(m.timeline and not m.exact for m in live):
             return None
+        # CPU miners (no device timeline) count continuously: their wall-clock rate is already smooth
         return sum(m.hashrate for m in live)
 
     def hashrate_of(self, device_id: str) -> float:

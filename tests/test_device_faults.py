@@ -238,3 +238,16 @@ def test_node_total_hashrate_from_each_ranks_device_timeline():
     assert node.exact_total() == pytest.approx((2 << 32) / 0.5 + (3 << 32) / 1.0 + (1 << 32) / 0.5)
     tick(4 << 32, 1.75, {1: (5 << 32, 51.25), 2: (2 << 32, 7.5)})   # rank 2 counted nothing new
     assert node.exact_total() is None
+
+
+def test_total_hashrate_adds_continuous_cpu_rates_to_exact_gpu_rates():
+    ms = _set(2)
+    ms.set_job(_tmpl())
+    gpu, cpu = ms.miners
+    gpu.native.hashes, gpu.native.done_at = 1 << 32, 5.0
+    ms.update_hashrates()
+    gpu.native.hashes, gpu.native.done_at = 3 << 32, 5.5
+    cpu.native.hashes = 1_000_000                       # no device timeline: a continuous counter
+    ms.update_hashrates()
+    assert ms.exact_total() == pytest.approx((2 << 32) / 0.5 + cpu.hashrate)
+    assert not cpu.exact and not cpu.timeline and gpu.exact
