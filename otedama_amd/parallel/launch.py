@@ -149,6 +149,7 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
         while True:
             if stopping:
                 log(f"signal {stopping[0]}: stopping the node")
+                store.set("otd/stopping", "1")  # the leader then takes a follower's exit for the shutdown it is
                 _stop_all(list(procs.values()), grace=30.0)
                 rc0 = procs[0].returncode if 0 in procs else None
                 return 0 if rc0 in (0, -signal.SIGTERM, 128 + signal.SIGTERM) else (rc0 or 0)

@@ -524,6 +524,10 @@ class NodeMinerSet:
                             if gi < len(info.members):
                                 self._rows_by_orig[info.members[gi]] = list(row)
                 except Exception as exc:  # noqa: BLE001 - a collective failed: find who is gone and re-form
+                    if self.store is not None and _store_get(self.store, _k("stopping")) is not None:
+                        # the supervisor is stopping every rank (SIGTERM): a follower that left first is no loss
+                        self.log("info", "node: stopping (the supervisor is shutting the node down)")
+                        return
                     self.log("warn", f"node: collective failed ({type(exc).__name__}: {exc}); checking ranks")
                     self.link.error = exc
                     # the peer that broke it shows up as dead within one heartbeat timeout (its process exited, or

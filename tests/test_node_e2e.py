@@ -89,6 +89,8 @@ def test_otedama_node_keeps_mining_through_a_rank_loss(tmp_path):
         try:
             rc = sup.wait(timeout=40)
             assert rc == 0, (rc, (tmp_path / "node.out").read_text()[-3000:])  # a clean stop, like `otedama run`
+            tail = (tmp_path / "node.out").read_text().split("stopping the node", 1)[-1]
+            assert "lost" not in tail, tail[-3000:]  # followers leaving during the shutdown are not rank losses
         except subprocess.TimeoutExpired:
             for c in psutil.Process(sup.pid).children(recursive=True):
                 c.kill()

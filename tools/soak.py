@@ -81,6 +81,8 @@ def main() -> int:
                     help="stop the pool this many seconds in, restart it on the same ports after --bounce-down s "
                          "(the engine must reconnect and resume; samples within 20 s after it skip the rate check)")
     ap.add_argument("--bounce-down", type=float, default=3.0)
+    ap.add_argument("--node", type=int, default=0,
+                    help="run `otedama node --gpus N` over gloo (ranks share the GPU) instead of `otedama run`")
     ap.add_argument("--extended", action="store_true", help="SV2 extended channel (miner-side extranonce rolling)")
     ap.add_argument("--noise", choices=("", "ellswift", "legacy"), default="",
                     help="SV2 Noise NX with this suite, pinned to the pool's authority key")
@@ -123,9 +125,14 @@ def main() -> int:
     cfg.write_text(f"bitcoin_address: {ADDR}\npools:\n  - url: {url}\n{extra}mining:\n  algorithm: {a.algorithm}\n")
     env = dict(os.environ, HOME=str(work), PYTHONPATH=str(ROOT), OTEDAMA_DATA_DIR=str(work / "data"))
     log = open(work / "miner.log", "w")
-    proc = subprocess.Popen([sys.executable, "-u", "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
-                             "--http-addr", "127.0.0.1:0", "--gpus", "0"], stdout=subprocess.PIPE,
-                            stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
+    if a.node:
+        env["OTEDAMA_DIST_BACKEND"] = "gloo"
+        cmd = [sys.executable, "-u", "-m", "otedama_amd", "node", "--gpus", str(a.node), "--config", str(cfg),
+               "--no-tui", "--http-addr", "127.0.0.1:0"]
+    else:
+        cmd = [sys.executable, "-u", "-m", "otedama_amd", "run", "--config", str(cfg), "--no-tui",
+               "--http-addr", "127.0.0.1:0", "--gpus", "0"]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
     http = None
     t_start = time.time()
     while time.time() - t_start < 120 and http is None:
@@ -200,7 +207,7 @@ def main() -> int:
     rss0 = steady[0]["rss_mb"] if steady else 0.0
     last = samples[-1] if samples else {}
     summary = {"summary": True, "seconds": a.seconds, "protocol": a.protocol, "algorithm": a.algorithm,
-               "extended_channel": a.extended, "noise": a.noise or None, "bounce": bounce,
+               "extended_channel": a.extended, "noise": a.noise or None, "bounce": bounce, "node_ranks": a.node or None,
                "median_hashrate_ghs": med, "min_hashrate_ghs": min(rates) if rates else 0.0,
                "accepted": last.get("accepted"), "rejected": last.get("rejected"),
                "pool_accepted": last.get("pool_accepted"), "pool_rejected": last.get("pool_rejected"),
