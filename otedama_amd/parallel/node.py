@@ -194,7 +194,9 @@ class NodeMinerSet:
         self.row_times: dict[int, float] = {}  # wall time at which each remote rank's counter row was produced
         self.row_done_at: dict[int, float] = {}  # device-timeline time its counted hashes had completed
         self._prev_rows: dict[int, list[int]] = {}
-        self._prev_done: dict[int, float] = {}  # row_done_at of _prev_rows (device timeline of that rank's GPU)
+        self._hb_pairs: dict[int, tuple[int, float]] = {}  # (hashes, device-timeline time they had completed) of
+        # a rank's latest heartbeat: one consistent pair (R3 rows carry no completion time)
+        self._prev_pairs: dict[int, tuple[int, float]] = {}
         self._exact: dict[int, bool] = {}  # the rank's last rate came from a device-timeline span
         self._rates: dict[str, float] = {}
         self._t_last = time.monotonic()
@@ -362,10 +364,11 @@ class NodeMinerSet:
             rid = f"rank{r}"
             # as MinerSet.update_hashrates: between two counted completions on the rank's own device timeline the
             # rate is exact; a wall-clock sample of launch-sized counter steps jitters by a launch per interval
-            done, pdone = self.row_done_at.get(r, 0.0), self._prev_done.get(r, 0.0)
-            self._exact[r] = done > 0 and pdone > 0 and done > pdone and row[0] > prev[0]
-            rates[rid] = (row[0] - prev[0]) / (done - pdone) if self._exact[r] else max(row[0] - prev[0], 0) / dt
-            self._prev_done[r] = done
+            (h, done), (ph, pdone) = self._hb_pairs.get(r, (0, 0.0)), self._prev_pairs.get(r, (0, 0.0))
+            self._exact[r] = done > 0 and pdone > 0 and done > pdone and h > ph
+            rates[rid] = (h - ph) / (done - pdone) if self._exact[r] else max(row[0] - prev[0], 0) / dt
+            if r in self._hb_pairs:
+                self._prev_pairs[r] = self._hb_pairs[r]
             idle = working and r in members and rid not in self._paused and row[0] == prev[0]
             self._remote_idle[r] = self._remote_idle.get(r, 0) + 1 if idle else 0
             self._prev_rows[r] = list(row)
@@ -414,6 +417,7 @@ class NodeMinerSet:
                                          int(hb.get("dropped", 0)), int(hb.get("faulted", 0))]
                 self.row_times[r] = float(hb["t"])
                 self.row_done_at[r] = float(hb.get("done", 0.0) or 0.0)
+                self._hb_pairs[r] = (int(hb.get("hashes", 0)), self.row_done_at[r])
         dead = []
         grace = time.monotonic() - self._gen_started < self.hb_timeout  # members of a new generation get one
         for r in members[1:]:                                           # timeout to (re)start heartbeating

@@ -224,13 +224,13 @@ def test_node_total_hashrate_from_each_ranks_device_timeline():
     node = NodeMinerSet.__new__(NodeMinerSet)
     node.local, node.capacity, node._blob, node._paused = local, 3, None, set()
     node.comm = SimpleNamespace(info=SimpleNamespace(members=[0, 1, 2]))
-    node._rows_by_orig, node._prev_rows, node._prev_done, node._exact = {}, {}, {}, {}
+    node._rows_by_orig, node._prev_rows, node._hb_pairs, node._prev_pairs, node._exact = {}, {}, {}, {}, {}
     node.row_done_at, node._rates, node._remote_idle, node._t_last = {}, {}, {}, time.monotonic()
 
     def tick(local_h, local_t, rows):
         local.miners[0].native.hashes, local.miners[0].native.done_at = local_h, local_t
-        for r, (h, t) in rows.items():
-            node._rows_by_orig[r], node.row_done_at[r] = [h, 0, 0, 0], t
+        for r, (h, t) in rows.items():  # as the heartbeat reader stores them
+            node._rows_by_orig[r], node.row_done_at[r], node._hb_pairs[r] = [h, 0, 0, 0], t, (h, t)
         node.update_hashrates()
 
     tick(1 << 32, 1.0, {1: (1 << 32, 50.0), 2: (1 << 32, 7.0)})
