@@ -70,7 +70,8 @@ def stop_pool(proc: subprocess.Popen) -> dict:
     return {}
 
 
-async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, batch_nonces: int) -> dict:
+async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, batch_nonces: int,
+                 warmup: float = 3.0) -> dict:
     from otedama_amd import hal
     from otedama_amd.config import Config, MiningConfig, PoolConfig
     from otedama_amd.engine.run import Engine, Options
@@ -83,6 +84,14 @@ async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, b
                  mining=MiningConfig(algorithm=algorithm, batch_nonces=batch_nonces))
     eng = Engine(Options(config=cfg, devices=devs, rate_fetcher=StaticRateSource(95000), stats_interval=1.0))
     task = asyncio.ensure_future(eng.run())
+    # Warm-up: the first shares of a fresh engine / pool pair take the cold paths (first submit and validation in
+    # each process; 1.0 ms device hit -> accept vs 0.5 ms for the next probes on the same box, profiles/r3/au_latency)
+    # and are not recorded.
+    await asyncio.sleep(warmup)
+    from otedama_amd.engine.stats import LatencyTracker
+
+    eng.latency, eng.pipeline_latency, eng.device_latency = LatencyTracker(256), LatencyTracker(4096), \
+        LatencyTracker(4096)
     await asyncio.sleep(seconds)
     task.cancel()
     try:
@@ -110,7 +119,7 @@ def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm
         "hit_to_accept_p50_ms": pipe.quantile(0.5), "hit_to_accept_p95_ms": pipe.quantile(0.95),
         "accepted": eng.m.shares_accepted.value(), "rejected": eng.m.shares_rejected.value(),
         "pool_accepted": pool.get("accepted"), "pool_rejected": pool.get("rejected"), "share_difficulty": diff,
-        "batch_nonces": batch_nonces, "seconds": seconds,
+        "batch_nonces": batch_nonces, "seconds": seconds, "warmup_seconds": 3.0,
         "protocol": "stratum-v2 over loopback TCP; pool in a separate process (otedama pool)",
         "engine_hashrate": eng.current_hashrate,
     }
