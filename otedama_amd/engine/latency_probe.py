@@ -92,7 +92,11 @@ async def _probe(device_index: int, seconds: float, algorithm: str, addr: str, b
 
     eng.latency, eng.pipeline_latency, eng.device_latency = LatencyTracker(256), LatencyTracker(4096), \
         LatencyTracker(4096)
-    await asyncio.sleep(seconds)
+    trace, end = [], time.monotonic() + seconds
+    while time.monotonic() < end:  # the engine's hashrate at each stats tick of the recorded window
+        await asyncio.sleep(0.5)
+        trace.append(round(eng.current_hashrate / 1e9, 3))
+    eng.hashrate_trace_ghs = trace
     task.cancel()
     try:
         await task
@@ -121,7 +125,10 @@ def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm
         "pool_accepted": pool.get("accepted"), "pool_rejected": pool.get("rejected"), "share_difficulty": diff,
         "batch_nonces": batch_nonces, "seconds": seconds, "warmup_seconds": 3.0,
         "protocol": "stratum-v2 over loopback TCP; pool in a separate process (otedama pool)",
-        "engine_hashrate": eng.current_hashrate,
+        # median over the recorded window's stats ticks (a single tick can catch a launch boundary)
+        "engine_hashrate": (statistics.median(getattr(eng, "hashrate_trace_ghs", [])) * 1e9
+                            if getattr(eng, "hashrate_trace_ghs", []) else eng.current_hashrate),
+        "engine_hashrate_trace_ghs": getattr(eng, "hashrate_trace_ghs", []),
     }
 
 

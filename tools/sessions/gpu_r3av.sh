@@ -11,7 +11,7 @@ import json
 from otedama_amd.engine.latency_probe import measure_share_latency
 for i in range(3):
     r = measure_share_latency(device_index=0, seconds=6.0)
-    print(json.dumps({k: r[k] for k in ('p50_ms', 'device_hit_to_accept_p50_ms', 'device_hit_to_accept_p95_ms', 'hit_to_accept_p50_ms', 'accepted', 'engine_hashrate')}), flush=True)
+    print(json.dumps({k: r[k] for k in ('p50_ms', 'device_hit_to_accept_p50_ms', 'device_hit_to_accept_p95_ms', 'hit_to_accept_p50_ms', 'accepted', 'engine_hashrate', 'engine_hashrate_trace_ghs')}), flush=True)
 " > $O/latency.jsonl 2> $O/latency.err && echo "latency ok" &&
 timeout -k 10 200 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_devproc.py -k share_latency > $O/pytest_latency.txt 2>&1 && echo "test ok"
