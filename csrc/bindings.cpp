@@ -128,6 +128,10 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["job_switches"] = s.job_switches;
   d["last_job_switch_ms"] = s.last_job_switch_ms;
   d["job_switch_ms"] = s.job_switch_ms;
+  d["ring_overflow"] = s.ring_overflow;
+  d["verify_dropped"] = s.verify_dropped;
+  d["verify_queue_peak"] = s.verify_queue_peak;
+  d["launch_hashes"] = s.launch_hashes;
   d["aborted_launches"] = s.aborted_launches;
   d["ring_hits"] = s.ring_hits;
   d["clock_calib_rtt_us"] = s.clock_calib_rtt_us;

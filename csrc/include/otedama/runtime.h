@@ -89,6 +89,13 @@ struct MinerStats {
   std::vector<double> job_switch_ms;  // most recent samples (<= 64)
   uint64_t aborted_launches = 0;      // batches stopped early by the device abort word
   uint64_t ring_hits = 0;             // hits consumed from the host-coherent ring while their launch was running
+  // Candidates lost on the way to the share queue, each counted (the reference counts every dropped share,
+  // internal/miner/worker.go:266-275): kernel hits past a launch's hit-ring capacity, and scrypt candidates refused
+  // by the bounded host-verifier queue.
+  uint64_t ring_overflow = 0;
+  uint64_t verify_dropped = 0;
+  uint64_t verify_queue_peak = 0;     // deepest the scrypt verifier queue has been
+  uint64_t launch_hashes = 0;         // hashes per launch of the last batch (capped from the share target)
   double clock_calib_rtt_us = 0;      // round trip of the device-clock calibration that is in use
   // Device-timeline time (s, from the miner's start) at which the batches counted in `hashes` had completed: a
   // rate over two samples, (hashes1 - hashes0) / (done_at1 - done_at0), is exact instead of quantized by launches.

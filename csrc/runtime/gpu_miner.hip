@@ -7,7 +7,7 @@
 // therefore on its way to the pool while the launch that found it is still running, instead of after the
 // batch (2^29 nonces, ~28 ms) and its copy-back.
 //
-// Job switches: new work (or a pause) opens a new launch epoch and writes it to an uncached device word on a
+// Job switches: new work opens a new launch epoch and writes it to an uncached device word on a
 // control stream (hipStreamWriteValue32). Every wave polls that word once per grid-stride trip, so batches of
 // the old epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first
 // batch of the new work starts right behind them. The switch time (set_job -> new batch running) is recorded.
@@ -85,7 +85,11 @@ __global__ void otd_rt_probe(uint64_t* out) {
 namespace otedama {
 
 namespace {
-constexpr uint32_t kHitCap = 1024;
+// Hit-ring records per launch (16 B each, host-coherent). Launches are sized from the share target so the expected
+// candidates per launch stay at or below kHitCap / 8 (see launch_cap); what still overflows is counted.
+constexpr uint32_t kHitCap = 4096;
+constexpr uint64_t kMinLaunchHashes = 1ull << 22;  // below ~0.2 ms per launch the launch overhead would dominate
+constexpr size_t kVerifyCap = 8192;                // scrypt candidates waiting for host verification (~1 ms each)
 constexpr int kInflight = 2;
 constexpr double kRtHz = 100e6;
 constexpr auto kIdlePoll = std::chrono::microseconds(100);
@@ -352,20 +356,24 @@ void GpuMiner::loop() {
   double switch_t0 = 0;
   double rate_hpms = 0;  // hashes per ms of completed full batches (for aborted-batch accounting)
   std::deque<int> fifo;  // in-flight slots, issue order
-  std::deque<Candidate> vq;  // scrypt candidates awaiting host verification
+  std::deque<Candidate> vq;  // scrypt candidates awaiting host verification (at most kVerifyCap)
+  uint64_t verify_refused = 0, vq_peak = 0;  // guarded by vq_mu
   std::mutex vq_mu;
   std::condition_variable vq_cv;
   bool vq_stop = false;
   std::thread verifier;
 
-  // New work or a pause opens a new launch epoch and moves the device abort word: batches of older epochs stop at
+  // New work opens a new launch epoch and moves the device abort word: batches of older epochs stop at
   // their next poll. Called at the top of every loop trip and between hit verifications (a burst of scrypt hits
   // costs ~1 ms of CPU each and must not delay a switch).
   auto check_epoch = [&](uint64_t* gen_out) {
     uint64_t gen = 0;
     double set_at = 0;
     auto job = peek_job(&gen, &set_at);
-    const uint64_t want_gen = job ? gen : 0;
+    // A pause (no job) keeps the batches in flight running to their end (<= kInflight launches): moving the abort
+    // word for it would skip the unsearched rest of those batches for good when the same work resumes, since the
+    // cursor already moved past them. Only new work stops them.
+    const uint64_t want_gen = job ? gen : epoch_gen;
     if (want_gen != epoch_gen) {
       epoch_gen = want_gen;
       ++epoch;
@@ -449,10 +457,16 @@ void GpuMiner::loop() {
       const uint32_t stamp = __atomic_load_n(&r->stamp, __ATOMIC_RELAXED);
       if (b.job->algo == Algo::kScrypt) {
         // host scrypt costs ~1 ms per candidate: verified on the verifier thread so a burst of candidates never
-        // holds up a job switch or the next launch
+        // holds up a job switch or the next launch. The queue is bounded: past kVerifyCap a candidate is refused
+        // and counted (a share target far below the device's rate would otherwise grow it without limit).
         std::lock_guard<std::mutex> g(vq_mu);
-        vq.push_back(Candidate{b.job, b.group, b.gen, nonce, vi, stamp, b.enq_host, b.rt_enq, b.nvar});
-        vq_cv.notify_one();
+        if (vq.size() >= kVerifyCap) {
+          ++verify_refused;
+        } else {
+          vq.push_back(Candidate{b.job, b.group, b.gen, nonce, vi, stamp, b.enq_host, b.rt_enq, b.nvar});
+          vq_peak = std::max<uint64_t>(vq_peak, vq.size());
+          vq_cv.notify_one();
+        }
       } else {
         verify_push(Candidate{b.job, b.group, b.gen, 0, 0, 0, b.enq_host, b.rt_enq, b.nvar}, nonce, vi, stamp, true,
                     cur, cur_g, &good, &bad);
@@ -461,10 +475,18 @@ void GpuMiner::loop() {
       ++handled;
     }
     if (handled || lost) {
+      uint64_t refused = 0, peak = 0;
+      {
+        std::lock_guard<std::mutex> g(vq_mu);
+        refused = verify_refused;
+        peak = vq_peak;
+      }
       std::lock_guard<std::mutex> g(stats_mu_);
       stats_.shares += good;
       stats_.rejected_candidates += bad + lost;
       if (final_n == ~0u) stats_.ring_hits += handled;
+      stats_.verify_dropped = refused;
+      stats_.verify_queue_peak = peak;
     }
     return uint32_t(handled);
   };
@@ -483,6 +505,12 @@ void GpuMiner::loop() {
     if (aborted && rate_hpms > 0) done_hashes = std::min<uint64_t>(full, uint64_t(rate_hpms * double(ms)));
     if (!aborted && ms > 0) rate_hpms = rate_hpms > 0 ? 0.8 * rate_hpms + 0.2 * (double(full) / ms) : double(full) / ms;
     std::lock_guard<std::mutex> g(stats_mu_);
+    if (n > kHitCap) {  // the kernel counted these candidates but had no ring slot left to publish them
+      if (stats_.ring_overflow == 0)
+        std::fprintf(stderr, "otedama: %s: launch found %u candidates, hit ring holds %u: %u lost (counted in "
+                     "ring_overflow)\n", device_id_.c_str(), n, kHitCap, n - kHitCap);
+      stats_.ring_overflow += n - kHitCap;
+    }
     stats_.hashes += done_hashes;
     if (have_done) stats_.hashes_done_at_s = std::max(stats_.hashes_done_at_s, double(done_ms) * 1e-3);
     stats_.candidates += n;
@@ -535,6 +563,18 @@ void GpuMiner::loop() {
     return gp;
   };
 
+  // Hashes per launch for a share target: the kernels' prefilter passes a hash whose top word is <= the target's,
+  // i.e. with probability (target_hi + 1) / 2^32, so expected candidates per launch = hashes * that. Launches are cut
+  // (powers of two, so they still tile 2^32) until that is <= kHitCap / 8; the hit ring then overflows only on a
+  // draw ~8 sigma above the mean at the floor target, and any overflow is counted.
+  auto launch_cap = [&](const JobTemplate& job) -> uint64_t {
+    const double p = (double(load_le32(job.target + 28)) + 1.0) / 4294967296.0;
+    const double lim = double(kHitCap / 8) / p;
+    uint64_t cap = 1ull << 40;
+    while (cap > kMinLaunchHashes && double(cap) > lim) cap >>= 1;
+    return cap;
+  };
+
   auto enqueue = [&](Batch& s, const std::shared_ptr<const JobTemplate>& job, uint64_t gen, const Batch* prev) {
     hipStream_t stream = s.stream;
     if (!group || group->gen != gen || group->k != k) group = build_group(job, gen);
@@ -572,7 +612,7 @@ void GpuMiner::loop() {
       ScryptParams p;
       scrypt_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
-      s.count = remaining < scrypt_batch ? remaining : scrypt_batch;
+      s.count = std::min<uint64_t>({remaining, scrypt_batch, launch_cap(*job)});
       OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, sink,
                                    scrypt_grid, stream));
     } else if (job->algo == Algo::kX11) {
@@ -580,7 +620,7 @@ void GpuMiner::loop() {
       X11Params p;
       x11_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
-      s.count = remaining < x11_batch ? remaining : x11_batch;
+      s.count = std::min<uint64_t>({remaining, x11_batch, launch_cap(*job)});
       OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), &sink, stream));
     } else if (group->use_v) {
       const bool two = group->nvar == kSha256dV2Group;
@@ -593,7 +633,9 @@ void GpuMiner::loop() {
       OTD_HIP(hipMemcpyAsync(s.d_vars, s.h_vars, table_bytes, hipMemcpyHostToDevice, stream));
       // W3 (big-endian nonce word) windows tile [0, 2^32) exactly like the nonce windows of the other kernels;
       // the kernel reports nonce = bswap(W3). Launch duration stays batch_ hashes.
-      s.count = batch_ >= uint64_t(group->nvar) ? batch_ / uint64_t(group->nvar) : 1;
+      const uint64_t launch = std::min(batch_, launch_cap(*job));
+      s.count = std::min<uint64_t>(launch >= uint64_t(group->nvar) ? launch / uint64_t(group->nvar) : 1,
+                                   (1ull << 32) - nonce_off);
       OTD_HIP(launch_sha256d_search_v(vp, s.d_vars, uint32_t(nonce_off), s.count, sink, two ? grid_v2_ : grid_v_,
                                       stream, 256, two ? 2 : 1));
     } else if (group->nvar > 1) {
@@ -603,24 +645,27 @@ void GpuMiner::loop() {
       if (!sha256d_prepare_k(hs, group->nvar, job->target, &p)) throw std::runtime_error("sha256d_prepare_k");
       // Keep one launch's duration about independent of K: nonces per variant = batch / (largest power of two
       // <= K); batch is a power of two that tiles 2^32, so this still tiles it.
+      const uint64_t launch = std::min(batch_, launch_cap(*job));
       uint64_t div = 1;
-      while (div * 2 <= (uint64_t)group->nvar && div * 2 <= batch_) div *= 2;
-      s.count = batch_ / div;
+      while (div * 2 <= (uint64_t)group->nvar && div * 2 <= launch) div *= 2;
+      s.count = std::min<uint64_t>(launch / div, (1ull << 32) - nonce_off);
       OTD_HIP(launch_sha256d_search_k(p, uint32_t(nonce_off), s.count, sink, grid_k_, stream));
     } else {
       Sha256dParams p;
       sha256d_prepare(group->header[0], job->target, &p);
-      s.count = batch_;
+      s.count = std::min<uint64_t>(std::min(batch_, launch_cap(*job)), (1ull << 32) - nonce_off);
       OTD_HIP(launch_sha256d_search(p, uint32_t(nonce_off), s.count, sink, grid_, stream));
     }
     OTD_HIP(hipMemcpyAsync(s.h_count, s.d_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     OTD_HIP(hipEventRecord(s.done, stream));
     s.busy = true;
     nonce_off += s.count;
+    const uint64_t launch_hashes = s.count * uint64_t(s.nvar);
     const uint64_t group_n = uint64_t(group->nvar);
     if (nonce_off >= (1ull << 32)) { nonce_off = 0; k += group_n; }
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.variant_epoch = job->epoch;
+    stats_.launch_hashes = launch_hashes;
     stats_.variant_next = job->variant_start + (nonce_off == 0 ? k : k + group_n) * job->variant_stride;
   };
 

@@ -58,6 +58,7 @@ def cmd_pool(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     fs.string("listen-v1", "127.0.0.1:3333", "Stratum V1 listen address (port +1 per extra algorithm).")
     fs.string("payout-address", "", "Operator address paid by the coinbase (empty = OP_RETURN).")
     fs.float("difficulty", 1.0, "Initial share difficulty.")
+    fs.bool("fixed-difficulty", False, "Pin every connection at --difficulty (vardiff off).")
     fs.float("share-seconds", 10.0, "Vardiff target seconds between shares per connection.")
     fs.float("retarget-seconds", 30.0, "Vardiff retarget window.")
     fs.float("block-interval", 600.0, "Seconds between synthetic network blocks.")
@@ -120,6 +121,7 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
             journal = journal.replace(".db", f".{algo}.db") if journal.endswith(".db") else f"{journal}.{algo}"
         opts = PoolOptions(algorithm=algo, listen_sv2=_bump(fs["listen-sv2"], k), listen_v1=_bump(fs["listen-v1"], k),
                            payout_address=fs["payout-address"] or None, initial_difficulty=fs["difficulty"],
+                           fixed_difficulty=fs["fixed-difficulty"],
                            target_share_seconds=fs["share-seconds"], retarget_seconds=fs["retarget-seconds"],
                            block_interval=fs["block-interval"], job_interval=fs["job-interval"],
                            journal_path=journal or ":memory:", payout_scheme=fs["payout-scheme"],

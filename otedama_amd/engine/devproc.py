@@ -40,7 +40,7 @@ MAX_FRAME = 64 << 20
 
 # counters that survive a respawn (summed over the device's processes)
 _CUMULATIVE = ("hashes", "candidates", "shares", "dropped", "launches", "rejected_candidates", "variant_launches",
-               "busy_seconds", "job_switches", "aborted_launches", "ring_hits")
+               "busy_seconds", "job_switches", "aborted_launches", "ring_hits", "ring_overflow", "verify_dropped")
 
 
 def _send(sock: socket.socket, obj, lock: threading.Lock | None = None) -> None:
@@ -183,7 +183,8 @@ class DeviceProcess:
     # ------------------------------------------------------------- miner interface
     def set_job(self, template: dict | None) -> None:
         self._job = dict(template) if template is not None else None
-        self._post({"op": "job", "t": self._job})
+        # "sent" (CLOCK_MONOTONIC, shared by both processes): the child reports the hop, frame -> native set_job
+        self._post({"op": "job", "t": self._job, "sent": time.monotonic()})
 
     def poll(self, max_items: int = 256) -> list[dict]:
         out = []
@@ -313,6 +314,7 @@ def _child(argv: list[str]) -> int:
     poller.register(sock.fileno(), select.POLLIN)
     poller.register(efd, select.POLLIN)
     fr = _Framer()
+    hops: collections.deque = collections.deque(maxlen=64)  # job frame sent (parent) -> native set_job, ms
     next_stats = 0.0
     first_hash = False  # until the first batch is running: poll fast and report it at once (start-up timing)
     rc = 0
@@ -337,6 +339,8 @@ def _child(argv: list[str]) -> int:
                 for msg in fr.feed(data):
                     if msg.get("op") == "job":
                         m.set_job(msg.get("t"))
+                        if msg.get("sent"):
+                            hops.append((time.monotonic() - float(msg["sent"])) * 1e3)
                         t_job = t_job or time.time()
                     elif msg.get("op") == "stop":
                         return 0
@@ -349,6 +353,7 @@ def _child(argv: list[str]) -> int:
                 next_stats = 0.0
             if time.monotonic() >= next_stats:
                 st = m.stats()
+                st["job_hop_ms"] = list(hops)
                 _send(sock, {"op": "stats", "st": st})
                 next_stats = time.monotonic() + STATS_PERIOD
                 if st.get("faulted"):
@@ -365,7 +370,9 @@ def _child(argv: list[str]) -> int:
             except OSError:
                 pass
         try:
-            _send(sock, {"op": "stats", "st": m.stats()})
+            st = m.stats()
+            st["job_hop_ms"] = list(hops)
+            _send(sock, {"op": "stats", "st": st})
         except OSError:
             pass
 

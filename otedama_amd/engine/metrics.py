@@ -141,6 +141,7 @@ class EngineMetrics:
         self._device_hashrate: dict[str, object] = {}
         self._device_busy: dict[str, object] = {}
         self._device_launches: dict[str, object] = {}
+        self._device_lost: dict[tuple[str, str], object] = {}
         self._payout_info: dict[str, object] = {}
 
     def reject_reason(self, category: str):
@@ -215,6 +216,23 @@ class EngineMetrics:
                 c = self.reg.new_counter("otedama_device_kernel_launches_total",
                                          "Search-kernel launches (batches) completed by the device.", {"device": device})
                 self._device_launches[device] = c
+        c.add(n)
+
+    def add_device_candidates_lost(self, device: str, reason: str, n: int) -> None:
+        """Candidates a device found but never queued as shares: ``ring_overflow`` (past a launch's hit-ring
+        capacity) or ``verify_queue_full`` (scrypt host-verifier queue bound)."""
+        if n <= 0:
+            return
+        with self._lock:
+            c = self._device_lost.get((device, reason))
+            if c is None:
+                if len(self._device_lost) >= 128:
+                    return
+                c = self.reg.new_counter("otedama_device_candidates_lost_total",
+                                         "Kernel candidates lost before host verification, by cause (ring_overflow: "
+                                         "more hits than a launch's hit ring holds; verify_queue_full: scrypt "
+                                         "verifier queue at its bound).", {"device": device, "reason": reason})
+                self._device_lost[(device, reason)] = c
         c.add(n)
 
     def set_active_payout(self, masked: str) -> None:

@@ -179,6 +179,7 @@ class Engine:
         self._sats = SatsAccountant()
         self._last_dropped = 0
         self._busy_prev: dict[str, tuple[float, float, int]] = {}  # device -> (busy_seconds, at, launches)
+        self._lost_prev: dict[tuple[str, str], int] = {}  # (device, cause) -> candidates lost so far
         self.dashboard = opts.dashboard
 
     # ---------------------------------------------------------------- API
@@ -273,6 +274,13 @@ class Engine:
         # first job handed to the devices; seconds after process start
         out["engine_phases_s"] = {k: (v - t0) for k, v in self._marks.items()} if t0 else {}
         return out
+
+    def enforced_share_difficulty(self) -> float | None:
+        """Difficulty of the share target in force for the active job (the pool's SetTarget /
+        OpenMiningChannelSuccess / set_difficulty), as diff1 / target; None without a job."""
+        job = self._active_job
+        tgt = self._job_targets.get(job.job_id) if job is not None else None
+        return self.algorithm.diff1 / tgt if tgt else None
 
     def device_list(self) -> list[dict]:
         return [{"id": d.identity().id, "family": d.identity().family.value, "vendor": d.identity().vendor,
@@ -770,6 +778,7 @@ class Engine:
         stalled_devs = self.miners.stalled()
         dstats = self.miners.device_stats()
         self._publish_device_activity(dstats, now)
+        self._publish_candidate_losses(dstats)
         link = getattr(self.miners, "link", None)
         if link is not None:
             self.m.node_ranks.set(link.world)
@@ -835,6 +844,19 @@ class Engine:
                 threads = max(int(st.get("threads", 1) or 1), 1)
                 self.m.set_device_busy(dev, min(max((busy - prev[0]) / (dt * threads), 0.0), 1.0))
             self.m.add_device_launches(dev, launches - prev[2])
+
+    def _publish_candidate_losses(self, dstats: dict) -> None:
+        """Kernel candidates that never reached the share queue (device hit-ring overflow, scrypt verifier queue
+        bound): counted per device and cause, and warned about when they grow."""
+        for dev, st in dstats.items():
+            for key, cause in (("ring_overflow", "ring_overflow"), ("verify_dropped", "verify_queue_full")):
+                n = int(st.get(key, 0) or 0)
+                prev = self._lost_prev.get((dev, cause), 0)
+                if n > prev:
+                    self.m.add_device_candidates_lost(dev, cause, n - prev)
+                    self.log("warn", f"engine: device {dev} lost {n - prev} candidate(s) ({cause}); the share "
+                                     "target is too easy for the device's launch size / verifier")
+                self._lost_prev[(dev, cause)] = n
 
 
 def _ack_eventfd(fd: int, wake: asyncio.Event) -> None:

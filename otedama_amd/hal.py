@@ -183,11 +183,21 @@ class KFDDriver:
     Used when every device runs in its own process (engine/devproc.py): the engine process never opens the GPU,
     so the devices it hands out can only be named here and are opened by their own processes."""
 
-    def __init__(self, base_path: str | None = None):
+    def __init__(self, base_path: str | None = None, dri_path: str = "/dev/dri"):
         self.base_path = base_path or KFD_TOPOLOGY_PATH
+        self.dri_path = dri_path
 
     def name(self) -> str:
         return "hip"
+
+    def _openable(self, props: dict[str, int]) -> bool:
+        """The ROCm runtime skips a GPU node whose render device this process cannot open (a container given
+        some of the host's GPUs still sees every node in the topology): the HIP ordinal space counts only the
+        openable ones, so the list here must too, or ordinal i would name another GPU."""
+        minor = props.get("drm_render_minor", -1)
+        if minor is None or minor <= 0:
+            return True  # an old kernel without the property: nothing to check against
+        return os.access(os.path.join(self.dri_path, f"renderD{minor}"), os.R_OK | os.W_OK)
 
     def enumerate(self) -> list:
         try:
@@ -201,6 +211,8 @@ class KFDDriver:
             p = _kfd_props(os.path.join(self.base_path, str(n), "properties"))
             if p.get("simd_count", 0) <= 0 or not p.get("gfx_target_version"):
                 continue  # a CPU node
+            if not self._openable(p):
+                continue  # not ours: the runtime will not count it either
             v = p["gfx_target_version"]
             arch = f"gfx{v // 10000}{(v // 100) % 100:x}{v % 100:x}"
             cus = p["simd_count"] // max(p.get("simd_per_cu", 4), 1)

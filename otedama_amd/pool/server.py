@@ -27,7 +27,7 @@ import json
 import os
 import struct
 import time
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from dataclasses import dataclass, field
 
 from otedama_amd.metrics import Registry
@@ -55,6 +55,9 @@ class PoolOptions:
     listen_v1: str = "127.0.0.1:0"
     payout_address: str | None = None
     initial_difficulty: float = 1.0
+    # Pin every connection at initial_difficulty: no vardiff retargets, no start from the channel's nominal hashrate,
+    # no saved difficulty (the latency probe and benchmarks measure at a known, enforced difficulty).
+    fixed_difficulty: bool = False
     target_share_seconds: float = 10.0
     retarget_seconds: float = 30.0
     min_difficulty: float = 1e-6
@@ -110,6 +113,9 @@ class _Worker:
         self.version_mask = version_mask
         self.accepted = 0
         self.rejected = 0
+        self.opened_at = time.monotonic()
+        self.retargets = 0
+        self.last_retarget_at = 0.0  # monotonic time of the last difficulty change (0 = never moved)
 
     def retargeted(self, old: float) -> None:
         """The worker's difficulty just moved away from `old`. Shares already in flight were found against some
@@ -119,6 +125,8 @@ class _Worker:
         recent = now - self.retarget_at < RETARGET_GRACE
         self.prev_difficulty = min(self.prev_difficulty, old) if recent else old
         self.retarget_at = now
+        self.retargets += 1
+        self.last_retarget_at = now
 
 
 class PoolServer:
@@ -171,6 +179,8 @@ class PoolServer:
         self.accepted = 0
         self.rejected = 0
         self.reject_reasons: dict[str, int] = {}
+        self.started_at = time.monotonic()
+        self._validate_ms: deque = deque(maxlen=8192)  # submit received -> verdict, per share
         self._init_metrics(registry)
 
     # ------------------------------------------------------------ metrics
@@ -303,15 +313,19 @@ class PoolServer:
                              version: int) -> Verdict:
         """validate() with the header hash off the event loop for slow algorithms (scrypt: ~ms per share,
         GIL released), so a burst of shares from many GPUs does not stall every other connection."""
+        t0 = time.perf_counter()
         pre = self._precheck(worker, job_id, extranonce, ntime, nonce, version)
         if isinstance(pre, Verdict):
-            return pre
-        job, key, hdr = pre
-        if self.algo.name == "sha256d":
-            h = self.algo.hash(hdr)  # ~1 us: cheaper inline than a thread hop
+            v = pre
         else:
-            h = await asyncio.get_running_loop().run_in_executor(self._hash_pool, self._slow_hash, hdr)
-        return self._finish(worker, job_id, job, key, h)
+            job, key, hdr = pre
+            if self.algo.name == "sha256d":
+                h = self.algo.hash(hdr)  # ~1 us: cheaper inline than a thread hop
+            else:
+                h = await asyncio.get_running_loop().run_in_executor(self._hash_pool, self._slow_hash, hdr)
+            v = self._finish(worker, job_id, job, key, h)
+        self._validate_ms.append((time.perf_counter() - t0) * 1e3)
+        return v
 
     def share_target(self, difficulty: float) -> bytes:
         """Share target for a difficulty, clamped to 2^256-1 (below ~diff1/2^256 the target would overflow)."""
@@ -390,10 +404,22 @@ class PoolServer:
         return Verdict(False, reason, 0.0, h)
 
     def new_worker(self, name: str, version_mask: int) -> _Worker:
-        d = self.journal.load_worker(name) or self.opts.initial_difficulty
-        return _Worker(name, self.vardiff.new_state(d), version_mask)
+        d = None if self.opts.fixed_difficulty else self.journal.load_worker(name)
+        return _Worker(name, self.vardiff.new_state(d or self.opts.initial_difficulty), version_mask)
+
+    def start_difficulty(self, w: _Worker, nominal_hashrate: float) -> None:
+        """SV2 OpenMiningChannel / UpdateChannel: start a worker without saved state from its nominal hashrate
+        (pinned pools keep initial_difficulty)."""
+        if self.opts.fixed_difficulty or nominal_hashrate <= 0:
+            return
+        w.vd.difficulty = self.vardiff.difficulty_for_hashrate(nominal_hashrate)
+        w.prev_difficulty = w.vd.difficulty
 
     def after_accept(self, w: _Worker) -> float | None:
+        if self.opts.fixed_difficulty:
+            w.vd.shares += 1
+            w.vd.total_shares += 1
+            return None
         old = w.vd.difficulty
         new = self.vardiff.on_share(w.vd)
         if new is not None:
@@ -423,12 +449,30 @@ class PoolServer:
     def blocks(self, limit: int = 20) -> list[dict]:
         return [dict(b, algorithm=self.algo.name) for b in self.journal.recent_blocks(limit)]
 
+    def validation_ms(self, q: float) -> float | None:
+        """Nearest-rank quantile of submit-received -> verdict (header rebuild, PoW hash, duplicate check)."""
+        xs = sorted(self._validate_ms)
+        return xs[min(len(xs) - 1, int(q * len(xs)))] if xs else None
+
     def stats(self) -> dict:
+        now = time.monotonic()
+        live = self._live_workers()
         return {
             "algorithm": self.algo.name, "height": self.block.height if self.block else 0,
             "clients_v1": len(self._v1), "clients_v2": len(self._v2), "accepted": self.accepted,
             "rejected": self.rejected, "reject_reasons": dict(self.reject_reasons), "blocks_found": self.blocks_found,
             "hashrate": self.m_hashrate.value(), "sv2": self.addr_sv2, "v1": self.addr_v1,
+            "uptime_s": now - self.started_at,
+            "accepted_per_s": self.accepted / max(now - self.started_at, 1e-9),
+            "validate_ms": {"p50": self.validation_ms(0.5), "p95": self.validation_ms(0.95),
+                            "p99": self.validation_ms(0.99), "samples": len(self._validate_ms)},
+            "fixed_difficulty": self.opts.fixed_difficulty,
+            # per live connection: the difficulty in force, how often vardiff moved it, and when it last moved
+            # (seconds after the channel opened: the time vardiff took to reach the difficulty it holds)
+            "workers": [{"name": w.name, "difficulty": w.vd.difficulty, "accepted": w.accepted,
+                         "rejected": w.rejected, "retargets": w.retargets, "age_s": now - w.opened_at,
+                         "settled_after_s": (w.last_retarget_at - w.opened_at) if w.retargets else 0.0}
+                        for w in live],
         }
 
     # ------------------------------------------------------------ listeners
@@ -672,9 +716,8 @@ class _V2Conn:
             self._next_channel += 1
             prefix = self.pool.next_extranonce(EN1_SIZE if extended else EN1_SIZE + EN2_SIZE)
             w = self.pool.new_worker(msg.user, BIP320_MASK if self.version_rolling else 0)
-            if msg.nominal_hashrate > 0 and self.pool.journal.load_worker(msg.user) is None:
-                w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
-                w.prev_difficulty = w.vd.difficulty
+            if self.pool.opts.fixed_difficulty or self.pool.journal.load_worker(msg.user) is None:
+                self.pool.start_difficulty(w, msg.nominal_hashrate)
             self.channels[ch] = (w, prefix)
             target = self.pool.share_target(w.vd.difficulty)
             if extended:
@@ -707,7 +750,7 @@ class _V2Conn:
                 self._send(M.SubmitSharesError(msg.channel_id, msg.sequence_number, v.reason))
         elif isinstance(msg, M.UpdateChannel):
             ent = self.channels.get(msg.channel_id)
-            if ent is not None and msg.nominal_hashrate > 0:
+            if ent is not None and msg.nominal_hashrate > 0 and not self.pool.opts.fixed_difficulty:
                 w = ent[0]
                 w.retargeted(w.vd.difficulty)
                 w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)

@@ -130,6 +130,28 @@ def test_kfd_topology_enumeration_without_a_runtime(tmp_path, monkeypatch):
     assert [(d.index, d.extra["arch"]) for d in devs] == [(0, "gfx950"), (1, "gfx90a")]
 
 
+def test_kfd_topology_skips_nodes_whose_render_device_is_not_openable(tmp_path, monkeypatch):
+    """A container given some of the host's GPUs sees every KFD node but can open only its own render devices;
+    the runtime skips the others, so the KFD list must too or ordinal i names another GPU."""
+    topo, dri = tmp_path / "topo", tmp_path / "dri"
+    topo.mkdir()
+    dri.mkdir()
+    for n, minor in ((1, 128), (2, 129), (3, 130)):
+        d = topo / str(n)
+        d.mkdir()
+        (d / "properties").write_text(f"simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n"
+                                      f"drm_render_minor {minor}\n")
+    (dri / "renderD128").write_text("")
+    (dri / "renderD130").write_text("")  # renderD129 is another container's GPU: absent here
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    devs = hal.KFDDriver(str(topo), dri_path=str(dri)).enumerate()
+    assert [(d.identity().id, d.index) for d in devs] == [("gpu-0", 0), ("gpu-1", 1)]
+    os.chmod(dri / "renderD130", 0)  # present but not openable (root ignores modes: only check when it matters)
+    if not os.access(dri / "renderD130", os.R_OK | os.W_OK):
+        assert len(hal.KFDDriver(str(topo), dri_path=str(dri)).enumerate()) == 1
+
+
 def test_process_isolation_engine_side_does_not_load_the_extension():
     """The engine of a GPU node hands every GPU to a device process: building its MinerSet must not import the
     native extension (which links the HIP runtime; ~1 GB of RSS once a GPU context exists)."""

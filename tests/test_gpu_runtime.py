@@ -203,5 +203,9 @@ def test_job_switch_with_other_streams_in_the_process():
     torch.cuda.synchronize()
     res = measure_job_switch(0, "sha256d", switches=6, batch_nonces=1 << 32)
     print("job switch at 2^32:", res)
-    assert res["p50_ms"] is not None and res["p50_ms"] < 20.0, res
+    assert res["path"] == "devproc"
+    assert res["p50_ms"] is not None and res["p50_ms"] < 20.0, res  # engine -> device process -> new batch
     assert res["max_ms"] < 50.0, res
+    inproc = res["in_process"]  # the miner in this process, next to torch's streams
+    assert inproc["p50_ms"] is not None and inproc["p50_ms"] < 20.0, inproc
+    assert inproc["max_ms"] < 50.0, inproc
