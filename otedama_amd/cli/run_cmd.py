@@ -108,10 +108,9 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         # supervisor restarted after a loss joins the running node instead of forming it.
         from otedama_amd.parallel.comm import NodeComm, init_from_env, join_from_env
 
+        # a replacement process: followers join the running node; rank 0 restarted by the supervisor takes the
+        # node over as its leader (parallel/node.py NodeMinerSet._take_over)
         joining = os.environ.get("OTEDAMA_NODE_JOIN") == "1"
-        if joining and int(os.environ.get("RANK", "0")) == 0:
-            stderr.write("otedama run: rank 0 cannot join a node (it forms it)\n")
-            return EXIT_CONFIG
         info = join_from_env() if joining else init_from_env()
         # the rank's HIP ordinal (init_from_env maps local ranks onto the visible GPUs; on an 8-GPU node it is the
         # local rank, on a 1-GPU rehearsal over gloo every rank shares GPU 0)
@@ -146,14 +145,18 @@ def _run_node_worker(cfg, info, comm, stdout, joining: bool = False) -> int:
     from otedama_amd.parallel.node import NodeWorker
 
     on_gpu = info.device.type == "cuda"
-    devs = hal.Detector(hal.default_registry(cfg.mining.cpu_threads)).detect()
+    # the GPU's miner runs in a device process of its own (engine/devproc.py): a kernel fault kills that child, not
+    # this rank and its RCCL communicator; the devices are named from the KFD topology
+    isolation = cfg.mining.isolation
+    devs = hal.Detector(hal.default_registry(cfg.mining.cpu_threads, gpu_free=isolation == "process")).detect()
     gpu = info.device.index if on_gpu else info.local_rank
     if on_gpu:
         devs = [d for d in devs if d.identity().family == hal.Family.GPU and d.index == gpu]
     else:  # CPU-only rehearsal node: this rank's CPU miner
         devs = [d for d in devs if d.identity().family == hal.Family.CPU]
     local = MinerSet(devs, cfg.mining.algorithm, cfg.mining.batch_nonces, 0 if on_gpu else cfg.mining.cpu_threads,
-                     rank=max(info.rank, 0), world_size=max(info.world_size, 1), sha_variants=cfg.mining.sha_variants)
+                     rank=max(info.rank, 0), world_size=max(info.world_size, 1), sha_variants=cfg.mining.sha_variants,
+                     isolation=isolation, log=lambda lvl, msg: stdout.write(f"[{lvl}] {msg}\n"))
     stdout.write(f"[info] node: rank {info.orig_rank} {'joining' if joining else f'of {info.world_size}'} mining on "
                  f"GPU {gpu} ({len(local)} device(s))\n")
     try:

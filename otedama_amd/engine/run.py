@@ -27,6 +27,8 @@ rebalance the rest.
 from __future__ import annotations
 
 import asyncio
+import collections
+import json
 import os
 import sys
 import time
@@ -156,6 +158,11 @@ class Engine:
         self.latency = LatencyTracker(256)           # submit -> accept (reference semantics)
         self.pipeline_latency = LatencyTracker(4096)  # host-verified hit -> accept
         self.device_latency = LatencyTracker(4096)    # the kernel's hit (device clock) -> accept
+        # the same, split by where the share was found: this process's devices, or another rank of the node (its
+        # share crossed the R2 gather; parallel/node.py)
+        self.device_latency_by_origin = {"local": LatencyTracker(4096), "remote": LatencyTracker(4096)}
+        # accepted shares: (monotonic, device hit -> accept ms | None, origin, device, host verify -> accept ms | None)
+        self.accept_log: collections.deque = collections.deque(maxlen=16384)
         self.hash_window = HashrateWindow()
         self.current_hashrate = 0.0
         self.device_hashrates: dict[str, float] = {}
@@ -308,14 +315,15 @@ class Engine:
             for d in self.devices:
                 self.log("info", f"engine: device {d.identity()} caps={d.capabilities()}")
             node = self.opts.node_comm
-            world = node.info.world_size if node is not None else 1
-            # one process per GPU unless this process is already one rank of a node (a rank owns one GPU)
+            world = max(node.info.world_size, 1) if node is not None else 1
+            # one process per GPU; a node rank runs its GPU's miner in a device process too, so a kernel fault never
+            # takes the pool session or the RCCL communicator with it
             gpus = any(d.identity().family == hal.Family.GPU for d in self.devices)
-            isolation = "process" if (cfg.mining.isolation == "process" and gpus and node is None) else "thread"
+            isolation = "process" if (cfg.mining.isolation == "process" and (gpus or node is not None)) else "thread"
             self.miners = MinerSet(self.devices, self.algorithm.name, cfg.mining.batch_nonces, cfg.mining.cpu_threads,
                                    rank=0, world_size=world, log=self.log, sha_variants=cfg.mining.sha_variants,
                                    isolation=isolation)
-            if node is not None and world > 1:
+            if node is not None and node.info.capacity > 1:
                 from otedama_amd.parallel.node import NodeMinerSet
 
                 self.miners = NodeMinerSet(self.miners, node, log=self.log)
@@ -335,6 +343,9 @@ class Engine:
             self._tasks.append(asyncio.ensure_future(self._arbitration_loop()))
             if self.dashboard is not None:
                 self.dashboard.start()
+            report = os.environ.get("OTEDAMA_NODE_REPORT", "")
+            if report:
+                self._tasks.append(asyncio.ensure_future(self._report_loop(report)))
             await self._reconnect_loop()
         finally:
             for t in self._tasks:
@@ -350,9 +361,81 @@ class Engine:
             if self.opts.on_ready:
                 self.opts.on_ready(False)
 
+    # ---------------------------------------------------------------- node report
+    def timeline_counters(self) -> dict[str, list]:
+        """Per device (local) and per rank (remote): [cumulative hashes, device-timeline time they had completed]
+        — one consistent pair each, so a rate over two samples is exact (bench.py's node section)."""
+        out: dict[str, list] = {}
+        ms = self.miners
+        if ms is None:
+            return out
+        for dev, st in ms.device_stats().items():
+            out[dev] = [int(st.get("hashes", 0)), float(st.get("hashes_done_at_s", 0.0) or 0.0)]
+        for r, (h, done) in dict(getattr(ms, "_hb_pairs", {})).items():  # remote ranks: their heartbeat's pair
+            out[f"rank{r}"] = [int(h), float(done)]
+        return out
+
+    def node_report(self) -> dict:
+        """Snapshot of the node as rank 0 sees it (OTEDAMA_NODE_REPORT): counters, device-timeline pairs, share
+        verdicts, hit -> accept latency by origin and the collective accounting."""
+        ms = self.miners
+        link = getattr(ms, "link", None)
+        info = link.comm.info if link is not None else None
+
+        def q(t: LatencyTracker) -> dict:
+            return {"p50": t.quantile(0.5), "p95": t.quantile(0.95), "p99": t.quantile(0.99), "samples": t.count()}
+
+        rep = {
+            "mono": time.monotonic(), "wall": time.time(), "pid": os.getpid(),
+            "connected": self.connected, "algorithm": self.algorithm.name,
+            "hashrate": self.current_hashrate, "counters": self.timeline_counters(),
+            "shares_found": self.m.shares_found.value(), "submitted": self.m.shares_submitted.value(),
+            "accepted": self.m.shares_accepted.value(), "rejected": self.m.shares_rejected.value(),
+            "stale_skipped": self.m.stale_skipped.value(), "below_target_skipped": self.m.below_target_skipped.value(),
+            "hit_to_accept_ms": {k: q(t) for k, t in self.device_latency_by_origin.items()},
+            "submit_to_accept_ms": q(self.latency),
+            "share_difficulty": self.enforced_share_difficulty(),
+            "world": info.world_size if info is not None else 1,
+            "members": list(info.members) if info is not None else [0],
+            "backend": info.backend if info is not None else "none",
+            "generation": info.generation if info is not None else 0,
+        }
+        if link is not None:
+            hbs = {}
+            try:
+                hbs = ms._heartbeats()
+            except Exception:  # noqa: BLE001 - store gone: shutting down
+                pass
+            rep.update({
+                "leader_collectives": link.comm.collectives,
+                "follower_collectives": {f"rank{r}": int(hb.get("coll", 0)) for r, hb in hbs.items()},
+                "follower_pending": {f"rank{r}": int(hb.get("pending", 0)) for r, hb in hbs.items()},
+                "ops": link.ops_run, "reforms": link.reforms, "lost_ranks": list(ms.lost_ranks),
+                "leader_incarnation": ms.incarnation, "remote_stale": ms.remote_stale,
+                "op_p50_ms": link.tick_quantile(0.5) * 1e3, "op_p99_ms": link.tick_quantile(0.99) * 1e3})
+        return rep
+
+    async def _report_loop(self, path: str, period: float = 0.5) -> None:
+        """Write node_report() to ``path`` every ``period`` s (atomic rename), with the accepted shares'
+        (monotonic, hit -> accept ms, origin) and a bounded series of counter samples."""
+        samples: collections.deque = collections.deque(maxlen=2400)
+        while True:
+            await asyncio.sleep(period)
+            try:
+                rep = self.node_report()
+                samples.append([rep["mono"], rep["counters"]])
+                rep["samples"] = list(samples)
+                rep["accept_log"] = list(self.accept_log)
+                tmp = f"{path}.tmp"
+                with open(tmp, "w") as f:
+                    json.dump(rep, f)
+                os.replace(tmp, path)
+            except Exception as exc:  # noqa: BLE001 - reporting never stops the engine
+                self.log("warn", f"engine: node report: {exc}")
+
     def _detect_devices(self) -> list:
         # device processes open their GPUs themselves: name them from the KFD topology without a HIP runtime here
-        gpu_free = self.cfg.mining.isolation == "process" and self.opts.node_comm is None
+        gpu_free = self.cfg.mining.isolation == "process"
         reg = hal.default_registry(self.cfg.mining.cpu_threads, gpu_free=gpu_free)
         devs = hal.Detector(reg, lambda drv, msg, err: self.log("warn", f"hal: {drv}: {msg}: {err}")).detect()
         sel = self.cfg.mining.gpus.strip().lower()
@@ -718,12 +801,12 @@ class Engine:
                 self._submitted.add(key)
                 sub = ShareSubmission(s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
                 t = asyncio.ensure_future(self._submit(session, sub, s.get("found_at", 0.0),
-                                                       s.get("device_found_at", 0.0)))
+                                                       s.get("device_found_at", 0.0), s.get("device_id", "")))
                 self._submit_tasks.add(t)
                 t.add_done_callback(self._submit_tasks.discard)
 
     async def _submit(self, session, sub: ShareSubmission, found_at: float = 0.0,
-                      device_found_at: float = 0.0) -> None:
+                      device_found_at: float = 0.0, device_id: str = "") -> None:
         self.m.shares_submitted.inc()
         trace_mark("otd.share.submit")
         try:
@@ -736,10 +819,16 @@ class Engine:
             self.m.shares_accepted.inc()
             self.latency.record(res.latency_ms)
             now = time.monotonic()
+            origin = "remote" if device_id.startswith("rank") else "local"
+            host_ms = dev_ms = None
             if found_at > 0:  # host verify -> pool accept (native queue + submit + pool validation)
-                self.pipeline_latency.record((now - found_at) * 1e3)
+                host_ms = (now - found_at) * 1e3
+                self.pipeline_latency.record(host_ms)
             if device_found_at > 0:  # the kernel's hit (s_memrealtime on the host clock) -> pool accept
-                self.device_latency.record((now - device_found_at) * 1e3)
+                dev_ms = (now - device_found_at) * 1e3
+                self.device_latency.record(dev_ms)
+                self.device_latency_by_origin[origin].record(dev_ms)
+            self.accept_log.append((now, dev_ms, origin, device_id, host_ms))
             self.log("info", f"engine: share accepted job={sub.job_id} nonce=0x{sub.nonce:08X} "
                              f"({res.latency_ms:.1f} ms)")
         else:

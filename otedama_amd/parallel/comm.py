@@ -37,7 +37,10 @@ import torch.distributed as dist
 
 JOB_BLOB_BYTES = 64 << 10  # a real V1 job (coinbase parts + 12 merkle branches, hex in JSON) can pass 4 KiB
 SHARE_SLOTS = 64
-SHARE_WORDS = 9  # epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_hi, rank|device, found_at_us
+# epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_hi, rank|device, found_at_us, device_found_at_us
+# (both times CLOCK_MONOTONIC, which every process of the host shares: the leader computes the kernel-hit -> accept
+# latency of a remote rank's share directly)
+SHARE_WORDS = 10
 COUNTER_WORDS = 4  # hashes, shares, dropped, faulted
 
 
@@ -59,12 +62,15 @@ class DistInfo:
     generation: int = 0      # process-group generation (store prefix otd-g<gen>)
     members: list = field(default_factory=list)  # orig ranks of the current group, in group-rank order
     store: object = None     # the rendezvous TCPStore (node control plane)
+    capacity: int = 0        # ranks the node was launched with (WORLD_SIZE at start; orig ranks 0..capacity-1)
 
     def __post_init__(self):
         if self.orig_rank < 0:
             self.orig_rank = self.rank
         if not self.members:
             self.members = list(range(self.world_size))
+        if self.capacity <= 0:
+            self.capacity = max(self.world_size, 1)
 
     @property
     def is_primary(self) -> bool:
@@ -131,7 +137,7 @@ def join_from_env(backend: str | None = None, use_gpu: bool | None = None) -> Di
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
     store = _connect_store(rank, world)
     return DistInfo(-1, 0, local, backend or ("nccl" if use_gpu else "gloo"), device, orig_rank=rank,
-                    generation=-1, members=[], store=store)
+                    generation=-1, members=[], store=store, capacity=world)
 
 
 def barrier(info: DistInfo) -> None:
@@ -256,7 +262,7 @@ class NodeComm:
             host[i] = torch.tensor([
                 e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
                 en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
-                int(s.get("found_at", 0.0) * 1e6),
+                int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6),
             ], dtype=torch.int64)
         self._slots.copy_(host)
         if self.info.world_size > 1:
@@ -274,7 +280,7 @@ class NodeComm:
                     "epoch": rec[0] | ((rec[1] & 0x7FFFFFFF) << 32), "nonce": rec[2] & 0xFFFFFFFF,
                     "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
                     "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
-                    "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6,
+                    "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6, "device_found_at": rec[9] / 1e6,
                     "orig_rank": self.info.members[r] if r < len(self.info.members) else r,
                 })
         return out

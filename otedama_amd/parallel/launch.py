@@ -23,6 +23,7 @@ import time
 from typing import Sequence
 
 MASTER_ADDR = "127.0.0.1"  # the container hostname may not resolve
+FINAL_EXIT_CODES = (0, 64, 78)  # rank 0 exit codes that end a node: clean stop, usage error, configuration error
 
 
 def free_port() -> int:
@@ -111,8 +112,12 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
 
     A follower (rank > 0) that exits is marked ``otd/dead/<r>`` in the store (the leader re-forms the process
     group without it within one liveness check, parallel/node.py) and, with ``respawn``, restarted after a backoff
-    (1 s doubling to 64 s, internal/engine/run.go:56-63) as a joiner that the leader re-admits. Rank 0 is the
-    pool session: when it exits the node stops and its exit code is returned."""
+    (1 s doubling to 64 s, internal/engine/run.go:56-63) as a joiner that the leader re-admits.
+
+    Rank 0 (the leader: pool session + job fan-out) that dies is restarted the same way, as a leader that takes the
+    running node over (parallel/node.py ``NodeMinerSet._take_over``); the followers keep hashing meanwhile. Only a
+    clean exit (0), a usage / configuration error (64 / 78, which a restart cannot fix) or ``respawn=False`` ends
+    the node with rank 0's exit code."""
     import datetime
 
     import torch.distributed as dist
@@ -155,15 +160,16 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
                 return 0 if rc0 in (0, -signal.SIGTERM, 128 + signal.SIGTERM) else (rc0 or 0)
             if stop_event is not None and stop_event.is_set():
                 return 0
-            rc0 = procs[0].poll()
-            if rc0 is not None:
+            rc0 = procs[0].poll() if 0 in procs else None
+            if rc0 is not None and (not respawn or rc0 in FINAL_EXIT_CODES):
                 log(f"rank 0 exited with code {rc0}; stopping the node")
                 return rc0
             now = time.monotonic()
-            for r in range(1, world):
+            for r in range(world):
                 p = procs.get(r)
                 if p is not None and p.poll() is not None:
-                    log(f"rank {r} exited with code {p.returncode}")
+                    log(f"rank {r} exited with code {p.returncode}" + (
+                        "; the followers keep hashing their last job until it is back" if r == 0 else ""))
                     store.set(f"otd/dead/{r}", str(p.returncode))
                     del procs[r]
                     if now - started.get(r, now) > 60.0:

@@ -7,14 +7,23 @@ fan-out / fan-in are RCCL collectives over xGMI, issued only when there is somet
   control plane (rendezvous TCPStore, no device work)     data plane (RCCL, bounded, per generation)
   ─────────────────────────────────────────────────────   ───────────────────────────────────────────
   otd/op/<k>     the leader's ordered op log              R1 broadcast job blob      on a new job / re-form
-  otd/pending    shares waiting on followers (counter)    R2 all_gather share slots  when otd/pending > 0
+  otd/next       ops posted so far                        R2 all_gather share slots  when a follower rings
   otd/hb/<r>     heartbeat: time, cursor, counters (2 Hz)  R3 all_gather counters     once per stats interval
+  otd/bell/<r>   the rank's doorbell port (loopback UDP)
+  otd/gen        the current process-group generation
   otd/dead/<r>   set by the supervisor when r exits
   otd/join/<r>   a replacement process asking to join
 
 Every rank runs the ops of the log in order; a collective is entered only when the leader has posted it, so in
 steady state a rank issues about one device collective per stats interval (10 s) plus one per share burst — not
-hundreds per second. Hashing never waits on any of this: kernels run on the miners' HIP streams.
+hundreds per second. Hashing never waits on any of this: kernels run in each rank's device process (engine/devproc.py),
+so a GPU fault kills that child, not the rank that holds the RCCL communicator and, on rank 0, the pool session.
+
+Nothing on the share path sleeps on a timer: a follower whose device process pushed a share rings the leader's
+doorbell, the leader posts an R2 gather and rings every follower's doorbell, and the followers enter the gather at
+once (a doorbell is a one-byte datagram on loopback; the store stays the source of truth, so a lost datagram costs
+one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
+pool accept for remote ranks' shares the same way as for its own.
 
 Rank loss (reference analogues: the partial-failure-tolerant detector
 internal/hal/registry.go:138-201 and the failover loop internal/engine/run.go:368-521): the leader declares a
@@ -23,8 +32,14 @@ or passes its deadline. It then posts a re-form: every survivor aborts the proce
 generation (store prefix otd-g<gen>) with the survivors, ranks renumbered, and the leader re-broadcasts the job
 with a ``variant_base`` past every cursor the ranks reported, so the dead rank's residue class is searched by
 the survivors from there on and nothing is searched twice. A replacement process (supervisor respawn) asks to
-join and is added by the next re-form. Rank 0 is the pool session: its loss ends the node (the supervisor
-restarts it). Over gloo (CPU hosts, tests) one limit remains: a rank blocked in a ring collective that the dead
+join and is added by the next re-form.
+
+Leader loss: rank 0 holds the pool session; when it dies the supervisor restarts it after a backoff. Meanwhile the
+followers keep hashing their last job (their collectives with the dead leader fail at their deadline and they wait
+for a re-form). The restarted leader resumes the op log after the last op its predecessor posted, forms the next
+generation from every follower that is still heartbeating, reconnects to the pool and broadcasts the new work. Its
+job epochs live in a namespace of their own (incarnation << 40), so a follower's share of the old leader's job can
+never be mapped onto a new job: it is dropped as stale. Over gloo (CPU hosts, tests) one limit remains: a rank blocked in a ring collective that the dead
 rank's neighbours abandoned gives up after its bounded deadline, but tearing that group down waits out gloo's own
 op timeout (OTEDAMA_PG_TIMEOUT), so that re-form can take that long; RCCL groups are aborted at once.
 
@@ -35,6 +50,8 @@ from __future__ import annotations
 import collections
 import json
 import os
+import select
+import socket
 import threading
 import time
 
@@ -42,12 +59,14 @@ from otedama_amd.engine.miners import GROUP, RESPLIT_GROUPS, MinerSet
 from otedama_amd.parallel.comm import SHARE_SLOTS, NodeComm
 from otedama_amd.utils.trace import span
 
-DEFAULT_TICK = 0.005       # leader control-loop period (store polls only; no device work)
+DEFAULT_TICK = 0.005       # reported control-loop granularity (the loop itself waits on its doorbell)
 HB_INTERVAL = 0.5          # heartbeat period
 HB_TIMEOUT = 2.0           # a follower whose heartbeat is older is dead
 LIVENESS_EVERY = 0.25      # leader liveness check period
 STATS_INTERVAL = 10.0      # R3 cadence (the reference's stats tick, internal/engine/run.go:377-380)
-OP_POLL_MAX = 0.004        # follower op-log poll interval ceiling
+BELL_FALLBACK = 0.05       # doorbell wait ceiling: a lost datagram delays an op or a gather by at most this
+PENDING_CAP = 8192         # shares a follower holds for the leader (drop-oldest past it, counted)
+EPOCH_SHIFT = 40           # leader incarnation i numbers its job epochs from (i - 1) << EPOCH_SHIFT
 PREFIX = "otd/"
 
 
@@ -64,14 +83,86 @@ def _store_get(store, key: str):
         return None
 
 
+def _clone(store):
+    return store.clone() if hasattr(store, "clone") else store
+
+
+class _Bell:
+    """A rank's doorbell: a loopback UDP socket whose port is published at otd/bell/<orig>. ``ring(r)`` sends one
+    byte to rank r (ports are looked up in the store and cached for a couple of seconds: a restarted rank has a new
+    one); ``wait(t)`` blocks until a datagram arrives or t passes and returns the bytes received."""
+
+    PORT_TTL = 2.0
+
+    def __init__(self, store, orig_rank: int):
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        self.sock.bind(("127.0.0.1", 0))
+        self.sock.setblocking(False)
+        self.port = self.sock.getsockname()[1]
+        self.orig = orig_rank
+        self.store = _clone(store) if store is not None else None
+        self._lock = threading.Lock()
+        self._ports: dict[int, tuple[int, float]] = {}
+        self.rings = 0
+        if self.store is not None:
+            self.store.set(_k("bell", orig_rank), str(self.port))
+
+    def _port_of(self, orig: int) -> int | None:
+        if orig == self.orig:
+            return self.port
+        now = time.monotonic()
+        with self._lock:
+            hit = self._ports.get(orig)
+            if hit is not None and now - hit[1] < self.PORT_TTL:
+                return hit[0]
+            raw = _store_get(self.store, _k("bell", orig)) if self.store is not None else None
+            if raw is None:
+                return hit[0] if hit else None
+            port = int(raw)
+            self._ports[orig] = (port, now)
+            return port
+
+    def ring(self, orig: int, kind: bytes = b"o") -> None:
+        port = self._port_of(orig)
+        if port is None:
+            return
+        try:
+            self.sock.sendto(kind, ("127.0.0.1", port))
+            self.rings += 1
+        except OSError:
+            pass  # the store stays authoritative: the peer's fallback poll picks the work up
+
+    def wait(self, timeout: float) -> bytes:
+        got = b""
+        try:
+            ready, _, _ = select.select([self.sock], [], [], max(timeout, 0.0))
+        except (OSError, ValueError):
+            return got
+        if ready:
+            while True:
+                try:
+                    got += self.sock.recv(64)
+                except (BlockingIOError, OSError):
+                    break
+        return got
+
+    def close(self) -> None:
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
 class _Heartbeat:
     """Publishes this rank's liveness and cursor every HB_INTERVAL on a store connection of its own (the rank's
     op loop may sit in a bounded collective meanwhile)."""
 
-    def __init__(self, store, orig_rank: int, local: MinerSet):
-        self.store = store.clone() if hasattr(store, "clone") else store
+    def __init__(self, store, orig_rank: int, local: MinerSet, comm: NodeComm | None = None):
+        self.store = _clone(store)
         self.orig = orig_rank
         self.local = local
+        self.comm = comm
+        self.extra: dict = {}  # owner-supplied fields (e.g. pending shares)
         self.stop = threading.Event()
         self.th = threading.Thread(target=self._loop, name=f"otedama-hb-{orig_rank}", daemon=True)
 
@@ -85,7 +176,9 @@ class _Heartbeat:
                 "dropped": sum(s["dropped"] for s in st), "faulted": sum(1 for s in st if s["faulted"]),
                 # device-timeline completion time of the counted hashes (one GPU per rank): exact rate windows
                 "done": st[0].get("hashes_done_at_s", 0.0) if len(st) == 1 else 0.0,
-                "pid": os.getpid()}
+                "coll": self.comm.collectives if self.comm is not None else 0,
+                "gen": self.comm.info.generation if self.comm is not None else 0,
+                "pid": os.getpid(), **self.extra}
 
     def _loop(self):
         while not self.stop.is_set():
@@ -173,7 +266,9 @@ class NodeMinerSet:
         self.algorithm = local.algorithm
         self.store = comm.info.store
         self._lock = threading.Lock()
-        self._wake = threading.Event()
+        self._bell = _Bell(self.store, comm.info.orig_rank) if self.store is not None else None
+        self._wake = threading.Event()  # stores without doorbells (single-rank tests)
+        self._gather_wanted = False
         self._seq = 0
         self._sent_seq = 0
         self._stop = False
@@ -189,7 +284,14 @@ class NodeMinerSet:
         self._op_k = 0
         self._gen = comm.info.generation
         self._gen_started = time.monotonic()
-        self.capacity = comm.info.world_size       # orig ranks 0..capacity-1 may exist
+        self.capacity = max(comm.info.capacity, comm.info.world_size, 1)  # orig ranks 0..capacity-1 may exist
+        # A leader that the supervisor restarted joins the store without a process group (generation -1): it takes
+        # the op log over and forms the next generation with the live followers before anything else.
+        self.takeover = comm.info.generation < 0
+        self.incarnation = int(self.store.add(_k("leader_inc"), 1)) if self.store is not None else 1
+        self._epoch = (self.incarnation - 1) << EPOCH_SHIFT
+        local._epoch = max(local._epoch, self._epoch)
+        self.remote_stale = 0  # remote shares of a job the leader no longer knows (e.g. a previous incarnation's)
         self._rows_by_orig: dict[int, list[int]] = {}
         self.row_times: dict[int, float] = {}  # wall time at which each remote rank's counter row was produced
         self.row_done_at: dict[int, float] = {}  # device-timeline time its counted hashes had completed
@@ -203,7 +305,7 @@ class NodeMinerSet:
         self._remote_faults: dict[int, int] = {}
         self._remote_idle: dict[int, int] = {}
         self.lost_ranks: list[int] = []
-        self._hb = _Heartbeat(self.store, comm.info.orig_rank, local) if self.store is not None else None
+        self._hb = _Heartbeat(self.store, comm.info.orig_rank, local, comm) if self.store is not None else None
 
     # MinerSet API ------------------------------------------------------------
     @property
@@ -211,7 +313,7 @@ class NodeMinerSet:
         return [f"rank{r}" for r in range(1, self.capacity)]
 
     def __len__(self) -> int:
-        return len(self.local) * self.comm.info.world_size
+        return len(self.local) * max(self.comm.info.world_size, 1)
 
     @property
     def miners(self):
@@ -225,21 +327,30 @@ class NodeMinerSet:
         self.local.start()
         if self._hb is not None:
             self._hb.start()
-        if self.store is not None:
+        if self.store is not None and not self.takeover:
             self.store.set(_k("next"), "0")
+            self.store.set(_k("gen"), str(self._gen))
         self._thread = threading.Thread(target=self._loop, name="otedama-node-r0", daemon=True)
         self._thread.start()
 
     def stop(self) -> None:
         with self._lock:
             self._stop = True
-        self._wake.set()
+        self._poke()
         if self._thread is not None:
             self._thread.join(timeout=30)
             self._thread = None
         if self._hb is not None:
             self._hb.stop.set()
         self.local.stop()
+        if self._bell is not None:
+            self._bell.close()
+
+    def _poke(self) -> None:
+        """Wake the leader loop (a new job, a pause, stop)."""
+        self._wake.set()
+        if self._bell is not None:
+            self._bell.ring(self._bell.orig, b"w")
 
     def set_job(self, template: dict | None) -> int:
         with self._lock:
@@ -262,7 +373,7 @@ class NodeMinerSet:
                 for old in [e for e in self._jobs if e < ep - 64]:
                     del self._jobs[old]
             self._publish()
-        self._wake.set()
+        self._poke()
         return ep
 
     def _with_base(self, template: dict | None) -> dict | None:
@@ -290,7 +401,7 @@ class NodeMinerSet:
                 else:
                     self._paused.discard(device_id)
                 self._publish()
-            self._wake.set()
+            self._poke()
             return True
         return False
 
@@ -394,6 +505,11 @@ class NodeMinerSet:
         self.store.set(_k("op", self._op_k), json.dumps(op))
         self._op_k += 1
         self.store.set(_k("next"), str(self._op_k))
+        if self._bell is not None:  # the followers' op loops wait on their doorbells
+            targets = op["members"] if op.get("op") == "reform" else self.comm.info.members
+            for r in targets:
+                if r != self.comm.info.orig_rank:
+                    self._bell.ring(r)
 
     def _heartbeats(self) -> dict[int, dict]:
         keys = [_k("hb", r) for r in range(1, self.capacity)]
@@ -435,10 +551,11 @@ class NodeMinerSet:
                 joiners.append(r)
         return dead, joiners
 
-    def _reform(self, dead: list[int], joiners: list[int], why: str) -> None:
+    def _reform(self, dead: list[int], joiners: list[int], why: str, members: list[int] | None = None) -> None:
         info = self.comm.info
         old_world = info.world_size
-        members = [r for r in info.members if r not in dead] + sorted(joiners)
+        if members is None:
+            members = [r for r in info.members if r not in dead] + sorted(joiners)
         members = [0] + sorted(r for r in members if r != 0)
         # every cursor of the current work: the survivors' heartbeats and this rank's own devices
         hw = self.local.high_water()
@@ -450,6 +567,7 @@ class NodeMinerSet:
         self._gen += 1
         self._gen_started = time.monotonic()
         with span("otd.node.reform"):
+            self.store.set(_k("gen"), str(self._gen))
             self._post({"op": "reform", "gen": self._gen, "members": members})
             self.link.run_op({"op": "reform", "members": members, "gen": self._gen}, None, [])
         for r in dead:
@@ -478,13 +596,47 @@ class NodeMinerSet:
         self.log("warn", f"node: {why}; generation {self._gen}: ranks {members} (world {len(members)}), "
                          f"variants re-split from {base}")
 
-    def _try_reform(self, dead: list[int], joiners: list[int], why: str) -> None:
+    def _try_reform(self, dead: list[int], joiners: list[int], why: str, members: list[int] | None = None) -> None:
         try:
-            self._reform(dead, joiners, why)
+            self._reform(dead, joiners, why, members)
         except Exception as exc:  # noqa: BLE001 - e.g. a member died during the re-form: the next check retries
             self.log("error", f"node: re-form failed ({type(exc).__name__}: {exc}); retrying")
             self.comm.abort()
         self._sent_seq = -1  # (re-)broadcast the job on the new generation
+
+    def _take_over(self) -> None:
+        """A restarted leader: continue the op log after the last op the previous leader posted (it may have died
+        between posting an op and bumping otd/next), and form the next generation from every follower whose
+        heartbeat is fresh. Followers keep hashing their last job until the new job arrives."""
+        store = self.store
+        k = int(_store_get(store, _k("next")) or 0)
+        while store.check([_k("op", k)]):
+            k += 1
+        self._op_k = k
+        self._gen = int(_store_get(store, _k("gen")) or 0)
+        try:
+            store.delete_key(_k("dead", 0))
+        except Exception:  # noqa: BLE001
+            pass
+        # followers heartbeat every HB_INTERVAL: give one a full timeout to show up after this process's start-up
+        end = time.monotonic() + self.hb_timeout
+        live: list[int] = []
+        while True:
+            now = time.time()
+            live = sorted(r for r, hb in self._heartbeats().items()
+                          if now - hb["t"] <= self.hb_timeout and _store_get(store, _k("dead", r)) is None)
+            if len(live) >= self.capacity - 1 or time.monotonic() >= end:
+                break
+            time.sleep(0.1)
+        for r in live:
+            try:
+                store.delete_key(_k("join", r))
+            except Exception:  # noqa: BLE001
+                pass
+        self.lost_ranks = [r for r in range(1, self.capacity) if r not in live]
+        self._try_reform([], [], f"leader restarted (incarnation {self.incarnation}); followers {live}",
+                         members=[0] + live)
+        self.takeover = False
 
     def _loop(self) -> None:
         info = self.comm.info
@@ -494,6 +646,8 @@ class NodeMinerSet:
             torch.cuda.set_device(info.device)
         next_live = next_stats = time.monotonic()
         try:
+            if self.takeover and self.store is not None:
+                self._take_over()
             while True:
                 with self._lock:
                     stop = self._stop
@@ -515,7 +669,8 @@ class NodeMinerSet:
                         self._post({"op": "job"})
                         self.link.run_op({"op": "job"}, blob, [])
                         self._sent_seq = seq
-                    if info.world_size > 1 and int(self.store.add(_k("pending"), 0)) > 0:
+                    if info.world_size > 1 and self._gather_wanted:
+                        self._gather_wanted = False
                         self._post({"op": "gather"})
                         _, shares = self.link.run_op({"op": "gather"}, None, [])
                         self._take(shares or [])
@@ -543,26 +698,40 @@ class NodeMinerSet:
                         dead, joiners = self._dead_and_joiners()
                     self._try_reform(dead, joiners, "collective failure" + (f", ranks {dead} lost" if dead else ""))
                     continue
-                self._wake.wait(self.tick)
-                self._wake.clear()
+                self._wait(min(next_live, next_stats) - time.monotonic())
         except BaseException as exc:  # noqa: BLE001
             self.link.error = exc
             self.log("error", f"node: control loop failed: {exc}")
+
+    def _wait(self, timeout: float) -> None:
+        """Sleep until a doorbell (a follower's shares, a local job / pause / stop) or ``timeout``."""
+        timeout = min(max(timeout, 0.0), LIVENESS_EVERY)
+        if self._bell is None:
+            self._wake.wait(min(timeout, self.tick))
+            self._wake.clear()
+            return
+        got = self._bell.wait(timeout)
+        self._wake.clear()
+        if b"s" in got:
+            self._gather_wanted = True
 
     def _take(self, shares: list[dict]) -> None:
         n = 0
         for s in shares:
             if s["orig_rank"] == self.comm.info.orig_rank:
                 continue
-            n += 1
             meta = self._jobs.get(s["epoch"])
             if meta is None:
-                continue  # job older than the retained window: stale
+                self.remote_stale += 1  # a job older than the retained window, or a previous leader's
+                continue
             s.update(meta)
             s["device_id"] = f"rank{s['orig_rank']}"
             self._remote.append(s)
+            n += 1
+        per_rank = collections.Counter(s["orig_rank"] for s in shares)
+        if per_rank and max(per_rank.values()) >= SHARE_SLOTS:
+            self._gather_wanted = True  # a rank filled its slot array: it may hold more
         if n:
-            self.store.add(_k("pending"), -n)
             os.eventfd_write(self._remote_efd, 1)
 
 
@@ -578,21 +747,22 @@ class NodeWorker:
         self.rank_id = f"rank{comm.info.orig_rank}"
         self.store = comm.info.store
         self.joining = joining
-        self._hb = _Heartbeat(self.store, comm.info.orig_rank, local)
+        self._hb = _Heartbeat(self.store, comm.info.orig_rank, local, comm)
+        self._bell = _Bell(self.store, comm.info.orig_rank)
         self._pending: list[dict] = []
+        self.pending_dropped = 0  # shares dropped past PENDING_CAP (a leader that stays away)
         self._plock = threading.Lock()
         self._stop = threading.Event()
 
     def _share_loop(self) -> None:
-        """Wake on the local miners' share eventfds and announce new shares to the leader at once (otd/pending);
-        they travel with the next R2 gather the leader posts."""
-        import select
-
-        store = self.store.clone() if hasattr(self.store, "clone") else self.store
+        """Wake on the local miners' share eventfds and ring the leader's doorbell at once; the shares travel with
+        the R2 gather the leader posts in response. While shares are still waiting (a lost datagram, a leader that
+        is being restarted, more than one gather's worth) the bell is rung again every BELL_FALLBACK."""
         fds = list(self.local.share_fds())
+        last_ring = 0.0
         while not self._stop.is_set():
             if fds:
-                ready, _, _ = select.select(fds, [], [], 0.25)
+                ready, _, _ = select.select(fds, [], [], BELL_FALLBACK)
                 for fd in ready:
                     try:
                         os.read(fd, 8)
@@ -601,13 +771,19 @@ class NodeWorker:
             else:
                 self._stop.wait(0.01)
             new = self.local.poll(256)
-            if new:
-                with self._plock:
+            with self._plock:
+                if new:
                     self._pending.extend(new)
-                try:
-                    store.add(_k("pending"), len(new))
-                except Exception:  # noqa: BLE001 - store gone: shutting down
-                    return
+                    over = len(self._pending) - PENDING_CAP
+                    if over > 0:
+                        del self._pending[:over]
+                        self.pending_dropped += over
+                waiting = len(self._pending)
+            self._hb.extra["pending"] = waiting
+            now = time.monotonic()
+            if new or (waiting and now - last_ring >= BELL_FALLBACK):
+                self._bell.ring(0, b"s")
+                last_ring = now
 
     def run(self) -> None:
         self.local.start()
@@ -622,16 +798,13 @@ class NodeWorker:
             self.store.set(_k("join", info.orig_rank), "1")
         broken = False  # the current group failed a collective: skip collectives until the next re-form
         try:
-            idle = 0.0
             while True:
                 key = _k("op", k)
-                # poll, backing off from 0.5 ms to OP_POLL_MAX while the log is quiet (store.wait would log a c10d
-                # warning on every timeout); an op is picked up within OP_POLL_MAX
+                # the leader rings this rank's doorbell after posting an op; the store check is the truth, the
+                # fallback wait bounds a lost datagram
                 if not self.store.check([key]):
-                    idle = min(OP_POLL_MAX, idle * 2 if idle else 0.0005)
-                    time.sleep(idle)
+                    self._bell.wait(BELL_FALLBACK)
                     continue
-                idle = 0.0
                 op = json.loads(self.store.get(key))
                 k += 1
                 kind = op["op"]
@@ -667,6 +840,10 @@ class NodeWorker:
                             with self._plock:  # not delivered: keep them for the next gather
                                 self._pending[:0] = out
                             raise
+                        with self._plock:
+                            more = bool(self._pending)
+                        if more:
+                            self._bell.ring(0, b"s")
                     elif kind == "stats":
                         self.link.run_op(op, None, [])
                         self.local.retire_faulted()  # survivors re-split this rank's class at once
@@ -679,6 +856,7 @@ class NodeWorker:
             self._hb.stop.set()
             share_th.join(timeout=5)
             self.local.stop()
+            self._bell.close()
 
     def _apply(self, blob: dict) -> None:
         job = blob.get("job")
