@@ -345,15 +345,15 @@ void CpuMiner::stop() {
 }
 
 void CpuMiner::loop(int /*tid*/) {
-  constexpr uint64_t kChunk = 1ull << 16;
   while (running_.load()) {
     uint64_t gen = 0;
     auto job = current_job(&gen);
     if (!job) continue;
-    if (job->algo != Algo::kSha256d) {  // CPU scrypt mining is not a supported config
-      std::this_thread::sleep_for(std::chrono::milliseconds(10));
-      continue;
-    }
+    // SHA-256d: 64Ki-nonce chunks through the SHA-NI scanner. scrypt / X11 (CPU hosts, rehearsals): 256-nonce chunks
+    // hashed one by one with the host reference functions (verify_share), ~1000x slower per nonce. A work
+    // generation has one algorithm, so one chunk size per cursor generation.
+    const bool sha = job->algo == Algo::kSha256d;
+    const uint64_t kChunk = sha ? (1ull << 16) : 256;
     uint64_t claim;
 #ifdef OTEDAMA_STRESS_HOOKS
     // tools/sanitize: widen the snapshot -> claim window so job switches land inside it.
@@ -384,7 +384,16 @@ void CpuMiner::loop(int /*tid*/) {
     uint64_t en2;
     job->variant_header(v, hdr, &ver, &nt, &en2);
     const auto t0 = std::chrono::steady_clock::now();
-    auto hits = cpu_scan_sha256d(hdr, job->target, nonce0, kChunk);
+    std::vector<uint32_t> hits;
+    if (sha) {
+      hits = cpu_scan_sha256d(hdr, job->target, nonce0, kChunk);
+    } else {
+      uint8_t h[32];
+      for (uint64_t i = 0; i < kChunk && running_.load(); ++i) {
+        store_le32(hdr + 76, nonce0 + uint32_t(i));
+        if (verify_share(job->algo, hdr, job->target, h)) hits.push_back(nonce0 + uint32_t(i));
+      }
+    }
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t n : hits) {
       ShareRecord s{};
@@ -393,7 +402,8 @@ void CpuMiner::loop(int /*tid*/) {
       s.extranonce2_size = job->extranonce2_size; s.device_id = device_id_;
       s.found_at = monotonic_seconds();
       store_le32(hdr + 76, n);
-      sha256d(hdr, 80, s.hash);
+      if (sha) sha256d(hdr, 80, s.hash);
+      else verify_share(job->algo, hdr, job->target, s.hash);
       queue_.push(std::move(s));
     }
     std::lock_guard<std::mutex> g(stats_mu_);

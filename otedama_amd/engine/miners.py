@@ -115,8 +115,8 @@ class MinerSet:
                 m = N.GpuMiner(d.index, d.identity().id, batch_nonces=batch_nonces, grid=sha256d_grid(cus), queue_cap=queue_cap,
                                sha_variants=sha_variants)
             self.miners.append(DeviceMiner(d, m))
-        cpus = [d for d in devices if d.identity().family == Family.CPU]
-        if cpus and algorithm == "sha256d" and (cpu_threads > 0 or not gpus):
+        cpus = [d for d in devices if d.identity().family == Family.CPU and d.capabilities().supports(algorithm)]
+        if cpus and (cpu_threads > 0 or not gpus):
             if isolation == "process":
                 # one process per CPU device (production has one, cpu-0; tests model several devices this way)
                 from otedama_amd.engine.devproc import DeviceProcess

@@ -111,8 +111,10 @@ class CPUDriver:
 
     def enumerate(self) -> list:
         model = _cpu_model()
+        # SHA-256d through the SHA-NI scanner; scrypt / X11 through the host reference chains (slow, CPU-only hosts)
         return [SimpleDevice(Identity("cpu-0", Family.CPU, _cpu_vendor(), model),
-                             Capabilities(sha256d=True, general_compute=True), threads=self.threads)]
+                             Capabilities(sha256d=True, general_compute=True, scrypt=True, x11=True),
+                             threads=self.threads)]
 
 
 # ISA -> kernels compiled into the native extension (csrc/kernels)

@@ -177,6 +177,38 @@ def test_cpu_miner_runtime_emits_verified_shares():
         assert s["epoch"] == 7 and s["job_id"] == "abc" and s["device_id"] == "cpu-0"
 
 
+@pytest.mark.parametrize("algo", ["scrypt", "x11"])
+def test_cpu_miner_scrypt_and_x11_emit_verified_shares(algo):
+    """CPU-only hosts mine scrypt / X11 through the host reference chains (256-nonce chunks): every share is
+    re-hashed here (hashlib.scrypt / the native X11 oracle) and meets the target; stripes stay disjoint."""
+    m = N.CpuMiner(2, "cpu-0")
+    tgt_int = (1 << 251) - 1  # ~1 share per 32 hashes
+    m.set_job(_job(target=int_to_hash(tgt_int), version_mask=0x1FFFE000, epoch=3, job_id="s", algo=algo))
+    m.start()
+    deadline = time.time() + 20
+    shares = []
+    while time.time() < deadline and len(shares) < 6:
+        shares += m.poll(64)
+        time.sleep(0.05)
+    m.stop()
+    shares += m.poll(4096)
+    st = m.stats()
+    assert st["hashes"] > 0 and shares, st
+    seen = set()
+    for s in shares[:40]:
+        hdr = bytearray(GEN)
+        struct.pack_into("<I", hdr, 0, s["version"])
+        struct.pack_into("<I", hdr, 76, s["nonce"])
+        if algo == "scrypt":
+            h = hashlib.scrypt(bytes(hdr), salt=bytes(hdr), n=1024, r=1, p=1, dklen=32)
+        else:
+            h = N.x11(bytes(hdr))
+        assert h == s["hash"] and int.from_bytes(h, "little") <= tgt_int
+        key = (s["version"], s["nonce"])
+        assert key not in seen
+        seen.add(key)
+
+
 def test_cpu_miner_pause_with_none_job():
     m = N.CpuMiner(1, "cpu-0")
     m.start()

@@ -329,7 +329,8 @@ def test_hal_capabilities_match_kernels():
     from otedama_amd.models import algorithms
 
     cpu = hal.CPUDriver(2).enumerate()[0]
-    assert cpu.capabilities().sha256d and not cpu.capabilities().scrypt  # CpuMiner is SHA-256d only
+    # CpuMiner: SHA-256d through SHA-NI, scrypt / X11 through the host reference chains
+    assert cpu.capabilities().sha256d and cpu.capabilities().scrypt and cpu.capabilities().x11
     gfx950 = hal.KERNEL_ISAS["gfx950"]
     assert gfx950.sha256d and gfx950.scrypt and gfx950.x11
     assert set(algorithms.ALGORITHMS) == {"sha256d", "scrypt", "x11"}
