@@ -92,6 +92,15 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=1,
                     help="synthetic header seed: the hit count of a seed is one Poisson draw, repeated on every run")
     ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--node-seconds", type=float, default=-1.0,
+                    help="production node section (otedama node --gpus N + local pool): recorded seconds "
+                         "(-1 = 10 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+    ap.add_argument("--node-warmup", type=float, default=3.0)
+    ap.add_argument("--pool-seconds", type=float, default=-1.0,
+                    help="BASELINE config 5 (mixed SHA-256d + scrypt pool, vardiff on): recorded seconds "
+                         "(-1 = 12 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0,
+                    help="BASELINE config 1 (native CPU miner, single thread and all cores): seconds each (0 = skip)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="gloo + native CPU scanner instead of the GPU kernels (launcher / collective tests)")
     ap.add_argument("--cpu-nonces", type=int, default=1 << 12, help="rehearsal: nonces per variant per step")
@@ -496,6 +505,16 @@ def run_rank(args) -> int:
         del xs
         torch.cuda.empty_cache()
 
+    # ------------------------------------------------------------ BASELINE config 1: the CPU miner
+    cpu_cfg = None
+    if args.cpu_seconds > 0 and info.is_primary:
+        from otedama_amd.cli.bench_cmd import bench_cpu, cpu_share
+
+        try:
+            cpu_cfg = bench_cpu(args.cpu_seconds, cpu_share(), single_seconds=args.cpu_seconds)
+        except Exception as exc:  # noqa: BLE001 - auxiliary: never fail the headline
+            cpu_cfg = {"error": f"{type(exc).__name__}: {exc}"}
+
     # ---------------------------------------------------------- share latency
     # End-to-end share latency against the local pool in a separate process (default 2^29-nonce batches), then the
     # job-switch time of the native miner for SHA-256d, scrypt and X11 (set_job -> first batch of the new work running).
@@ -519,6 +538,28 @@ def run_rank(args) -> int:
             startup = measure_device_startup(device_index=dev.index or 0)
         except Exception as exc:  # noqa: BLE001
             startup = {"error": f"{type(exc).__name__}: {exc}"}
+
+    # ------------------------------------------------ the production node, and BASELINE config 5
+    # Both run after every other rank has finished its kernel sections (they exit after X11): `otedama node --gpus N`
+    # starts its own N ranks (RCCL) with a device process per GPU, and the pool section its own miners.
+    node_res = pool_res = None
+    node_s = args.node_seconds if args.node_seconds >= 0 else (0.0 if cpu else 10.0)
+    pool_s = args.pool_seconds if args.pool_seconds >= 0 else (0.0 if cpu else 12.0)
+    if info.is_primary and node_s > 0:
+        from otedama_amd.parallel.node_probe import measure_node
+
+        try:
+            node_res = measure_node(world, seconds=node_s, warmup=args.node_warmup, cpu=cpu,
+                                    expected_per_gpu=8e6 if cpu else 19e9, shares_per_gpu=4.0 if cpu else 25.0)
+        except Exception as exc:  # noqa: BLE001
+            node_res = {"error": f"{type(exc).__name__}: {exc}"}
+    if info.is_primary and pool_s > 0:
+        from otedama_amd.pool.pool_probe import measure_pool
+
+        try:
+            pool_res = measure_pool(world, seconds=pool_s, cpu=cpu, difficulty=0.001 if cpu else 1.0)
+        except Exception as exc:  # noqa: BLE001
+            pool_res = {"error": f"{type(exc).__name__}: {exc}"}
 
     if info.is_primary:
         out = {
@@ -582,6 +623,15 @@ def run_rank(args) -> int:
             "job_switch": switch or None,
             "device_process_startup_s": (startup or {}).get("spawn_to_first_batch_s"),
             "device_process_startup": startup,
+            # the production node (otedama node: supervisor + N RCCL ranks + device processes + local pool)
+            "node_hashes_per_sec": (node_res or {}).get("total_hashes_per_sec"),
+            "node": node_res,
+            # BASELINE config 1 (reference: ~2.5 MH/s single thread, ~75 MH/s whole 7950X; BENCHMARKS.md:25-28,44-49)
+            "cpu_single_thread_hashes_per_sec": (cpu_cfg or {}).get("sha256d_single_thread_hps"),
+            "cpu_all_cores_hashes_per_sec": (cpu_cfg or {}).get("sha256d_all_threads_hps"),
+            "cpu": cpu_cfg,
+            # BASELINE config 5: mixed SHA-256d + scrypt pool with vardiff
+            "pool": pool_res,
         }
         print(json.dumps(out), flush=True)
     shutdown(info)

@@ -17,17 +17,35 @@ from otedama_amd.cli.flags import FlagSet
 from otedama_amd.cli.main import EXIT_OK, EXIT_RUNTIME, parse_subcommand
 
 
-def bench_cpu(seconds: float = 2.0, threads: int = 0) -> dict:
+def cpu_share() -> int:
+    """CPUs this process may use: its affinity mask, capped by OMP_NUM_THREADS when set (a GPU box exposes the
+    whole machine in os.cpu_count() but gives a job a share of it)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else max(1, n)
+
+
+def bench_cpu(seconds: float = 2.0, threads: int = 0, single_seconds: float = 0.0) -> dict:
+    """BASELINE config 1 on this host: the SHA-NI scanner on one thread over a synthetic 80-byte header, then the
+    production CpuMiner on ``threads`` threads (BENCHMARKS.md:25-28 single thread, :44-49 whole CPU)."""
     from otedama_amd.models.header import GENESIS_HEADER_HEX
     from otedama_amd.ops.native import require_native
 
     N = require_native()
     hdr = bytes.fromhex(GENESIS_HEADER_HEX)
-    # single thread: fixed nonce range, timed
-    n = 1 << 21
+    # single thread: 2^20-nonce scans until single_seconds (at least one), timed
+    n, done = 1 << 21, 0
     t0 = time.perf_counter()
-    N.cpu_scan_sha256d(hdr, bytes(32), 0, n)
-    single = n / (time.perf_counter() - t0)
+    while True:
+        N.cpu_scan_sha256d(hdr, bytes(32), done & 0xFFFFFFFF, n)
+        done += n
+        if time.perf_counter() - t0 >= single_seconds:
+            break
+    single_s = time.perf_counter() - t0
+    single = done / single_s
     threads = threads or (os.cpu_count() or 1)
     m = N.CpuMiner(threads, "cpu-0")
     m.set_job({"header": hdr, "target": bytes(32), "version_mask": 0x1FFFE000})
@@ -39,7 +57,10 @@ def bench_cpu(seconds: float = 2.0, threads: int = 0) -> dict:
     m.stop()
     allc = (h1 - h0) / (t1 - t0)
     return {"sha256d_single_thread_hps": single, "sha256d_all_threads_hps": allc, "threads": threads,
-            "scaling": allc / (single * threads), "sha_ni": bool(N.cpu_has_sha_ni())}
+            "scaling": allc / (single * threads), "sha_ni": bool(N.cpu_has_sha_ni()),
+            "single_thread_seconds": round(single_s, 3), "single_thread_nonces": done,
+            "all_threads_seconds": seconds, "header": "synthetic 80-byte header (Bitcoin genesis)",
+            "reference": "~2.5 MH/s / ~75 MH/s on a Ryzen 9 7950X (BENCHMARKS.md:25,46)"}
 
 
 def bench_gpu(device: int = 0, reps: int = 3, scrypt_batches: int = 4) -> dict:

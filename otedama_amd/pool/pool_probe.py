@@ -1,0 +1,177 @@
+"""BASELINE config 5, measured: the full Stratum pool with mixed SHA-256d + scrypt workers (bench.py ``pool``).
+
+``otedama pool --algorithms sha256d,scrypt`` (one process, one SV2 listener, vardiff state, journal and validator per
+algorithm) serves production miners: one ``otedama run`` per (GPU, algorithm) stream, each with its GPU's miner in a
+device process. At one GPU both streams share GPU 0 (a SHA-256d and a scrypt device process); at N GPUs the first
+ceil(N/2) GPUs mine SHA-256d and the rest scrypt. Vardiff is ON and every connection starts at the same initial
+difficulty, so the record shows the pool converging each worker to its own rate. Reported per algorithm, over the
+recorded window: validated shares/s (every accepted share was re-hashed by the pool: SHA-256d inline, scrypt on the
+pool's native hash workers), rejects by reason, the pool's validation time (submit received -> verdict) quantiles,
+each worker's difficulty in force / retarget count / time from channel open to its last retarget, and the miners'
+device-timeline hashrates.
+
+[NO REFERENCE CODE]: v3 removed the pool; BASELINE.json names this config without a number.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import signal
+import subprocess
+import sys
+import tempfile
+import time
+import urllib.request
+
+from otedama_amd.engine.latency_probe import PROBE_ADDR, ROOT
+from otedama_amd.parallel.launch import free_port
+from otedama_amd.parallel.node_probe import _DROP_ENV, _read, window_rates
+
+
+def spawn_mixed_pool(algorithms: list[str], difficulty: float, share_seconds: float, retarget_seconds: float,
+                     http: str, timeout: float = 120.0) -> tuple[subprocess.Popen, dict[str, str]]:
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "otedama_amd", "pool", "--algorithms", ",".join(algorithms),
+           "--listen-sv2", "127.0.0.1:0", "--listen-v1=", "--difficulty", repr(difficulty),
+           "--share-seconds", repr(share_seconds), "--retarget-seconds", repr(retarget_seconds),
+           "--job-interval", "3600", "--block-interval", "3600", "--payout-address", PROBE_ADDR, "--http-addr", http]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, cwd=ROOT)
+    addrs: dict[str, str] = {}
+    deadline = time.monotonic() + timeout
+    seen = []
+    while time.monotonic() < deadline and len(addrs) < len(algorithms):
+        line = proc.stdout.readline()
+        if not line:
+            break
+        seen.append(line)
+        if "listening sv2=" in line and "pool[" in line:
+            algo = line.split("pool[", 1)[1].split("]", 1)[0]
+            addrs[algo] = line.split("listening sv2=", 1)[1].split()[0]
+    if len(addrs) < len(algorithms):
+        proc.kill()
+        raise RuntimeError("pool process did not start: " + "".join(seen[-5:]))
+    return proc, addrs
+
+
+def stop_pool_all(proc: subprocess.Popen) -> list[dict]:
+    """SIGTERM the pool; it prints one JSON stats line per algorithm on the way out."""
+    proc.send_signal(signal.SIGTERM)
+    try:
+        out, _ = proc.communicate(timeout=30)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        out, _ = proc.communicate()
+    res = []
+    for line in (out or "").splitlines():
+        if line.startswith("{"):
+            try:
+                res.append(json.loads(line))
+            except ValueError:
+                pass
+    return res
+
+
+def _pool_api(http: str) -> list[dict]:
+    with urllib.request.urlopen(f"http://{http}/api/v1/pool", timeout=5) as r:
+        return json.loads(r.read())
+
+
+def layout(gpus: int) -> list[tuple[int, str]]:
+    """(GPU, algorithm) streams: both algorithms on GPU 0 at one GPU, else the first ceil(N/2) GPUs SHA-256d."""
+    if gpus <= 1:
+        return [(0, "sha256d"), (0, "scrypt")]
+    half = math.ceil(gpus / 2)
+    return [(i, "sha256d" if i < half else "scrypt") for i in range(gpus)]
+
+
+def measure_pool(gpus: int = 1, seconds: float = 12.0, warmup: float = 2.0, share_seconds: float = 1.0,
+                 retarget_seconds: float = 4.0, difficulty: float = 1.0, cpu: bool = False,
+                 startup_timeout: float = 180.0) -> dict:
+    streams = layout(gpus)
+    algos = sorted({a for _, a in streams}, key=["sha256d", "scrypt"].index)
+    http = f"127.0.0.1:{free_port()}"
+    pool, addrs = spawn_mixed_pool(algos, difficulty, share_seconds, retarget_seconds, http)
+    tmp = tempfile.mkdtemp(prefix="otedama-pool-")
+    env = {k: v for k, v in os.environ.items() if k not in _DROP_ENV}
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    if cpu:
+        env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    miners = []
+    try:
+        for gpu, algo in streams:
+            name = f"{'cpu' if cpu else 'gpu'}{gpu}-{algo}"
+            cfg = os.path.join(tmp, f"{name}.yaml")
+            with open(cfg, "w") as f:
+                f.write(f"bitcoin_address: {PROBE_ADDR}\npools:\n  - url: stratum+v2://{addrs[algo]}\n"
+                        f"workers:\n  name: {name}\nmining:\n  algorithm: {algo}\n"
+                        + ("  cpu_threads: 1\n  gpus: none\n" if cpu else f"  gpus: '{gpu}'\n"))
+            rep = os.path.join(tmp, f"{name}.json")
+            log = open(os.path.join(tmp, f"{name}.log"), "w")
+            p = subprocess.Popen([sys.executable, "-m", "otedama_amd", "run", "--config", cfg, "--no-tui"],
+                                 env=dict(env, OTEDAMA_NODE_REPORT=rep), cwd=ROOT, stdout=log,
+                                 stderr=subprocess.STDOUT)
+            miners.append({"name": name, "gpu": gpu, "algorithm": algo, "proc": p, "report": rep, "logf": log})
+        end = time.monotonic() + startup_timeout
+        while time.monotonic() < end:
+            reps = [_read(m["report"]) for m in miners]
+            if all(r.get("accepted", 0) > 0 for r in reps):
+                break
+            dead = [m["name"] for m in miners if m["proc"].poll() is not None]
+            if dead:
+                raise RuntimeError(f"miner(s) exited: {dead}")
+            time.sleep(0.25)
+        else:
+            raise RuntimeError(f"miners not accepted within {startup_timeout:.0f} s")
+        time.sleep(warmup)
+        a0, t0 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
+        time.sleep(seconds)
+        a1, t1 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
+        time.sleep(0.6)
+        reps = {m["name"]: _read(m["report"]) for m in miners}
+    finally:
+        for m in miners:
+            if m["proc"].poll() is None:
+                m["proc"].send_signal(signal.SIGTERM)
+        for m in miners:
+            try:
+                m["exit_code"] = m["proc"].wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                m["proc"].kill()
+                m["exit_code"] = m["proc"].wait()
+            m["logf"].close()
+        final = {s["algorithm"]: s for s in stop_pool_all(pool)}
+    dt = t1 - t0
+    out: dict = {}
+    for algo in algos:
+        s0, s1, fin = a0.get(algo, {}), a1.get(algo, {}), final.get(algo, {})
+        acc = s1.get("accepted", 0) - s0.get("accepted", 0)
+        rej = s1.get("rejected", 0) - s0.get("rejected", 0)
+        ms = [m for m in miners if m["algorithm"] == algo]
+        rates = {}
+        for m in ms:
+            r = window_rates(reps[m["name"]].get("samples", []), t0, t1 + 0.75)
+            rates[m["name"]] = sum(r.values())
+        workers = []
+        for w in s1.get("workers", []):
+            got = sum(1 for v in s1.get("workers", []) if v["name"] == w["name"])
+            prev = next((v for v in s0.get("workers", []) if v["name"] == w["name"]), {})
+            n = w["accepted"] - prev.get("accepted", 0)
+            workers.append({"name": w["name"], "difficulty": w["difficulty"], "retargets": w["retargets"],
+                            "settled_after_s": w["settled_after_s"], "connections": got,
+                            "share_interval_s": dt / n if n else None})
+        out[algo] = {
+            "validated_shares_per_sec": acc / dt, "accepted": acc, "rejected": rej,
+            "reject_reasons": fin.get("reject_reasons", {}), "accepted_total": fin.get("accepted"),
+            "rejected_total": fin.get("rejected"), "validate_ms": fin.get("validate_ms"),
+            "target_share_seconds": share_seconds, "workers": workers,
+            "miner_hashes_per_sec": rates, "miners": [{"name": m["name"], "gpu": m["gpu"], "exit_code": m["exit_code"]}
+                                                      for m in ms],
+        }
+    return {"algorithms": out, "layout": [f"{'cpu' if cpu else 'gpu'}{g}:{a}" for g, a in streams],
+            "recorded_seconds": dt, "warmup_seconds": warmup, "initial_difficulty": difficulty,
+            "retarget_seconds": retarget_seconds, "vardiff": True,
+            "definition": ("otedama pool --algorithms sha256d,scrypt (one process) + one `otedama run` per "
+                           "(GPU, algorithm) stream over SV2; every accepted share re-hashed by the pool; windowed "
+                           "after the warm-up")}

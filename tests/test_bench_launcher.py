@@ -109,3 +109,55 @@ def test_bench_ranks_get_a_long_collective_bound(monkeypatch):
     monkeypatch.setenv("OTEDAMA_PG_TIMEOUT", "45")
     bench.main(["--gpus", "0"])
     assert os.environ["OTEDAMA_PG_TIMEOUT"] == "45"
+
+
+NODE_KEYS = {"total_hashes_per_sec", "per_rank_hashes_per_sec", "accepted", "rejected", "pool_accepted",
+             "pool_rejected", "ranks_seen", "dist_backend", "collectives", "collectives_total",
+             "hit_to_accept_rank0", "hit_to_accept_remote", "host_verify_to_accept_rank0",
+             "host_verify_to_accept_remote", "share_difficulty"}
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("n", [4, 8])
+def test_node_section_json_contract(n):
+    """after the kernel sections, bench.py runs the production node (`otedama node --gpus N`:
+    supervisor, N ranks, a device process per rank, rank 0 on the pool session) against the local pool and reports
+    it. The CPU rehearsal runs the same processes over gloo with CPU miners."""
+    res = _bench("--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--node-seconds", "3",
+                 "--node-warmup", "2", "--cpu-seconds", "0", timeout=360)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    node = d["node"]
+    assert "error" not in node, node
+    assert NODE_KEYS <= set(node), sorted(node)
+    assert node["n_ranks"] == n and node["ranks_seen"] == list(range(n)) and node["dist_backend"] == "gloo"
+    assert len(node["per_rank_hashes_per_sec"]) == n and all(r > 0 for r in node["per_rank_hashes_per_sec"])
+    assert node["total_hashes_per_sec"] == pytest.approx(sum(node["per_rank_hashes_per_sec"]))
+    assert d["node_hashes_per_sec"] == node["total_hashes_per_sec"]
+    assert node["rejected"] == 0 and node["pool_rejected"] == 0 and node["pool_accepted"] > 0
+    assert set(node["collectives"]) == {"rank0", *(f"rank{r}" for r in range(1, n))}
+    assert all(c > 0 for c in node["collectives"].values())
+    # remote ranks' shares crossed R2 and were accepted; CPU miners carry no kernel clock, so the host timeline is used
+    assert node["host_verify_to_accept_remote"]["samples"] > 0 and node["accepted_remote_in_window"] > 0
+    assert node["share_difficulty"] == pytest.approx(node["share_difficulty_requested"], rel=1e-6)
+    assert node["exit_code"] == 0
+
+
+@pytest.mark.timeout(300)
+def test_pool_and_cpu_sections_json_contract():
+    """BASELINE configs 1 and 5 in the bench JSON: the native CPU miner (single thread, all cores) and the mixed
+    SHA-256d + scrypt pool with vardiff (here CPU miners for both algorithms)."""
+    res = _bench("--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--pool-seconds", "3", "--cpu-seconds", "0.5",
+                 timeout=280)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d["cpu_single_thread_hashes_per_sec"] > 0 and d["cpu_all_cores_hashes_per_sec"] > 0
+    assert d["cpu"]["threads"] >= 1 and d["cpu"]["sha_ni"] in (True, False)
+    pool = d["pool"]
+    assert "error" not in pool, pool
+    assert set(pool["algorithms"]) == {"sha256d", "scrypt"}
+    for algo, a in pool["algorithms"].items():
+        assert a["accepted_total"] > 0 and a["rejected_total"] == 0, (algo, a)
+        assert a["validate_ms"]["p50"] is not None and a["validate_ms"]["samples"] == a["accepted_total"]
+        assert a["workers"] and all(w["difficulty"] > 0 for w in a["workers"])
+        assert all(m["exit_code"] == 0 for m in a["miners"])
