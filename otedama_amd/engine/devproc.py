@@ -152,12 +152,13 @@ class DeviceProcess:
             except OSError:
                 pass
 
-    def restart(self, replay_job: bool = True) -> None:
-        """Replace a dead child with a fresh process. ``replay_job``: re-send the last job at once; a MinerSet passes
+    def restart(self, replay_job: bool = True) -> bool:
+        """Replace a dead child with a fresh process; False (nothing spawned) while the old child has not been
+        reaped yet — the caller retries later. ``replay_job``: re-send the last job at once; a MinerSet passes
         False and applies a fresh stripe when the process reports ready, because replaying the dead process's
         stripe would search its nonces a second time."""
         if self.alive:
-            return
+            return False
         if not replay_job:
             self._job = None
         with self._lock:
@@ -166,6 +167,7 @@ class DeviceProcess:
             self._child = {}
         self.restarts += 1
         self._spawn()
+        return True
 
     def kill(self, sig: int = signal.SIGKILL) -> None:
         """Fault injection (tests / chaos): signal the child."""
@@ -269,6 +271,8 @@ class DeviceProcess:
         except subprocess.TimeoutExpired:
             proc.kill()
             rc = proc.wait()
+        if proc is not self._proc:
+            return  # a restart already replaced this child: its exit says nothing about the new one
         last_err = self._child.get("error", "")
         self.exit_code = rc
         self.error = (f"device process exited with code {rc}" if rc >= 0 else

@@ -240,6 +240,9 @@ class MinerSet:
         node_base = int(t.get("variant_base", 0) or 0)
         hw = self.high_water()
         base = max(hw - node_base, 0) + RESPLIT_GROUPS * GROUP * old_stride
+        # a device cursor sits in this rank's residue class (rank mod world): the offset itself must stay a multiple
+        # of world_size, or the new stripes would land in another rank's class (duplicates there, a gap here)
+        base = -(-base // self.world_size) * self.world_size
         probe = {k: v for k, v in t.items() if k != "variant_base"}
         try:
             space = int(self.N.variant_space(probe)) if self.N is not None else variant_space(probe)
@@ -289,11 +292,14 @@ class MinerSet:
             if self._stopped or not m.retired:
                 return
         try:
-            m.native.restart(replay_job=False)  # its stripe is re-assigned past every cursor once it is ready
+            spawned = m.native.restart(replay_job=False)  # its stripe is re-assigned past every cursor once ready
         except Exception as exc:  # noqa: BLE001
             self.log("error", f"miners: restart of {m.id} failed: {exc}")
+            spawned = False
+        if spawned is False:  # failed, or the killed child was not reaped yet (restart() refuses a live process)
             with self._lock:
-                self._schedule_respawn(m)
+                if not self._stopped and m.retired:
+                    self._schedule_respawn(m)
 
     def _on_process_ready(self, dp) -> None:
         """A (re)spawned device process is mining: bring its device back into the stripe plan."""

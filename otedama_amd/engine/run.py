@@ -68,6 +68,8 @@ DEFAULT_HYSTERESIS = 0.05
 SHARE_POLL_INTERVAL = 0.005  # share-queue poll for miner sets without wake-up fds (test fakes)
 SHARE_WAKE_FALLBACK = 0.25   # with eventfds: safety re-poll interval (a missed wake-up costs at most this)
 SUBMIT_KEYS_CAP = 1024  # unacked-submit map bound (internal/engine/run.go:726)
+TARGET_GRACE = 10.0     # seconds a raised share target still lets shares found under the previous one through (the
+                        # local pool credits them for the same window, pool/server.py RETARGET_GRACE)
 
 
 @dataclass
@@ -175,6 +177,9 @@ class Engine:
         self._active_job: Job | None = None
         self._valid_jobs: set[str] = set()
         self._job_targets: dict[str, int | None] = {}  # job id -> its current share target (int, LE)
+        # job id -> (the easier target in force before the last raise, monotonic time of the raise): a share found
+        # against it and still queued is submitted within TARGET_GRACE (pools credit such in-flight shares)
+        self._prev_targets: dict[str, tuple[int, float]] = {}
         self._submitted = BoundedSet(SUBMIT_KEYS_CAP)  # run.go:720-726: cap 1024, oldest half dropped
         self._session = None
         self._providers: list = []
@@ -714,6 +719,7 @@ class Engine:
             self._active_job = None
             self._valid_jobs.clear()
             self._job_targets.clear()
+            self._prev_targets.clear()
 
     async def _notice_pump(self, session) -> None:
         while True:
@@ -728,6 +734,7 @@ class Engine:
                 self._active_job = None
                 self._valid_jobs.clear()
                 self._job_targets.clear()
+                self._prev_targets.clear()
                 self.miners.pause_all()
                 continue
             if job.clean_jobs:
@@ -735,10 +742,15 @@ class Engine:
                     self._submitted.clear()
                 self._valid_jobs = {job.job_id}
                 self._job_targets = {k: v for k, v in self._job_targets.items() if k == job.job_id}
+                self._prev_targets = {k: v for k, v in self._prev_targets.items() if k == job.job_id}
             else:
                 self._valid_jobs.add(job.job_id)
             # the job's current share target: a target-only update (SV2 SetTarget) re-issues the same job id
-            self._job_targets[job.job_id] = int.from_bytes(job.target, "little") if job.target else None
+            new_t = int.from_bytes(job.target, "little") if job.target else None
+            old_t = self._job_targets.get(job.job_id)
+            if old_t is not None and new_t is not None and new_t < old_t:
+                self._prev_targets[job.job_id] = (old_t, time.monotonic())
+            self._job_targets[job.job_id] = new_t
             self._active_job = job
             publish_difficulty(self.m, session.suggested_difficulty(), self.current_hashrate,
                                float(2 ** 256) / self.algorithm.diff1)
@@ -792,8 +804,11 @@ class Engine:
                 # connect), so it is dropped here instead.
                 tgt, h = self._job_targets.get(s["job_id"]), s.get("hash")
                 if tgt is not None and h and int.from_bytes(h, "little") > tgt:
-                    self.m.below_target_skipped.inc()
-                    continue
+                    prev = self._prev_targets.get(s["job_id"])
+                    hv = int.from_bytes(h, "little")
+                    if prev is None or hv > prev[0] or time.monotonic() - prev[1] > TARGET_GRACE:
+                        self.m.below_target_skipped.inc()
+                        continue
                 en2 = extranonce2_bytes(s["extranonce2"], s["extranonce2_size"])
                 key = (s["job_id"], s["nonce"], s["ntime"], s["version"], en2)
                 if key in self._submitted:  # defence in depth: never send a pool a duplicate

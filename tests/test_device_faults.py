@@ -176,6 +176,26 @@ def test_node_variant_base_adds_to_the_local_resplit():
     assert "variant_base" not in ms.miners[0].native.jobs[-1]
 
 
+@pytest.mark.parametrize("rank,world", [(1, 2), (1, 4), (3, 4), (5, 8)])
+def test_local_resplit_keeps_the_rank_residue_class(rank, world):
+    """a device cursor sits in the rank's class (rank mod world), so the re-split offset must be a
+    multiple of world_size; otherwise rank 1 of 2 moved to even variants (rank 0's class: duplicate shares) and left
+    its own class unsearched. Every new start stays congruent to rank mod world and the survivors cover the class."""
+    ms = _set(2, rank=rank, world=world)
+    ep = ms.set_job(dict(_real_tmpl(), variant_base=4096))
+    first = [m.native.jobs[-1]["variant_start"] for m in ms.miners]
+    assert all(v % world == rank for v in first)
+    # device cursors as the native miners report them: the next unstarted variant of their own stripe
+    ms.miners[0].native.cursor = (first[0] + 37 * ms.miners[0].stripe_stride, ep)
+    ms.miners[1].native.cursor = (first[1] + 41 * ms.miners[1].stripe_stride, ep)
+    ms.miners[1].native.fault = "hipErrorLaunchFailure"
+    ms.retire_faulted()
+    survivor = ms.miners[0].native.jobs[-1]
+    assert survivor["variant_start"] % world == rank, survivor
+    assert survivor["variant_stride"] == world
+    assert survivor["variant_start"] >= max(c for c, _ in (ms.miners[0].native.cursor, ms.miners[1].native.cursor))
+
+
 def test_python_variant_space_matches_native():
     from otedama_amd.engine.miners import variant_space
     from otedama_amd.ops.native import require_native

@@ -811,8 +811,12 @@ def test_share_pump_skips_stale_job_shares():
 
 
 def test_share_pump_drops_shares_below_a_raised_target():
-    """SV2 SetTarget re-issues the job with a higher difficulty: shares the device verified against the old target
-    and still queued would be rejected as low-difficulty, so they are dropped (counted) instead of submitted."""
+    """SV2 SetTarget re-issues the job with a higher difficulty. A queued share the device verified against the
+    previous target is still submitted for TARGET_GRACE seconds after the raise (the pool credits in-flight shares
+    at the previous difficulty for that long); after the grace, or below even the previous target, it
+    would be rejected as low-difficulty, so it is dropped (counted) instead."""
+    from otedama_amd.engine import run as run_mod
+
     async def go():
         eng, _ = make_engine()
         sess = FakeSession()
@@ -821,10 +825,18 @@ def test_share_pump_drops_shares_below_a_raised_target():
         await sess.jobs.put(Job("j1", clean_jobs=True, target=hard))   # the re-issue after SetTarget
         await run_pump_until(eng._job_pump(sess), lambda: len(eng.miners.jobs) == 2)
         weak, strong = (1 << 245).to_bytes(32, "little"), (1 << 230).to_bytes(32, "little")
-        eng.miners.queue = [share(nonce=1, digest=weak), share(nonce=2, digest=strong), share(nonce=3)]
-        await run_pump_until(eng._share_pump(sess), lambda: len(sess.submitted) == 2)
-        assert sorted(s.nonce for s in sess.submitted) == [2, 3]   # no hash (CPU-style share): not filtered
+        too_weak = (1 << 252).to_bytes(32, "little")  # above even the previous target
+        eng.miners.queue = [share(nonce=1, digest=weak), share(nonce=2, digest=strong), share(nonce=3),
+                            share(nonce=4, digest=too_weak)]
+        await run_pump_until(eng._share_pump(sess), lambda: len(sess.submitted) == 3)
+        assert sorted(s.nonce for s in sess.submitted) == [1, 2, 3]   # in grace; no hash (CPU-style): not filtered
         assert eng.m.below_target_skipped.value() == 1
+        old, at = eng._prev_targets["j1"]
+        eng._prev_targets["j1"] = (old, at - run_mod.TARGET_GRACE - 1)  # the grace has passed
+        eng.miners.queue = [share(nonce=5, digest=weak), share(nonce=6, digest=strong)]
+        await run_pump_until(eng._share_pump(sess), lambda: len(sess.submitted) == 4)
+        assert sorted(s.nonce for s in sess.submitted) == [1, 2, 3, 6]
+        assert eng.m.below_target_skipped.value() == 2
     asyncio.run(go())
 
 

@@ -333,7 +333,7 @@ def test_registry_rules():
 def test_cpu_driver_device():
     (d,) = hal.CPUDriver(3).enumerate()
     assert d.identity().id == "cpu-0" and d.identity().family == hal.Family.CPU and d.threads == 3
-    assert d.capabilities().sha256d and d.capabilities().general_compute and not d.capabilities().scrypt
+    assert d.capabilities().sha256d and d.capabilities().general_compute and d.capabilities().scrypt  # host chains
 
 
 class _Drv:
