@@ -145,6 +145,7 @@ __device__ __forceinline__ u64 groestl_lk(const u64* T, u32 lo, u32 w, int k) {
 
 // Grid for a grid-stride kernel: enough resident blocks to fill every CU `per_cu` times over.
 int x11_device_cus();
+bool x11_midstage_polls();  // stages after BLAKE poll the abort word (OTEDAMA_X11_MIDPOLL=0 turns it off)
 
 }  // namespace x11k
 
@@ -157,16 +158,24 @@ enum X11Stage : int {
 // Stage 0 writes H from the header + nonces; stages 1..10 transform H in place.
 // Stage 10 with `out` != null compares against the target and appends nonces
 // instead of writing H (search mode).
-// Abort word of the batch (otedama/hitsink.h), polled by the first stage (BLAKE skips its digests) and the last
-// (ECHO publishes nothing) once the host moved it past `epoch`; word == nullptr: never. The nine stages between
-// run a superseded batch to its end (~18 ms): polling in them cost 1-7% per stage (CubeHash +6.8%, Keccak +4%,
-// profiles/r3/f_regressions) for a job-switch saving the SHA-256d / scrypt paths do not need from X11.
+// Abort word of the batch (otedama/hitsink.h), polled by every stage once the host moved it past `epoch`
+// (word == nullptr: never). BLAKE checks before hashing; each later stage issues the load before its digest load and
+// tests it after (x11_abort_issue / x11_abort_seen), so the poll's latency hides under the digest read instead of
+// stalling the wave (round 3's stall-on-load polls cost 1-7% per stage, profiles/r3/f_regressions). A superseded
+// batch then stops at the next stage boundary instead of running its remaining stages (~18 ms at 2^23 nonces).
 struct X11Abort {
   const uint32_t* word = nullptr;
   uint32_t epoch = 0;
 };
 __device__ __forceinline__ bool x11_stop(const X11Abort& a) {
   return otedama_dev::abort_newer(otedama_dev::abort_peek(a.word, a.epoch), a.epoch);
+}
+__device__ __forceinline__ uint32_t x11_abort_issue(const X11Abort& a) {
+  if (a.word == nullptr) return a.epoch;
+  return __hip_atomic_load(const_cast<uint32_t*>(a.word), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool x11_abort_seen(uint32_t raw, const X11Abort& a) {
+  return otedama_dev::abort_seen(raw, a.epoch);
 }
 hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint64_t* H, uint32_t stride, uint32_t n,
                               X11Abort ab, hipStream_t s);

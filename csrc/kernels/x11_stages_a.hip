@@ -220,13 +220,16 @@ __device__ __forceinline__ void groestl_perm(const u64* T, u32 lo, u64 a[16]) {
   }
 }
 
-__global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_groestl512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
+__global__ __launch_bounds__(kGroestlBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_groestl512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
   __shared__ u64 T[kGroestlPrivQwords];
   groestl_priv_fill(T);
   const u32 lo = groestl_laneoff();
   for (u32 i = blockIdx.x * kGroestlBlock + threadIdx.x; i < n; i += gridDim.x * kGroestlBlock) {
     u64 m[16], p[16], q[16];
+    const u32 a0 = x11_abort_issue(ab);
     load_hash(Hb, stride, i, m);
+    if (x11_abort_seen(a0, ab)) return;
     m[8] = 0x80;
 #pragma unroll
     for (int k = 9; k < 15; ++k) m[k] = 0;
@@ -645,14 +648,16 @@ __device__ __forceinline__ void cubehash512_64(u64 h[8]) {
 }
 
 // One kernel per stage: each stage runs at its own register budget / occupancy.
-#define X11_STAGE_KERNEL(NAME, FN)                                                          \
-  __global__ __launch_bounds__(kBlock) void NAME(u64* __restrict__ Hb, u32 stride, u32 n) { \
-    const u32 i = blockIdx.x * kBlock + threadIdx.x;                                        \
-    if (i >= n) return;                                                                     \
-    u64 h[8];                                                                               \
-    load_hash(Hb, stride, i, h);                                                            \
-    FN(h);                                                                                  \
-    store_hash(Hb, stride, i, h);                                                           \
+#define X11_STAGE_KERNEL(NAME, FN)                                                                       \
+  __global__ __launch_bounds__(kBlock) void NAME(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) { \
+    const u32 i = blockIdx.x * kBlock + threadIdx.x;                                                     \
+    if (i >= n) return;                                                                                  \
+    const u32 a0 = x11_abort_issue(ab);                                                                  \
+    u64 h[8];                                                                                            \
+    load_hash(Hb, stride, i, h);                                                                         \
+    if (x11_abort_seen(a0, ab)) return;                                                                  \
+    FN(h);                                                                                               \
+    store_hash(Hb, stride, i, h);                                                                        \
   }
 X11_STAGE_KERNEL(k_bmw512_64, bmw512_64)
 X11_STAGE_KERNEL(k_skein512_64, skein512_64)
@@ -661,14 +666,17 @@ X11_STAGE_KERNEL(k_luffa512_64, luffa512_64)
 X11_STAGE_KERNEL(k_cubehash512_64, cubehash512_64)
 #undef X11_STAGE_KERNEL
 
-__device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u32 n, bool reload) {
+__device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u32 n, bool reload,
+                                             X11Abort ab = X11Abort{}) {
   __shared__ __attribute__((aligned(16))) u32 BC[42][8];
   for (u32 t = threadIdx.x; t < 42 * 8; t += kBlock) BC[t / 8][t % 8] = x11t::JH_BC[t / 8][t % 8];
   __syncthreads();
   const u32 i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  const u32 a0 = x11_abort_issue(ab);
   u64 h[8];
   load_hash(Hb, stride, i, h);
+  if (x11_abort_seen(a0, ab)) return;
   if (reload) jh512_64<true>(h, BC, Hb, stride, i);
   else jh512_64(h, BC);
   store_hash(Hb, stride, i, h);
@@ -679,8 +687,8 @@ __device__ __forceinline__ void jh_stage_lds(u64* __restrict__ Hb, u32 stride, u
 // the scalar-cache kernel in four sessions: -4.4%, -2.0%, -1.3%, +1.0% (tools/x11_variants.hip,
 // profiles/r3/h_jh, l_shavite, x_simd).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
-  jh_stage_lds(Hb, stride, n, true);
+    u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
+  jh_stage_lds(Hb, stride, n, true, ab);
 }
 #ifdef OTEDAMA_X11_VARIANTS
 // Alternatives timed by tools/x11_variants.hip (not built into the extension).
@@ -715,19 +723,20 @@ hipError_t x11_launch_stage_a(int stage, const X11Params& p, uint32_t base, uint
                               X11Abort ab, hipStream_t s) {
   using namespace x11k;
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+  const X11Abort mid = x11_midstage_polls() ? ab : X11Abort{};
   switch (stage) {
     case kX11Blake: k_blake512_80<<<grid, block, 0, s>>>(p, base, H, stride, n, ab); break;
-    case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Bmw: k_bmw512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
     case kX11Groestl: {
       const u32 want = (n + kGroestlBlock - 1) / kGroestlBlock, cap = (u32)x11_device_cus() * 2 * 4;
-      k_groestl512_64<<<dim3(want < cap ? want : cap), dim3(kGroestlBlock), 0, s>>>(H, stride, n);
+      k_groestl512_64<<<dim3(want < cap ? want : cap), dim3(kGroestlBlock), 0, s>>>(H, stride, n, mid);
       break;
     }
-    case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n); break;
-    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n); break;
+    case kX11Skein: k_skein512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
+    case kX11Jh: k_jh512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
+    case kX11Keccak: k_keccak512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
+    case kX11Luffa: k_luffa512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
+    case kX11Cubehash: k_cubehash512_64<<<grid, block, 0, s>>>(H, stride, n, mid); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -11,6 +11,8 @@
 // keep state column j in lane j and exchange one word per step with an xor
 // shuffle inside the 8-lane group.
 // Bit-exact oracle: csrc/cpu/x11_cpu.cpp (tests/test_x11_gpu.py compares every stage).
+#include <cstdlib>
+
 #include "otedama/x11_launch.h"
 #include "x11_common.h"
 
@@ -121,17 +123,22 @@ __device__ __forceinline__ void shavite512_64(const u32* T, u32 lo, u64 h[8]) {
   }
 }
 
-__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(
-    u64* __restrict__ Hb, u32 stride, u32 n) {
+__device__ __forceinline__ void shavite_stage(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
   __shared__ u32 T[kAesPrivWords];
   aes_priv_fill(T);
   const u32 lo = aes_laneoff();
   for (u32 i = blockIdx.x * kAesBlock + threadIdx.x; i < n; i += gridDim.x * kAesBlock) {
+    const u32 a0 = x11_abort_issue(ab);
     u64 h[8];
     load_hash(Hb, stride, i, h);
+    if (x11_abort_seen(a0, ab)) return;
     shavite512_64(T, lo, h);
     store_hash(Hb, stride, i, h);
   }
+}
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64(
+    u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
+  shavite_stage(Hb, stride, n, ab);
 }
 #ifdef OTEDAMA_X11_VARIANTS
 // The round-2 kernel, verbatim (one round per trip of a rolled loop), timed by tools/x11_variants.hip.
@@ -334,7 +341,7 @@ constexpr u32 kSimdLds = 624;
 
 // Eight lanes per hash: launch with 8 * n threads.
 template <bool kSw>
-__device__ __forceinline__ void simd_stage(u64* __restrict__ Hb, u32 stride, u32 n) {
+__device__ __forceinline__ void simd_stage(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab = X11Abort{}) {
   __shared__ __attribute__((aligned(16))) u32 L[kSimdLds];
   for (u32 t = threadIdx.x; t < kSimdLds; t += kSimdBlock) {
     u32 v = 0;
@@ -355,8 +362,10 @@ __device__ __forceinline__ void simd_stage(u64* __restrict__ Hb, u32 stride, u32
   const u32 t = blockIdx.x * kSimdBlock + threadIdx.x;
   const u32 i = t >> 3, j = t & 7;
   if (i >= n) return;  // whole 8-lane groups exit together
+  const u32 a0 = x11_abort_issue(ab);
   u64 h[8];
   load_hash(Hb, stride, i, h);
+  if (x11_abort_seen(a0, ab)) return;  // wave-uniform: whole waves (eight 8-lane groups) leave together
   u32 xw[16];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { xw[2 * k] = lo32(h[k]); xw[2 * k + 1] = hi32(h[k]); }
@@ -409,8 +418,8 @@ __device__ __forceinline__ void simd_stage(u64* __restrict__ Hb, u32 stride, u32
   }
 }
 
-__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n) {
-  simd_stage<true>(Hb, stride, n);
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64(u64* __restrict__ Hb, u32 stride, u32 n, X11Abort ab) {
+  simd_stage<true>(Hb, stride, n, ab);
 }
 #ifdef OTEDAMA_X11_VARIANTS
 __global__ __launch_bounds__(kSimdBlock) void k_simd512_64_dpp(u64* __restrict__ Hb, u32 stride, u32 n) {
@@ -525,6 +534,16 @@ __global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4)
 }  // namespace x11k
 
 namespace x11k {
+// OTEDAMA_X11_MIDPOLL=0: the stages after BLAKE get no abort word (the A/B baseline for the cost of their polls:
+// same code, a uniform kernel-argument branch instead of the load).
+bool x11_midstage_polls() {
+  static const bool on = [] {
+    const char* v = std::getenv("OTEDAMA_X11_MIDPOLL");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 int x11_device_cus() {
   static int cache[64] = {0};
   int dev = 0;
@@ -545,11 +564,12 @@ hipError_t x11_launch_stage_b(int stage, const X11Params& p, uint32_t base, uint
   // bank-private AES table (64 KiB): 2 resident blocks of 512 per CU, grid-stride over the batch
   const u32 aes_want = (n + kAesBlock - 1) / kAesBlock, aes_cap = (u32)x11_device_cus() * 2 * 4;
   const dim3 aes_grid(aes_want < aes_cap ? aes_want : aes_cap), aes_block(kAesBlock);
+  const X11Abort mid = sink && x11_midstage_polls() ? X11Abort{sink->abort, sink->epoch} : X11Abort{};
   switch (stage) {
-    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n); break;
+    case kX11Shavite: k_shavite512_64<<<aes_grid, aes_block, 0, s>>>(H, stride, n, mid); break;
     case kX11Simd: {
       const dim3 g8((8ull * n + kBlock - 1) / kBlock);
-      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n);
+      k_simd512_64<<<g8, block, 0, s>>>(H, stride, n, mid);
       break;
     }
     case kX11Echo:

@@ -21,10 +21,11 @@ from otedama_amd.ops.native import require_native
 from otedama_amd.models.header import int_to_hash
 N = require_native()
 secs = float(sys.argv[2])
+algo = sys.argv[3] if len(sys.argv) > 3 else "sha256d"
 m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32, grid=N.gpu_cu_count(0) * 6, queue_cap=4096, sha_variants=128)
 hdr = bytes(range(76)) + bytes(4)
-m.set_job({"header": hdr, "target": int_to_hash((1 << 224) - 1), "job_id": "ab", "epoch": 1, "algo": "sha256d",
-           "version_mask": 0x1FFFE000})
+m.set_job({"header": hdr, "target": int_to_hash((1 << (224 if algo == "sha256d" else 200)) - 1), "job_id": "ab",
+           "epoch": 1, "algo": algo, "version_mask": 0x1FFFE000})
 m.start()
 time.sleep(3.0)
 
@@ -54,6 +55,7 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--env-a", default="", help="KEY=VALUE[,KEY=VALUE] for the A processes")
     ap.add_argument("--env-b", default="", help="KEY=VALUE[,KEY=VALUE] for the B processes")
+    ap.add_argument("--algo", default="sha256d", choices=("sha256d", "scrypt", "x11"))
     a = ap.parse_args()
 
     def env_of(spec: str) -> dict:
@@ -66,7 +68,7 @@ def main() -> int:
     res = {"a": [], "b": []}
     for _ in range(a.rounds):
         for key, tree, spec in (("a", a.a, a.env_a), ("b", a.b, a.env_b)):
-            out = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(tree), str(a.seconds)],
+            out = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(tree), str(a.seconds), a.algo],
                                  capture_output=True, text=True, timeout=120, env=env_of(spec))
             line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
             if out.returncode != 0 or not line:
@@ -75,6 +77,7 @@ def main() -> int:
             res[key].append(json.loads(line[0])["hps"])
     res["median_a"], res["median_b"] = statistics.median(res["a"]), statistics.median(res["b"])
     res["a_over_b"] = res["median_a"] / res["median_b"]
+    res["algo"], res["env_a"], res["env_b"] = a.algo, a.env_a, a.env_b
     print(json.dumps(res))
     return 0
 

@@ -36,6 +36,21 @@ __global__ void fill(u64* H, size_t n) {
   }
 }
 
+// the production kernels take the batch's abort word: wrapped here without one (the variants have none)
+namespace otedama::x11k {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_jh512_64_prod(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  jh_stage_lds(Hb, stride, n, true);
+}
+__global__ __launch_bounds__(kAesBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_shavite512_64_prod(
+    u64* __restrict__ Hb, u32 stride, u32 n) {
+  shavite_stage(Hb, stride, n, X11Abort{});
+}
+__global__ __launch_bounds__(kSimdBlock) void k_simd512_64_prod(u64* __restrict__ Hb, u32 stride, u32 n) {
+  simd_stage<true>(Hb, stride, n);
+}
+}  // namespace otedama::x11k
+
 typedef void (*StageFn)(u64*, u32, u32);
 struct Variant {
   const char* name;
@@ -55,13 +70,13 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, src, words);
   CK(hipGetLastError());
   using namespace otedama::x11k;
-  std::vector<Variant> vs = {{"jh_lds_reload_w7 (production)", k_jh512_64, 0, 0},
+  std::vector<Variant> vs = {{"jh_lds_reload_w7 (production)", k_jh512_64_prod, 0, 0},
                              {"jh_sgpr", k_jh512_64_sgpr, 0, 0},
                              {"jh_lds_w7", k_jh512_64_w7, 0, 0},
                              {"jh_lds", k_jh512_64_lds, 0, 0},
-                             {"shavite_4round_trips (production)", k_shavite512_64, 1, 1},
+                             {"shavite_4round_trips (production)", k_shavite512_64_prod, 1, 1},
                              {"shavite_r2 (round-2 kernel)", k_shavite512_64_r2, 1, 1},
-                             {"simd_swizzle (production)", k_simd512_64, 2, 2},
+                             {"simd_swizzle (production)", k_simd512_64_prod, 2, 2},
                              {"simd_dpp (round-2 lane exchange)", k_simd512_64_dpp, 2, 2}};
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
