@@ -6,8 +6,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <array>
+#include <atomic>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 #include "otedama/aead.h"
 #include "otedama/job.h"
@@ -15,6 +18,7 @@
 #include "otedama/trace.h"
 #include "otedama/sha256.h"
 #include "otedama/sv2_frame.h"
+#include "otedama/work_queue.h"
 #include "otedama/x11.h"
 
 namespace py = pybind11;
@@ -191,6 +195,37 @@ PYBIND11_MODULE(_native, m) {
     { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }
     return to_bytes(o, 32);
   });
+  // Test hook: the scrypt verifier's bounded queue (BoundedWorkQueue) flooded by a producer that never waits, with
+  // a consumer hashing every item on the host (scrypt_1024_1_1, as the GPU miner's verifier does).
+  m.def("_work_queue_flood", [](size_t cap, size_t n, bool hash_each) {
+    BoundedWorkQueue<std::array<uint8_t, 80>> q(cap);
+    std::atomic<uint64_t> processed{0};
+    uint64_t accepted = 0;
+    {
+      py::gil_scoped_release r;
+      std::thread consumer([&] {
+        std::array<uint8_t, 80> h;
+        uint8_t out[32];
+        while (q.pop(&h)) {
+          if (hash_each) scrypt_1024_1_1(h.data(), out);
+          processed.fetch_add(1);
+        }
+      });
+      for (size_t i = 0; i < n; ++i) {
+        std::array<uint8_t, 80> h{};
+        std::memcpy(h.data() + 76, &i, 4);
+        if (q.push(std::move(h))) ++accepted;
+      }
+      q.stop(~size_t(0));
+      consumer.join();
+    }
+    py::dict d;
+    d["accepted"] = accepted;
+    d["refused"] = q.refused();
+    d["peak"] = q.peak();
+    d["processed"] = processed.load();
+    return d;
+  }, py::arg("cap"), py::arg("n"), py::arg("hash_each") = true);
   m.attr("X11_STAGES") = kX11StageCount;
   m.def("x11", [](const py::bytes& msg) {
     std::string s = msg; uint8_t o[32];

@@ -14,7 +14,11 @@
 //
 // Launch overlap: the two batches in flight sit on two streams (one per slot), so the next SHA-256d batch's waves
 // fill the CUs that the running batch's tail leaves idle; without it a 2^29-nonce launch (28 ms) lost ~2.5% to its
-// tail (profiles/r3/e_rehearsal). scrypt / X11 batches share their scratch buffers and are chained with an event.
+// tail (profiles/r3/e_rehearsal). scrypt and X11 batches have per-slot buffers too (two 64 GiB halves of the scrypt
+// pad, two X11 digest planes): the two scrypt half-batches run staggered by half a hash so that one of them reaches a
+// ROMix phase boundary (its abort poll) every quarter hash, and a job switch waits ~T/8 instead of ~T/4 for the
+// first half of the GPU to take the new work. OTEDAMA_SCRYPT_HALVES=0 / OTEDAMA_X11_OVERLAP=0 restore one shared
+// buffer per algorithm with the batches chained (the A/B baselines).
 //
 // Device time: s_memrealtime (100 MHz) is mapped to CLOCK_MONOTONIC by a probe kernel at start-up (min round
 // trip of several probes) and re-checked every 10 s by a calibration thread on a stream of its own (a probe
@@ -42,6 +46,7 @@
 #include "otedama/runtime.h"
 #include "otedama/sha256.h"
 #include "otedama/trace.h"
+#include "otedama/work_queue.h"
 #include "otedama/x11_launch.h"
 
 namespace otedama {
@@ -198,9 +203,9 @@ void GpuMiner::loop() {
   std::atomic<bool> cal_stop{false};
   std::mutex cal_mu;
   std::condition_variable cal_cv;
-  void* scratch = nullptr;       // scrypt pad, allocated on the first scrypt job
+  void* scratch = nullptr;       // scrypt pad, allocated on the first scrypt job (one half per slot)
   void* xbuf = nullptr;
-  uint64_t* x11_h = nullptr;     // X11 intermediate digests (8 u64 planes x batch)
+  uint64_t* x11_h = nullptr;     // X11 intermediate digests (8 u64 planes x batch, one set per slot)
   // Released on every exit, including a HIP error thrown mid-loop (device fault): in-flight batches are drained
   // first so nothing is freed under a running kernel or copy.
   struct Release {
@@ -284,6 +289,11 @@ void GpuMiner::loop() {
   const int scrypt_gap = kScryptCoop;
   const int scrypt_grid = cus * 16;
   const uint32_t scrypt_batch = uint32_t(scrypt_grid) * 256u;
+  const char* halves_env = std::getenv("OTEDAMA_SCRYPT_HALVES");
+  const bool scrypt_halves = !(halves_env && halves_env[0] == '0');
+  const char* x11ov_env = std::getenv("OTEDAMA_X11_OVERLAP");
+  const bool x11_overlap = !(x11ov_env && x11ov_env[0] == '0');
+  double scrypt_hash_s = 0.064;  // one lane's scrypt hash (= one full batch) on the device; refined per batch
   // X11: eleven stage kernels per batch over a 64 B/nonce digest buffer (512 MiB at 2^23).
   const uint32_t x11_batch = 1u << 23;
   // K-variant SHA-256d kernel: 16 blocks of 256 per CU (tools/bench_sha_k.py, profiles/r2/).
@@ -356,11 +366,7 @@ void GpuMiner::loop() {
   double switch_t0 = 0;
   double rate_hpms = 0;  // hashes per ms of completed full batches (for aborted-batch accounting)
   std::deque<int> fifo;  // in-flight slots, issue order
-  std::deque<Candidate> vq;  // scrypt candidates awaiting host verification (at most kVerifyCap)
-  uint64_t verify_refused = 0, vq_peak = 0;  // guarded by vq_mu
-  std::mutex vq_mu;
-  std::condition_variable vq_cv;
-  bool vq_stop = false;
+  BoundedWorkQueue<Candidate> vq(kVerifyCap);  // scrypt candidates awaiting host verification
   std::thread verifier;
 
   // New work opens a new launch epoch and moves the device abort word: batches of older epochs stop at
@@ -406,34 +412,21 @@ void GpuMiner::loop() {
   };
 
   verifier = std::thread([&] {
-    std::unique_lock<std::mutex> lk(vq_mu);
-    for (;;) {
-      vq_cv.wait(lk, [&] { return vq_stop || !vq.empty(); });
-      if (vq.empty()) return;  // stopping and drained
-      Candidate c = std::move(vq.front());
-      vq.pop_front();
-      lk.unlock();
+    Candidate c;
+    while (vq.pop(&c)) {  // false once stopped and drained
       uint64_t good = 0, bad = 0, g = 0;
       auto cur = peek_job(&g, nullptr);
       verify_push(c, c.nonce, c.vi, c.stamp, true, cur, g, &good, &bad);
-      {
-        std::lock_guard<std::mutex> sg(stats_mu_);
-        stats_.shares += good;
-        stats_.rejected_candidates += bad;
-      }
-      lk.lock();
+      std::lock_guard<std::mutex> sg(stats_mu_);
+      stats_.shares += good;
+      stats_.rejected_candidates += bad;
     }
   });
   struct VerifierJoin {
     std::function<void()> f;
     ~VerifierJoin() { f(); }
   } verifier_join{[&] {
-    {
-      std::lock_guard<std::mutex> g(vq_mu);
-      vq_stop = true;
-      if (!running_.load() && vq.size() > 64) vq.resize(64);  // shutting down: bound the work left (~1 ms each)
-    }
-    vq_cv.notify_all();
+    vq.stop(running_.load() ? ~size_t(0) : 64);  // shutting down: bound the work left (~1 ms each)
     if (verifier.joinable()) verifier.join();
   }};
 
@@ -459,14 +452,7 @@ void GpuMiner::loop() {
         // host scrypt costs ~1 ms per candidate: verified on the verifier thread so a burst of candidates never
         // holds up a job switch or the next launch. The queue is bounded: past kVerifyCap a candidate is refused
         // and counted (a share target far below the device's rate would otherwise grow it without limit).
-        std::lock_guard<std::mutex> g(vq_mu);
-        if (vq.size() >= kVerifyCap) {
-          ++verify_refused;
-        } else {
-          vq.push_back(Candidate{b.job, b.group, b.gen, nonce, vi, stamp, b.enq_host, b.rt_enq, b.nvar});
-          vq_peak = std::max<uint64_t>(vq_peak, vq.size());
-          vq_cv.notify_one();
-        }
+        vq.push(Candidate{b.job, b.group, b.gen, nonce, vi, stamp, b.enq_host, b.rt_enq, b.nvar});
       } else {
         verify_push(Candidate{b.job, b.group, b.gen, 0, 0, 0, b.enq_host, b.rt_enq, b.nvar}, nonce, vi, stamp, true,
                     cur, cur_g, &good, &bad);
@@ -475,12 +461,7 @@ void GpuMiner::loop() {
       ++handled;
     }
     if (handled || lost) {
-      uint64_t refused = 0, peak = 0;
-      {
-        std::lock_guard<std::mutex> g(vq_mu);
-        refused = verify_refused;
-        peak = vq_peak;
-      }
+      const uint64_t refused = vq.refused(), peak = vq.peak();
       std::lock_guard<std::mutex> g(stats_mu_);
       stats_.shares += good;
       stats_.rejected_candidates += bad + lost;
@@ -504,6 +485,7 @@ void GpuMiner::loop() {
     uint64_t done_hashes = full;
     if (aborted && rate_hpms > 0) done_hashes = std::min<uint64_t>(full, uint64_t(rate_hpms * double(ms)));
     if (!aborted && ms > 0) rate_hpms = rate_hpms > 0 ? 0.8 * rate_hpms + 0.2 * (double(full) / ms) : double(full) / ms;
+    if (!aborted && ms > 0 && b.job && b.job->algo == Algo::kScrypt) scrypt_hash_s = 0.7 * scrypt_hash_s + 0.3e-3 * ms;
     std::lock_guard<std::mutex> g(stats_mu_);
     if (n > kHitCap) {  // the kernel counted these candidates but had no ring slot left to publish them
       if (stats_.ring_overflow == 0)
@@ -567,7 +549,10 @@ void GpuMiner::loop() {
   // i.e. with probability (target_hi + 1) / 2^32, so expected candidates per launch = hashes * that. Launches are cut
   // (powers of two, so they still tile 2^32) until that is <= kHitCap / 8; the hit ring then overflows only on a
   // draw ~8 sigma above the mean at the floor target, and any overflow is counted.
+  const char* cap_env = std::getenv("OTEDAMA_LAUNCH_CAP");  // "0": launches keep batch_ hashes (overflow tests)
+  const bool cap_launches = !(cap_env && cap_env[0] == '0');
   auto launch_cap = [&](const JobTemplate& job) -> uint64_t {
+    if (!cap_launches) return 1ull << 40;
     const double p = (double(load_le32(job.target + 28)) + 1.0) / 4294967296.0;
     const double lim = double(kHitCap / 8) / p;
     uint64_t cap = 1ull << 40;
@@ -598,7 +583,9 @@ void GpuMiner::loop() {
     sink.epoch = s.epoch;
     sink.words = 2;
     // scrypt pad / X11 digests are shared by the batches: chain them; SHA-256d batches overlap freely
-    if (prev && prev->busy && job->algo != Algo::kSha256d) OTD_HIP(hipStreamWaitEvent(stream, prev->done, 0));
+    const bool shared_buf = (job->algo == Algo::kScrypt && !scrypt_halves) || (job->algo == Algo::kX11 && !x11_overlap);
+    if (prev && prev->busy && shared_buf) OTD_HIP(hipStreamWaitEvent(stream, prev->done, 0));
+    const int slot_i = int(&s - slots);
     OTD_HIP(hipMemsetAsync(s.d_count, 0, 64, stream));
     OTD_HIP(hipEventRecord(s.start, stream));
     s.enq_host = monotonic_seconds();
@@ -612,16 +599,23 @@ void GpuMiner::loop() {
       ScryptParams p;
       scrypt_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
-      s.count = std::min<uint64_t>({remaining, scrypt_batch, launch_cap(*job)});
-      OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xbuf, scratch, scrypt_gap, sink,
-                                   scrypt_grid, stream));
+      // halves: each slot owns half the pad / X buffer and half the grid (the two run side by side)
+      const int grid = scrypt_halves ? scrypt_grid / 2 : scrypt_grid;
+      const uint32_t lanes = scrypt_halves ? scrypt_batch / 2 : scrypt_batch;
+      char* pad = static_cast<char*>(scratch) +
+                  (scrypt_halves ? uint64_t(slot_i) * scrypt_scratch_bytes(grid, scrypt_gap) : 0);
+      char* xb = static_cast<char*>(xbuf) + (scrypt_halves ? uint64_t(slot_i) * lanes * 128ull : 0);
+      s.count = std::min<uint64_t>({remaining, lanes, launch_cap(*job)});
+      OTD_HIP(launch_scrypt_search(p, uint32_t(nonce_off), uint32_t(s.count), xb, pad, scrypt_gap, sink, grid,
+                                   stream));
     } else if (job->algo == Algo::kX11) {
-      if (!x11_h) OTD_HIP(hipMalloc(&x11_h, uint64_t(x11_batch) * 64));
+      if (!x11_h) OTD_HIP(hipMalloc(&x11_h, uint64_t(x11_batch) * 64 * (x11_overlap ? kInflight : 1)));
       X11Params p;
       x11_prepare(group->header[0], job->target, &p);
       const uint64_t remaining = (1ull << 32) - nonce_off;
       s.count = std::min<uint64_t>({remaining, x11_batch, launch_cap(*job)});
-      OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), x11_h, x11_batch, uint32_t(s.count), &sink, stream));
+      uint64_t* H = x11_h + (x11_overlap ? uint64_t(slot_i) * x11_batch * 8 : 0);
+      OTD_HIP(x11_launch_chain(p, uint32_t(nonce_off), H, x11_batch, uint32_t(s.count), &sink, stream));
     } else if (group->use_v) {
       const bool two = group->nvar == kSha256dV2Group;
       Sha256dParamsV vp = group->v_params;
@@ -717,6 +711,12 @@ void GpuMiner::loop() {
     while (job && (int)fifo.size() < kInflight) {
       const uint64_t v = job->variant_start + k * job->variant_stride;
       if (v >= job->variant_space()) break;  // stripe exhausted: wait for fresh work
+      // scrypt halves: keep the two in flight half a hash apart (the second waits until the first is half way), so
+      // their phase-boundary polls interleave; re-established after every switch
+      if (job->algo == Algo::kScrypt && scrypt_halves && fifo.size() == 1) {
+        const Batch& only = slots[fifo.front()];
+        if (only.epoch == epoch && monotonic_seconds() - only.enq_host < 0.5 * scrypt_hash_s) break;
+      }
       int free_slot = -1;
       for (int i = 0; i < kInflight; ++i)
         if (!slots[i].busy) { free_slot = i; break; }

@@ -209,3 +209,67 @@ def test_job_switch_with_other_streams_in_the_process():
     inproc = res["in_process"]  # the miner in this process, next to torch's streams
     assert inproc["p50_ms"] is not None and inproc["p50_ms"] < 20.0, inproc
     assert inproc["max_ms"] < 50.0, inproc
+
+
+def _drain(m, seconds):
+    shares, end = [], time.monotonic() + seconds
+    while time.monotonic() < end:
+        shares += m.poll(1 << 16)
+        time.sleep(0.002)
+    return shares
+
+
+def test_launches_are_sized_from_the_share_target_and_nothing_is_lost():
+    """at a target giving ~4000 candidates per 2^32 hashes, launches shrink (powers of two) until
+    the expected candidates per launch are <= hit-ring capacity / 8, so no candidate overflows the ring: every
+    candidate the kernels counted is a verified share or a counted top-word tie, and the share count matches the
+    Poisson expectation of the hashes searched."""
+    N = _native()
+    hdr = os.urandom(76) + bytes(4)
+    target = (4000 << 224) - 1
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32, queue_cap=1 << 22)
+    m.set_job(_job(hdr, target, 1, "d"))
+    m.start()
+    try:
+        shares = _drain(m, 1.5)
+    finally:
+        m.stop()
+    shares += m.poll(1 << 22)
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["launch_hashes"] <= 1 << 29, st["launch_hashes"]  # 2^32 cut to keep <= 512 expected candidates
+    assert st["ring_overflow"] == 0 and st["dropped"] == 0, st
+    assert st["candidates"] == st["shares"] + st["rejected_candidates"], st
+    assert len(shares) == st["shares"]
+    expected = st["hashes"] * (target + 1) / 2.0 ** 256
+    assert abs(len(shares) - expected) < 6 * expected ** 0.5 + 0.01 * expected, (len(shares), expected)
+    keys = {(s["version"], s["nonce"]) for s in shares}
+    assert len(keys) == len(shares)  # no duplicate
+    for s in shares[:400]:
+        _check_share(hdr, s, target)
+
+
+def test_ring_overflow_is_counted_exactly(monkeypatch):
+    """With launch sizing off (OTEDAMA_LAUNCH_CAP=0: 2^32-hash launches) at ~16000 candidates per launch, the 4096-
+    record hit ring overflows; every candidate past it is counted in ring_overflow, so candidates = verified shares +
+    top-word ties + ring_overflow exactly, and the engine-facing counter reports the loss."""
+    N = _native()
+    monkeypatch.setenv("OTEDAMA_LAUNCH_CAP", "0")
+    hdr = os.urandom(76) + bytes(4)
+    target = (16000 << 224) - 1
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32, queue_cap=1 << 22)
+    m.set_job(_job(hdr, target, 1, "o"))
+    m.start()
+    try:
+        shares = _drain(m, 1.2)
+    finally:
+        m.stop()
+    shares += m.poll(1 << 22)
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["launch_hashes"] == 1 << 32
+    assert st["ring_overflow"] > 0, st
+    assert st["candidates"] == st["shares"] + st["rejected_candidates"] + st["ring_overflow"], st
+    assert len(shares) == st["shares"] and st["dropped"] == 0
+    for s in shares[:200]:
+        _check_share(hdr, s, target)

@@ -261,3 +261,15 @@ def test_v1_coinbase_variants_group_by_version_first():
     stride = 8
     hs = [N.variant_header(j, 3 + k * stride)[0] for k in range(4)]
     assert all(x[36:] == hs[0][36:] for x in hs)
+
+
+def test_scrypt_verifier_queue_is_bounded_under_a_flood():
+    """the GPU miner's scrypt candidates wait for host verification (~0.2-1 ms each) in a
+    BoundedWorkQueue. A producer that never waits (a share target far below the device's rate) fills it to its cap
+    and every further candidate is refused and counted; nothing is lost uncounted and memory stays bounded."""
+    for cap, n in ((64, 5000), (8192, 20000)):
+        r = N._work_queue_flood(cap, n, True)
+        assert r["peak"] <= cap and r["refused"] > 0, r
+        assert r["accepted"] + r["refused"] == n and r["processed"] == r["accepted"], r
+    r = N._work_queue_flood(64, 50, False)  # below the cap nothing is refused
+    assert r == {"accepted": 50, "refused": 0, "peak": r["peak"], "processed": 50} and r["peak"] <= 50
