@@ -78,7 +78,7 @@ def window_rates(samples: list, t0: float, t1: float) -> dict[str, float]:
 
 
 def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_per_gpu: float = 25.0,
-                 expected_per_gpu: float = 19e9, startup_timeout: float = 240.0, cpu: bool = False,
+                 expected_per_gpu: float = 19e9, startup_timeout: float = 150.0, cpu: bool = False,
                  log_path: str | None = None) -> dict:
     """Run ``otedama node --gpus N`` against a pinned-difficulty pool for ``warmup`` + ``seconds`` and measure it.
     ``cpu``: a CPU rehearsal (gloo ranks, one CPU miner thread per rank) of the same processes."""
