@@ -136,7 +136,7 @@ def measure_share_latency(device_index: int = 0, seconds: float = 6.0, algorithm
         # the difficulty the pool enforced (from the share target it sent, SetTarget / OpenMiningChannelSuccess),
         # next to the one the probe asked for; the pool pins it (--fixed-difficulty)
         "share_difficulty": getattr(eng, "enforced_difficulty", None), "requested_difficulty": diff,
-        "pool_worker_difficulty": [w.get("difficulty") for w in pool.get("workers", [])],
+        "pool_fixed_difficulty": pool.get("fixed_difficulty"),
         "pool_validate_ms": pool.get("validate_ms"),
         "batch_nonces": batch_nonces, "seconds": round(getattr(eng, "recorded_seconds", seconds), 2),
         "warmup_seconds": 3.0,
