@@ -77,6 +77,31 @@ def window_rates(samples: list, t0: float, t1: float) -> dict[str, float]:
     return out
 
 
+def process_rss(sup_pid: int) -> dict:
+    """Resident set (MiB) of the node's processes by role: the supervisor, each rank (torch + the RCCL communicator),
+    and each rank's device process (the GPU miner)."""
+    try:
+        import psutil
+    except ImportError:
+        return {}
+    out: dict = {}
+    try:
+        sup = psutil.Process(sup_pid)
+        out["supervisor"] = round(sup.memory_info().rss / 2**20, 1)
+        for rank in sup.children():
+            try:
+                r = rank.environ().get("RANK", "?")
+                out[f"rank{r}"] = round(rank.memory_info().rss / 2**20, 1)
+                for c in rank.children():
+                    if "otedama_amd.engine.devproc" in " ".join(c.cmdline()):
+                        out[f"rank{r}_device_process"] = round(c.memory_info().rss / 2**20, 1)
+            except (psutil.NoSuchProcess, psutil.AccessDenied):
+                pass
+    except (psutil.NoSuchProcess, psutil.AccessDenied):
+        pass
+    return out
+
+
 def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_per_gpu: float = 25.0,
                  expected_per_gpu: float = 19e9, startup_timeout: float = 150.0, cpu: bool = False,
                  log_path: str | None = None) -> dict:
@@ -128,6 +153,7 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
         while _read(report).get("mono", 0.0) < t1 + 0.5 and time.monotonic() < t1 + 5:  # a sample past the window
             time.sleep(0.1)
         rep = _read(report)
+        res["rss_mib"] = process_rss(sup.pid)
     finally:
         sup.send_signal(signal.SIGTERM)
         try:
