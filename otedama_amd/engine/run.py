@@ -408,7 +408,7 @@ class Engine:
         if link is not None:
             hbs = {}
             try:
-                hbs = ms._heartbeats()
+                hbs = ms.heartbeats_snapshot()
             except Exception:  # noqa: BLE001 - store gone: shutting down
                 pass
             rep.update({

@@ -499,6 +499,15 @@ class NodeMinerSet:
     def hashrate_of(self, device_id: str) -> float:
         return self._rates.get(device_id, self.local.hashrate_of(device_id))
 
+    def heartbeats_snapshot(self) -> dict[int, dict]:
+        """The followers' latest heartbeats, read on a store connection of the caller's own (the engine's report
+        task runs in another thread than the leader loop, which owns ``self.store``)."""
+        if self.store is None:
+            return {}
+        if getattr(self, "_snap_store", None) is None:
+            self._snap_store = _clone(self.store)
+        return self._heartbeats(self._snap_store)
+
     # leader loop --------------------------------------------------------------
     def _post(self, op: dict) -> None:
         op["gen"] = op.get("gen", self._gen)
@@ -511,11 +520,12 @@ class NodeMinerSet:
                 if r != self.comm.info.orig_rank:
                     self._bell.ring(r)
 
-    def _heartbeats(self) -> dict[int, dict]:
+    def _heartbeats(self, store=None) -> dict[int, dict]:
+        store = store or self.store
         keys = [_k("hb", r) for r in range(1, self.capacity)]
         out = {}
         for r, key in zip(range(1, self.capacity), keys):
-            raw = _store_get(self.store, key)
+            raw = _store_get(store, key)
             if raw is not None:
                 try:
                     out[r] = json.loads(raw)
@@ -750,6 +760,7 @@ class NodeWorker:
         self._hb = _Heartbeat(self.store, comm.info.orig_rank, local, comm)
         self._bell = _Bell(self.store, comm.info.orig_rank)
         self._pending: list[dict] = []
+        self._hb.extra["pending"] = 0  # before the heartbeat thread starts: the share thread only updates it
         self.pending_dropped = 0  # shares dropped past PENDING_CAP (a leader that stays away)
         self._plock = threading.Lock()
         self._stop = threading.Event()
