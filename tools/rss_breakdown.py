@@ -4,7 +4,8 @@ Each variant is a fresh torch-free child (the device process's own import path) 
 phase, its RSS and an smaps breakdown grouped by mapping (anonymous private memory, the ROCm / HIP libraries, the
 extension, /dev/kfd and render-node mappings), and finally the production miner's SHA-256d rate over an exact
 device-timeline window. Variants: the default, the HIP queue ring buffers / context-save areas in device memory
-(HSA_ALLOCATE_QUEUE_DEV_MEM=1), one search stream instead of two (OTEDAMA_SEARCH_STREAMS=1), and both.
+(HSA_ALLOCATE_QUEUE_DEV_MEM=1), one search stream instead of two (OTEDAMA_SEARCH_STREAMS=1), both, and the two
+search streams sharing one hardware queue (GPU_MAX_HW_QUEUES=1).
 
 Usage: python tools/rss_breakdown.py [--seconds 6]   (one JSON line per variant)
 """
@@ -86,6 +87,8 @@ VARIANTS = [
     ("queue_dev_mem", {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1"}),
     ("one_search_stream", {"OTEDAMA_SEARCH_STREAMS": "1"}),
     ("queue_dev_mem+one_search_stream", {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1", "OTEDAMA_SEARCH_STREAMS": "1"}),
+    # both search streams multiplexed onto one normal-priority hardware queue (the control stream keeps its own)
+    ("hw_queues_1", {"GPU_MAX_HW_QUEUES": "1"}),
 ]
 
 
