@@ -139,6 +139,8 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["aborted_launches"] = s.aborted_launches;
   d["ring_hits"] = s.ring_hits;
   d["clock_calib_rtt_us"] = s.clock_calib_rtt_us;
+  d["clock_samples"] = s.clock_samples;
+  d["host_abort"] = s.host_abort;
   d["hashes_done_at_s"] = s.hashes_done_at_s;
   {
     py::dict ph;

@@ -96,7 +96,9 @@ struct MinerStats {
   uint64_t verify_dropped = 0;
   uint64_t verify_queue_peak = 0;     // deepest the scrypt verifier queue has been
   uint64_t launch_hashes = 0;         // hashes per launch of the last batch (capped from the share target)
-  double clock_calib_rtt_us = 0;      // round trip of the device-clock calibration that is in use
+  double clock_calib_rtt_us = 0;      // round trip of the start-up device-clock calibration
+  uint64_t clock_samples = 0;         // per-launch clock stamps folded into the device -> host clock mapping
+  bool host_abort = false;            // the abort word is stored by the CPU through the BAR (no control stream)
   // Device-timeline time (s, from the miner's start) at which the batches counted in `hashes` had completed: a
   // rate over two samples, (hashes1 - hashes0) / (done_at1 - done_at0), is exact instead of quantized by launches.
   double hashes_done_at_s = 0;

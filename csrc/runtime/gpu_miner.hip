@@ -7,10 +7,12 @@
 // therefore on its way to the pool while the launch that found it is still running, instead of after the
 // batch (2^29 nonces, ~28 ms) and its copy-back.
 //
-// Job switches: new work opens a new launch epoch and writes it to an uncached device word on a
-// control stream (hipStreamWriteValue32). Every wave polls that word once per grid-stride trip, so batches of
-// the old epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first
-// batch of the new work starts right behind them. The switch time (set_job -> new batch running) is recorded.
+// Job switches: new work opens a new launch epoch and writes it to an uncached device word. The CPU stores it
+// straight into VRAM through the PCIe BAR when the runtime lets the CPU agent map the word; otherwise the store is a
+// hipStreamWriteValue32 on a high-priority control stream, one more hardware queue (~190 MB of host memory for its
+// context-save area, profiles/r3/o_rss). Every wave polls that word once per grid-stride trip, so batches of the old
+// epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first batch of the new
+// work starts right behind them. The switch time (set_job -> new batch running) is recorded.
 //
 // Launch overlap: the two batches in flight sit on two streams (one per slot), so the next SHA-256d batch's waves
 // fill the CUs that the running batch's tail leaves idle; without it a 2^29-nonce launch (28 ms) lost ~2.5% to its
@@ -21,12 +23,18 @@
 // buffer per algorithm with the batches chained (the A/B baselines).
 //
 // Device time: s_memrealtime (100 MHz) is mapped to CLOCK_MONOTONIC by a probe kernel at start-up (min round
-// trip of several probes) and re-checked every 10 s by a calibration thread on a stream of its own (a probe
-// that queued behind busy CUs is rejected by its round trip), so a share carries the kernel's own hit time.
+// trip of several probes, before any search runs). After that every launch carries its own probe, queued on its
+// stream just ahead of the search kernel: the host sees the stamp land while polling the hit rings, and each
+// sighting bounds the offset from above (the store happened before it was seen). The mapping in use is the lowest
+// bound of the last 2 s, so it follows drift between the two clocks without a stream or thread of its own, and a
+// share carries the kernel's own hit time.
 //
 // Parity: the reference's worker sends each share as it is found (internal/miner/worker.go:262-275) and picks
 // up new work between 1024-nonce batches (worker.go:231-248).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -98,6 +106,35 @@ constexpr size_t kVerifyCap = 8192;                // scrypt candidates waiting 
 constexpr int kInflight = 2;
 constexpr double kRtHz = 100e6;
 constexpr auto kIdlePoll = std::chrono::microseconds(100);
+constexpr double kClockWindowS = 2.0;  // per-launch clock bounds kept for the device -> host mapping
+
+// Let the CPU store to a device allocation directly: grant the CPU agent access (the allocation is VRAM, reachable
+// through the PCIe BAR when the runtime exposes it) and confirm that the range is now mapped in this process before
+// anything touches it. False leaves the word device-only (stores then go through a stream).
+bool cpu_store_map(void* p, size_t n) {
+  hsa_agent_t cpu{};
+  auto pick = [](hsa_agent_t a, void* data) -> hsa_status_t {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+      *static_cast<hsa_agent_t*>(data) = a;
+      return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+  };
+  if (hsa_iterate_agents(pick, &cpu) != HSA_STATUS_INFO_BREAK) return false;
+  if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS) return false;
+  FILE* f = std::fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + n;
+  char line[512];
+  bool mapped = false;
+  while (!mapped && std::fgets(line, sizeof line, f)) {
+    unsigned long a = 0, b = 0;
+    mapped = std::sscanf(line, "%lx-%lx", &a, &b) == 2 && a <= lo && hi <= b;
+  }
+  std::fclose(f);
+  return mapped;
+}
 
 // Header variants of one stripe group (up to 128 consecutive positions sharing block 2). Built once per
 // (work generation, group) and shared by every launch of the group (~1000 launches at 2^29 nonces each).
@@ -143,6 +180,9 @@ struct Batch {
   HitRecord* ring_dev = nullptr;  // the same records, device address
   Sha256dVariant* d_vars = nullptr;
   Sha256dVariant* h_vars = nullptr;
+  uint64_t* h_clk = nullptr;  // this launch's clock probe (host-coherent; 0 until the probe ran)
+  uint64_t* d_clk = nullptr;
+  bool clk_pending = false;   // probe queued, its stamp not seen yet
   TraceId range = 0;
 };
 }  // namespace
@@ -193,16 +233,13 @@ void GpuMiner::loop() {
   OTD_HIP(hipSetDevice(device_));
   OTD_HIP(hipFree(nullptr));  // force runtime / context creation here so the phase below is honest
   phase("hip_set_device");
-  hipStream_t ctl = nullptr, cal = nullptr;
+  hipStream_t ctl = nullptr;      // control stream: only when the CPU cannot store the abort word itself
+  bool host_abort = false;       // the CPU stores the abort word through the BAR
   Batch slots[kInflight];
   uint32_t* d_abort = nullptr;   // uncached device word: the newest launch epoch that must keep running
   hipEvent_t ref_ev = nullptr;   // device-timeline origin of hashes_done_at_s
-  uint64_t* h_rt = nullptr;      // probe output (pinned, host-coherent)
-  uint64_t* d_rt = nullptr;      // its device address
-  std::thread cal_th;            // device-clock re-calibration
-  std::atomic<bool> cal_stop{false};
-  std::mutex cal_mu;
-  std::condition_variable cal_cv;
+  uint64_t* h_rt = nullptr;      // probe outputs (pinned, host-coherent): start-up probe, then one line per slot
+  uint64_t* d_rt = nullptr;      // their device address
   void* scratch = nullptr;       // scrypt pad, allocated on the first scrypt job (one half per slot)
   void* xbuf = nullptr;
   uint64_t* x11_h = nullptr;     // X11 intermediate digests (8 u64 planes x batch, one set per slot)
@@ -212,18 +249,9 @@ void GpuMiner::loop() {
     std::function<void()> f;
     ~Release() { f(); }
   } release{[&] {
-    if (cal_th.joinable()) {
-      {
-        std::lock_guard<std::mutex> g(cal_mu);
-        cal_stop = true;
-      }
-      cal_cv.notify_all();
-      cal_th.join();
-    }
     for (auto& s : slots)
       if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (ctl) (void)hipStreamSynchronize(ctl);
-    if (cal && cal != ctl) (void)hipStreamSynchronize(cal);
     for (auto& s : slots) {
       if (s.d_count) (void)hipFree(s.d_count);
       if (s.h_count) (void)hipHostFree(s.h_count);
@@ -242,7 +270,6 @@ void GpuMiner::loop() {
     for (auto& s : slots)
       if (s.stream && (&s == &slots[0] || s.stream != slots[0].stream)) (void)hipStreamDestroy(s.stream);
     if (ctl) (void)hipStreamDestroy(ctl);
-    if (cal && cal != ctl) (void)hipStreamDestroy(cal);
   }};
   // Search streams: one per in-flight batch, so a launch's tail overlaps the next launch's first waves; with
   // OTEDAMA_SEARCH_STREAMS=1 the batches share one stream (one hardware queue less, ~190 MB of host memory).
@@ -252,21 +279,34 @@ void GpuMiner::loop() {
     if (one_stream && i > 0) slots[i].stream = slots[0].stream;
     else OTD_HIP(hipStreamCreateWithFlags(&slots[i].stream, hipStreamNonBlocking));
   }
-  // The abort-word writes and the clock probes must never queue behind a search kernel: HIP multiplexes streams of
-  // one priority onto GPU_MAX_HW_QUEUES (4) hardware queues, and with two search streams plus torch's in the same
-  // process a control stream can land on a busy queue, where its write waits for a whole 2^32-hash launch (the
-  // job switch grew from 0.3 ms to ~110 ms). High-priority streams come from a separate queue pool. The probes share
-  // the control stream: every hardware queue costs ~190 MB of pinned host memory (tools/stream_rss.hip,
-  // profiles/r3/o_rss), so the miner holds three (two search, one control) instead of four.
-  int prio_lo = 0, prio_hi = 0;
-  OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  OTD_HIP(hipStreamCreateWithPriority(&ctl, hipStreamNonBlocking, prio_hi));
-  cal = ctl;
-  phase("streams");
+  // The abort word must never wait behind a search kernel. The CPU stores it itself when it can map the word
+  // (OTEDAMA_HOST_ABORT=0 forces the stream form). Otherwise the store goes on a high-priority stream: HIP
+  // multiplexes streams of one priority onto GPU_MAX_HW_QUEUES (4) hardware queues, and with two search streams
+  // plus torch's in the same process a control stream can land on a busy queue, where its write waits for a whole
+  // 2^32-hash launch (the job switch grew from 0.3 ms to ~110 ms); high-priority streams come from a separate pool.
+  // Every hardware queue costs ~190 MB of host memory (tools/stream_rss.hip, profiles/r3/o_rss).
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
   OTD_HIP(hipMemset(d_abort, 0, 256));
-  OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_rt), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  OTD_HIP(hipDeviceSynchronize());
+  const char* ha_env = std::getenv("OTEDAMA_HOST_ABORT");
+  host_abort = !(ha_env && ha_env[0] == '0') && cpu_store_map(d_abort, 256);
+  if (!host_abort) {
+    int prio_lo = 0, prio_hi = 0;
+    OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    OTD_HIP(hipStreamCreateWithPriority(&ctl, hipStreamNonBlocking, prio_hi));
+  }
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.host_abort = host_abort;
+  }
+  phase("streams");
+  OTD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_rt), 64 * (1 + kInflight), hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(h_rt, 0, 64 * (1 + kInflight));
   OTD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_rt), h_rt, 0));
+  for (int i = 0; i < kInflight; ++i) {
+    slots[i].h_clk = h_rt + 8 * (1 + i);
+    slots[i].d_clk = d_rt + 8 * (1 + i);
+  }
   phase("control_words");
   for (auto& s : slots) {
     OTD_HIP(hipMalloc(&s.d_count, 64));
@@ -306,9 +346,7 @@ void GpuMiner::loop() {
   // ---- device clock -> host clock
   std::atomic<double> rt_offset{0.0};  // host monotonic seconds at device realtime 0
   double calib_rtt = 1e9;
-  // One probe: (host midpoint, device realtime) bracketed by the launch and the stream sync; the tightest
-  // bracket wins, and a later probe replaces it only when its round trip is within 2x of the best (50 us floor):
-  // that tracks clock drift without accepting a probe that waited for a CU behind the search waves.
+  // Start-up: probes bracketed by the launch and the stream sync on an idle device; the tightest bracket wins.
   auto probe = [&](hipStream_t on) {
     __atomic_store_n(h_rt, 0ull, __ATOMIC_RELEASE);
     const double t0 = monotonic_seconds();
@@ -317,9 +355,9 @@ void GpuMiner::loop() {
     OTD_HIP(hipStreamSynchronize(on));
     const double t1 = monotonic_seconds();
     const uint64_t rt = __atomic_load_n(h_rt, __ATOMIC_ACQUIRE);
-    if (rt && (t1 - t0) < std::max(2.0 * calib_rtt, 50e-6)) {
+    if (rt && (t1 - t0) < calib_rtt) {
       rt_offset.store(0.5 * (t0 + t1) - double(rt) / kRtHz);
-      calib_rtt = std::min(calib_rtt, t1 - t0);
+      calib_rtt = t1 - t0;
       std::lock_guard<std::mutex> g(stats_mu_);
       stats_.clock_calib_rtt_us = (t1 - t0) * 1e6;
     }
@@ -328,33 +366,32 @@ void GpuMiner::loop() {
   rt_offset_ = rt_offset.load();
   phase("clock_calibration");
   OTD_HIP(hipEventCreate(&ref_ev));
-  OTD_HIP(hipEventRecord(ref_ev, ctl));
+  OTD_HIP(hipEventRecord(ref_ev, slots[0].stream));  // before any search: the device-timeline origin
   bool first_switch = true;
-  cal_th = std::thread([&] {
-    try {
-      OTD_HIP(hipSetDevice(device_));
-      std::unique_lock<std::mutex> lk(cal_mu);
-      while (!cal_cv.wait_for(lk, std::chrono::seconds(10), [&] { return cal_stop.load(); })) {
-        lk.unlock();
-        for (int t = 0; t < 4 && !cal_stop.load(); ++t) probe(cal);
-        lk.lock();
-      }
-    } catch (const std::exception&) {
-      // a failing probe is a device fault the miner thread reports through its own launches
+  // Running: every launch's probe gives an upper bound on the offset (host time it was seen minus its device
+  // time); the lowest bound of the last kClockWindowS seconds is the mapping in use.
+  std::deque<std::pair<double, double>> clk_bounds;  // (seen at, offset bound), oldest first
+  auto clock_seen = [&](Batch& b, double now) {
+    const uint64_t rt = __atomic_load_n(b.h_clk, __ATOMIC_ACQUIRE);
+    if (!rt) return;
+    b.clk_pending = false;
+    const double bound = now - double(rt) / kRtHz;
+    // monotonic deque: bounds increase from front to back, so the front is the window's minimum
+    while (!clk_bounds.empty() && clk_bounds.back().second >= bound) clk_bounds.pop_back();
+    clk_bounds.emplace_back(now, bound);
+    while (now - clk_bounds.front().first > kClockWindowS) clk_bounds.pop_front();  // the newest always stays
+    rt_offset.store(clk_bounds.front().second);
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.clock_samples += 1;
+  };
+  auto write_abort = [&](uint32_t e) {
+    if (host_abort) {
+      __atomic_store_n(d_abort, e, __ATOMIC_RELEASE);
+      _mm_sfence();  // out of the write-combining buffers and onto the bus now
+    } else {
+      OTD_HIP(hipStreamWriteValue32(ctl, d_abort, e, 0));
     }
-  });
-  // The thread uses locals declared after `release`: join it before they go out of scope (on every exit path).
-  struct Joiner {
-    std::function<void()> f;
-    ~Joiner() { f(); }
-  } cal_join{[&] {
-    {
-      std::lock_guard<std::mutex> g(cal_mu);
-      cal_stop = true;
-    }
-    cal_cv.notify_all();
-    if (cal_th.joinable()) cal_th.join();
-  }};
+  };
 
   std::shared_ptr<Group> group;  // current stripe group
   uint64_t cur_gen = ~0ull;
@@ -383,7 +420,7 @@ void GpuMiner::loop() {
     if (want_gen != epoch_gen) {
       epoch_gen = want_gen;
       ++epoch;
-      if (!fifo.empty()) OTD_HIP(hipStreamWriteValue32(ctl, d_abort, epoch, 0));
+      if (!fifo.empty()) write_abort(epoch);
       if (job) { switch_pending = true; switch_t0 = set_at; }
     }
     if (gen_out) *gen_out = gen;
@@ -588,6 +625,10 @@ void GpuMiner::loop() {
     const int slot_i = int(&s - slots);
     OTD_HIP(hipMemsetAsync(s.d_count, 0, 64, stream));
     OTD_HIP(hipEventRecord(s.start, stream));
+    __atomic_store_n(s.h_clk, 0ull, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(otd_rt_probe, dim3(1), dim3(64), 0, stream, s.d_clk);
+    OTD_HIP(hipGetLastError());
+    s.clk_pending = true;
     s.enq_host = monotonic_seconds();
     rt_offset_ = rt_offset.load();
     s.rt_enq = uint32_t(uint64_t((s.enq_host - rt_offset_) * kRtHz));
@@ -668,7 +709,10 @@ void GpuMiner::loop() {
     auto job = check_epoch(&gen);
     bool progressed = false;
     if (job && gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
-    // 1) hits of the batches in flight, oldest first
+    // 1) hits of the batches in flight, oldest first, and the clock stamps of launches that just started
+    const double t_poll = monotonic_seconds();
+    for (int i : fifo)
+      if (slots[i].clk_pending) clock_seen(slots[i], t_poll);
     for (int i : fifo) progressed |= drain_ring(slots[i], ~0u, job, gen) > 0;
     // 2) retire completed batches (the two streams may complete out of issue order)
     for (auto it = fifo.begin(); it != fifo.end();) {
@@ -737,7 +781,11 @@ void GpuMiner::loop() {
   // drain: let the batches in flight finish (abort them first: the miner is stopping)
   if (!fifo.empty()) {
     ++epoch;
-    (void)hipStreamWriteValue32(ctl, d_abort, epoch, 0);
+    try {
+      write_abort(epoch);
+    } catch (const std::exception&) {
+      // a faulted device: the drain below reports it
+    }
   }
   uint64_t gen = 0;
   auto job = peek_job(&gen, nullptr);

@@ -120,7 +120,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         # first, so the extension binds to the runtime already in the process
         # (two HIP/HSA runtimes in one process fail to enumerate the GPU).
         link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread", "-lcrypto",
-                "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx"]
+                "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lhsa-runtime64"]
         _compile(link, verbose)
         os.replace(tmp, out)
     return out

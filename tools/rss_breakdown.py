@@ -78,12 +78,16 @@ time.sleep(secs)
 st = m.stats()
 out["sha256d_hps"] = (st["hashes"] - h0) / max(st["hashes_done_at_s"] - d0, 1e-9)
 out["faulted"] = st["faulted"]
+out["host_abort"] = st.get("host_abort")
+out["clock_samples"] = st.get("clock_samples")
 m.stop()
 print(json.dumps(out))
 '''
 
 VARIANTS = [
     ("default", {}),
+    # the round-3 layout: the abort word stored through a high-priority control stream (one more hardware queue)
+    ("control_stream", {"OTEDAMA_HOST_ABORT": "0"}),
     ("queue_dev_mem", {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1"}),
     ("one_search_stream", {"OTEDAMA_SEARCH_STREAMS": "1"}),
     ("queue_dev_mem+one_search_stream", {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1", "OTEDAMA_SEARCH_STREAMS": "1"}),
