@@ -28,6 +28,18 @@ __device__ __forceinline__ uint32_t abort_issue(const otedama::HitSink& s) {
   return __hip_atomic_load(const_cast<uint32_t*>(s.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Scalar-unit poll: one s_load from the word's (uniform) address straight into an SGPR, glc so it is served from
+// memory and not from a stale scalar-cache line, and waited for in the same statement (the compiler does not track
+// the counter of a load issued in asm). It holds no VGPR, so a loop at its VGPR budget (scrypt ROMix, 64) can poll
+// without new spills. The wait also retires the wave's LDS operations in flight: place it where the loop waits for
+// those anyway.
+__device__ __forceinline__ uint32_t abort_peek_scalar(const otedama::HitSink& s) {
+  if (s.abort == nullptr) return s.epoch;
+  uint32_t v;
+  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(s.abort));
+  return v;
+}
+
 // True once the host has moved the abort word past this batch's epoch (serial-number compare: wrap-safe).
 __device__ __forceinline__ bool abort_newer(uint32_t word, uint32_t epoch) {
   return static_cast<int32_t>(word - epoch) > 0;

@@ -20,6 +20,8 @@
 
 #include "cdna_bitops.h"
 #include "hitsink_dev.h"
+#include <cstdlib>
+
 #include "otedama/job.h"
 
 namespace {
@@ -307,17 +309,27 @@ __device__ __forceinline__ void coop_consume(uint32_t X[32], uint4* __restrict__
 }
 
 // The abort word (otedama/hitsink.h) is polled before each ROMix phase (a wave's hash takes ~32 ms, its phases
-// ~16 ms each): an obsolete batch stops within half a hash instead of finishing two launches. Polling inside the
-// BlockMix loops made the allocator reload spilled values every iteration (64-VGPR budget), and splitting each
-// loop in two for quarter polls cost 0.9% of ROMix time (four loop bodies in the instruction cache instead of
-// two, profiles/r3/f_regressions). Returns false when aborted.
-template <int LCPOL>
+// ~16 ms each), and every POLL iterations of the write phase by the scalar unit. A vector poll inside the BlockMix
+// loops made the allocator reload spilled values every iteration (64-VGPR budget), and splitting each loop in two
+// cost 0.9% of ROMix time (four loop bodies in the instruction cache, profiles/r3/f_regressions). The scalar poll
+// between chunks of the write loop keeps that loop's body and allocation (+1 instruction per iteration, no new
+// spill); in the read loop the same structure cost 2 scratch reloads and ~30 instructions per iteration, so the read
+// phase keeps only its boundary poll. The miner runs its two batches half a hash apart (gpu_miner.hip), so one of
+// them is always in its write phase and stops within ~1 ms of new work. POLL = 1024: boundary polls only.
+// Returns false when aborted.
+template <int LCPOL, int POLL>
 __device__ __forceinline__ bool scrypt_romix_coop(uint32_t X[32], __amdgpu_buffer_rsrc_t rs, uint4* __restrict__ tile,
                                                   uint32_t lane, const otedama::HitSink& sink) {
+  static_assert(POLL > 0 && 1024 % POLL == 0, "poll interval must divide the ROMix loop");
   if (abort_newer(abort_peek(sink), sink.epoch)) return false;
-  for (uint32_t i = 0; i < 1024; ++i) {
-    coop_store_entry(X, rs, tile, lane, i);
-    blockmix(X);
+  // chunks of POLL iterations, the scalar poll (no VGPR) between them: an exit edge inside the loop itself cost 10
+  // more spilled VGPRs
+  for (uint32_t c = 0; c < 1024; c += POLL) {
+    if (c && abort_newer(abort_peek_scalar(sink), sink.epoch)) return false;
+    for (uint32_t i = c; i < c + POLL; ++i) {
+      coop_store_entry(X, rs, tile, lane, i);
+      blockmix(X);
+    }
   }
   if (abort_newer(abort_peek(sink), sink.epoch)) return false;
   for (int i = 0; i < 1024; ++i) {
@@ -403,7 +415,7 @@ __global__ __launch_bounds__(256) void otd_scrypt_romix(uint32_t count, uint4* _
   }
 }
 
-template <int LCPOL>
+template <int LCPOL, int POLL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop(uint32_t count, uint4* __restrict__ xbuf,
                                                              uint4* __restrict__ V, const otedama::HitSink sink) {
   __shared__ uint4 tiles[4 * 256];  // 4 waves x 4 KiB half-tiles
@@ -423,7 +435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (uint64_t i = slot; i < count; i += nslots) {
     uint32_t X[32];
     load_entry(xbuf + (i << 3), X);
-    if (!scrypt_romix_coop<LCPOL>(X, rs, tile, lane, sink)) return;  // aborted: pbkdf_out publishes nothing
+    if (!scrypt_romix_coop<LCPOL, POLL>(X, rs, tile, lane, sink)) return;  // aborted: pbkdf_out publishes nothing
     store_entry(xbuf + (i << 3), X);
   }
 }
@@ -522,6 +534,15 @@ uint64_t scrypt_scratch_bytes(int grid, int gap) {
   return uint64_t(grid) * 256ull * (1024ull / uint64_t(gap)) * 128ull;
 }
 
+// OTEDAMA_SCRYPT_POLL=0: the ROMix write loop without its scalar abort polls (the A/B baseline; boundary polls only).
+static bool scrypt_write_polls() {
+  static const bool on = [] {
+    const char* v = std::getenv("OTEDAMA_SCRYPT_POLL");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
 // gap: 1/2/4 = per-lane ROMix with that lookup gap; kScryptCoop = lane-cooperative ROMix (gap 1).
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
@@ -537,7 +558,10 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
     case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
-      hipLaunchKernelGGL(otd_scrypt_romix_coop<2>, dim3(grid), dim3(256), 0, stream, count64, X, V, sink);
+      if (scrypt_write_polls())
+        hipLaunchKernelGGL((otd_scrypt_romix_coop<2, 64>), dim3(grid), dim3(256), 0, stream, count64, X, V, sink);
+      else
+        hipLaunchKernelGGL((otd_scrypt_romix_coop<2, 1024>), dim3(grid), dim3(256), 0, stream, count64, X, V, sink);
       break;
     case kScryptLaneW8:
       hipLaunchKernelGGL(otd_scrypt_romix_w8, dim3(grid), dim3(256), 0, stream, count, X, V);
