@@ -118,9 +118,11 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         # equal device count per rank keeps the stripes disjoint: the rank's GPU, or (a CPU-only rehearsal node over
         # gloo) one CPU miner per rank
         cfg.mining.cpu_threads = 0 if info.device.type == "cuda" else max(1, cfg.mining.cpu_threads)
+        # gloo is a CPU transport: its node buffers stay in host memory (RCCL's live on the rank's GPU)
+        host_buffers = info.backend == "gloo"
         if info.orig_rank > 0:
-            return _run_node_worker(cfg, info, NodeComm(info), stdout, joining)
-        node = NodeComm(info)
+            return _run_node_worker(cfg, info, NodeComm(info, host_buffers=host_buffers), stdout, joining)
+        node = NodeComm(info, host_buffers=host_buffers)
         no_tui = True
     logln("info", i18n.STARTUP_READY)
     pool_url = cfg.pools[0].url if cfg.pools else C.DEFAULT_POOL_URL

@@ -32,6 +32,7 @@ import os
 import time
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -157,14 +158,19 @@ class NodeComm:
     """R1/R2/R3 over torch.distributed with preallocated fixed-size buffers.
 
     ``bounded=True`` (the node): every collective is issued async and polled against ``deadline`` seconds; a
-    collective that fails or times out raises (CollectiveTimeout / RuntimeError) instead of blocking forever."""
+    collective that fails or times out raises (CollectiveTimeout / RuntimeError) instead of blocking forever.
 
-    def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0):
+    ``host_buffers=True``: the buffers live in host memory and there is no comm stream. That is the node's layout
+    over gloo, a CPU transport: with device buffers every gloo collective adds device<->host staging and stream
+    syncs (a 2-rank R2 gather took 4.7 ms p50 on the MI355X that way)."""
+
+    def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0, host_buffers: bool = False):
         self.info = info
         self.bounded = bounded
         self.deadline = deadline
         self.collectives = 0  # device collectives issued by this rank (node tick accounting)
-        dev = info.device
+        dev = torch.device("cpu") if host_buffers else info.device
+        self.dev = dev
         self._job = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8, device=dev)
         self._slots = torch.zeros(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
         self._counters = torch.zeros(COUNTER_WORDS, dtype=torch.int64, device=dev)
@@ -173,7 +179,7 @@ class NodeComm:
         self.stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
 
     def _alloc_world(self, world: int) -> None:
-        dev = self.info.device
+        dev = self.dev
         self._gathered = torch.zeros(world, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
         self._counter_rows = torch.zeros(world, COUNTER_WORDS, dtype=torch.int64, device=dev)
 
@@ -255,34 +261,30 @@ class NodeComm:
     # ---------------------------------------------------------------- R2
     def gather_shares(self, shares: list[dict], device_index: int = 0) -> list[dict]:
         """All-gather up to SHARE_SLOTS share records per rank; returns every rank's shares."""
-        host = torch.zeros(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64)
+        rows = np.zeros((SHARE_SLOTS, SHARE_WORDS), dtype=np.int64)
         for i, s in enumerate(shares[:SHARE_SLOTS]):
             e = int(s.get("epoch", 0))
             en2 = int(s.get("extranonce2", 0))
-            host[i] = torch.tensor([
-                e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
-                en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
-                int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6),
-            ], dtype=torch.int64)
-        self._slots.copy_(host)
+            rows[i] = (e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
+                       en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
+                       int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6))
+        self._slots.copy_(torch.from_numpy(rows))
         if self.info.world_size > 1:
             self._collect(lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
                                                                 async_op=a))
         else:
             self._gathered[0].copy_(self._slots)
         out = []
-        g = self._gathered.cpu().tolist()
-        for r in range(self.info.world_size):
-            for rec in g[r]:
-                if not rec[1] >> 31:
-                    continue
-                out.append({
-                    "epoch": rec[0] | ((rec[1] & 0x7FFFFFFF) << 32), "nonce": rec[2] & 0xFFFFFFFF,
-                    "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
-                    "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
-                    "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6, "device_found_at": rec[9] / 1e6,
-                    "orig_rank": self.info.members[r] if r < len(self.info.members) else r,
-                })
+        g = self._gathered.cpu().numpy()
+        for r, i in zip(*np.nonzero(g[:, :, 1] >> 31)):  # valid records only, in rank then slot order
+            r, rec = int(r), g[r, i].tolist()
+            out.append({
+                "epoch": rec[0] | ((rec[1] & 0x7FFFFFFF) << 32), "nonce": rec[2] & 0xFFFFFFFF,
+                "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
+                "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
+                "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6, "device_found_at": rec[9] / 1e6,
+                "orig_rank": self.info.members[r] if r < len(self.info.members) else r,
+            })
         return out
 
     # ---------------------------------------------------------------- R3
@@ -312,7 +314,7 @@ class NodeComm:
         return self._ctl.cpu().tolist()
 
     def allreduce_max(self, value: float) -> float:
-        t = torch.tensor([value], dtype=torch.float64, device=self.info.device)
+        t = torch.tensor([value], dtype=torch.float64, device=self.dev)
         if self.info.world_size > 1:
             self._collect(lambda a: dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=a))
         return float(t.item())

@@ -20,9 +20,10 @@ hundreds per second. Hashing never waits on any of this: kernels run in each ran
 so a GPU fault kills that child, not the rank that holds the RCCL communicator and, on rank 0, the pool session.
 
 Nothing on the share path sleeps on a timer: a follower whose device process pushed a share rings the leader's
-doorbell, the leader posts an R2 gather and rings every follower's doorbell, and the followers enter the gather at
-once (a doorbell is a one-byte datagram on loopback; the store stays the source of truth, so a lost datagram costs
-one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
+doorbell, the leader rings every follower's doorbell with the R2 gather op itself and then logs it in the store, and
+the followers enter the gather at once (a doorbell is a loopback datagram; an op travels inline, so no store round
+trip sits between the leader's decision and a follower entering the collective; the store stays the source of truth,
+so a lost datagram costs one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
 pool accept for remote ranks' shares the same way as for its own.
 
 Rank loss (reference analogues: the partial-failure-tolerant detector
@@ -88,9 +89,10 @@ def _clone(store):
 
 
 class _Bell:
-    """A rank's doorbell: a loopback UDP socket whose port is published at otd/bell/<orig>. ``ring(r)`` sends one
-    byte to rank r (ports are looked up in the store and cached for a couple of seconds: a restarted rank has a new
-    one); ``wait(t)`` blocks until a datagram arrives or t passes and returns the bytes received."""
+    """A rank's doorbell: a loopback UDP socket whose port is published at otd/bell/<orig>. ``ring(r, msg)`` sends
+    one datagram to rank r (ports are looked up in the store and cached for a couple of seconds: a restarted rank has
+    a new one): b"s" (a follower has shares), b"o" (look at the op log), or b"o" + an op inline (``op_msg``).
+    ``wait(t)`` blocks until a datagram arrives or t passes and returns the datagrams received."""
 
     PORT_TTL = 2.0
 
@@ -132,8 +134,8 @@ class _Bell:
         except OSError:
             pass  # the store stays authoritative: the peer's fallback poll picks the work up
 
-    def wait(self, timeout: float) -> bytes:
-        got = b""
+    def wait(self, timeout: float) -> list[bytes]:
+        got: list[bytes] = []
         try:
             ready, _, _ = select.select([self.sock], [], [], max(timeout, 0.0))
         except (OSError, ValueError):
@@ -141,7 +143,7 @@ class _Bell:
         if ready:
             while True:
                 try:
-                    got += self.sock.recv(64)
+                    got.append(self.sock.recv(65536))
                 except (BlockingIOError, OSError):
                     break
         return got
@@ -151,6 +153,21 @@ class _Bell:
             self.sock.close()
         except OSError:
             pass
+
+
+def op_msg(k: int, raw: str) -> bytes:
+    """Doorbell datagram carrying op ``k`` of the log (its JSON exactly as stored at otd/op/<k>)."""
+    return b"o" + k.to_bytes(8, "little") + raw.encode()
+
+
+def parse_op_msg(msg: bytes) -> tuple[int, dict] | None:
+    """(k, op) of an inline-op datagram; None for a bare wake-up or anything unparsable."""
+    if len(msg) <= 9 or msg[:1] != b"o":
+        return None
+    try:
+        return int.from_bytes(msg[1:9], "little"), json.loads(msg[9:])
+    except ValueError:
+        return None
 
 
 class _Heartbeat:
@@ -511,14 +528,17 @@ class NodeMinerSet:
     # leader loop --------------------------------------------------------------
     def _post(self, op: dict) -> None:
         op["gen"] = op.get("gen", self._gen)
-        self.store.set(_k("op", self._op_k), json.dumps(op))
-        self._op_k += 1
-        self.store.set(_k("next"), str(self._op_k))
-        if self._bell is not None:  # the followers' op loops wait on their doorbells
+        raw, k = json.dumps(op), self._op_k
+        if self._bell is not None:  # the followers' op loops wait on their doorbells: the op rides the datagram
+            msg = op_msg(k, raw)
             targets = op["members"] if op.get("op") == "reform" else self.comm.info.members
             for r in targets:
                 if r != self.comm.info.orig_rank:
-                    self._bell.ring(r)
+                    self._bell.ring(r, msg)
+        # then the log (while the followers wake): a follower that missed the datagram, or joins later, reads it here
+        self.store.set(_k("op", k), raw)
+        self._op_k += 1
+        self.store.set(_k("next"), str(self._op_k))
 
     def _heartbeats(self, store=None) -> dict[int, dict]:
         store = store or self.store
@@ -722,7 +742,7 @@ class NodeMinerSet:
             return
         got = self._bell.wait(timeout)
         self._wake.clear()
-        if b"s" in got:
+        if any(m[:1] == b"s" for m in got):
             self._gather_wanted = True
 
     def _take(self, shares: list[dict]) -> None:
@@ -808,15 +828,21 @@ class NodeWorker:
             k = int(raw) if raw is not None else 0
             self.store.set(_k("join", info.orig_rank), "1")
         broken = False  # the current group failed a collective: skip collectives until the next re-form
+        inline: dict[int, dict] = {}  # ops that arrived on the doorbell ahead of this loop reaching them
         try:
             while True:
-                key = _k("op", k)
-                # the leader rings this rank's doorbell after posting an op; the store check is the truth, the
-                # fallback wait bounds a lost datagram
-                if not self.store.check([key]):
-                    self._bell.wait(BELL_FALLBACK)
-                    continue
-                op = json.loads(self.store.get(key))
+                # the leader rings this rank's doorbell with each op as it posts it; the store log is the truth for
+                # an op whose datagram was lost, and the fallback wait bounds that case
+                op = inline.pop(k, None)
+                if op is None:
+                    key = _k("op", k)
+                    if not self.store.check([key]):
+                        for msg in self._bell.wait(BELL_FALLBACK):
+                            got = parse_op_msg(msg)
+                            if got is not None and got[0] >= k and len(inline) < 4096:
+                                inline[got[0]] = got[1]
+                        continue
+                    op = json.loads(self.store.get(key))
                 k += 1
                 kind = op["op"]
                 if kind == "stop":

@@ -142,6 +142,50 @@ def test_nodecomm_single_rank_paths(n):
     assert got[0]["extranonce2"] == 1 << 40 and got[0]["found_at"] == 12.5 and got[0]["epoch"] == 3
 
 
+def test_host_buffers_keep_node_collectives_off_the_device():
+    """Over gloo the node's buffers live in host memory (no comm stream); records round-trip in rank/slot order
+    with every field, and empty slots are skipped."""
+    import torch
+
+    from otedama_amd.parallel.comm import SHARE_SLOTS, DistInfo, NodeComm
+
+    c = NodeComm(DistInfo(backend="gloo"), host_buffers=True)
+    assert c.dev == torch.device("cpu") and c.stream is None and c._slots.device.type == "cpu"
+    shares = [{"epoch": (5 << 32) | 9, "nonce": 0xFFFFFFFF - i, "ntime": 100 + i, "version": 0x20000000 | i,
+               "extranonce2": i << 33, "found_at": 1.25 + i, "device_found_at": 1.0 + i} for i in range(SHARE_SLOTS + 3)]
+    got = c.gather_shares(shares)
+    assert len(got) == SHARE_SLOTS  # one gather carries at most SHARE_SLOTS per rank
+    for i, g in enumerate(got):
+        s = shares[i]
+        assert (g["epoch"], g["nonce"], g["ntime"], g["version"], g["extranonce2"]) == \
+            (s["epoch"], s["nonce"], s["ntime"], s["version"], s["extranonce2"])
+        assert g["found_at"] == s["found_at"] and g["device_found_at"] == s["device_found_at"] and g["orig_rank"] == 0
+    assert c.gather_shares([]) == []
+
+
+def test_ops_ride_the_doorbell_datagram():
+    """The leader's op travels inline in the follower's doorbell datagram (no store round trip on the share path);
+    bare wake-ups and share rings parse as no op."""
+    from otedama_amd.parallel.node import _Bell, op_msg, parse_op_msg
+
+    raw = json.dumps({"op": "gather", "gen": 3})
+    assert parse_op_msg(op_msg(17, raw)) == (17, {"op": "gather", "gen": 3})
+    assert parse_op_msg(b"o") is None and parse_op_msg(b"s") is None and parse_op_msg(b"o" + bytes(8) + b"{") is None
+    a, b = _Bell(None, 0), _Bell(None, 1)
+    try:
+        a._ports[1] = (b.port, time.monotonic())
+        a.ring(1, op_msg(4, raw))
+        a.ring(1, b"s")
+        got = []
+        end = time.monotonic() + 2
+        while len(got) < 2 and time.monotonic() < end:
+            got += b.wait(0.1)
+        assert [parse_op_msg(m) for m in got] == [(4, {"op": "gather", "gen": 3}), None]
+    finally:
+        a.close()
+        b.close()
+
+
 def _blob_worker(rank: int, port: int, out_path: str) -> None:
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
