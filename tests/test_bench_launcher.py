@@ -95,6 +95,35 @@ def test_driver_torchrun_invocation():
     assert d["hits_duplicate"] == 0 and d["hits_verified"] == d["hits_found"]
 
 
+@pytest.mark.timeout(400)
+def test_driver_torchrun_invocation_with_the_node_section():
+    """The driver's N>1 command line end to end, node section included: torchrun's ranks run the kernel sections,
+    then rank 0 (still a torchrun worker, its agent's store on MASTER_PORT) starts `otedama node --gpus N` with its
+    own supervisor store, and the JSON carries that node's object."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "4",
+                          "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--node-seconds", "3",
+                          "--node-warmup", "2", "--cpu-seconds", "0"],
+                         capture_output=True, text=True, timeout=360, env=e, cwd=ROOT)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d["n_gpus"] == 4 and d["rccl_ranks_seen"] == [0, 1, 2, 3]
+    node = d["node"]
+    assert "error" not in node, node
+    assert node["n_ranks"] == 4 and node["ranks_seen"] == [0, 1, 2, 3] and node["exit_code"] == 0
+    assert all(r > 0 for r in node["per_rank_hashes_per_sec"]) and node["accepted_remote_in_window"] > 0
+    assert node["rejected"] == 0 and node["pool_rejected"] == 0
+
+
 def test_bench_ranks_get_a_long_collective_bound(monkeypatch):
     """The bench is not the fault-tolerant node: its ranks run with a 600 s collective bound (a cold rank start on
     a fresh 8-GPU node must not trip the node's 30 s default), unless the caller set one."""
