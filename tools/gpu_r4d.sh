@@ -9,6 +9,7 @@ mkdir -p $D
 export TMPDIR=/tmp
 export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
 HW1=GPU_MAX_HW_QUEUES=1
+timeout -k 10 60 tools/bin/queue_rss > $D/queue_rss_default.json && GPU_MAX_HW_QUEUES=1 timeout -k 10 60 tools/bin/queue_rss > $D/queue_rss_hw1.json && cat $D/queue_rss_*.json &&
 timeout -k 10 300 python tools/ab_miner.py --a . --b . --algo sha256d --rounds 6 --seconds 6 --env-b $HW1 > $D/ab_sha256d_hw1.json 2> $D/ab_sha256d_hw1.err && cat $D/ab_sha256d_hw1.json &&
 timeout -k 10 400 python tools/ab_miner.py --a . --b . --algo scrypt --rounds 4 --seconds 8 --env-b $HW1 > $D/ab_scrypt_hw1.json 2> $D/ab_scrypt_hw1.err && cat $D/ab_scrypt_hw1.json &&
 timeout -k 10 300 python tools/ab_miner.py --a . --b . --algo x11 --rounds 4 --seconds 6 --env-b $HW1 > $D/ab_x11_hw1.json 2> $D/ab_x11_hw1.err && cat $D/ab_x11_hw1.json &&
