@@ -89,6 +89,8 @@ def parse_args(argv=None):
     ap.add_argument("--scrypt-gap", type=int, default=1)
     ap.add_argument("--scrypt-kernel", choices=("coop", "lane"), default="coop")
     ap.add_argument("--x11-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
+    ap.add_argument("--miner-seconds", type=float, default=-1.0,
+                    help="scrypt / X11 through the production GpuMiner: recorded seconds each (-1 = 8 on GPUs; 0 = skip)")
     ap.add_argument("--seed", type=int, default=1,
                     help="synthetic header seed: the hit count of a seed is one Poisson draw, repeated on every run")
     ap.add_argument("--no-latency", action="store_true")
@@ -503,6 +505,48 @@ def run_rank(args) -> int:
                     "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20",
                     "hits_expected": _poisson(xfound, xtotal, xtarget_int)[0]}
         del xs
+        torch.cuda.empty_cache()
+
+    # ------------------------------------------------- scrypt and X11 through the production miner
+    # The kernel sections above time the ops-API launches one after another. The device process's GpuMiner runs
+    # scrypt as two half-grid batches side by side and X11 with a digest plane per slot; its exact rate over whole
+    # launches, with every share re-verified, is the scrypt / X11 figure (the kernel-path rate stays beside it).
+    scrypt_kernel_hps, x11_kernel_hps = scrypt_hps, x11_hps
+    miner_s = args.miner_seconds if args.miner_seconds >= 0 else (0.0 if cpu else 8.0)
+    if miner_s > 0:
+        from otedama_amd.engine.miner_probe import measure_miner
+        from otedama_amd.models.algorithms import ALGORITHMS
+
+        for algo, tgt in (("scrypt", ALGORITHMS["scrypt"].diff1), ("x11", (1 << 236) - 1)):
+            if (algo == "scrypt" and ssteps <= 0) or (algo == "x11" and xsteps <= 0):
+                continue
+            barrier(info)
+            try:
+                r = measure_miner(N, dev.index or 0, algo, tgt, seconds=miner_s, rank=info.rank, world=world,
+                                  seed=args.seed)
+                err = ""
+            except Exception as exc:  # noqa: BLE001 - auxiliary: the kernel-path figure stays
+                r, err = {"hashes_per_sec": 0.0, "shares": 0, "shares_rechecked": 0, "shares_recheck_ok": 0,
+                          "faulted": True}, f"{type(exc).__name__}: {exc}"
+            tot, shares_n, chk, chk_ok = comm.allreduce_counters(int(r["hashes_per_sec"]), r["shares"],
+                                                                 r["shares_rechecked"], r["shares_recheck_ok"])
+            faults = comm.allreduce_counters(int(bool(r.get("faulted")) or bool(err)))[0]
+            info_d = scrypt_info if algo == "scrypt" else x11_info
+            miner = dict(r, node_hashes_per_sec=float(tot), node_shares=shares_n, node_shares_rechecked=chk,
+                         node_shares_recheck_ok=chk_ok, ranks_faulted=faults, window_seconds=miner_s)
+            if err:
+                miner["error"] = err
+            info_d["miner"] = miner
+            used = not faults and chk == chk_ok and tot > 0  # every re-hashed share held and no rank faulted
+            if used and algo == "scrypt":
+                scrypt_hps = float(tot)
+            elif used:
+                x11_hps = float(tot)
+            info_d["rate_source"] = "production miner (see miner)" if used else "kernel path"
+        if scrypt_info:
+            scrypt_info["kernel_path_hashes_per_sec"] = scrypt_kernel_hps
+        if x11_info:
+            x11_info["kernel_path_hashes_per_sec"] = x11_kernel_hps
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ BASELINE config 1: the CPU miner
