@@ -22,6 +22,6 @@ OTEDAMA_DIST_BACKEND=gloo timeout -k 10 300 python -c "
 import json
 from otedama_amd.parallel.node_probe import measure_node
 print(json.dumps(measure_node(2, seconds=10, expected_per_gpu=9.7e9, shares_per_gpu=25.0)))
-" > $D/node2_gloo.json 2> $D/node2_gloo.err && echo "node2 ok"
+" > $D/node2_gloo.json 2> $D/node2_gloo.err && echo "node2 ok" &&
 timeout -k 10 200 python -u -m pytest tests/test_miner_probe.py -m gpu -x -v --timeout 120 --timeout-method thread > $D/pytest_miner_probe.log 2>&1 && tail -3 $D/pytest_miner_probe.log &&
 timeout -k 10 600 python bench.py --steps 5 --warmup 1 > $D/bench.json 2> $D/bench.err && echo "bench ok" && cut -c1-600 $D/bench.json
