@@ -17,7 +17,7 @@ for a in sha256d scrypt x11; do
   timeout -k 10 360 python tools/switch_ab.py --algo $a --env-b $HW1 > $D/switch_${a}_hw1.jsonl 2> $D/switch_${a}_hw1.err || exit 1
   cut -c1-300 $D/switch_${a}_hw1.jsonl
 done &&
-timeout -k 10 200 python tools/rss_breakdown.py --only default,hw_queues_1 > $D/rss.jsonl 2> $D/rss.err && echo "rss ok" &&
+timeout -k 10 200 python tools/rss_breakdown.py --only default,hw_queues_1,hw_queues_1+no_fragments > $D/rss.jsonl 2> $D/rss.err && echo "rss ok" &&
 OTEDAMA_DIST_BACKEND=gloo timeout -k 10 300 python -c "
 import json
 from otedama_amd.parallel.node_probe import measure_node

@@ -93,6 +93,8 @@ VARIANTS = [
     ("queue_dev_mem+one_search_stream", {"HSA_ALLOCATE_QUEUE_DEV_MEM": "1", "OTEDAMA_SEARCH_STREAMS": "1"}),
     # both search streams multiplexed onto one normal-priority hardware queue (the control stream keeps its own)
     ("hw_queues_1", {"GPU_MAX_HW_QUEUES": "1"}),
+    # ... and ROCr's host-memory fragment allocator off (the /dev/zero mappings, ~55 MiB)
+    ("hw_queues_1+no_fragments", {"GPU_MAX_HW_QUEUES": "1", "HSA_DISABLE_FRAGMENT_ALLOCATOR": "1"}),
 ]
 
 
