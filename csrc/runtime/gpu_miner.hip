@@ -9,8 +9,8 @@
 //
 // Job switches: new work opens a new launch epoch and writes it to an uncached device word. The CPU stores it
 // straight into VRAM through the PCIe BAR when the runtime lets the CPU agent map the word; otherwise the store is a
-// hipStreamWriteValue32 on a high-priority control stream, one more hardware queue (~190 MB of host memory for its
-// context-save area, profiles/r3/o_rss). Every wave polls that word once per grid-stride trip, so batches of the old
+// hipStreamWriteValue32 on a high-priority control stream, one more hardware queue (a 173 MiB host mapping,
+// profiles/r4/c_host_abort/rss.jsonl). Every wave polls that word once per grid-stride trip, so batches of the old
 // epoch stop within one trip (tens of us for SHA-256d, <= ~2 ms of ROMix for scrypt) and the first batch of the new
 // work starts right behind them. The switch time (set_job -> new batch running) is recorded.
 //
@@ -272,7 +272,7 @@ void GpuMiner::loop() {
     if (ctl) (void)hipStreamDestroy(ctl);
   }};
   // Search streams: one per in-flight batch, so a launch's tail overlaps the next launch's first waves; with
-  // OTEDAMA_SEARCH_STREAMS=1 the batches share one stream (one hardware queue less, ~190 MB of host memory).
+  // OTEDAMA_SEARCH_STREAMS=1 the batches share one stream (one hardware queue less, 173 MiB of host memory).
   const char* ss_env = std::getenv("OTEDAMA_SEARCH_STREAMS");
   const bool one_stream = ss_env && std::atoi(ss_env) == 1;
   for (int i = 0; i < kInflight; ++i) {
@@ -284,7 +284,7 @@ void GpuMiner::loop() {
   // multiplexes streams of one priority onto GPU_MAX_HW_QUEUES (4) hardware queues, and with two search streams
   // plus torch's in the same process a control stream can land on a busy queue, where its write waits for a whole
   // 2^32-hash launch (the job switch grew from 0.3 ms to ~110 ms); high-priority streams come from a separate pool.
-  // Every hardware queue costs ~190 MB of host memory (tools/stream_rss.hip, profiles/r3/o_rss).
+  // Every hardware queue costs a 173 MiB host mapping (tools/queue_rss.hip, profiles/r4/c_host_abort/rss.jsonl).
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
   OTD_HIP(hipMemset(d_abort, 0, 256));
   OTD_HIP(hipDeviceSynchronize());
@@ -371,9 +371,10 @@ void GpuMiner::loop() {
   // Running: every launch's probe gives an upper bound on the offset (host time it was seen minus its device
   // time); the lowest bound of the last kClockWindowS seconds is the mapping in use.
   std::deque<std::pair<double, double>> clk_bounds;  // (seen at, offset bound), oldest first
-  auto clock_seen = [&](Batch& b, double now) {
+  auto clock_seen = [&](Batch& b) {
     const uint64_t rt = __atomic_load_n(b.h_clk, __ATOMIC_ACQUIRE);
     if (!rt) return;
+    const double now = monotonic_seconds();  // after the load that saw the stamp: a valid upper bound
     b.clk_pending = false;
     const double bound = now - double(rt) / kRtHz;
     // monotonic deque: bounds increase from front to back, so the front is the window's minimum
@@ -710,9 +711,8 @@ void GpuMiner::loop() {
     bool progressed = false;
     if (job && gen != cur_gen) { cur_gen = gen; k = 0; nonce_off = 0; }
     // 1) hits of the batches in flight, oldest first, and the clock stamps of launches that just started
-    const double t_poll = monotonic_seconds();
     for (int i : fifo)
-      if (slots[i].clk_pending) clock_seen(slots[i], t_poll);
+      if (slots[i].clk_pending) clock_seen(slots[i]);
     for (int i : fifo) progressed |= drain_ring(slots[i], ~0u, job, gen) > 0;
     // 2) retire completed batches (the two streams may complete out of issue order)
     for (auto it = fifo.begin(); it != fifo.end();) {
