@@ -71,6 +71,9 @@ class _Framer:
         return out
 
 
+DEVICE_HW_QUEUES = ""  # default cap on a device process's normal-priority hardware queues ("" = the runtime's 4)
+
+
 class DeviceProcess:
     """Parent-side handle with the native miner's interface (start/stop/set_job/poll/stats/share_fd)."""
 
@@ -115,6 +118,11 @@ class DeviceProcess:
         env = dict(os.environ if self.env is None else self.env)
         env["OTEDAMA_NO_TORCH"] = "1"
         env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        # Hardware queues of the child's HIP runtime (each one a 173 MiB host mapping, profiles/r4/c_host_abort):
+        # OTEDAMA_DEVICE_HW_QUEUES caps them through GPU_MAX_HW_QUEUES unless that is set explicitly.
+        hwq = env.get("OTEDAMA_DEVICE_HW_QUEUES", DEVICE_HW_QUEUES)
+        if hwq and "GPU_MAX_HW_QUEUES" not in env:
+            env["GPU_MAX_HW_QUEUES"] = str(hwq)
         a = self.args
         cmd = [sys.executable, "-m", "otedama_amd.engine.devproc", "--fd", str(child.fileno()),
                "--device", str(self.device_index), "--id", self.device_id, "--batch", str(a["batch"]),
