@@ -18,6 +18,7 @@
 #include "otedama/trace.h"
 #include "otedama/sha256.h"
 #include "otedama/sv2_frame.h"
+#include "otedama/clock_bounds.h"
 #include "otedama/work_queue.h"
 #include "otedama/x11.h"
 
@@ -196,6 +197,14 @@ PYBIND11_MODULE(_native, m) {
     std::string s = need(h, 80, "header"); uint8_t o[32];
     { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }
     return to_bytes(o, 32);
+  });
+  // Test hook: the miner's device-clock estimate (ClockBounds) over a sequence of (seen at, offset bound) pairs;
+  // returns the estimate after each.
+  m.def("_clock_bounds", [](double window, const std::vector<std::pair<double, double>>& samples) {
+    ClockBounds cb(window);
+    std::vector<double> out;
+    for (const auto& s : samples) out.push_back(cb.add(s.first, s.second));
+    return out;
   });
   // Test hook: the scrypt verifier's bounded queue (BoundedWorkQueue) flooded by a producer that never waits, with
   // a consumer hashing every item on the host (scrypt_1024_1_1, as the GPU miner's verifier does).

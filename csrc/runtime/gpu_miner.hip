@@ -49,6 +49,7 @@
 #include <string>
 #include <unistd.h>
 
+#include "otedama/clock_bounds.h"
 #include "otedama/hitsink.h"
 #include "otedama/job.h"
 #include "otedama/runtime.h"
@@ -370,18 +371,13 @@ void GpuMiner::loop() {
   bool first_switch = true;
   // Running: every launch's probe gives an upper bound on the offset (host time it was seen minus its device
   // time); the lowest bound of the last kClockWindowS seconds is the mapping in use.
-  std::deque<std::pair<double, double>> clk_bounds;  // (seen at, offset bound), oldest first
+  ClockBounds clk_bounds(kClockWindowS);
   auto clock_seen = [&](Batch& b) {
     const uint64_t rt = __atomic_load_n(b.h_clk, __ATOMIC_ACQUIRE);
     if (!rt) return;
     const double now = monotonic_seconds();  // after the load that saw the stamp: a valid upper bound
     b.clk_pending = false;
-    const double bound = now - double(rt) / kRtHz;
-    // monotonic deque: bounds increase from front to back, so the front is the window's minimum
-    while (!clk_bounds.empty() && clk_bounds.back().second >= bound) clk_bounds.pop_back();
-    clk_bounds.emplace_back(now, bound);
-    while (now - clk_bounds.front().first > kClockWindowS) clk_bounds.pop_front();  // the newest always stays
-    rt_offset.store(clk_bounds.front().second);
+    rt_offset.store(clk_bounds.add(now, now - double(rt) / kRtHz));
     std::lock_guard<std::mutex> g(stats_mu_);
     stats_.clock_samples += 1;
   };

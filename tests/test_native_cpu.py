@@ -273,3 +273,21 @@ def test_scrypt_verifier_queue_is_bounded_under_a_flood():
         assert r["accepted"] + r["refused"] == n and r["processed"] == r["accepted"], r
     r = N._work_queue_flood(64, 50, False)  # below the cap nothing is refused
     assert r == {"accepted": 50, "refused": 0, "peak": r["peak"], "processed": 50} and r["peak"] <= 50
+
+
+def test_clock_bounds_track_the_window_minimum():
+    """The GPU miner's device-clock estimate (otedama/clock_bounds.h): the lowest offset bound seen in the last
+    `window` seconds, following drift once older, lower bounds age out."""
+    from otedama_amd.ops.native import require_native
+
+    N = require_native()
+    # true offset 10.000 at t<3, drifting to 10.003 later; every sighting is late by 0..50 us (an upper bound)
+    seq = [(0.0, 10.00004), (0.2, 10.00001), (0.4, 10.00003), (1.0, 10.00002), (2.1, 10.00005),
+           (3.0, 10.00302), (3.5, 10.00301), (4.0, 10.00304), (4.2, 10.00303)]
+    got = N._clock_bounds(2.0, seq)
+    assert got[:5] == [10.00004, 10.00001, 10.00001, 10.00001, 10.00001]  # the 0.2 s bound is 1.9 s old at 2.1
+    assert got[5] == pytest.approx(10.00002)   # t=3.0: 0.2 and 0.4 aged out, 1.0 is exactly 2 s old
+    assert got[6] == pytest.approx(10.00005)   # t=3.5: 2.1's bound is the lowest left
+    assert got[7] == pytest.approx(10.00005)
+    assert got[8] == pytest.approx(10.00301)   # t=4.2: only the drifted bounds remain
+    assert N._clock_bounds(2.0, [(0.0, 5.0)]) == [5.0]
