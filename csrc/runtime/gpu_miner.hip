@@ -287,8 +287,10 @@ void GpuMiner::loop() {
   // 2^32-hash launch (the job switch grew from 0.3 ms to ~110 ms); high-priority streams come from a separate pool.
   // Every hardware queue costs a 173 MiB host mapping (tools/queue_rss.hip, profiles/r4/c_host_abort/rss.jsonl).
   OTD_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_abort), 256, hipDeviceMallocUncached));
-  OTD_HIP(hipMemset(d_abort, 0, 256));
-  OTD_HIP(hipDeviceSynchronize());
+  // on a search stream: the first use of the null stream would give this process one more hardware queue
+  // (tools/queue_rss.hip, profiles/r4/d_queues)
+  OTD_HIP(hipMemsetAsync(d_abort, 0, 256, slots[0].stream));
+  OTD_HIP(hipStreamSynchronize(slots[0].stream));
   const char* ha_env = std::getenv("OTEDAMA_HOST_ABORT");
   host_abort = !(ha_env && ha_env[0] == '0') && cpu_store_map(d_abort, 256);
   if (!host_abort) {
