@@ -44,22 +44,34 @@ def measure_miner(N, device_index: int, algo: str, target_int: int, seconds: flo
                "version_mask": 0x1FFFE000, "variant_start": rank, "variant_stride": world})
     shares: list[dict] = []
     m.start()
+
+    def edge(after: dict, limit: float) -> dict:
+        """The first stats whose completed-hash counter moved past ``after``'s: its device-timeline time is then
+        that of a launch that has just completed, not a stale one (a window must start and end on such edges)."""
+        nonlocal shares
+        end = time.monotonic() + limit
+        st = m.stats()
+        while st["hashes"] == after["hashes"] and time.monotonic() < end:
+            shares += m.poll(65536)
+            time.sleep(0.002)
+            st = m.stats()
+        return st
+
     try:
-        end = time.monotonic() + warmup
+        # warm-up: the time given, and at least 4 launches (the first scrypt job allocates a 128 GiB pad, which takes
+        # seconds right after another process or allocator released one)
+        end, cap = time.monotonic() + warmup, time.monotonic() + warmup + 60.0
+        while time.monotonic() < end or (m.stats()["launches"] < 4 and time.monotonic() < cap):
+            shares += m.poll(65536)
+            time.sleep(0.05)
+        s0 = edge(m.stats(), 10.0)
+        w0 = time.monotonic()
+        end = w0 + seconds
         while time.monotonic() < end:
             shares += m.poll(65536)
             time.sleep(0.1)
-        s0 = m.stats()
-        end = time.monotonic() + seconds
-        while time.monotonic() < end:
-            shares += m.poll(65536)
-            time.sleep(0.1)
-        # the first sample past the window whose counter has moved (a completed launch)
-        s1 = m.stats()
-        deadline = time.monotonic() + 5.0
-        while s1["hashes"] == s0["hashes"] and time.monotonic() < deadline:
-            time.sleep(0.01)
-            s1 = m.stats()
+        s1 = edge(m.stats(), 10.0)  # the first completion past the window
+        w1 = time.monotonic()
     finally:
         m.stop()
     shares += m.poll(65536)
@@ -82,7 +94,7 @@ def measure_miner(N, device_index: int, algo: str, target_int: int, seconds: flo
         ok += int.from_bytes(d, "little") <= target_int
     return {
         "hashes_per_sec": hps,
-        "window_hashes": s1["hashes"] - s0["hashes"], "window_device_seconds": span,
+        "window_hashes": s1["hashes"] - s0["hashes"], "window_device_seconds": span, "window_wall_seconds": w1 - w0,
         "launches": st["launches"], "aborted_launches": st.get("aborted_launches", 0),
         "candidates": st["candidates"], "shares": st["shares"], "rejected_candidates": st["rejected_candidates"],
         "dropped": st["dropped"], "ring_overflow": st.get("ring_overflow", 0),
