@@ -17,11 +17,39 @@ CHILD = r'''
 import json, os, sys
 sys.path.insert(0, sys.argv[1])
 algo, secs, with_torch, target_bits = sys.argv[2], float(sys.argv[3]), sys.argv[4] == "1", int(sys.argv[5])
+hold = None
 if with_torch:
     import torch
     torch.cuda.init()
     torch.zeros(1, device="cuda:0")
     streams = [torch.cuda.Stream("cuda:0") for _ in range(3)]
+    pad = os.environ.get("CTX_PAD", "")
+    if pad:  # a 128 GiB torch allocation like bench.py's ops-API scrypt pad, written once, then freed or held
+        big = torch.empty(128 << 30, dtype=torch.uint8, device="cuda:0")
+        big.fill_(1)
+        torch.cuda.synchronize()
+        if pad == "freed":
+            del big
+            torch.cuda.empty_cache()
+        else:
+            hold = big
+    heat = float(os.environ.get("CTX_HEAT", "0"))
+    if heat > 0:  # keep the GPU busy first (bench.py's kernel sections run ~1 min before the miner sections)
+        import time as _t
+        from otedama_amd.ops.search import ScryptSearch
+        from otedama_amd.models.header import int_to_hash as _ih
+        from otedama_amd.ops.native import require_native as _rn
+        _N = _rn()
+        sc = ScryptSearch("cuda:0")
+        prm = _N.scrypt_prepare(bytes(80), _ih((1 << 200) - 1))
+        t_end = _t.monotonic() + heat
+        b = 0
+        while _t.monotonic() < t_end:
+            sc.launch(prm, b)
+            torch.cuda.synchronize()
+            b += sc.batch
+        del sc
+        torch.cuda.empty_cache()
 else:
     os.environ["OTEDAMA_NO_TORCH"] = "1"
 from otedama_amd.ops.native import require_native
@@ -38,12 +66,19 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--algo", default="scrypt")
     ap.add_argument("--seconds", type=float, default=6.0)
+    ap.add_argument("--pad", action="store_true", help="variants: a bench-like 128 GiB torch pad freed / held, 60 s of "
+                                                     "scrypt load first")
     a = ap.parse_args()
     hits = 0 if a.algo == "scrypt" else 236  # scrypt: diff 1 (0xFFFF << 224); X11: 2^-20, as in bench.py
-    for name, torch_on, bits in (("torch_free_hits", "0", hits), ("torch_free_no_hits", "0", 200),
-                                 ("torch_hits", "1", hits), ("torch_no_hits", "1", 200)):
+    variants = [("torch_free_hits", "0", hits, {}), ("torch_free_no_hits", "0", 200, {}),
+                ("torch_hits", "1", hits, {}), ("torch_no_hits", "1", 200, {})]
+    if a.pad:
+        variants = [("torch_hits", "1", hits, {}), ("torch_pad_freed", "1", hits, {"CTX_PAD": "freed"}),
+                    ("torch_pad_held", "1", hits, {"CTX_PAD": "held"}),
+                    ("torch_heat_60s", "1", hits, {"CTX_HEAT": "60"}), ("torch_hits_again", "1", hits, {})]
+    for name, torch_on, bits, extra in variants:
         out = subprocess.run([sys.executable, "-c", CHILD, ROOT, a.algo, str(a.seconds), torch_on, str(bits)],
-                             capture_output=True, text=True, timeout=150)
+                             capture_output=True, text=True, timeout=200, env=dict(os.environ, **extra))
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         rec = json.loads(line[0]) if line else {"error": out.returncode, "stderr": out.stderr[-800:]}
         print(json.dumps({"variant": name, "algo": a.algo, **rec}), flush=True)
