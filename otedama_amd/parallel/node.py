@@ -20,10 +20,10 @@ hundreds per second. Hashing never waits on any of this: kernels run in each ran
 so a GPU fault kills that child, not the rank that holds the RCCL communicator and, on rank 0, the pool session.
 
 Nothing on the share path sleeps on a timer: a follower whose device process pushed a share rings the leader's
-doorbell, the leader rings every follower's doorbell with the R2 gather op itself and then logs it in the store, and
-the followers enter the gather at once (a doorbell is a loopback datagram; an op travels inline, so no store round
-trip sits between the leader's decision and a follower entering the collective; the store stays the source of truth,
-so a lost datagram costs one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
+doorbell, the leader logs the R2 gather op in the store and rings every follower's doorbell with the op itself, and
+the followers enter the gather at once (a doorbell is a loopback datagram; the op travels inline, so no store round
+trip sits between a follower's wake-up and the collective; the store stays the source of truth, so a lost datagram
+costs one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
 pool accept for remote ranks' shares the same way as for its own.
 
 Rank loss (reference analogues: the partial-failure-tolerant detector
@@ -529,15 +529,17 @@ class NodeMinerSet:
     def _post(self, op: dict) -> None:
         op["gen"] = op.get("gen", self._gen)
         raw, k = json.dumps(op), self._op_k
+        # The log first: a follower may act on an op it got from the doorbell, so that op must already be the log's
+        # entry k (a leader that died between ringing and logging would leave a successor free to post a different
+        # op k, which such a follower would skip).
+        self.store.set(_k("op", k), raw)
+        self._op_k += 1
         if self._bell is not None:  # the followers' op loops wait on their doorbells: the op rides the datagram
             msg = op_msg(k, raw)
             targets = op["members"] if op.get("op") == "reform" else self.comm.info.members
             for r in targets:
                 if r != self.comm.info.orig_rank:
                     self._bell.ring(r, msg)
-        # then the log (while the followers wake): a follower that missed the datagram, or joins later, reads it here
-        self.store.set(_k("op", k), raw)
-        self._op_k += 1
         self.store.set(_k("next"), str(self._op_k))
 
     def _heartbeats(self, store=None) -> dict[int, dict]:
