@@ -508,9 +508,11 @@ def run_rank(args) -> int:
         torch.cuda.empty_cache()
 
     # ------------------------------------------------- scrypt and X11 through the production miner
-    # The kernel sections above time the ops-API launches one after another. The device process's GpuMiner runs
-    # scrypt as two half-grid batches side by side and X11 with a digest plane per slot; its exact rate over whole
-    # launches, with every share re-verified, is the scrypt / X11 figure (the kernel-path rate stays beside it).
+    # The kernel sections above time the ops-API launches one after another. The production miner runs scrypt as two
+    # half-grid batches side by side and X11 with a digest plane per slot, in a device process of its own; its exact
+    # rate over whole launches there, with every share re-verified, is the scrypt / X11 figure (the kernel-path rate
+    # stays beside it). In this torch process the same miner measured 16.2-16.4 MH/s against 17.2-17.5 in fresh
+    # processes, with no section of this script responsible (profiles/r4/h_bench_sections, i_bisect).
     scrypt_kernel_hps, x11_kernel_hps = scrypt_hps, x11_hps
     miner_s = args.miner_seconds if args.miner_seconds >= 0 else (0.0 if cpu else 8.0)
     if miner_s > 0:
@@ -523,7 +525,7 @@ def run_rank(args) -> int:
             barrier(info)
             try:
                 r = measure_miner(N, dev.index or 0, algo, tgt, seconds=miner_s, rank=info.rank, world=world,
-                                  seed=args.seed)
+                                  seed=args.seed, process=True)
                 err = ""
             except Exception as exc:  # noqa: BLE001 - auxiliary: the kernel-path figure stays
                 r, err = {"hashes_per_sec": 0.0, "shares": 0, "shares_rechecked": 0, "shares_recheck_ok": 0,

@@ -28,10 +28,13 @@ def test_share_header_matches_the_native_variant_header():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("algo,target,floor", [("scrypt", 0xFFFF << 224, 12e6), ("x11", (1 << 236) - 1, 300e6)])
-def test_production_miner_rate_and_shares(algo, target, floor):
+@pytest.mark.parametrize("algo,target,floor,process", [("scrypt", 0xFFFF << 224, 12e6, False),
+                                                       ("x11", (1 << 236) - 1, 300e6, False),
+                                                       ("scrypt", 0xFFFF << 224, 12e6, True)])
+def test_production_miner_rate_and_shares(algo, target, floor, process):
+    """In this process and through a device process (bench.py's path): exact rate, shares re-hashed, nothing lost."""
     N = _native()
-    r = measure_miner(N, 0, algo, target, seconds=2.0, warmup=1.5, recheck=16)
+    r = measure_miner(N, 0, algo, target, seconds=2.0, warmup=1.5, recheck=16, process=process)
     assert not r["faulted"] and r["hashes_per_sec"] > floor, r
     assert r["shares"] > 0 and r["shares_rechecked"] > 0 and r["shares_recheck_ok"] == r["shares_rechecked"], r
     assert r["dropped"] == 0 and r["ring_overflow"] == 0 and r["verify_dropped"] == 0, r
