@@ -102,6 +102,39 @@ def test_new_work_aborts_the_running_batch():
         _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target)
 
 
+@pytest.mark.parametrize("host_abort", ["1", "0"])
+def test_abort_word_store_paths(monkeypatch, host_abort):
+    """The CPU stores the abort word straight into VRAM on the MI355X (no control stream); with
+    OTEDAMA_HOST_ABORT=0 the store goes through a high-priority stream. Both stop the running batch for new work,
+    and the per-launch clock probes keep the device -> host clock mapping (shares stamped before their host
+    verification, within a launch)."""
+    monkeypatch.setenv("OTEDAMA_HOST_ABORT", host_abort)
+    N = _native()
+    hdr_a, hdr_b = os.urandom(76) + bytes(4), os.urandom(76) + bytes(4)
+    target = (1 << 236) - 1
+    m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 32)
+    m.set_job(_job(hdr_a, target, 1, "a"))
+    m.start()
+    try:
+        time.sleep(0.5)
+        m.poll(4096)
+        m.set_job(_job(hdr_b, target, 2, "b"))
+        time.sleep(0.5)
+        shares = m.poll(4096)
+    finally:
+        m.stop()
+    st = m.stats()
+    assert not st["faulted"], st
+    assert st["host_abort"] is (host_abort == "1"), st
+    assert st["last_job_switch_ms"] < 20.0 and st["aborted_launches"] >= 1, st
+    assert st["clock_samples"] >= 2, st
+    b = [s for s in shares if s["job_id"] == "b"]
+    assert b
+    for s in b:
+        _check_share(hdr_b, s, target)
+        assert 0 < s["device_found_at"] <= s["found_at"] + 0.002 and s["found_at"] - s["device_found_at"] < 0.05, s
+
+
 def test_target_only_update_reaches_the_running_group():
     """Same work, easier target, partway through a 128-variant group: shares at the new target appear within a
     couple of 2^29-nonce launches (the version-parallel variant table stays cached; its target must not)."""
