@@ -9,8 +9,9 @@
 //    carries the low 32 bits of s_memrealtime (100 MHz) so the host can time the path from
 //    the kernel's hit to the pool's accept.
 // The abort word lives in uncached device memory (hipDeviceMallocUncached); the host bumps it
-// with hipStreamWriteValue32 on a control stream when the work changes, and every wave checks
-// it once per grid-stride iteration: a batch whose launch epoch is older stops early.
+// when the work changes (a CPU store through the PCIe BAR, or hipStreamWriteValue32 on a control
+// stream where the CPU cannot map it), and every wave checks it once per grid-stride iteration:
+// a batch whose launch epoch is older stops early.
 //
 // Parity: the reference hands each share to the session the moment the worker finds it
 // (internal/miner/worker.go:262-275) and switches work between 1024-nonce batches

@@ -8,8 +8,8 @@
 
 namespace otedama_dev {
 
-// Abort word as of now (system-scope relaxed load: the word is uncached device memory written by the host's
-// control stream). Wave-uniform by construction (one address), made provably so for a scalar branch. Without
+// Abort word as of now (system-scope relaxed load: the word is uncached device memory the host stores to, through
+// the BAR or a control stream). Wave-uniform by construction (one address), made provably so for a scalar branch. Without
 // an abort word the batch's own epoch comes back, which never reads as newer.
 __device__ __forceinline__ uint32_t abort_peek(const uint32_t* word, uint32_t epoch) {
   if (word == nullptr) return epoch;
