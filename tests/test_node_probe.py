@@ -1,0 +1,41 @@
+"""parallel/node_probe.py: the node object of bench.py — exact window rates from (hashes, device-timeline time)
+pairs, nearest-rank quantiles with sample counts, and the per-role RSS map."""
+import os
+
+import pytest
+
+from otedama_amd.parallel.node_probe import _quantiles, _rank_of, process_rss, window_rates
+
+
+def test_window_rates_use_the_device_timeline_span():
+    # rank0: a GPU whose counter moves a launch at a time; the wall times of the samples are irregular, the
+    # device-timeline completion times are what the hashes belong to
+    samples = [
+        (10.0, {"rank0": (1000, 5.0), "rank1": (0, 0.0)}),
+        (10.5, {"rank0": (1000, 5.0), "rank1": (50, 0.0)}),
+        (11.2, {"rank0": (3000, 7.0), "rank1": (120, 0.0)}),
+        (12.0, {"rank0": (5000, 9.0), "rank1": (200, 0.0)}),
+        (30.0, {"rank0": (9999, 99.0), "rank1": (999, 0.0)}),  # outside the window
+    ]
+    r = window_rates(samples, 10.0, 12.0)
+    assert r["rank0"] == pytest.approx((5000 - 1000) / (9.0 - 5.0))
+    # no device timeline (a CPU miner): the wall span of the samples
+    assert r["rank1"] == pytest.approx(200 / 2.0)
+
+
+def test_window_rates_need_two_samples():
+    assert window_rates([(1.0, {"rank0": (10, 1.0)})], 0.0, 5.0) == {}
+    assert window_rates([], 0.0, 5.0) == {}
+
+
+def test_nearest_rank_quantiles_report_their_sample_count():
+    q = _quantiles([float(x) for x in range(1, 201)])
+    assert q == {"p50_ms": 100.0, "p95_ms": 190.0, "p99_ms": 198.0, "samples": 200}
+    assert _quantiles([]) == {"p50_ms": None, "p95_ms": None, "p99_ms": None, "samples": 0}
+    assert _quantiles([3.0])["p99_ms"] == 3.0
+
+
+def test_rank_keys_and_rss_roles():
+    assert _rank_of("rank7") == 7 and _rank_of("gpu-0") == 0
+    rss = process_rss(os.getpid())  # this process as the "supervisor": its children (if any) are not ranks here
+    assert rss.get("supervisor", 0) > 0
