@@ -39,3 +39,16 @@ def test_rank_keys_and_rss_roles():
     assert _rank_of("rank7") == 7 and _rank_of("gpu-0") == 0
     rss = process_rss(os.getpid())  # this process as the "supervisor": its children (if any) are not ranks here
     assert rss.get("supervisor", 0) > 0
+
+
+@pytest.mark.parametrize("gpus,want", [
+    (1, [(0, "sha256d"), (0, "scrypt")]),
+    (2, [(0, "sha256d"), (1, "scrypt")]),
+    (8, [(0, "sha256d"), (1, "sha256d"), (2, "sha256d"), (3, "sha256d"),
+         (4, "scrypt"), (5, "scrypt"), (6, "scrypt"), (7, "scrypt")]),
+])
+def test_mixed_pool_layout(gpus, want):
+    """BASELINE config 5: both algorithms on GPU 0 at N=1, else the first ceil(N/2) GPUs SHA-256d, the rest scrypt."""
+    from otedama_amd.pool.pool_probe import layout
+
+    assert layout(gpus) == want
