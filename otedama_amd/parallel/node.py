@@ -51,6 +51,7 @@ from __future__ import annotations
 import collections
 import json
 import os
+import random
 import select
 import socket
 import threading
@@ -95,6 +96,9 @@ class _Bell:
     ``wait(t)`` blocks until a datagram arrives or t passes and returns the datagrams received."""
 
     PORT_TTL = 2.0
+    # Fault injection (tests, SURVEY §5.3): this fraction of datagrams is dropped, so the store-poll fallback carries
+    # every op and share ring (the node must still work, only slower).
+    DROP = float(os.environ.get("OTEDAMA_FAULT_BELL_DROP", "0") or 0)
 
     def __init__(self, store, orig_rank: int):
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
@@ -106,6 +110,7 @@ class _Bell:
         self._lock = threading.Lock()
         self._ports: dict[int, tuple[int, float]] = {}
         self.rings = 0
+        self.dropped = 0  # fault injection only
         if self.store is not None:
             self.store.set(_k("bell", orig_rank), str(self.port))
 
@@ -127,6 +132,9 @@ class _Bell:
     def ring(self, orig: int, kind: bytes = b"o") -> None:
         port = self._port_of(orig)
         if port is None:
+            return
+        if self.DROP and random.random() < self.DROP:
+            self.dropped += 1
             return
         try:
             self.sock.sendto(kind, ("127.0.0.1", port))
@@ -561,6 +569,10 @@ class NodeMinerSet:
         members = self.comm.info.members
         for r, hb in hbs.items():  # per-rank counters between R3 rounds (store only, no device collective)
             if r in members and now - hb["t"] <= self.hb_timeout:
+                if int(hb.get("pending", 0) or 0) > 0:
+                    # shares waiting on a follower: gather even if its doorbell rings were lost (the store is the
+                    # truth for the share path too; this bounds a lost ring by LIVENESS_EVERY + HB_INTERVAL)
+                    self._gather_wanted = True
                 self._rows_by_orig[r] = [int(hb.get("hashes", 0)), int(hb.get("shares", 0)),
                                          int(hb.get("dropped", 0)), int(hb.get("faulted", 0))]
                 self.row_times[r] = float(hb["t"])

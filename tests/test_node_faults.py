@@ -154,3 +154,17 @@ def test_quiet_node_issues_about_one_collective_per_second(tmp_path):
     assert all(c == 0 for c in codes.values()), codes
     res = json.loads((tmp_path / "result.json").read_text())
     assert res["collectives_per_s"] <= 1.0, res
+
+
+@pytest.mark.timeout(300)
+def test_node_mines_with_every_doorbell_datagram_lost(monkeypatch):
+    """Fault injection (OTEDAMA_FAULT_BELL_DROP=1): no doorbell datagram arrives, so followers take every op from the
+    store log (50 ms polls) and the leader learns of their shares from the heartbeats' pending counts. The node still
+    mines: remote shares are gathered over R2 and accepted, nothing is rejected, and it stops cleanly."""
+    from otedama_amd.parallel.node_probe import measure_node
+
+    monkeypatch.setenv("OTEDAMA_FAULT_BELL_DROP", "1")
+    r = measure_node(2, seconds=5, warmup=2, cpu=True, expected_per_gpu=8e6, shares_per_gpu=6.0)
+    assert "error" not in r, r
+    assert r["accepted_remote_in_window"] > 0 and r["rejected"] == 0 and r["pool_rejected"] == 0, r
+    assert r["exit_code"] == 0, r
