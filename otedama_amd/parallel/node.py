@@ -23,7 +23,7 @@ Nothing on the share path sleeps on a timer: a follower whose device process pus
 doorbell, the leader logs the R2 gather op in the store and rings every follower's doorbell with the op itself, and
 the followers enter the gather at once (a doorbell is a loopback datagram; the op travels inline, so no store round
 trip sits between a follower's wake-up and the collective; the store stays the source of truth, so a lost datagram
-costs one fallback poll, <= 50 ms). Share records carry the kernel's own hit time, so the leader records device hit ->
+costs one fallback poll, <= 50 ms; a lost share ring is covered by the pending count in the follower's heartbeat). Share records carry the kernel's own hit time, so the leader records device hit ->
 pool accept for remote ranks' shares the same way as for its own.
 
 Rank loss (reference analogues: the partial-failure-tolerant detector
