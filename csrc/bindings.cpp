@@ -290,6 +290,17 @@ PYBIND11_MODULE(_native, m) {
     }
     return hits;
   }, py::arg("header"), py::arg("target"), py::arg("start"), py::arg("count"));
+  // A/B hook: the CPU scan with a given number of nonces in flight per step (1..4).
+  m.def("_cpu_scan_lanes", [](int lanes, const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
+    std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
+    std::vector<uint32_t> hits;
+    {
+      py::gil_scoped_release r;
+      hits = cpu_scan_sha256d_lanes(lanes, reinterpret_cast<const uint8_t*>(hs.data()),
+                                    reinterpret_cast<const uint8_t*>(ts.data()), start, count);
+    }
+    return hits;
+  });
   m.def("merkle_root", [](const py::dict& job, uint64_t en2) {
     auto j = make_job(job); uint8_t root[32];
     merkle_root_from_coinbase(*j, en2, root);

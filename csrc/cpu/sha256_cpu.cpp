@@ -193,6 +193,18 @@ void sha256_compress_x2(uint32_t s0[8], const uint8_t b0[64], uint32_t s1[8], co
   }
 }
 
+void sha256_compress_xn(int n, uint32_t* const state[], const uint8_t* const block[]) {
+  if (!cpu_has_sha_ni()) {
+    for (int i = 0; i < n; ++i) sha256_compress_portable(state[i], block[i]);
+    return;
+  }
+  int i = 0;
+  for (; i + 4 <= n; i += 4) sha256_compress_shani_xn<4>(state + i, block + i);
+  if (n - i == 3) sha256_compress_shani_xn<3>(state + i, block + i);
+  else if (n - i == 2) sha256_compress_shani_xn<2>(state + i, block + i);
+  else if (n - i == 1) sha256_compress_shani(state[i], block[i]);
+}
+
 void sha256(const uint8_t* data, size_t len, uint8_t out[32]) {
   uint32_t st[8];
   std::memcpy(st, kSha256IV, sizeof st);

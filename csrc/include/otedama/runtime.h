@@ -214,6 +214,8 @@ class CpuMiner : public MinerBase {
 // Returns the nonces (header byte order) whose SHA-256d meets the target.
 std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
                                        uint64_t count);
+std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[80], const uint8_t target[32],
+                                             uint32_t start, uint64_t count);
 
 // Seconds on CLOCK_MONOTONIC (same clock as Python time.monotonic()).
 double monotonic_seconds();

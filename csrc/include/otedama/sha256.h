@@ -36,6 +36,8 @@ void sha256_compress_portable(uint32_t state[8], const uint8_t block[64]);
 void sha256_compress(uint32_t state[8], const uint8_t block[64]);
 // Two independent compressions, interleaved on SHA-NI (latency hiding); same results as two calls.
 void sha256_compress_x2(uint32_t s0[8], const uint8_t b0[64], uint32_t s1[8], const uint8_t b1[64]);
+// n independent compressions, interleaved in groups of up to 4 on SHA-NI (portable one by one otherwise).
+void sha256_compress_xn(int n, uint32_t* const state[], const uint8_t* const block[]);
 bool cpu_has_sha_ni();
 
 // Full SHA-256 of an arbitrary message.

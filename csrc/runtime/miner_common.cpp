@@ -260,6 +260,8 @@ MinerStats MinerBase::stats() {
 
 // ---------------------------------------------------------- CPU SHA-256d scan
 
+constexpr int kCpuScanLanes = 2;  // nonces in flight per step (tools: N._cpu_scan_lanes A/B)
+
 // Per-nonce work with a midstate: block 2 (16 B of header + padding) and the
 // 32-byte digest block. 2 compressions per nonce instead of the reference's 3.
 static inline void sha256d_from_mid(const uint32_t mid[8], uint8_t blk2[64], uint8_t dblk[64],
@@ -273,8 +275,60 @@ static inline void sha256d_from_mid(const uint32_t mid[8], uint8_t blk2[64], uin
   for (int i = 0; i < 8; ++i) store_be32(out + 4 * i, st[i]);
 }
 
-std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
-                                       uint64_t count) {
+// L nonces per step through the interleaved compressor (SHA-NI is latency-bound in one chain: independent chains
+// fill its pipeline). H7 first: the early reject.
+template <int L>
+static void cpu_scan_lanes(const uint32_t mid[8], const uint8_t blk2_tmpl[64], const uint8_t target[32], uint32_t start,
+                           uint64_t count, std::vector<uint32_t>* hits, uint64_t* done) {
+  uint8_t blk[L][64], dblk[L][64];
+  uint32_t st[L][8];
+  uint32_t* sp[L];
+  const uint8_t* bp[L];
+  const uint8_t* dp[L];
+  for (int l = 0; l < L; ++l) {
+    std::memcpy(blk[l], blk2_tmpl, 64);
+    std::memset(dblk[l], 0, 64);
+    dblk[l][32] = 0x80;
+    dblk[l][62] = 0x01;  // 256 bits
+    sp[l] = st[l];
+    bp[l] = blk[l];
+    dp[l] = dblk[l];
+  }
+  const uint32_t thi = load_le32(target + 28);
+  uint8_t h[32];
+  uint64_t i = 0;
+  for (; i + L <= count; i += L) {
+    for (int l = 0; l < L; ++l) {
+      store_le32(blk[l] + 12, start + uint32_t(i) + uint32_t(l));
+      std::memcpy(st[l], mid, 32);
+    }
+    sha256_compress_xn(L, sp, bp);
+    for (int l = 0; l < L; ++l) {
+      for (int w = 0; w < 8; ++w) store_be32(dblk[l] + 4 * w, st[l][w]);
+      std::memcpy(st[l], kSha256IV, 32);
+    }
+    sha256_compress_xn(L, sp, dp);
+    for (int l = 0; l < L; ++l) {
+      if (__builtin_bswap32(st[l][7]) > thi) continue;
+      for (int w = 0; w < 8; ++w) store_be32(h + 4 * w, st[l][w]);
+      if (le256_leq(h, target)) hits->push_back(start + uint32_t(i) + uint32_t(l));
+    }
+  }
+  *done = i;
+}
+
+// Lanes per step of the CPU scan (OTEDAMA_CPU_LANES overrides; 1..4).
+static int cpu_scan_lanes_default() {
+  static const int lanes = [] {
+    const char* v = std::getenv("OTEDAMA_CPU_LANES");
+    const int n = v ? std::atoi(v) : 0;
+    return n >= 1 && n <= 4 ? n : kCpuScanLanes;
+  }();
+  return lanes;
+}
+
+std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[80], const uint8_t target[32],
+                                             uint32_t start, uint64_t count) {
   uint32_t mid[8];
   std::memcpy(mid, kSha256IV, 32);
   sha256_compress(mid, header80);
@@ -283,46 +337,31 @@ std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t
   blk2[16] = 0x80;
   blk2[62] = 0x02;  // 640 bits
   blk2[63] = 0x80;
+  std::vector<uint32_t> hits;
+  uint64_t i = 0;
+  switch (lanes) {
+    case 1: cpu_scan_lanes<1>(mid, blk2, target, start, count, &hits, &i); break;
+    case 3: cpu_scan_lanes<3>(mid, blk2, target, start, count, &hits, &i); break;
+    case 4: cpu_scan_lanes<4>(mid, blk2, target, start, count, &hits, &i); break;
+    default: cpu_scan_lanes<2>(mid, blk2, target, start, count, &hits, &i); break;
+  }
   uint8_t dblk[64] = {0};
   dblk[32] = 0x80;
-  dblk[62] = 0x01;  // 256 bits
-  std::vector<uint32_t> hits;
+  dblk[62] = 0x01;
   uint8_t h[32];
   const uint32_t thi = load_le32(target + 28);
-  uint64_t i = 0;
-  // Two nonces per step through the interleaved compressor (SHA-NI latency hiding).
-  uint8_t blkB[64], dblkB[64];
-  std::memcpy(blkB, blk2, 64);
-  std::memcpy(dblkB, dblk, 64);
-  for (; i + 2 <= count; i += 2) {
-    const uint32_t n0 = start + uint32_t(i), n1 = n0 + 1;
-    store_le32(blk2 + 12, n0);
-    store_le32(blkB + 12, n1);
-    uint32_t s0[8], s1[8];
-    std::memcpy(s0, mid, 32);
-    std::memcpy(s1, mid, 32);
-    sha256_compress_x2(s0, blk2, s1, blkB);
-    for (int w = 0; w < 8; ++w) { store_be32(dblk + 4 * w, s0[w]); store_be32(dblkB + 4 * w, s1[w]); }
-    std::memcpy(s0, kSha256IV, 32);
-    std::memcpy(s1, kSha256IV, 32);
-    sha256_compress_x2(s0, dblk, s1, dblkB);
-    // H7 (big-endian word 7 = LE bytes 28..31 of the digest) first: the early reject
-    if (__builtin_bswap32(s0[7]) <= thi) {
-      for (int w = 0; w < 8; ++w) store_be32(h + 4 * w, s0[w]);
-      if (le256_leq(h, target)) hits.push_back(n0);
-    }
-    if (__builtin_bswap32(s1[7]) <= thi) {
-      for (int w = 0; w < 8; ++w) store_be32(h + 4 * w, s1[w]);
-      if (le256_leq(h, target)) hits.push_back(n1);
-    }
-  }
-  for (; i < count; ++i) {
+  for (; i < count; ++i) {  // the tail, one nonce at a time
     const uint32_t nonce = start + uint32_t(i);
     store_le32(blk2 + 12, nonce);
     sha256d_from_mid(mid, blk2, dblk, h);
     if (load_le32(h + 28) <= thi && le256_leq(h, target)) hits.push_back(nonce);
   }
   return hits;
+}
+
+std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
+                                       uint64_t count) {
+  return cpu_scan_sha256d_lanes(cpu_scan_lanes_default(), header80, target, start, count);
 }
 
 // ------------------------------------------------------------------ CPU miner
