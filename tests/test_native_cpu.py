@@ -291,3 +291,18 @@ def test_clock_bounds_track_the_window_minimum():
     assert got[7] == pytest.approx(10.00005)
     assert got[8] == pytest.approx(10.00301)   # t=4.2: only the drifted bounds remain
     assert N._clock_bounds(2.0, [(0.0, 5.0)]) == [5.0]
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+def test_cpu_scan_lanes_agree(lanes):
+    """Every interleave width of the CPU scan finds the same hits (genesis nonce at its target; an easy target over
+    a window that is not a multiple of the width, so the one-at-a-time tail runs too)."""
+    from otedama_amd.models.header import GENESIS_HEADER_HEX, int_to_hash
+    from otedama_amd.ops.native import require_native
+
+    N = require_native()
+    hdr = bytes.fromhex(GENESIS_HEADER_HEX)
+    nonce = int.from_bytes(hdr[76:80], "little")
+    assert nonce in N._cpu_scan_lanes(lanes, hdr, int_to_hash(0xFFFF << 208), nonce - 1001, 4003)
+    easy = int_to_hash((1 << 248) - 1)
+    assert N._cpu_scan_lanes(lanes, hdr, easy, 7, 3001) == N._cpu_scan_lanes(1, hdr, easy, 7, 3001)
