@@ -260,7 +260,7 @@ MinerStats MinerBase::stats() {
 
 // ---------------------------------------------------------- CPU SHA-256d scan
 
-constexpr int kCpuScanLanes = 2;  // nonces in flight per step (tools: N._cpu_scan_lanes A/B)
+constexpr int kCpuScanLanes = 4;  // nonces in flight per step: EPYC 9575F 13.2 / 22.2 / 25.3 / 26.8 MH/s for 1-4 (tools/cpu_lanes_ab.py)
 
 // Per-nonce work with a midstate: block 2 (16 B of header + padding) and the
 // 32-byte digest block. 2 compressions per nonce instead of the reference's 3.
