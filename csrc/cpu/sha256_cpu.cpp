@@ -8,6 +8,9 @@
 #include <cpuid.h>
 #include <immintrin.h>
 
+#include <type_traits>
+#include <vector>
+
 namespace otedama {
 
 const uint32_t kSha256K[64] = {
@@ -159,6 +162,128 @@ __attribute__((target("sha,sse4.1"))) static void sha256_compress_shani_xn(uint3
     _mm_storeu_si128((__m128i*)&state[l][0], S0[l]);
     _mm_storeu_si128((__m128i*)&state[l][4], S1[l]);
   }
+}
+
+// SHA-256d of L consecutive nonces of one 80-byte header, up to the word the share filter needs (H7), on SHA-NI.
+// Specialised for mining: rounds 0-1 of the header's second block use only W0, W1 (no nonce) and are hashed once
+// per call (s1_pre); the first hash's state goes to the second block's message registers directly (no store,
+// byte swap and reload); the second hash stops after round 61, where the F lane of the ABEF register already holds
+// e61 = h64, so H7 = F + IV7 (rounds 62-63 and the feed-forward of the other words are skipped).
+template <int L>
+__attribute__((target("sha,sse4.1"))) static void sha256d_h7_shani(__m128i abef_mid, __m128i cdgh_mid, __m128i s1_pre,
+                                                                  __m128i m0_tmpl, uint32_t nonce0, uint32_t h7[L]) {
+  const __m128i* K = (const __m128i*)kSha256K;
+  const __m128i PAD1 = _mm_set_epi32(0, 0, 0, int(0x80000000u));  // W4 = 0x80000000 (dword 0), W5..W7 = 0
+  const __m128i LEN1 = _mm_set_epi32(640, 0, 0, 0);               // W15 = 640 bits
+  const __m128i LEN2 = _mm_set_epi32(256, 0, 0, 0);               // second block: W15 = 256 bits
+  const __m128i IV_ABEF = _mm_set_epi32(int(0x6a09e667u), int(0xbb67ae85u), int(0x510e527fu), int(0x9b05688cu));
+  const __m128i IV_CDGH = _mm_set_epi32(int(0x3c6ef372u), int(0xa54ff53au), int(0x1f83d9abu), int(0x5be0cd19u));
+  __m128i S0[L], S1[L], M0[L], M1[L], M2[L], M3[L], MSG[L], TMP[L];
+#define QR(Mi, k)                                                    \
+  for (int l = 0; l < L; ++l) {                                      \
+    MSG[l] = _mm_add_epi32(Mi[l], _mm_loadu_si128(K + (k)));         \
+    S1[l] = _mm_sha256rnds2_epu32(S1[l], S0[l], MSG[l]);             \
+    MSG[l] = _mm_shuffle_epi32(MSG[l], 0x0E);                        \
+    S0[l] = _mm_sha256rnds2_epu32(S0[l], S1[l], MSG[l]);             \
+  }
+#define SCHED(Ma, Mb, Mc, Md)                                         \
+  for (int l = 0; l < L; ++l) {                                       \
+    TMP[l] = _mm_alignr_epi8(Md[l], Mc[l], 4); Ma[l] = _mm_add_epi32(Ma[l], TMP[l]); \
+    Ma[l] = _mm_sha256msg2_epu32(Ma[l], Md[l]); Mc[l] = _mm_sha256msg1_epu32(Mc[l], Md[l]); \
+  }
+  // ---- first hash, block 2 (from the midstate); rounds 0-1 are s1_pre
+  for (int l = 0; l < L; ++l) {
+    M0[l] = _mm_insert_epi32(m0_tmpl, int(__builtin_bswap32(nonce0 + uint32_t(l))), 3);  // W3: nonce bytes, BE
+    M1[l] = PAD1;
+    M2[l] = _mm_setzero_si128();
+    M3[l] = LEN1;
+    MSG[l] = _mm_shuffle_epi32(_mm_add_epi32(M0[l], _mm_loadu_si128(K)), 0x0E);
+    S1[l] = s1_pre;
+    S0[l] = _mm_sha256rnds2_epu32(abef_mid, s1_pre, MSG[l]);  // rounds 2-3 (W2, W3 = nonce)
+  }
+  QR(M1, 1); for (int l = 0; l < L; ++l) M0[l] = _mm_sha256msg1_epu32(M0[l], M1[l]);
+  QR(M2, 2); for (int l = 0; l < L; ++l) M1[l] = _mm_sha256msg1_epu32(M1[l], M2[l]);
+  QR(M3, 3);
+  for (int k = 4; k < 16; k += 4) {
+    SCHED(M0, M1, M2, M3); QR(M0, k);
+    SCHED(M1, M2, M3, M0); QR(M1, k + 1);
+    SCHED(M2, M3, M0, M1); QR(M2, k + 2);
+    SCHED(M3, M0, M1, M2); QR(M3, k + 3);
+  }
+  // feed-forward, then the digest words straight into the second block's message registers (dword 0 = H0 / H4)
+  for (int l = 0; l < L; ++l) {
+    S0[l] = _mm_add_epi32(S0[l], abef_mid);
+    S1[l] = _mm_add_epi32(S1[l], cdgh_mid);
+    TMP[l] = _mm_shuffle_epi32(S0[l], 0x1B);
+    S1[l] = _mm_shuffle_epi32(S1[l], 0xB1);
+    M0[l] = _mm_blend_epi16(TMP[l], S1[l], 0xF0);
+    M1[l] = _mm_alignr_epi8(S1[l], TMP[l], 8);
+    M2[l] = PAD1;
+    M3[l] = LEN2;
+    S0[l] = IV_ABEF;
+    S1[l] = IV_CDGH;
+  }
+  // ---- second hash, rounds 0..61
+  QR(M0, 0);
+  QR(M1, 1); for (int l = 0; l < L; ++l) M0[l] = _mm_sha256msg1_epu32(M0[l], M1[l]);
+  QR(M2, 2); for (int l = 0; l < L; ++l) M1[l] = _mm_sha256msg1_epu32(M1[l], M2[l]);
+  QR(M3, 3);
+  for (int k = 4; k < 12; k += 4) {
+    SCHED(M0, M1, M2, M3); QR(M0, k);
+    SCHED(M1, M2, M3, M0); QR(M1, k + 1);
+    SCHED(M2, M3, M0, M1); QR(M2, k + 2);
+    SCHED(M3, M0, M1, M2); QR(M3, k + 3);
+  }
+  SCHED(M0, M1, M2, M3); QR(M0, 12);
+  SCHED(M1, M2, M3, M0); QR(M1, 13);
+  SCHED(M2, M3, M0, M1); QR(M2, 14);
+  for (int l = 0; l < L; ++l) {  // W60..W63, then rounds 60-61 only
+    TMP[l] = _mm_alignr_epi8(M2[l], M1[l], 4); M3[l] = _mm_add_epi32(M3[l], TMP[l]);
+    M3[l] = _mm_sha256msg2_epu32(M3[l], M2[l]);
+    MSG[l] = _mm_add_epi32(M3[l], _mm_loadu_si128(K + 15));
+    S1[l] = _mm_sha256rnds2_epu32(S1[l], S0[l], MSG[l]);
+    h7[l] = uint32_t(_mm_cvtsi128_si32(S1[l])) + 0x5be0cd19u;  // F lane of ABEF after round 61 = h64
+  }
+#undef QR
+#undef SCHED
+}
+
+__attribute__((target("sha,sse4.1"))) static void sha256d_scan_h7_shani(int lanes, const uint32_t mid[8],
+                                                                       const uint8_t tail12[12], uint32_t start,
+                                                                       uint64_t count, uint32_t thi,
+                                                                       std::vector<uint32_t>* cands,
+                                                                       uint64_t* done) {
+  __m128i TMP = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&mid[0]), 0xB1);
+  __m128i CDGH = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&mid[4]), 0x1B);
+  const __m128i ABEF = _mm_alignr_epi8(TMP, CDGH, 8);
+  CDGH = _mm_blend_epi16(CDGH, TMP, 0xF0);
+  const __m128i m0 = _mm_set_epi32(0, int(load_be32(tail12 + 8)), int(load_be32(tail12 + 4)), int(load_be32(tail12)));
+  const __m128i s1_pre = _mm_sha256rnds2_epu32(CDGH, ABEF, _mm_add_epi32(m0, _mm_loadu_si128((const __m128i*)kSha256K)));
+  uint32_t h7[4];
+  uint64_t i = 0;
+  auto scan = [&](auto lanes_c) {
+    constexpr int Lc = decltype(lanes_c)::value;
+    for (; i + Lc <= count; i += Lc) {
+      const uint32_t n0 = start + uint32_t(i);
+      sha256d_h7_shani<Lc>(ABEF, CDGH, s1_pre, m0, n0, h7);
+      for (int l = 0; l < Lc; ++l)
+        if (__builtin_bswap32(h7[l]) <= thi) cands->push_back(n0 + uint32_t(l));
+    }
+  };
+  switch (lanes) {
+    case 1: scan(std::integral_constant<int, 1>{}); break;
+    case 2: scan(std::integral_constant<int, 2>{}); break;
+    case 3: scan(std::integral_constant<int, 3>{}); break;
+    default: scan(std::integral_constant<int, 4>{}); break;
+  }
+  *done = i;
+}
+
+bool sha256d_scan_h7(int lanes, const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,
+                     uint32_t thi, std::vector<uint32_t>* cands, uint64_t* done) {
+  if (!cpu_has_sha_ni()) return false;
+  sha256d_scan_h7_shani(lanes, mid, tail12, start, count, thi, cands, done);
+  return true;
 }
 
 static bool detect_sha_ni() {

@@ -8,6 +8,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 #include <cstring>
 
 namespace otedama {
@@ -38,6 +39,11 @@ void sha256_compress(uint32_t state[8], const uint8_t block[64]);
 void sha256_compress_x2(uint32_t s0[8], const uint8_t b0[64], uint32_t s1[8], const uint8_t b1[64]);
 // n independent compressions, interleaved in groups of up to 4 on SHA-NI (portable one by one otherwise).
 void sha256_compress_xn(int n, uint32_t* const state[], const uint8_t* const block[]);
+// SHA-NI nonce scan of an 80-byte header (midstate of block 1, tail12 = header bytes 64..75): appends the nonces of
+// [start, start + done) whose H7 word passes the share filter (bswap(H7) <= thi; the caller re-verifies the full
+// hash) and sets *done to the nonces covered (a multiple of `lanes`, 1..4). False without SHA-NI.
+bool sha256d_scan_h7(int lanes, const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,
+                     uint32_t thi, std::vector<uint32_t>* cands, uint64_t* done);
 bool cpu_has_sha_ni();
 
 // Full SHA-256 of an arbitrary message.

@@ -339,17 +339,27 @@ std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[8
   blk2[63] = 0x80;
   std::vector<uint32_t> hits;
   uint64_t i = 0;
-  switch (lanes) {
-    case 1: cpu_scan_lanes<1>(mid, blk2, target, start, count, &hits, &i); break;
-    case 3: cpu_scan_lanes<3>(mid, blk2, target, start, count, &hits, &i); break;
-    case 4: cpu_scan_lanes<4>(mid, blk2, target, start, count, &hits, &i); break;
-    default: cpu_scan_lanes<2>(mid, blk2, target, start, count, &hits, &i); break;
-  }
   uint8_t dblk[64] = {0};
   dblk[32] = 0x80;
   dblk[62] = 0x01;
   uint8_t h[32];
   const uint32_t thi = load_le32(target + 28);
+  std::vector<uint32_t> cands;
+  if (sha256d_scan_h7(lanes, mid, header80 + 64, start, count, thi, &cands, &i)) {
+    // SHA-NI: the fused H7 scan; its candidates get the full hash and 256-bit compare here
+    for (uint32_t n : cands) {
+      store_le32(blk2 + 12, n);
+      sha256d_from_mid(mid, blk2, dblk, h);
+      if (le256_leq(h, target)) hits.push_back(n);
+    }
+  } else {
+    switch (lanes) {
+      case 1: cpu_scan_lanes<1>(mid, blk2, target, start, count, &hits, &i); break;
+      case 3: cpu_scan_lanes<3>(mid, blk2, target, start, count, &hits, &i); break;
+      case 4: cpu_scan_lanes<4>(mid, blk2, target, start, count, &hits, &i); break;
+      default: cpu_scan_lanes<2>(mid, blk2, target, start, count, &hits, &i); break;
+    }
+  }
   for (; i < count; ++i) {  // the tail, one nonce at a time
     const uint32_t nonce = start + uint32_t(i);
     store_le32(blk2 + 12, nonce);
