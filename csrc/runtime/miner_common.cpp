@@ -1,5 +1,6 @@
 // Host side of the mining runtime: job variants, share verification, the share
 // queue, the CPU miner and the CPU scrypt reference.
+#include <cpuid.h>
 #include <immintrin.h>
 #include <sys/eventfd.h>
 #include <unistd.h>
@@ -260,7 +261,19 @@ MinerStats MinerBase::stats() {
 
 // ---------------------------------------------------------- CPU SHA-256d scan
 
-constexpr int kCpuScanLanes = 4;  // nonces in flight per step: EPYC 9575F 13.2 / 22.2 / 25.3 / 26.8 MH/s for 1-4 (tools/cpu_lanes_ab.py)
+// Nonces in flight per step of the fused SHA-NI scan, single thread (tools/cpu_lanes_ab.py, profiles/r4/m_cpu_lanes):
+// AMD EPYC 9575F 21.2 / 31.3 / 35.0 / 36.4 MH/s for 1-4 lanes; the build container's Intel Xeon 9.8 / 11.6 / 10.3 /
+// 10.1. So 4 on AMD cores, 2 elsewhere.
+static int cpu_scan_lanes_for_this_cpu() {
+  unsigned a = 0, b = 0, c = 0, d = 0;
+  if (!__get_cpuid(0, &a, &b, &c, &d)) return 2;
+  char vendor[13];
+  std::memcpy(vendor, &b, 4);
+  std::memcpy(vendor + 4, &d, 4);
+  std::memcpy(vendor + 8, &c, 4);
+  vendor[12] = 0;
+  return std::strcmp(vendor, "AuthenticAMD") == 0 ? 4 : 2;
+}
 
 // Per-nonce work with a midstate: block 2 (16 B of header + padding) and the
 // 32-byte digest block. 2 compressions per nonce instead of the reference's 3.
@@ -322,7 +335,7 @@ static int cpu_scan_lanes_default() {
   static const int lanes = [] {
     const char* v = std::getenv("OTEDAMA_CPU_LANES");
     const int n = v ? std::atoi(v) : 0;
-    return n >= 1 && n <= 4 ? n : kCpuScanLanes;
+    return n >= 1 && n <= 4 ? n : cpu_scan_lanes_for_this_cpu();
   }();
   return lanes;
 }
