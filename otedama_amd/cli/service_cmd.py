@@ -43,12 +43,17 @@ def _install(args, stdout, stderr) -> int:
     fs.string("log-level", "", "Log level for the service (debug|info|warn|error).")
     fs.string("log-format", "", "Log format for the service (text|json).")
     fs.string("language", "", "UI language for the service (en, ja, ...).")
+    fs.int("node-gpus", 0, "Run the multi-GPU node (one rank per GPU over RCCL) on this many GPUs instead of "
+                           "`otedama run`.")
     rc = parse_subcommand(fs, args, stdout, stderr)
     if rc is not None:
         return rc
     try:
+        if fs["node-gpus"] < 0:
+            stderr.write("service install: --node-gpus must be >= 0\n")
+            return EXIT_USAGE
         mgr = new_daemon_manager(fs["config"], fs["data-dir"], daemon.ServiceFlags(
-            fs["bitcoin-address"], fs["log-level"], fs["log-format"], fs["language"]))
+            fs["bitcoin-address"], fs["log-level"], fs["log-format"], fs["language"], fs["node-gpus"]))
     except Exception as exc:  # noqa: BLE001
         stderr.write(f"service: {exc}\n")
         return EXIT_RUNTIME

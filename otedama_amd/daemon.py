@@ -55,6 +55,7 @@ class ServiceFlags:
     log_level: str = ""
     log_format: str = ""
     language: str = ""
+    node_gpus: int = 0  # > 0: the service runs the multi-GPU node (`otedama node --gpus N`) instead of `otedama run`
 
 
 @dataclass
@@ -109,7 +110,8 @@ class Manager:
 
     # ------------------------------------------------------------------ argv
     def service_argv(self) -> list[str]:
-        argv = ["run"]
+        # the node's supervisor restarts lost ranks itself; the service manager restarts the supervisor
+        argv = ["node", "--gpus", str(self.flags.node_gpus)] if self.flags.node_gpus > 0 else ["run"]
         if self.config_path:
             argv += ["--config", self.config_path]
         if self.data_dir:

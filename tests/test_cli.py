@@ -387,6 +387,16 @@ def test_service_install_success_passes_flags(fake_service):
     assert what == "install" and data_dir == "/d" and flags.bitcoin_address == ADDR and flags.log_level == "debug"
 
 
+def test_service_install_node_mode(fake_service):
+    """--node-gpus N: the service runs the multi-GPU node (its supervisor restarts ranks; the service manager restarts
+    the supervisor)."""
+    rc, _, _ = _cli("service", "install", "--bitcoin-address", ADDR, "--node-gpus", "8")
+    assert rc == 0
+    (_, (_, _, flags)), _ = fake_service
+    assert flags.node_gpus == 8
+    assert _cli("service", "install", "--node-gpus", "-1")[0] == 64
+
+
 def test_service_install_bad_flag(fake_service):
     assert _cli("service", "install", "--frob")[0] == 64 and fake_service == []
 

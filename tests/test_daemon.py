@@ -54,6 +54,14 @@ def test_service_argv_includes_only_set_flags(tmp_path):
     assert m2.program_argv()[:3] == [m2.executable, "-m", "otedama_amd"]
 
 
+def test_node_service_runs_the_supervisor(tmp_path):
+    m = mgr(tmp_path, config="/etc/otd.yaml", bitcoin_address=ADDR, node_gpus=8)
+    assert m.service_argv()[:3] == ["node", "--gpus", "8"]
+    assert m.service_argv()[3:] == ["--config", "/etc/otd.yaml", "--data-dir", str(tmp_path / "data"),
+                                    "--bitcoin-address", ADDR]
+    assert f"ExecStart={m.executable} -m otedama_amd node --gpus 8 --config /etc/otd.yaml" in m.systemd_unit()
+
+
 def test_all_flags_in_order(tmp_path):
     m = mgr(tmp_path, bitcoin_address=ADDR, log_level="warn", log_format="json", language="ja")
     argv = m.service_argv()
