@@ -42,6 +42,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 from __future__ import annotations
 
 import argparse
+import contextlib
 import hashlib
 import json
 import math
@@ -303,22 +304,27 @@ def run_rank(args) -> int:
                 lo = (i % steps_per_group) * V_COUNT
                 for j in range(SUB_LAUNCHES):
                     search.launch_into(prep, lo + j * sub, sub, out, s0 if j % 2 == 0 else s1)
-                s0.wait_stream(s1)
+                # The step's consumers (the hit copy, R2) go behind its last launch on s1, which waits for s0's last
+                # launch only: s0 starts the next step at once and that launch overlaps this step's tail, as the
+                # production miner's two streams never join.
+                s1.wait_stream(s0)
         else:
             hdr, params = variant_params(i)
             search.launch(params, 0, 1 << 32, out=out)  # K1: full 2^32 nonce space
-        if record:  # with the nonce window the step covered (W3 = bswap(nonce) for the v kernel)
-            lo = (i % steps_per_group) * V_COUNT if use_v else 0
-            hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
+        tail = s1 if (use_v and not cpu) else None
+        with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+            if record:  # with the nonce window the step covered (W3 = bswap(nonce) for the v kernel)
+                lo = (i % steps_per_group) * V_COUNT if use_v else 0
+                hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
 
-        def r2(o=out, g=gathered[b]):
-            if world > 1:
-                torch.distributed.all_gather_into_tensor(g.view(-1), o)
-            else:
-                g[0].copy_(o)
-            r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
+            def r2(o=out, g=gathered[b]):
+                if world > 1:
+                    torch.distributed.all_gather_into_tensor(g.view(-1), o)
+                else:
+                    g[0].copy_(o)
+                r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
 
-        r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
+            r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
 
     # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
     # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
