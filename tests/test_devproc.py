@@ -170,3 +170,23 @@ def test_process_isolation_engine_side_does_not_load_the_extension():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
                          env=dict(os.environ, OTEDAMA_NO_TORCH="1"))
     assert out.stdout.strip() == "False", out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("env,want", [({"OTEDAMA_DEVICE_HW_QUEUES": "1"}, "1"),
+                                      ({"OTEDAMA_DEVICE_HW_QUEUES": "1", "GPU_MAX_HW_QUEUES": "3"}, "3"),
+                                      ({}, None)])
+def test_device_process_hardware_queue_cap(env, want):
+    """OTEDAMA_DEVICE_HW_QUEUES reaches the child as GPU_MAX_HW_QUEUES (an explicit GPU_MAX_HW_QUEUES wins); by
+    default the runtime's own cap stays (the two search streams need their own queues, docs/RUNTIME.md)."""
+    from otedama_amd.engine.devproc import DeviceProcess
+
+    base = {k: v for k, v in os.environ.items() if k not in ("OTEDAMA_DEVICE_HW_QUEUES", "GPU_MAX_HW_QUEUES")}
+    dp = DeviceProcess(0, "cpu-q", cpu_threads=1, env=dict(base, **env))
+    dp.start()
+    try:
+        with open(f"/proc/{dp.pid}/environ", "rb") as f:
+            child = dict(kv.split(b"=", 1) for kv in f.read().split(b"\0") if b"=" in kv)
+    finally:
+        dp.stop()
+    got = child.get(b"GPU_MAX_HW_QUEUES")
+    assert (got.decode() if got is not None else None) == want
