@@ -167,30 +167,39 @@ def test_target_only_update_reaches_the_running_group():
 
 
 def test_scrypt_switch_stops_the_romix_batch():
+    """New scrypt work stops the running batches: polls at both ROMix phase boundaries and, from the scalar unit,
+    every 64 iterations of the write loop; the two half-grid batches run half a hash apart, so one of them is always
+    writing and frees its half within ~1 ms (under 10 ms p50; round 3 took 12-17 ms)."""
+    import statistics
+
     N = _native()
-    hdr_a, hdr_b = os.urandom(76) + bytes(4), os.urandom(76) + bytes(4)
+    hdrs = [os.urandom(76) + bytes(4) for _ in range(6)]
     target = (1 << 240) - 1  # ~16 hits per 1 Mi-hash batch
     m = N.GpuMiner(0, "gpu-0", batch_nonces=1 << 29)
-    m.set_job(_job(hdr_a, target, 1, "a", algo="scrypt"))
+    m.set_job(_job(hdrs[0], target, 1, "j0", algo="scrypt"))
     m.start()
+    shares = []
     try:
         t0 = time.monotonic()
         while m.stats()["job_switches"] < 1 and time.monotonic() - t0 < 30:  # 128 GiB scratch + first batch
             time.sleep(0.01)
-        time.sleep(0.3)
-        m.set_job(_job(hdr_b, target, 2, "b", algo="scrypt"))
-        time.sleep(0.5)
-        shares = m.poll(4096)
+        for k in range(1, 6):
+            time.sleep(0.3)
+            m.set_job(_job(hdrs[k], target, k + 1, f"j{k}", algo="scrypt"))
+            shares += m.poll(4096)
+        time.sleep(0.4)
+        shares += m.poll(4096)
     finally:
         m.stop()
     st = m.stats()
     assert not st["faulted"], st
-    print("scrypt switch ms:", st["job_switch_ms"])
-    # polls at both ROMix phase boundaries: a running wave stops within one phase (~15 ms)
-    assert st["job_switches"] >= 2 and st["last_job_switch_ms"] < 45.0, st
+    sw = st["job_switch_ms"][-5:]
+    print("scrypt switch ms:", sw)
+    assert st["job_switches"] >= 6 and statistics.median(sw) < 10.0 and max(sw) < 45.0, st
     assert st["aborted_launches"] >= 1
+    by_id = {f"j{k}": h for k, h in enumerate(hdrs)}
     for s in shares[:40]:
-        _check_share(hdr_b if s["job_id"] == "b" else hdr_a, s, target, "scrypt")
+        _check_share(by_id[s["job_id"]], s, target, "scrypt")
 
 
 def test_startup_phases_are_recorded():
