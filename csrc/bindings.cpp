@@ -193,6 +193,24 @@ PYBIND11_MODULE(_native, m) {
   m.attr("SCRYPT_COOP_SPLIT") = kScryptCoopSplit;
   m.attr("AEAD_AES256GCM") = 0;
   m.attr("AEAD_CHACHA20POLY1305") = 1;
+  m.def("scrypt_1024_1_1_batch", [](const std::vector<py::bytes>& hs) {
+    std::vector<std::string> in;
+    for (const auto& h : hs) in.push_back(need(h, 80, "header"));
+    std::vector<std::array<uint8_t, 32>> out(in.size());
+    std::vector<const uint8_t*> ip;
+    std::vector<uint8_t*> op;
+    for (size_t i = 0; i < in.size(); ++i) {
+      ip.push_back(reinterpret_cast<const uint8_t*>(in[i].data()));
+      op.push_back(out[i].data());
+    }
+    {
+      py::gil_scoped_release r;
+      scrypt_1024_1_1_batch(int(in.size()), ip.data(), op.data());
+    }
+    py::list res;
+    for (const auto& o : out) res.append(to_bytes(o.data(), 32));
+    return res;
+  });
   m.def("scrypt_1024_1_1", [](const py::bytes& h) {
     std::string s = need(h, 80, "header"); uint8_t o[32];
     { py::gil_scoped_release r; scrypt_1024_1_1(reinterpret_cast<const uint8_t*>(s.data()), o); }

@@ -111,6 +111,8 @@ struct MinerStats {
 // Full-target re-verification of a candidate (host SHA-256d / scrypt).
 bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32], uint8_t hash_out[32]);
 void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]);
+// n scrypt(1024, 1, 1) hashes, eight at a time on AVX2 (one at a time without it).
+void scrypt_1024_1_1_batch(int n, const uint8_t* const header80[], uint8_t* const out[]);
 void merkle_root_from_coinbase(const JobTemplate& job, uint64_t extranonce2, uint8_t root_out[32]);
 
 // Bounded share queue with an eventfd that becomes readable on every push, so a consumer (the asyncio engine

@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <deque>
 #include <mutex>
+#include <vector>
 
 namespace otedama {
 
@@ -36,6 +37,19 @@ class BoundedWorkQueue {
     *out = std::move(q_.front());
     q_.pop_front();
     return true;
+  }
+
+  // Blocks until at least one item or stop(); then takes up to `max` items. 0 once stopped and drained.
+  size_t pop_many(std::vector<T>* out, size_t max) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+    size_t n = 0;
+    while (!q_.empty() && n < max) {
+      out->push_back(std::move(q_.front()));
+      q_.pop_front();
+      ++n;
+    }
+    return n;
   }
 
   // Wake the consumer to drain and exit; keep at most `keep` items (a stopping miner bounds the work left).

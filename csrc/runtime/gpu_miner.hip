@@ -428,7 +428,7 @@ void GpuMiner::loop() {
 
   auto verify_push = [&](const Candidate& b, uint32_t nonce, uint32_t vi, uint32_t stamp, bool stamped,
                          const std::shared_ptr<const JobTemplate>& cur, uint64_t cur_g, uint64_t* good,
-                         uint64_t* bad) {
+                         uint64_t* bad, const uint8_t* pre_hash = nullptr) {
     if (vi >= (uint32_t)b.nvar) { ++*bad; return; }
     uint8_t hdr[80];
     std::memcpy(hdr, b.group->header[vi], 80);
@@ -437,7 +437,13 @@ void GpuMiner::loop() {
     // A target-only update (same work generation) applies to batches in flight too: their hits are checked
     // against, and reported under, the current template (its target and control-plane epoch).
     const JobTemplate* tj = (cur && cur_g == b.gen) ? cur.get() : b.job.get();
-    if (!verify_share(b.job->algo, hdr, tj->target, r.hash)) { ++*bad; return; }
+    if (pre_hash) {
+      std::memcpy(r.hash, pre_hash, 32);
+      if (!le256_leq(r.hash, tj->target)) { ++*bad; return; }
+    } else if (!verify_share(b.job->algo, hdr, tj->target, r.hash)) {
+      ++*bad;
+      return;
+    }
     r.epoch = tj->epoch; r.job_id = tj->job_id; r.channel_id = tj->channel_id;
     r.nonce = nonce; r.ntime = b.group->ntime[vi]; r.version = b.group->version[vi]; r.extranonce2 = b.group->en2[vi];
     r.extranonce2_size = b.job->extranonce2_size; r.device_id = device_id_;
@@ -447,12 +453,32 @@ void GpuMiner::loop() {
     ++*good;
   };
 
+  // Scrypt candidates are re-hashed eight at a time (AVX2 lanes, ~3x the scalar rate per hash), so a burst of
+  // easy-target hits drains in a third of the time.
   verifier = std::thread([&] {
-    Candidate c;
-    while (vq.pop(&c)) {  // false once stopped and drained
+    std::vector<Candidate> cs;
+    cs.reserve(8);
+    uint8_t hb[8][80], ho[8][32];
+    const uint8_t* ip[8];
+    uint8_t* op[8];
+    for (int l = 0; l < 8; ++l) { ip[l] = hb[l]; op[l] = ho[l]; }
+    while (cs.clear(), vq.pop_many(&cs, 8) > 0) {  // 0 once stopped and drained
       uint64_t good = 0, bad = 0, g = 0;
       auto cur = peek_job(&g, nullptr);
-      verify_push(c, c.nonce, c.vi, c.stamp, true, cur, g, &good, &bad);
+      int n = 0;
+      for (const Candidate& c : cs) {
+        if (c.job->algo != Algo::kScrypt || c.vi >= (uint32_t)c.nvar) continue;
+        std::memcpy(hb[n], c.group->header[c.vi], 80);
+        store_le32(hb[n] + 76, c.nonce);
+        ++n;
+      }
+      if (n > 0) scrypt_1024_1_1_batch(n, ip, op);
+      int l = 0;
+      for (const Candidate& c : cs) {
+        const bool batched = c.job->algo == Algo::kScrypt && c.vi < (uint32_t)c.nvar;
+        verify_push(c, c.nonce, c.vi, c.stamp, true, cur, g, &good, &bad, batched ? ho[l] : nullptr);
+        l += batched;
+      }
       std::lock_guard<std::mutex> sg(stats_mu_);
       stats_.shares += good;
       stats_.rejected_candidates += bad;

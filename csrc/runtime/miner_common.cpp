@@ -5,10 +5,14 @@
 #include <sys/eventfd.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <stdexcept>
+#include <vector>
 
 #include "otedama/job.h"
 #include "otedama/runtime.h"
@@ -159,6 +163,104 @@ void scrypt_1024_1_1(const uint8_t header80[80], uint8_t out[32]) {
   }
   for (int i = 0; i < 32; ++i) store_le32(b + 4 * i, X[i]);
   pbkdf2_sha256(header80, 80, b, 128, 1, out, 32);
+}
+
+// Eight scrypt(1024, 1, 1) hashes at once with AVX2: word k of lane l's 1 KiB-wide state lives in lane l of X[k], the
+// 1 MiB pad holds the eight lanes' entries interleaved the same way, and each lookup gathers its lanes' own rows.
+// The host verifier of the GPU miner and the CPU miner hash scrypt candidates in batches of up to eight this way.
+__attribute__((target("avx2"))) static inline __m256i rotl_x8(__m256i x, int n) {
+  return _mm256_or_si256(_mm256_slli_epi32(x, n), _mm256_srli_epi32(x, 32 - n));
+}
+
+__attribute__((target("avx2"))) static void salsa20_8_x8(__m256i B[16]) {
+  __m256i x[16];
+  for (int i = 0; i < 16; ++i) x[i] = B[i];
+#define QS(a, b, c, n) x[a] = _mm256_xor_si256(x[a], rotl_x8(_mm256_add_epi32(x[b], x[c]), n))
+  for (int i = 0; i < 8; i += 2) {
+    QS(4, 0, 12, 7);   QS(8, 4, 0, 9);    QS(12, 8, 4, 13);   QS(0, 12, 8, 18);
+    QS(9, 5, 1, 7);    QS(13, 9, 5, 9);   QS(1, 13, 9, 13);   QS(5, 1, 13, 18);
+    QS(14, 10, 6, 7);  QS(2, 14, 10, 9);  QS(6, 2, 14, 13);   QS(10, 6, 2, 18);
+    QS(3, 15, 11, 7);  QS(7, 3, 15, 9);   QS(11, 7, 3, 13);   QS(15, 11, 7, 18);
+    QS(1, 0, 3, 7);    QS(2, 1, 0, 9);    QS(3, 2, 1, 13);    QS(0, 3, 2, 18);
+    QS(6, 5, 4, 7);    QS(7, 6, 5, 9);    QS(4, 7, 6, 13);    QS(5, 4, 7, 18);
+    QS(11, 10, 9, 7);  QS(8, 11, 10, 9);  QS(9, 8, 11, 13);   QS(10, 9, 8, 18);
+    QS(12, 15, 14, 7); QS(13, 12, 15, 9); QS(14, 13, 12, 13); QS(15, 14, 13, 18);
+  }
+#undef QS
+  for (int i = 0; i < 16; ++i) B[i] = _mm256_add_epi32(B[i], x[i]);
+}
+
+__attribute__((target("avx2"))) static void scrypt_romix_x8(uint32_t Xs[8][32]) {
+  alignas(32) __m256i X[32];
+  for (int k = 0; k < 32; ++k)
+    X[k] = _mm256_setr_epi32(int(Xs[0][k]), int(Xs[1][k]), int(Xs[2][k]), int(Xs[3][k]), int(Xs[4][k]),
+                             int(Xs[5][k]), int(Xs[6][k]), int(Xs[7][k]));
+  // per thread, reused: 1024 entries x 32 words x 8 lanes (1 MiB). A std::vector<__m256i> would drop the type's
+  // 32-byte alignment (GCC ignores attributes on template arguments) and the aligned stores would fault.
+  struct Pad {
+    __m256i* p = static_cast<__m256i*>(std::aligned_alloc(64, 1024 * 32 * sizeof(__m256i)));
+    ~Pad() { std::free(p); }
+  };
+  thread_local Pad pad;
+  __m256i* V = pad.p;
+  if (V == nullptr) throw std::bad_alloc();
+  for (int i = 0; i < 1024; ++i) {
+    std::memcpy(&V[32 * size_t(i)], X, sizeof X);
+    for (int k = 0; k < 16; ++k) X[k] = _mm256_xor_si256(X[k], X[16 + k]);
+    salsa20_8_x8(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] = _mm256_xor_si256(X[16 + k], X[k]);
+    salsa20_8_x8(X + 16);
+  }
+  const int* base = reinterpret_cast<const int*>(V);
+  const __m256i lane = _mm256_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7);
+  const __m256i mask = _mm256_set1_epi32(1023);
+  for (int i = 0; i < 1024; ++i) {
+    // lane l's row j_l: 32-bit element (j_l * 32 + k) * 8 + l of the pad
+    const __m256i row = _mm256_add_epi32(_mm256_slli_epi32(_mm256_and_si256(X[16], mask), 8), lane);
+    for (int k = 0; k < 32; ++k)
+      X[k] = _mm256_xor_si256(X[k], _mm256_i32gather_epi32(base, _mm256_add_epi32(row, _mm256_set1_epi32(8 * k)), 4));
+    for (int k = 0; k < 16; ++k) X[k] = _mm256_xor_si256(X[k], X[16 + k]);
+    salsa20_8_x8(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] = _mm256_xor_si256(X[16 + k], X[k]);
+    salsa20_8_x8(X + 16);
+  }
+  alignas(32) uint32_t w[8];
+  for (int k = 0; k < 32; ++k) {
+    _mm256_store_si256(reinterpret_cast<__m256i*>(w), X[k]);
+    for (int l = 0; l < 8; ++l) Xs[l][k] = w[l];
+  }
+}
+
+static bool cpu_has_avx2() {
+  static const bool ok = __builtin_cpu_supports("avx2");
+  return ok;
+}
+
+void scrypt_1024_1_1_batch(int n, const uint8_t* const header80[], uint8_t* const out[]) {
+  if (n <= 0) return;
+  if (!cpu_has_avx2()) {
+    for (int i = 0; i < n; ++i) scrypt_1024_1_1(header80[i], out[i]);
+    return;
+  }
+  for (int at = 0; at < n; at += 8) {
+    const int m = std::min(8, n - at);
+    if (m < 3) {  // eight lanes cost ~3 scalar hashes: one or two headers go the scalar way
+      for (int l = 0; l < m; ++l) scrypt_1024_1_1(header80[at + l], out[at + l]);
+      continue;
+    }
+    uint32_t Xs[8][32];
+    uint8_t b[128];
+    for (int l = 0; l < 8; ++l) {  // unused lanes repeat the last header
+      const uint8_t* h = header80[at + std::min(l, m - 1)];
+      pbkdf2_sha256(h, 80, h, 80, 1, b, 128);
+      for (int k = 0; k < 32; ++k) Xs[l][k] = load_le32(b + 4 * k);
+    }
+    scrypt_romix_x8(Xs);
+    for (int l = 0; l < m; ++l) {
+      for (int k = 0; k < 32; ++k) store_le32(b + 4 * k, Xs[l][k]);
+      pbkdf2_sha256(header80[at + l], 80, b, 128, 1, out[at + l], 32);
+    }
+  }
 }
 
 bool verify_share(Algo algo, const uint8_t header80[80], const uint8_t target[32], uint8_t hash_out[32]) {
@@ -449,6 +551,23 @@ void CpuMiner::loop(int /*tid*/) {
     std::vector<uint32_t> hits;
     if (sha) {
       hits = cpu_scan_sha256d(hdr, job->target, nonce0, kChunk);
+    } else if (job->algo == Algo::kScrypt) {
+      // eight nonces per scrypt batch (AVX2 lanes)
+      uint8_t hb[8][80], ho[8][32];
+      const uint8_t* ip[8];
+      uint8_t* op[8];
+      for (int l = 0; l < 8; ++l) {
+        std::memcpy(hb[l], hdr, 80);
+        ip[l] = hb[l];
+        op[l] = ho[l];
+      }
+      for (uint64_t i = 0; i < kChunk && running_.load(); i += 8) {
+        const int n = int(std::min<uint64_t>(8, kChunk - i));
+        for (int l = 0; l < n; ++l) store_le32(hb[l] + 76, nonce0 + uint32_t(i) + uint32_t(l));
+        scrypt_1024_1_1_batch(n, ip, op);
+        for (int l = 0; l < n; ++l)
+          if (le256_leq(ho[l], job->target)) hits.push_back(nonce0 + uint32_t(i) + uint32_t(l));
+      }
     } else {
       uint8_t h[32];
       for (uint64_t i = 0; i < kChunk && running_.load(); ++i) {

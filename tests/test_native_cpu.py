@@ -36,6 +36,14 @@ def test_scrypt_reference_matches_hashlib():
         assert N.scrypt_1024_1_1(h) == hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32)
 
 
+def test_scrypt_batch_matches_hashlib_for_every_lane_count():
+    """The AVX2 8-lane scrypt (host verifier and CPU miner path) against hashlib for 1..8 headers and a 9-header
+    call (split internally into 8 + 1); hosts without AVX2 take the scalar chain under the same binding."""
+    for n in (1, 3, 8, 9):
+        hs = [os.urandom(80) for _ in range(n)]
+        assert N.scrypt_1024_1_1_batch(hs) == [hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32) for h in hs]
+
+
 def test_cpu_scan_finds_genesis_nonce():
     nonce = 2083236893
     tgt = int_to_hash(0xFFFF << 208)
