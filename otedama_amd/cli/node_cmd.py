@@ -43,9 +43,10 @@ def cmd_node(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         return EXIT_USAGE
     from otedama_amd.parallel.launch import supervise_node, visible_gpus
 
-    n = visible_gpus()
-    if os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo" and n < gpus:
-        stderr.write(f"otedama node: --gpus {gpus} needs {gpus} visible GPUs, this host has {n}\n")
-        return EXIT_USAGE
+    if os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
+        n = visible_gpus()
+        if n < gpus:
+            stderr.write(f"otedama node: --gpus {gpus} needs {gpus} visible GPUs, this host has {n}\n")
+            return EXIT_USAGE
     cmd = [sys.executable, "-m", "otedama_amd", "run", *rest]
     return supervise_node(cmd, gpus, respawn=respawn, log=lambda m: stderr.write(f"[node] {m}\n"))

@@ -35,7 +35,14 @@ def free_port() -> int:
 
 
 def visible_gpus() -> int:
-    """HIP devices visible to a child (honours HIP/ROCR/CUDA_VISIBLE_DEVICES) without initialising HIP here."""
+    """HIP devices visible to a child (honours HIP/ROCR/CUDA_VISIBLE_DEVICES) without initialising HIP here: from
+    the KFD topology in sysfs (no torch import, so the supervisor stays small), else torch's device count."""
+    from otedama_amd.hal import KFD_TOPOLOGY_PATH, KFDDriver
+
+    if os.path.isdir(KFD_TOPOLOGY_PATH):
+        n = len(KFDDriver().enumerate())
+        if n:
+            return n
     try:
         import torch
 
@@ -107,8 +114,9 @@ def run_ranks(cmd: Sequence[str], world: int, port: int | None = None, env: dict
 def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env: dict | None = None,
                    respawn: bool = True, backoff_initial: float = 1.0, backoff_max: float = 64.0, log=None,
                    stop_event=None) -> int:
-    """Run a fault-tolerant node: ``world`` ranks of ``cmd`` around a rendezvous TCPStore hosted HERE (this
-    process is GPU-free and outlives any rank).
+    """Run a fault-tolerant node: ``world`` ranks of ``cmd`` around a rendezvous store hosted HERE (this
+    process is GPU-free, torch-free and outlives any rank; parallel/kvstore.py serves torch's TCPStore protocol, so
+    the ranks join it with plain ``dist.TCPStore`` clients).
 
     A follower (rank > 0) that exits is marked ``otd/dead/<r>`` in the store (the leader re-forms the process
     group without it within one liveness check, parallel/node.py) and, with ``respawn``, restarted after a backoff
@@ -118,13 +126,11 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
     running node over (parallel/node.py ``NodeMinerSet._take_over``); the followers keep hashing meanwhile. Only a
     clean exit (0), a usage / configuration error (64 / 78, which a restart cannot fix) or ``respawn=False`` ends
     the node with rank 0's exit code."""
-    import datetime
-
-    import torch.distributed as dist
+    from .kvstore import StoreServer
 
     log = log or (lambda msg: print(f"[node] {msg}", file=sys.stderr, flush=True))
-    port = port or free_port()
-    store = dist.TCPStore(MASTER_ADDR, port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    store = StoreServer(MASTER_ADDR, port or 0)  # torch's TCPStore protocol without importing torch (~25 MiB)
+    port = store.port
     procs: dict[int, subprocess.Popen] = {}
     backoff = {r: backoff_initial for r in range(world)}
     respawn_at: dict[int, float] = {}
@@ -188,5 +194,6 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
             time.sleep(0.05)
     finally:
         _stop_all(list(procs.values()), grace=10.0)
+        store.close()
         for sig, h in prev.items():
             signal.signal(sig, h)

@@ -5,7 +5,6 @@ survivors and re-broadcasts the job with a variant base past every reported curs
 class is covered by the survivors; verified shares keep flowing; every process exits (nothing hangs). A
 replacement process started by the supervisor is re-admitted by the next re-form. In steady state with no shares
 and no job churn a rank issues at most about one device collective per second."""
-import datetime
 import json
 import os
 import signal
@@ -14,9 +13,9 @@ import sys
 import time
 
 import pytest
-import torch.distributed as dist
 
 from otedama_amd.models.header import sha256d
+from otedama_amd.parallel.kvstore import StoreServer
 from otedama_amd.parallel.launch import free_port, rank_env
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -83,7 +82,7 @@ def _verify(s):
 @pytest.mark.parametrize("world,victim,mark_dead", [(4, 2, True), (8, 5, True), (4, 3, False)])
 def test_rank_loss_reforms_and_keeps_mining(tmp_path, world, victim, mark_dead):
     port = free_port()
-    store = dist.TCPStore("127.0.0.1", port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    store = StoreServer("127.0.0.1", port)  # the supervisor's store
     procs = _spawn(world, tmp_path, "kill", port)
     try:
         assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
@@ -97,6 +96,7 @@ def test_rank_loss_reforms_and_keeps_mining(tmp_path, world, victim, mark_dead):
         for p in procs.values():
             if p.poll() is None:
                 p.kill()
+        store.close()
     assert all(c == 0 for c in codes.values()), (codes, open(tmp_path / "err0.txt").read()[-3000:])
     res = json.loads((tmp_path / "result.json").read_text())
     assert res["phase1_devices"] == sorted(["cpu-0"] + [f"rank{r}" for r in range(1, world)])
@@ -125,7 +125,7 @@ def test_rank_loss_reforms_and_keeps_mining(tmp_path, world, victim, mark_dead):
 def test_replacement_rank_rejoins(tmp_path):
     world, victim = 4, 1
     port = free_port()
-    store = dist.TCPStore("127.0.0.1", port, None, True, datetime.timedelta(seconds=60), wait_for_workers=False)
+    store = StoreServer("127.0.0.1", port)  # the supervisor's store
     procs = _spawn(world, tmp_path, "rejoin", port)
     try:
         assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
@@ -140,6 +140,7 @@ def test_replacement_rank_rejoins(tmp_path):
         for p in procs.values():
             if p.poll() is None:
                 p.kill()
+        store.close()
     res = json.loads((tmp_path / "result.json").read_text())
     assert codes[0] == 0, (codes, res.get("logs"))
     assert res["members_after_rejoin"] == [0, 1, 2, 3], res["logs"]
