@@ -236,29 +236,110 @@ static bool cpu_has_avx2() {
   return ok;
 }
 
-void scrypt_1024_1_1_batch(int n, const uint8_t* const header80[], uint8_t* const out[]) {
-  if (n <= 0) return;
-  if (!cpu_has_avx2()) {
-    for (int i = 0; i < n; ++i) scrypt_1024_1_1(header80[i], out[i]);
-    return;
+// Sixteen at once with AVX-512 (the MI355X hosts' Zen 5 cores have a full-width 512-bit datapath): same layout as
+// the eight-lane pass with 16 lanes per word, and Salsa's rotates as single vprold instructions (three operations
+// per step instead of the five AVX2 needs for add, shift, shift, or, xor).
+__attribute__((target("avx512f"))) static void salsa20_8_x16(__m512i B[16]) {
+  __m512i x[16];
+  for (int i = 0; i < 16; ++i) x[i] = B[i];
+#define QS(a, b, c, n) x[a] = _mm512_xor_si512(x[a], _mm512_rol_epi32(_mm512_add_epi32(x[b], x[c]), n))
+  for (int i = 0; i < 8; i += 2) {
+    QS(4, 0, 12, 7);   QS(8, 4, 0, 9);    QS(12, 8, 4, 13);   QS(0, 12, 8, 18);
+    QS(9, 5, 1, 7);    QS(13, 9, 5, 9);   QS(1, 13, 9, 13);   QS(5, 1, 13, 18);
+    QS(14, 10, 6, 7);  QS(2, 14, 10, 9);  QS(6, 2, 14, 13);   QS(10, 6, 2, 18);
+    QS(3, 15, 11, 7);  QS(7, 3, 15, 9);   QS(11, 7, 3, 13);   QS(15, 11, 7, 18);
+    QS(1, 0, 3, 7);    QS(2, 1, 0, 9);    QS(3, 2, 1, 13);    QS(0, 3, 2, 18);
+    QS(6, 5, 4, 7);    QS(7, 6, 5, 9);    QS(4, 7, 6, 13);    QS(5, 4, 7, 18);
+    QS(11, 10, 9, 7);  QS(8, 11, 10, 9);  QS(9, 8, 11, 13);   QS(10, 9, 8, 18);
+    QS(12, 15, 14, 7); QS(13, 12, 15, 9); QS(14, 13, 12, 13); QS(15, 14, 13, 18);
   }
-  for (int at = 0; at < n; at += 8) {
-    const int m = std::min(8, n - at);
-    if (m < 3) {  // eight lanes cost ~3 scalar hashes: one or two headers go the scalar way
-      for (int l = 0; l < m; ++l) scrypt_1024_1_1(header80[at + l], out[at + l]);
-      continue;
-    }
-    uint32_t Xs[8][32];
-    uint8_t b[128];
-    for (int l = 0; l < 8; ++l) {  // unused lanes repeat the last header
-      const uint8_t* h = header80[at + std::min(l, m - 1)];
-      pbkdf2_sha256(h, 80, h, 80, 1, b, 128);
-      for (int k = 0; k < 32; ++k) Xs[l][k] = load_le32(b + 4 * k);
-    }
-    scrypt_romix_x8(Xs);
-    for (int l = 0; l < m; ++l) {
-      for (int k = 0; k < 32; ++k) store_le32(b + 4 * k, Xs[l][k]);
-      pbkdf2_sha256(header80[at + l], 80, b, 128, 1, out[at + l], 32);
+#undef QS
+  for (int i = 0; i < 16; ++i) B[i] = _mm512_add_epi32(B[i], x[i]);
+}
+
+__attribute__((target("avx512f"))) static void scrypt_romix_x16(uint32_t Xs[16][32]) {
+  alignas(64) __m512i X[32];
+  alignas(64) uint32_t w[16];
+  for (int k = 0; k < 32; ++k) {
+    for (int l = 0; l < 16; ++l) w[l] = Xs[l][k];
+    X[k] = _mm512_load_si512(w);
+  }
+  struct Pad {  // per thread, reused: 1024 entries x 32 words x 16 lanes (2 MiB)
+    __m512i* p = static_cast<__m512i*>(std::aligned_alloc(64, 1024 * 32 * sizeof(__m512i)));
+    ~Pad() { std::free(p); }
+  };
+  thread_local Pad pad;
+  __m512i* V = pad.p;
+  if (V == nullptr) throw std::bad_alloc();
+  for (int i = 0; i < 1024; ++i) {
+    for (int k = 0; k < 32; ++k) _mm512_store_si512(&V[32 * size_t(i) + k], X[k]);
+    for (int k = 0; k < 16; ++k) X[k] = _mm512_xor_si512(X[k], X[16 + k]);
+    salsa20_8_x16(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] = _mm512_xor_si512(X[16 + k], X[k]);
+    salsa20_8_x16(X + 16);
+  }
+  const int* base = reinterpret_cast<const int*>(V);
+  const __m512i lane = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  const __m512i mask = _mm512_set1_epi32(1023);
+  for (int i = 0; i < 1024; ++i) {
+    // lane l's row j_l: 32-bit element (j_l * 32 + k) * 16 + l of the pad
+    const __m512i row = _mm512_add_epi32(_mm512_slli_epi32(_mm512_and_si512(X[16], mask), 9), lane);
+    for (int k = 0; k < 32; ++k)
+      X[k] = _mm512_xor_si512(X[k], _mm512_i32gather_epi32(_mm512_add_epi32(row, _mm512_set1_epi32(16 * k)), base, 4));
+    for (int k = 0; k < 16; ++k) X[k] = _mm512_xor_si512(X[k], X[16 + k]);
+    salsa20_8_x16(X);
+    for (int k = 0; k < 16; ++k) X[16 + k] = _mm512_xor_si512(X[16 + k], X[k]);
+    salsa20_8_x16(X + 16);
+  }
+  for (int k = 0; k < 32; ++k) {
+    _mm512_store_si512(w, X[k]);
+    for (int l = 0; l < 16; ++l) Xs[l][k] = w[l];
+  }
+}
+
+constexpr int kScryptMin16 = 9;  // below this many headers one 16-lane pass costs more than an 8-lane one
+
+static bool cpu_has_avx512() {
+  static const bool ok = [] {
+    const char* off = std::getenv("OTEDAMA_NO_AVX512");  // set (not "" / "0"): the AVX2 widths only
+    return __builtin_cpu_supports("avx512f") && !(off && *off && std::strcmp(off, "0") != 0);
+  }();
+  return ok;
+}
+
+// One pass of up to L lanes (8: AVX2, 16: AVX-512); lanes past m repeat the last header.
+template <int L>
+static void scrypt_pass(int m, const uint8_t* const header80[], uint8_t* const out[]) {
+  uint32_t Xs[L][32];
+  uint8_t b[128];
+  for (int l = 0; l < L; ++l) {
+    const uint8_t* h = header80[std::min(l, m - 1)];
+    pbkdf2_sha256(h, 80, h, 80, 1, b, 128);
+    for (int k = 0; k < 32; ++k) Xs[l][k] = load_le32(b + 4 * k);
+  }
+  if constexpr (L == 16) scrypt_romix_x16(Xs);
+  else scrypt_romix_x8(Xs);
+  for (int l = 0; l < m; ++l) {
+    for (int k = 0; k < 32; ++k) store_le32(b + 4 * k, Xs[l][k]);
+    pbkdf2_sha256(header80[l], 80, b, 128, 1, out[l], 32);
+  }
+}
+
+void scrypt_1024_1_1_batch(int n, const uint8_t* const header80[], uint8_t* const out[]) {
+  const bool w16 = cpu_has_avx512(), w8 = cpu_has_avx2();
+  for (int at = 0; at < n;) {
+    const int m = n - at;
+    if (w16 && m >= kScryptMin16) {
+      const int t = std::min(16, m);
+      scrypt_pass<16>(t, header80 + at, out + at);
+      at += t;
+    } else if (w8 && m >= 3) {  // eight lanes cost ~3 scalar hashes: one or two headers go the scalar way
+      const int t = std::min(8, m);
+      scrypt_pass<8>(t, header80 + at, out + at);
+      at += t;
+    } else {
+      scrypt_1024_1_1(header80[at], out[at]);
+      ++at;
     }
   }
 }
@@ -552,17 +633,17 @@ void CpuMiner::loop(int /*tid*/) {
     if (sha) {
       hits = cpu_scan_sha256d(hdr, job->target, nonce0, kChunk);
     } else if (job->algo == Algo::kScrypt) {
-      // eight nonces per scrypt batch (AVX2 lanes)
-      uint8_t hb[8][80], ho[8][32];
-      const uint8_t* ip[8];
-      uint8_t* op[8];
-      for (int l = 0; l < 8; ++l) {
+      // sixteen nonces per scrypt batch (AVX-512 lanes; two AVX2 passes without it)
+      uint8_t hb[16][80], ho[16][32];
+      const uint8_t* ip[16];
+      uint8_t* op[16];
+      for (int l = 0; l < 16; ++l) {
         std::memcpy(hb[l], hdr, 80);
         ip[l] = hb[l];
         op[l] = ho[l];
       }
-      for (uint64_t i = 0; i < kChunk && running_.load(); i += 8) {
-        const int n = int(std::min<uint64_t>(8, kChunk - i));
+      for (uint64_t i = 0; i < kChunk && running_.load(); i += 16) {
+        const int n = int(std::min<uint64_t>(16, kChunk - i));
         for (int l = 0; l < n; ++l) store_le32(hb[l] + 76, nonce0 + uint32_t(i) + uint32_t(l));
         scrypt_1024_1_1_batch(n, ip, op);
         for (int l = 0; l < n; ++l)

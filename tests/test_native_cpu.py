@@ -36,12 +36,34 @@ def test_scrypt_reference_matches_hashlib():
         assert N.scrypt_1024_1_1(h) == hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32)
 
 
-def test_scrypt_batch_matches_hashlib_for_every_lane_count():
-    """The AVX2 8-lane scrypt (host verifier and CPU miner path) against hashlib for 1..8 headers and a 9-header
-    call (split internally into 8 + 1); hosts without AVX2 take the scalar chain under the same binding."""
-    for n in (1, 3, 8, 9):
-        hs = [os.urandom(80) for _ in range(n)]
-        assert N.scrypt_1024_1_1_batch(hs) == [hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32) for h in hs]
+_BATCH_CHECK = r"""
+import hashlib, os, sys
+sys.path.insert(0, sys.argv[1])
+from otedama_amd.ops.native import require_native
+N = require_native()
+for n in (1, 2, 3, 8, 9, 16, 17, 33):
+    hs = [os.urandom(80) for _ in range(n)]
+    assert N.scrypt_1024_1_1_batch(hs) == [hashlib.scrypt(h, salt=h, n=1024, r=1, p=1, dklen=32) for h in hs], n
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("no_avx512", ["", "1"])
+def test_scrypt_batch_matches_hashlib_for_every_lane_count(no_avx512):
+    """The batched host scrypt (GPU miner's verifier, CPU miner) against hashlib for 1..33 headers: 16-lane AVX-512
+    passes from 9 headers on, 8-lane AVX2 passes from 3, the scalar chain below; OTEDAMA_NO_AVX512 forces the AVX2
+    widths (a host without AVX2 takes the scalar chain under the same binding)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("OTEDAMA_NO_AVX512", None)
+    if no_avx512:
+        env["OTEDAMA_NO_AVX512"] = no_avx512
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _BATCH_CHECK, root], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stderr[-2000:]
 
 
 def test_cpu_scan_finds_genesis_nonce():
