@@ -308,7 +308,8 @@ PYBIND11_MODULE(_native, m) {
     }
     return hits;
   }, py::arg("header"), py::arg("target"), py::arg("start"), py::arg("count"));
-  // A/B hook: the CPU scan with a given number of nonces in flight per step (1..4).
+  m.def("cpu_scan_method", &cpu_scan_method);
+  // A/B hook: the CPU scan with a given number of nonces in flight per step (1..4 SHA-NI chains, 16 AVX-512).
   m.def("_cpu_scan_lanes", [](int lanes, const py::bytes& h, const py::bytes& t, uint32_t start, uint64_t count) {
     std::string hs = need(h, 80, "header"), ts = need(t, 32, "target");
     std::vector<uint32_t> hits;

@@ -6,6 +6,8 @@
 #include "otedama/sha256.h"
 
 #include <cpuid.h>
+#include <cstdlib>
+#include <cstring>
 #include <immintrin.h>
 
 #include <type_traits>
@@ -277,6 +279,193 @@ __attribute__((target("sha,sse4.1"))) static void sha256d_scan_h7_shani(int lane
     default: scan(std::integral_constant<int, 4>{}); break;
   }
   *done = i;
+}
+
+// The same H7 scan for 16 nonces per step on AVX-512: one nonce per 32-bit lane, the eight working variables in
+// zmm registers, Ch / Maj / the three-rotate sums as single vpternlogd, rotates as vprord. What does not depend on
+// the nonce is hoisted out of the loop: rounds 0-2 of the first hash (W0-W2 come from the header), and the message
+// words W16, W17 of the first hash; the zero and padding words of both blocks are compile-time constants, so their
+// schedule terms fold away. The second hash stops at e61 = h64 as the SHA-NI scan does.
+#define ZROR(x, n) _mm512_ror_epi32((x), (n))
+#define ZS0(x) _mm512_ternarylogic_epi32(ZROR(x, 2), ZROR(x, 13), ZROR(x, 22), 0x96)
+#define ZS1(x) _mm512_ternarylogic_epi32(ZROR(x, 6), ZROR(x, 11), ZROR(x, 25), 0x96)
+#define Zs0(x) _mm512_ternarylogic_epi32(ZROR(x, 7), ZROR(x, 18), _mm512_srli_epi32((x), 3), 0x96)
+#define Zs1(x) _mm512_ternarylogic_epi32(ZROR(x, 17), ZROR(x, 19), _mm512_srli_epi32((x), 10), 0x96)
+#define ZCH(e, f, g) _mm512_ternarylogic_epi32((e), (f), (g), 0xCA)
+#define ZMAJ(a, b, c) _mm512_ternarylogic_epi32((a), (b), (c), 0xE8)
+#define ZADD(x, y) _mm512_add_epi32((x), (y))
+#define ZC(x) _mm512_set1_epi32(int(x))
+// one round on each of G independent groups (G chains in flight hide the round's dependency latency); kw(g) is
+// K[t] + W[t] of group g
+#define ZROUND(a, b, c, d, e, f, g, h, kw)                                         \
+  for (int q = 0; q < G; ++q) {                                                    \
+    const __m512i t1 = ZADD(ZADD(h[q], ZS1(e[q])), ZADD(ZCH(e[q], f[q], g[q]), (kw))); \
+    d[q] = ZADD(d[q], t1);                                                         \
+    h[q] = ZADD(t1, ZADD(ZS0(a[q]), ZMAJ(a[q], b[q], c[q])));                      \
+  }
+
+struct ScanPre {  // per header: the scalar prologue shared by every step
+  uint32_t w0, w1, w2, w16, w17;
+  uint32_t st[8];  // block-2 state after rounds 0-2
+};
+
+// G x 16 consecutive nonces from n0: pushes those whose bswap(H7) <= thi
+template <int G>
+__attribute__((target("avx512f,avx512bw"))) static inline void sha256d_h7_x16(const ScanPre& p, const uint32_t mid[8],
+                                                                          uint32_t n0, uint32_t thi,
+                                                                          std::vector<uint32_t>* cands) {
+  const __m512i bswap = _mm512_set4_epi32(0x0c0d0e0f, 0x08090a0b, 0x04050607, 0x00010203);
+  const __m512i lane = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  // ---- first hash, block 2: W3 = the nonce's header bytes read big-endian
+  __m512i W[G][64];
+  __m512i a[G], b[G], c[G], d[G], e[G], f[G], g[G], h[G];
+  for (int q = 0; q < G; ++q) {
+    W[q][3] = _mm512_shuffle_epi8(ZADD(ZC(n0 + 16u * uint32_t(q)), lane), bswap);
+    W[q][0] = ZC(p.w0); W[q][1] = ZC(p.w1); W[q][2] = ZC(p.w2); W[q][4] = ZC(0x80000000u);
+    for (int t = 5; t < 15; ++t) W[q][t] = ZC(0);
+    W[q][15] = ZC(640);
+    W[q][16] = ZC(p.w16);
+    W[q][17] = ZC(p.w17);
+    a[q] = ZC(p.st[0]); b[q] = ZC(p.st[1]); c[q] = ZC(p.st[2]); d[q] = ZC(p.st[3]);
+    e[q] = ZC(p.st[4]); f[q] = ZC(p.st[5]); g[q] = ZC(p.st[6]); h[q] = ZC(p.st[7]);
+  }
+#pragma GCC unroll 64
+  for (int t = 18; t < 64; ++t)
+    for (int q = 0; q < G; ++q)
+      W[q][t] = ZADD(ZADD(Zs1(W[q][t - 2]), W[q][t - 7]), ZADD(Zs0(W[q][t - 15]), W[q][t - 16]));
+#pragma GCC unroll 64
+  for (int t = 3; t < 64; t += 8) {
+    ZROUND(a, b, c, d, e, f, g, h, ZADD(ZC(kSha256K[t]), W[q][t]));
+    if (t + 1 < 64) ZROUND(h, a, b, c, d, e, f, g, ZADD(ZC(kSha256K[t + 1]), W[q][t + 1]));
+    if (t + 2 < 64) ZROUND(g, h, a, b, c, d, e, f, ZADD(ZC(kSha256K[t + 2]), W[q][t + 2]));
+    if (t + 3 < 64) ZROUND(f, g, h, a, b, c, d, e, ZADD(ZC(kSha256K[t + 3]), W[q][t + 3]));
+    if (t + 4 < 64) ZROUND(e, f, g, h, a, b, c, d, ZADD(ZC(kSha256K[t + 4]), W[q][t + 4]));
+    if (t + 5 < 64) ZROUND(d, e, f, g, h, a, b, c, ZADD(ZC(kSha256K[t + 5]), W[q][t + 5]));
+    if (t + 6 < 64) ZROUND(c, d, e, f, g, h, a, b, ZADD(ZC(kSha256K[t + 6]), W[q][t + 6]));
+    if (t + 7 < 64) ZROUND(b, c, d, e, f, g, h, a, ZADD(ZC(kSha256K[t + 7]), W[q][t + 7]));
+  }
+  // 61 rounds from round 3 leave the variables rotated by 61 mod 8 = 5 places: round t's "a" is in the slot
+  // named by (3 - t) mod 8. After round 63 the new a is in slot (3 - 64) mod 8 = 3 -> d, then e..h, a, b, c
+  // ---- second hash: the first hash's digest, padding, 256 bits
+  __m512i X[G][64];
+  __m512i A[G], B[G], Cc[G], D[G], E[G], F[G], Gg[G], H[G];
+  for (int q = 0; q < G; ++q) {
+    const __m512i o[8] = {d[q], e[q], f[q], g[q], h[q], a[q], b[q], c[q]};
+    for (int k = 0; k < 8; ++k) X[q][k] = ZADD(o[k], ZC(mid[k]));
+    X[q][8] = ZC(0x80000000u);
+    for (int t = 9; t < 15; ++t) X[q][t] = ZC(0);
+    X[q][15] = ZC(256);
+    A[q] = ZC(kSha256IV[0]); B[q] = ZC(kSha256IV[1]); Cc[q] = ZC(kSha256IV[2]); D[q] = ZC(kSha256IV[3]);
+    E[q] = ZC(kSha256IV[4]); F[q] = ZC(kSha256IV[5]); Gg[q] = ZC(kSha256IV[6]); H[q] = ZC(kSha256IV[7]);
+  }
+#pragma GCC unroll 64
+  for (int t = 16; t < 61; ++t)
+    for (int q = 0; q < G; ++q)
+      X[q][t] = ZADD(ZADD(Zs1(X[q][t - 2]), X[q][t - 7]), ZADD(Zs0(X[q][t - 15]), X[q][t - 16]));
+#pragma GCC unroll 64
+  for (int t = 0; t < 56; t += 8) {
+    ZROUND(A, B, Cc, D, E, F, Gg, H, ZADD(ZC(kSha256K[t]), X[q][t]));
+    ZROUND(H, A, B, Cc, D, E, F, Gg, ZADD(ZC(kSha256K[t + 1]), X[q][t + 1]));
+    ZROUND(Gg, H, A, B, Cc, D, E, F, ZADD(ZC(kSha256K[t + 2]), X[q][t + 2]));
+    ZROUND(F, Gg, H, A, B, Cc, D, E, ZADD(ZC(kSha256K[t + 3]), X[q][t + 3]));
+    ZROUND(E, F, Gg, H, A, B, Cc, D, ZADD(ZC(kSha256K[t + 4]), X[q][t + 4]));
+    ZROUND(D, E, F, Gg, H, A, B, Cc, ZADD(ZC(kSha256K[t + 5]), X[q][t + 5]));
+    ZROUND(Cc, D, E, F, Gg, H, A, B, ZADD(ZC(kSha256K[t + 6]), X[q][t + 6]));
+    ZROUND(B, Cc, D, E, F, Gg, H, A, ZADD(ZC(kSha256K[t + 7]), X[q][t + 7]));
+  }
+  // rounds 56-59 in full, round 60 only as far as e61 = d60 + T1
+  ZROUND(A, B, Cc, D, E, F, Gg, H, ZADD(ZC(kSha256K[56]), X[q][56]));
+  ZROUND(H, A, B, Cc, D, E, F, Gg, ZADD(ZC(kSha256K[57]), X[q][57]));
+  ZROUND(Gg, H, A, B, Cc, D, E, F, ZADD(ZC(kSha256K[58]), X[q][58]));
+  ZROUND(F, Gg, H, A, B, Cc, D, E, ZADD(ZC(kSha256K[59]), X[q][59]));
+  const __m512i vthi = ZC(thi);
+  for (int q = 0; q < G; ++q) {
+    // round 60: a = E, b..d = F, G, H, e = A, f..h = B, Cc, D
+    const __m512i t1 = ZADD(ZADD(D[q], ZS1(A[q])), ZADD(ZCH(A[q], B[q], Cc[q]), ZADD(ZC(kSha256K[60]), X[q][60])));
+    const __m512i h7 = ZADD(ZADD(H[q], t1), ZC(0x5be0cd19u));
+    const __mmask16 hit = _mm512_cmple_epu32_mask(_mm512_shuffle_epi8(h7, bswap), vthi);
+    if (hit) {
+      for (int l = 0; l < 16; ++l)
+        if (hit >> l & 1) cands->push_back(n0 + 16u * uint32_t(q) + uint32_t(l));
+    }
+  }
+}
+
+__attribute__((target("avx512f,avx512bw"))) static void sha256d_scan_h7_avx512(int groups, const uint32_t mid[8],
+                                                                             const uint8_t tail12[12], uint32_t start,
+                                                                             uint64_t count, uint32_t thi,
+                                                                             std::vector<uint32_t>* cands,
+                                                                             uint64_t* done) {
+  // scalar prologue: rounds 0-2 of block 2 and the nonce-free schedule words
+  ScanPre p;
+  p.w0 = load_be32(tail12); p.w1 = load_be32(tail12 + 4); p.w2 = load_be32(tail12 + 8);
+  std::memcpy(p.st, mid, 32);
+  auto rotr = [](uint32_t x, int n) { return (x >> n) | (x << (32 - n)); };
+  auto round_s = [&](uint32_t* v, uint32_t kw) {
+    const uint32_t t1 = v[7] + (rotr(v[4], 6) ^ rotr(v[4], 11) ^ rotr(v[4], 25)) + ((v[4] & v[5]) ^ (~v[4] & v[6])) + kw;
+    const uint32_t t2 = (rotr(v[0], 2) ^ rotr(v[0], 13) ^ rotr(v[0], 22)) + ((v[0] & v[1]) ^ (v[0] & v[2]) ^ (v[1] & v[2]));
+    for (int i = 7; i > 0; --i) v[i] = v[i - 1];
+    v[4] += t1;
+    v[0] = t1 + t2;
+  };
+  round_s(p.st, kSha256K[0] + p.w0);
+  round_s(p.st, kSha256K[1] + p.w1);
+  round_s(p.st, kSha256K[2] + p.w2);
+  auto ss0 = [&](uint32_t x) { return rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3); };
+  auto ss1 = [&](uint32_t x) { return rotr(x, 17) ^ rotr(x, 19) ^ (x >> 10); };
+  p.w16 = ss1(0) + 0 + ss0(p.w1) + p.w0;    // W14 = 0, W9 = 0
+  p.w17 = ss1(640) + 0 + ss0(p.w2) + p.w1;  // W15 = 640, W10 = 0
+  uint64_t i = 0;
+  if (groups == 4)
+    for (; i + 64 <= count; i += 64) sha256d_h7_x16<4>(p, mid, start + uint32_t(i), thi, cands);
+  if (groups == 3)
+    for (; i + 48 <= count; i += 48) sha256d_h7_x16<3>(p, mid, start + uint32_t(i), thi, cands);
+  if (groups >= 2)
+    for (; i + 32 <= count; i += 32) sha256d_h7_x16<2>(p, mid, start + uint32_t(i), thi, cands);
+  for (; i + 16 <= count; i += 16) sha256d_h7_x16<1>(p, mid, start + uint32_t(i), thi, cands);
+  *done = i;
+}
+#undef ZROUND
+#undef ZADD
+#undef ZC
+#undef ZMAJ
+#undef ZCH
+#undef Zs1
+#undef Zs0
+#undef ZS1
+#undef ZS0
+#undef ZROR
+
+bool cpu_has_avx512_sha_scan() {
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+  return ok;
+}
+
+int sha256d_scan_wide_groups() {
+  static const int groups = [] {
+    const char* v = std::getenv("OTEDAMA_CPU_SCAN_GROUPS");  // A/B: 16-lane groups in flight per step (1..4)
+    const int n = v ? std::atoi(v) : 0;
+    if (n >= 1 && n <= 4) return n;
+    // Measured single thread (tools/cpu_scan_ab.py, profiles/r4/r_cpu_avx512): AMD EPYC 9575F (Zen 5) 41.4 / 51.3 /
+    // 46.8 / 38.7 MH/s for 1-4 groups; the build container's Intel Xeon 28.1 / 24.4 / 21.9 / 19.2 (its 32 zmm
+    // registers spill from two groups on, where Zen 5's renamer and store forwarding absorb the spills).
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    char vendor[13] = {0};
+    if (__get_cpuid(0, &a, &b, &c, &d)) {
+      std::memcpy(vendor, &b, 4);
+      std::memcpy(vendor + 4, &d, 4);
+      std::memcpy(vendor + 8, &c, 4);
+    }
+    return std::strcmp(vendor, "AuthenticAMD") == 0 ? 2 : 1;
+  }();
+  return groups;
+}
+
+bool sha256d_scan_h7_wide(const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,
+                          uint32_t thi, std::vector<uint32_t>* cands, uint64_t* done) {
+  if (!cpu_has_avx512_sha_scan()) return false;
+  sha256d_scan_h7_avx512(sha256d_scan_wide_groups(), mid, tail12, start, count, thi, cands, done);
+  return true;
 }
 
 bool sha256d_scan_h7(int lanes, const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,

@@ -216,6 +216,7 @@ class CpuMiner : public MinerBase {
 // Returns the nonces (header byte order) whose SHA-256d meets the target.
 std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,
                                        uint64_t count);
+std::string cpu_scan_method();  // the CPU SHA-256d scan this host runs, e.g. "avx512 16 lanes x 2 groups"
 std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[80], const uint8_t target[32],
                                              uint32_t start, uint64_t count);
 

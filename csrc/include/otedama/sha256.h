@@ -45,6 +45,11 @@ void sha256_compress_xn(int n, uint32_t* const state[], const uint8_t* const blo
 bool sha256d_scan_h7(int lanes, const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,
                      uint32_t thi, std::vector<uint32_t>* cands, uint64_t* done);
 bool cpu_has_sha_ni();
+// The same scan, 16 nonces per step on AVX-512 (F + BW); *done is a multiple of 16. False without AVX-512.
+bool sha256d_scan_h7_wide(const uint32_t mid[8], const uint8_t tail12[12], uint32_t start, uint64_t count,
+                          uint32_t thi, std::vector<uint32_t>* cands, uint64_t* done);
+bool cpu_has_avx512_sha_scan();
+int sha256d_scan_wide_groups();  // 16-lane groups in flight per step (OTEDAMA_CPU_SCAN_GROUPS, else by CPU vendor)
 
 // Full SHA-256 of an arbitrary message.
 void sha256(const uint8_t* data, size_t len, uint8_t out[32]);

@@ -444,10 +444,15 @@ MinerStats MinerBase::stats() {
 
 // ---------------------------------------------------------- CPU SHA-256d scan
 
-// Nonces in flight per step of the fused SHA-NI scan, single thread (tools/cpu_lanes_ab.py, profiles/r4/m_cpu_lanes):
-// AMD EPYC 9575F 21.2 / 31.3 / 35.0 / 36.4 MH/s for 1-4 lanes; the build container's Intel Xeon 9.8 / 11.6 / 10.3 /
-// 10.1. So 4 on AMD cores, 2 elsewhere.
+constexpr int kScanWide = 16;  // "lanes" value selecting the 16-lane AVX-512 scan
+
+// The AVX-512 scan where the CPU has it: single thread 51-55 MH/s on the MI355X host's EPYC 9575F against 36.5 for
+// SHA-NI, 28 against 11-13 on the build container's Xeon (tools/cpu_scan_ab.py, profiles/r4/r_cpu_avx512).
+// Without AVX-512, nonces in flight per step of the fused SHA-NI scan, single thread (tools/cpu_lanes_ab.py,
+// profiles/r4/m_cpu_lanes): AMD EPYC 9575F 21.2 / 31.3 / 35.0 / 36.4 MH/s for 1-4 lanes; the build container's Intel
+// Xeon 9.8 / 11.6 / 10.3 / 10.1. So 4 on AMD cores, 2 elsewhere.
 static int cpu_scan_lanes_for_this_cpu() {
+  if (cpu_has_avx512_sha_scan()) return kScanWide;
   unsigned a = 0, b = 0, c = 0, d = 0;
   if (!__get_cpuid(0, &a, &b, &c, &d)) return 2;
   char vendor[13];
@@ -513,12 +518,12 @@ static void cpu_scan_lanes(const uint32_t mid[8], const uint8_t blk2_tmpl[64], c
   *done = i;
 }
 
-// Lanes per step of the CPU scan (OTEDAMA_CPU_LANES overrides; 1..4).
+// Lanes per step of the CPU scan (OTEDAMA_CPU_LANES overrides: 1..4 SHA-NI chains, 16 the AVX-512 scan).
 static int cpu_scan_lanes_default() {
   static const int lanes = [] {
     const char* v = std::getenv("OTEDAMA_CPU_LANES");
     const int n = v ? std::atoi(v) : 0;
-    return n >= 1 && n <= 4 ? n : cpu_scan_lanes_for_this_cpu();
+    return (n >= 1 && n <= 4) || n == kScanWide ? n : cpu_scan_lanes_for_this_cpu();
   }();
   return lanes;
 }
@@ -541,7 +546,8 @@ std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[8
   uint8_t h[32];
   const uint32_t thi = load_le32(target + 28);
   std::vector<uint32_t> cands;
-  if (sha256d_scan_h7(lanes, mid, header80 + 64, start, count, thi, &cands, &i)) {
+  if ((lanes == kScanWide && sha256d_scan_h7_wide(mid, header80 + 64, start, count, thi, &cands, &i)) ||
+      sha256d_scan_h7(lanes == kScanWide ? 4 : lanes, mid, header80 + 64, start, count, thi, &cands, &i)) {
     // SHA-NI: the fused H7 scan; its candidates get the full hash and 256-bit compare here
     for (uint32_t n : cands) {
       store_le32(blk2 + 12, n);
@@ -563,6 +569,14 @@ std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[8
     if (load_le32(h + 28) <= thi && le256_leq(h, target)) hits.push_back(nonce);
   }
   return hits;
+}
+
+std::string cpu_scan_method() {
+  const int lanes = cpu_scan_lanes_default();
+  if (lanes == kScanWide && cpu_has_avx512_sha_scan())
+    return "avx512 16 lanes x " + std::to_string(sha256d_scan_wide_groups()) + " groups";
+  if (cpu_has_sha_ni()) return "sha-ni x" + std::to_string(lanes == kScanWide ? 4 : lanes);
+  return "portable x" + std::to_string(lanes == kScanWide ? 2 : lanes);
 }
 
 std::vector<uint32_t> cpu_scan_sha256d(const uint8_t header80[80], const uint8_t target[32], uint32_t start,

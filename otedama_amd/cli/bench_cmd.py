@@ -29,8 +29,9 @@ def cpu_share() -> int:
 
 
 def bench_cpu(seconds: float = 2.0, threads: int = 0, single_seconds: float = 0.0) -> dict:
-    """BASELINE config 1 on this host: the SHA-NI scanner on one thread over a synthetic 80-byte header, then the
-    production CpuMiner on ``threads`` threads (BENCHMARKS.md:25-28 single thread, :44-49 whole CPU)."""
+    """BASELINE config 1 on this host: the CPU SHA-256d scan (16-lane AVX-512 where the CPU has it, else SHA-NI) on
+    one thread over a synthetic 80-byte header, then the production CpuMiner on ``threads`` threads
+    (BENCHMARKS.md:25-28 single thread, :44-49 whole CPU)."""
     from otedama_amd.models.header import GENESIS_HEADER_HEX
     from otedama_amd.ops.native import require_native
 
@@ -58,6 +59,7 @@ def bench_cpu(seconds: float = 2.0, threads: int = 0, single_seconds: float = 0.
     allc = (h1 - h0) / (t1 - t0)
     return {"sha256d_single_thread_hps": single, "sha256d_all_threads_hps": allc, "threads": threads,
             "scaling": allc / (single * threads), "sha_ni": bool(N.cpu_has_sha_ni()),
+            "scan": N.cpu_scan_method(),
             "single_thread_seconds": round(single_s, 3), "single_thread_nonces": done,
             "all_threads_seconds": seconds, "header": "synthetic 80-byte header (Bitcoin genesis)",
             "reference": "~2.5 MH/s / ~75 MH/s on a Ryzen 9 7950X (BENCHMARKS.md:25,46)"}

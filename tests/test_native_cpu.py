@@ -323,10 +323,11 @@ def test_clock_bounds_track_the_window_minimum():
     assert N._clock_bounds(2.0, [(0.0, 5.0)]) == [5.0]
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4, 16])
 def test_cpu_scan_lanes_agree(lanes):
     """Every interleave width of the CPU scan finds the same hits (genesis nonce at its target; an easy target over
-    a window that is not a multiple of the width, so the one-at-a-time tail runs too)."""
+    a window that is not a multiple of the width, so the one-at-a-time tail runs too). 16 is the AVX-512 scan (the
+    SHA-NI scan with 4 chains on a host without AVX-512)."""
     from otedama_amd.models.header import GENESIS_HEADER_HEX, int_to_hash
     from otedama_amd.ops.native import require_native
 
@@ -336,3 +337,49 @@ def test_cpu_scan_lanes_agree(lanes):
     assert nonce in N._cpu_scan_lanes(lanes, hdr, int_to_hash(0xFFFF << 208), nonce - 1001, 4003)
     easy = int_to_hash((1 << 248) - 1)
     assert N._cpu_scan_lanes(lanes, hdr, easy, 7, 3001) == N._cpu_scan_lanes(1, hdr, easy, 7, 3001)
+
+
+def test_avx512_scan_matches_python_over_random_headers():
+    """The 16-lane AVX-512 SHA-256d scan against hashlib over random headers and a nonce window that wraps 2^32:
+    every nonce whose double hash meets a 1-in-256 target, and no other."""
+    from otedama_amd.models.header import int_to_hash
+
+    tgt = (1 << 248) - 1
+    for start in (0xFFFFF000, 0x12345670):
+        h = os.urandom(80)
+        want = [(start + i) & 0xFFFFFFFF for i in range(5000)
+                if int.from_bytes(sha256d(h[:76] + ((start + i) & 0xFFFFFFFF).to_bytes(4, "little")), "little") <= tgt]
+        assert N._cpu_scan_lanes(16, h, int_to_hash(tgt), start, 5000) == want
+
+
+_GROUPS_CHECK = r"""
+import os, sys
+sys.path.insert(0, sys.argv[1])
+from otedama_amd.models.header import int_to_hash, sha256d
+from otedama_amd.ops.native import require_native
+N = require_native()
+tgt = (1 << 248) - 1
+h = os.urandom(80)
+start = 0xFFFFFF00
+want = [(start + i) & 0xFFFFFFFF for i in range(3001)
+        if int.from_bytes(sha256d(h[:76] + ((start + i) & 0xFFFFFFFF).to_bytes(4, "little")), "little") <= tgt]
+assert N._cpu_scan_lanes(16, h, int_to_hash(tgt), start, 3001) == want
+print(N.cpu_scan_method())
+"""
+
+
+@pytest.mark.parametrize("groups", ["1", "2", "3", "4"])
+def test_avx512_scan_groups_agree(groups):
+    """1-4 sixteen-lane groups in flight (OTEDAMA_CPU_SCAN_GROUPS; default 2 on AMD, 1 elsewhere): the same hits
+    as hashlib over a window that wraps 2^32 and is not a multiple of 64 (the smaller widths and the scalar tail
+    finish it)."""
+    import subprocess
+    import sys
+
+    if not N.cpu_scan_method().startswith("avx512"):
+        pytest.skip("no AVX-512 on this host")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _GROUPS_CHECK, root], capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, OTEDAMA_CPU_SCAN_GROUPS=groups))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip() == f"avx512 16 lanes x {groups} groups"
