@@ -256,22 +256,26 @@ class StoreServer:
             self._drop(c, conns)
 
     def _flush(self, c: _Conn, conns: dict) -> None:
-        try:
-            n = c.sock.send(c.tx)
-            del c.tx[:n]
-        except (BlockingIOError, InterruptedError):
-            pass
-        except OSError:
-            self._drop(c, conns)
-            return
-        if c.tx:  # a slow reader: block briefly rather than grow an event mask (replies are tiny)
+        # under the data lock: an in-process set() on the supervisor's thread appends WAIT replies to c.tx
+        with self._lock:
+            ok = True
             try:
-                c.sock.settimeout(5.0)
-                c.sock.sendall(c.tx)
-                c.tx.clear()
-                c.sock.setblocking(False)
+                n = c.sock.send(c.tx)
+                del c.tx[:n]
+            except (BlockingIOError, InterruptedError):
+                pass
             except OSError:
-                self._drop(c, conns)
+                ok = False
+            if ok and c.tx:  # a slow reader: block briefly rather than grow an event mask (replies are tiny)
+                try:
+                    c.sock.settimeout(5.0)
+                    c.sock.sendall(c.tx)
+                    c.tx.clear()
+                    c.sock.setblocking(False)
+                except OSError:
+                    ok = False
+        if not ok:
+            self._drop(c, conns)
 
     def _handle(self, c: _Conn, r: _Reader) -> bool:
         """Parse and serve one request (raises _Incomplete before changing any state). False = drop the peer."""

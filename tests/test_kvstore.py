@@ -146,3 +146,31 @@ def test_the_node_supervisor_does_not_import_torch():
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == "False"
     assert torch  # the test process itself uses torch's clients
+
+
+def test_in_process_sets_race_client_waits_without_desync():
+    """The supervisor's thread sets keys (waking WAITs, which queues replies) while the server thread answers the
+    same connections: 4 clients x 300 wait/get rounds on keys another thread publishes stay in step."""
+    with StoreServer() as srv:
+        errors = []
+
+        def publisher():
+            for i in range(300):
+                srv.set(f"k{i}", str(i))
+
+        def consumer(cid):
+            c = _client(srv.port, timeout=20)
+            try:
+                for i in range(300):
+                    assert c.get(f"k{i}") == str(i).encode()
+                    c.set(f"ack{cid}/{i}", "1")
+            except Exception as exc:  # noqa: BLE001
+                errors.append(repr(exc))
+
+        ths = [threading.Thread(target=consumer, args=(j,)) for j in range(4)] + [threading.Thread(target=publisher)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(60)
+        assert not errors, errors[:3]
+        assert srv.num_keys() == 300 + 4 * 300
