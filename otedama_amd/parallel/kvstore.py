@@ -96,6 +96,7 @@ class StoreServer:
         self._wake_r.setblocking(False)
         self._sel.register(self._wake_r, selectors.EVENT_READ, "wake")
         self._dirty: set[_Conn] = set()  # connections with replies to send
+        self.refused = 0  # peers dropped for a bad magic, a query before VALIDATE or a query type not served here
         self._stop = False
         self._thread = threading.Thread(target=self._run, name="otd-store", daemon=True)
         self._thread.start()
@@ -253,6 +254,7 @@ class StoreServer:
                     self._dirty.discard(c)
                     break
         if not ok:
+            self.refused += 1
             self._drop(c, conns)
 
     def _flush(self, c: _Conn, conns: dict) -> None:

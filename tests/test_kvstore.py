@@ -108,6 +108,7 @@ def test_a_bad_magic_or_unknown_query_drops_only_that_peer():
         assert s2.recv(16) == b""
         good.set("still", "here")
         assert good.get("still") == b"here"
+        assert srv.refused == 2
 
 
 _GLOO = r"""
@@ -131,7 +132,9 @@ def test_gloo_process_groups_rendezvous_through_it(world):
         procs = [subprocess.Popen([sys.executable, "-c", _GLOO, str(r), str(world), str(srv.port)], env=env,
                                   stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
         outs = [p.communicate(timeout=120) for p in procs]
+        refused = srv.refused
     assert [p.returncode for p in procs] == [0] * world, [o[1][-2000:] for o in outs]
+    assert refused == 0  # gloo's rendezvous used only query types the server implements
     assert all(o[0].strip().endswith("ok") for o in outs)  # gloo prints its own connection lines first
 
 

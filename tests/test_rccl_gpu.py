@@ -57,3 +57,33 @@ def test_rccl_collectives_on_the_comm_stream():
         dist.barrier(device_ids=[0])  # the form barrier() uses for the nccl backend
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_group_rendezvous_through_the_supervisors_store():
+    """`otedama node` ranks form their RCCL groups through the supervisor's torch-free store (parallel/kvstore.py),
+    one PrefixStore per group generation as parallel/comm.py does. At world 1 on the real MI355X: RCCL's bootstrap
+    uses only query types the server implements (none refused), and the group runs a collective."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from otedama_amd.parallel.kvstore import StoreServer
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    with StoreServer() as srv:
+        client = dist.TCPStore("127.0.0.1", srv.port, None, False, datetime.timedelta(seconds=60),
+                               wait_for_workers=False)
+        for gen in range(2):
+            dist.init_process_group("nccl", store=dist.PrefixStore(f"otd-g{gen}", client), rank=0, world_size=1,
+                                    device_id=dev)
+            try:
+                t = torch.full((4,), 3, dtype=torch.int64, device=dev)
+                dist.all_reduce(t)
+                torch.cuda.synchronize()
+                assert t.tolist() == [3, 3, 3, 3]
+            finally:
+                dist.destroy_process_group()
+        assert srv.refused == 0
+        assert srv.num_keys() > 0
