@@ -68,8 +68,18 @@ LIVENESS_EVERY = 0.25      # leader liveness check period
 STATS_INTERVAL = 10.0      # R3 cadence (the reference's stats tick, internal/engine/run.go:377-380)
 BELL_FALLBACK = 0.05       # doorbell wait ceiling: a lost datagram delays an op or a gather by at most this
 PENDING_CAP = 8192         # shares a follower holds for the leader (drop-oldest past it, counted)
+OP_RETAIN = 4096           # op log entries kept in the store (~1 h at the quiet node's ~1 op/s); older ones deleted
 EPOCH_SHIFT = 40           # leader incarnation i numbers its job epochs from (i - 1) << EPOCH_SHIFT
 PREFIX = "otd/"
+
+
+def op_retain() -> int:
+    """Op log entries the leader keeps (OTEDAMA_NODE_OP_RETAIN, tests shrink it). The store lives in the supervisor
+    for the node's lifetime, so an untrimmed log would grow by one entry per job, gather and stats op, for weeks."""
+    try:
+        return max(16, int(os.environ.get("OTEDAMA_NODE_OP_RETAIN", OP_RETAIN)))
+    except ValueError:
+        return OP_RETAIN
 
 
 def _k(*parts) -> str:
@@ -307,6 +317,7 @@ class NodeMinerSet:
         self._remote_efd = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
         self._thread: threading.Thread | None = None
         self._op_k = 0
+        self._retain = op_retain()
         self._gen = comm.info.generation
         self._gen_started = time.monotonic()
         self.capacity = max(comm.info.capacity, comm.info.world_size, 1)  # orig ranks 0..capacity-1 may exist
@@ -549,6 +560,11 @@ class NodeMinerSet:
                 if r != self.comm.info.orig_rank:
                     self._bell.ring(r, msg)
         self.store.set(_k("next"), str(self._op_k))
+        if k >= self._retain:  # trim: a follower this far behind re-joins from otd/next instead (its op loop)
+            try:
+                self.store.delete_key(_k("op", k - self._retain))
+            except Exception:  # noqa: BLE001 - trimming is best effort; the next post retries the next entry
+                pass
 
     def _heartbeats(self, store=None) -> dict[int, dict]:
         store = store or self.store
@@ -843,6 +859,7 @@ class NodeWorker:
             self.store.set(_k("join", info.orig_rank), "1")
         broken = False  # the current group failed a collective: skip collectives until the next re-form
         inline: dict[int, dict] = {}  # ops that arrived on the doorbell ahead of this loop reaching them
+        retain, lag_checked = op_retain(), time.monotonic()
         try:
             while True:
                 # the leader rings this rank's doorbell with each op as it posts it; the store log is the truth for
@@ -851,10 +868,21 @@ class NodeWorker:
                 if op is None:
                     key = _k("op", k)
                     if not self.store.check([key]):
-                        for msg in self._bell.wait(BELL_FALLBACK):
+                        msgs = self._bell.wait(BELL_FALLBACK)
+                        for msg in msgs:
                             got = parse_op_msg(msg)
                             if got is not None and got[0] >= k and len(inline) < 4096:
                                 inline[got[0]] = got[1]
+                        now = time.monotonic()
+                        if not msgs and now - lag_checked >= 1.0:
+                            lag_checked = now
+                            nxt = int(_store_get(self.store, _k("next")) or 0)
+                            if nxt - k > retain:  # op k was trimmed from the log: re-join from the current end
+                                self.log("warn", f"node: {self.rank_id} fell {nxt - k} ops behind the log; re-joining")
+                                k, broken = nxt, True
+                                inline.clear()
+                                self.comm.abort()
+                                self.store.set(_k("join", info.orig_rank), "1")
                         continue
                     op = json.loads(self.store.get(key))
                 k += 1

@@ -50,6 +50,40 @@ def main(out_dir: str, mode: str) -> int:
             res["collectives_per_s"] = (comm.collectives - c0) / (time.monotonic() - t0)
             res["tick_p50_s"], res["tick_p99_s"] = node.link.tick_quantile(0.5), node.link.tick_quantile(0.99)
             return 0
+        if mode == "trim":  # job churn past the op log's retention, a follower stopped meanwhile, then resumed
+            from otedama_amd.parallel.node import _k
+
+            def churn(seconds):
+                nonlocal shares
+                end = time.monotonic() + seconds
+                i = 0
+                while time.monotonic() < end:
+                    j = job(236)
+                    j["job_id"] = f"churn-{time.monotonic_ns()}-{i}"
+                    node.set_job(j)
+                    i += 1
+                    shares += node.poll(256)
+                    time.sleep(0.02)
+
+            churn(2.0)
+            with open(os.path.join(out_dir, "phase1.json.tmp"), "w") as f:
+                json.dump({"op_k": node._op_k}, f)
+            os.replace(os.path.join(out_dir, "phase1.json.tmp"), os.path.join(out_dir, "phase1.json"))
+            resumed = os.path.join(out_dir, "killed.json")
+            while not os.path.exists(resumed):
+                churn(0.2)
+            ep_resume = node.epoch
+            end = time.monotonic() + 40
+            got = False
+            while time.monotonic() < end and not got:
+                new = node.poll(256)
+                shares += new
+                got = any(s["device_id"] == "rank1" and s["epoch"] >= ep_resume for s in new)
+                time.sleep(0.02)
+            store = comm.info.store
+            res.update(ops_posted=node._op_k, victim_shares_after_resume=got, reforms=node.link.reforms,
+                       ops_kept=sum(1 for j in range(node._op_k) if store.check([_k("op", j)])))
+            return 0
         ep0 = node.set_job(job(236))
         end = time.monotonic() + 60
         while time.monotonic() < end:

@@ -169,3 +169,32 @@ def test_node_mines_with_every_doorbell_datagram_lost(monkeypatch):
     assert "error" not in r, r
     assert r["accepted_remote_in_window"] > 0 and r["rejected"] == 0 and r["pool_rejected"] == 0, r
     assert r["exit_code"] == 0, r
+
+
+def test_op_log_is_trimmed_and_a_follower_behind_it_rejoins(tmp_path, monkeypatch):
+    """The leader keeps the last OTEDAMA_NODE_OP_RETAIN ops of its log in the supervisor's store (the store lives for
+    the node's lifetime: an untrimmed log grows by an entry per job, gather and stats op). A follower stopped
+    (SIGSTOP) while the leader churns jobs far past that window finds its next op trimmed when it resumes, re-joins
+    from the log's end, and mines again."""
+    monkeypatch.setenv("OTEDAMA_NODE_OP_RETAIN", "16")
+    world = 2
+    port = free_port()
+    store = StoreServer("127.0.0.1", port)
+    procs = _spawn(world, tmp_path, "trim", port)
+    try:
+        assert _wait_file(tmp_path / "phase1.json", 120, procs), open(tmp_path / "err0.txt").read()[-3000:]
+        procs[1].send_signal(signal.SIGSTOP)
+        time.sleep(3.0)
+        procs[1].send_signal(signal.SIGCONT)
+        _write_json(tmp_path / "killed.json", {"rank": 1, "t": time.time()})
+        codes = _finish({0: procs[0]})
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.kill()
+        store.close()
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert codes[0] == 0, (codes, res.get("logs"))
+    assert res["ops_posted"] > 64, res
+    assert res["ops_kept"] <= 16, res
+    assert res["victim_shares_after_resume"], res["logs"][-20:]
