@@ -629,7 +629,9 @@ def check_native() -> Check:
         if n is None:
             return Result(status=Status.FAIL, detail="otedama_amd._native not built",
                           fix="python -m otedama_amd._build (needs ROCm hipcc for gfx950)")
-        return Result(detail=f"native extension loaded (SHA-NI={'yes' if n.cpu_has_sha_ni() else 'no'})")
+        scan = n.cpu_scan_method() if hasattr(n, "cpu_scan_method") else "?"
+        return Result(detail=f"native extension loaded (SHA-NI={'yes' if n.cpu_has_sha_ni() else 'no'}, "
+                             f"CPU scan: {scan})")
     return Check("Native extension", run)
 
 
