@@ -167,6 +167,7 @@ def test_in_process_sets_race_client_waits_without_desync():
                 for i in range(300):
                     assert c.get(f"k{i}") == str(i).encode()
                     c.set(f"ack{cid}/{i}", "1")
+                assert c.check([f"ack{cid}/299"])  # SET has no reply: a round trip orders it before the count below
             except Exception as exc:  # noqa: BLE001
                 errors.append(repr(exc))
 
@@ -177,3 +178,30 @@ def test_in_process_sets_race_client_waits_without_desync():
             th.join(60)
         assert not errors, errors[:3]
         assert srv.num_keys() == 300 + 4 * 300
+
+
+def test_garbage_from_one_peer_never_disturbs_another():
+    """Property: whatever bytes a validated peer sends (truncated requests, huge lengths, unknown query types), the
+    server thread survives, and a well-formed client on another connection keeps getting correct answers."""
+    import socket
+    import struct
+
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    with StoreServer() as srv:
+        good = _client(srv.port)
+
+        @settings(max_examples=60, deadline=None, suppress_health_check=list(HealthCheck))
+        @given(st.binary(min_size=0, max_size=96))
+        def one(blob):
+            s = socket.create_connection(("127.0.0.1", srv.port))
+            try:
+                s.sendall(b"\x00" + struct.pack("<I", 0x3C85F7CE) + blob)
+            finally:
+                s.close()
+            good.set("probe", blob.hex() or "-")
+            assert good.get("probe") == (blob.hex() or "-").encode()
+
+        one()
+        assert srv._thread.is_alive()
