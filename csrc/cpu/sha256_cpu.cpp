@@ -307,6 +307,11 @@ __attribute__((target("sha,sse4.1"))) static void sha256d_scan_h7_shani(int lane
 struct ScanPre {  // per header: the scalar prologue shared by every step
   uint32_t w0, w1, w2, w16, w17;
   uint32_t st[8];  // block-2 state after rounds 0-2
+  // nonce-free parts of the first hash's schedule (W3 = nonce, W4 = 0x80000000, W5..W14 = 0, W15 = 640)
+  uint32_t c18, c19, c30, c31, c32;
+  uint32_t r3_t1, r3_t2;  // round 3: T1 without K3 + W3, and T2 (the state after round 2 is nonce-free)
+  // the second hash's constants (X8 = 0x80000000, X9..X14 = 0, X15 = 256; round 0 on the IV)
+  uint32_t x17, x23, x30, r0_t1, r0_t2;
 };
 
 // G x 16 consecutive nonces from n0: pushes those whose bswap(H7) <= thi
@@ -329,13 +334,32 @@ __attribute__((target("avx512f,avx512bw"))) static inline void sha256d_h7_x16(co
     a[q] = ZC(p.st[0]); b[q] = ZC(p.st[1]); c[q] = ZC(p.st[2]); d[q] = ZC(p.st[3]);
     e[q] = ZC(p.st[4]); f[q] = ZC(p.st[5]); g[q] = ZC(p.st[6]); h[q] = ZC(p.st[7]);
   }
+  for (int q = 0; q < G; ++q) {  // W18..W32: the terms on the constant words W4..W17 are scalars (ScanPre)
+    __m512i* w = W[q];
+    w[18] = ZADD(ZC(p.c18), Zs0(w[3]));
+    w[19] = ZADD(ZC(p.c19), w[3]);
+    w[20] = ZADD(Zs1(w[18]), ZC(0x80000000u));
+    w[21] = Zs1(w[19]);
+    w[22] = ZADD(Zs1(w[20]), ZC(640));
+    w[23] = ZADD(Zs1(w[21]), ZC(p.w16));
+    w[24] = ZADD(Zs1(w[22]), ZC(p.w17));
+    for (int t = 25; t < 30; ++t) w[t] = ZADD(Zs1(w[t - 2]), w[t - 7]);
+    w[30] = ZADD(ZADD(Zs1(w[28]), w[23]), ZC(p.c30));
+    w[31] = ZADD(ZADD(Zs1(w[29]), w[24]), ZC(p.c31));
+    w[32] = ZADD(ZADD(Zs1(w[30]), w[25]), ZC(p.c32));
+  }
 #pragma GCC unroll 64
-  for (int t = 18; t < 64; ++t)
+  for (int t = 33; t < 64; ++t)
     for (int q = 0; q < G; ++q)
       W[q][t] = ZADD(ZADD(Zs1(W[q][t - 2]), W[q][t - 7]), ZADD(Zs0(W[q][t - 15]), W[q][t - 16]));
+  for (int q = 0; q < G; ++q) {  // round 3: everything but K3 + W3 is nonce-free
+    const __m512i t1 = ZADD(ZC(p.r3_t1 + kSha256K[3]), W[q][3]);
+    d[q] = ZADD(d[q], t1);
+    h[q] = ZADD(t1, ZC(p.r3_t2));
+  }
 #pragma GCC unroll 64
   for (int t = 3; t < 64; t += 8) {
-    ZROUND(a, b, c, d, e, f, g, h, ZADD(ZC(kSha256K[t]), W[q][t]));
+    if (t != 3) ZROUND(a, b, c, d, e, f, g, h, ZADD(ZC(kSha256K[t]), W[q][t]));
     if (t + 1 < 64) ZROUND(h, a, b, c, d, e, f, g, ZADD(ZC(kSha256K[t + 1]), W[q][t + 1]));
     if (t + 2 < 64) ZROUND(g, h, a, b, c, d, e, f, ZADD(ZC(kSha256K[t + 2]), W[q][t + 2]));
     if (t + 3 < 64) ZROUND(f, g, h, a, b, c, d, e, ZADD(ZC(kSha256K[t + 3]), W[q][t + 3]));
@@ -358,13 +382,30 @@ __attribute__((target("avx512f,avx512bw"))) static inline void sha256d_h7_x16(co
     A[q] = ZC(kSha256IV[0]); B[q] = ZC(kSha256IV[1]); Cc[q] = ZC(kSha256IV[2]); D[q] = ZC(kSha256IV[3]);
     E[q] = ZC(kSha256IV[4]); F[q] = ZC(kSha256IV[5]); Gg[q] = ZC(kSha256IV[6]); H[q] = ZC(kSha256IV[7]);
   }
+  for (int q = 0; q < G; ++q) {  // X16..X31: the terms on the padding words X8..X15 are constants
+    __m512i* x = X[q];
+    x[16] = ZADD(Zs0(x[1]), x[0]);
+    x[17] = ZADD(ZADD(Zs0(x[2]), x[1]), ZC(p.x17));
+    for (int t = 18; t < 22; ++t) x[t] = ZADD(ZADD(Zs1(x[t - 2]), Zs0(x[t - 15])), x[t - 16]);
+    x[22] = ZADD(ZADD(Zs1(x[20]), Zs0(x[7])), ZADD(x[6], ZC(256)));
+    x[23] = ZADD(ZADD(Zs1(x[21]), x[16]), ZADD(x[7], ZC(p.x23)));
+    x[24] = ZADD(ZADD(Zs1(x[22]), x[17]), ZC(0x80000000u));
+    for (int t = 25; t < 30; ++t) x[t] = ZADD(Zs1(x[t - 2]), x[t - 7]);
+    x[30] = ZADD(ZADD(Zs1(x[28]), x[23]), ZC(p.x30));
+    x[31] = ZADD(ZADD(Zs1(x[29]), x[24]), ZADD(Zs0(x[16]), ZC(256)));
+  }
 #pragma GCC unroll 64
-  for (int t = 16; t < 61; ++t)
+  for (int t = 32; t < 61; ++t)
     for (int q = 0; q < G; ++q)
       X[q][t] = ZADD(ZADD(Zs1(X[q][t - 2]), X[q][t - 7]), ZADD(Zs0(X[q][t - 15]), X[q][t - 16]));
+  for (int q = 0; q < G; ++q) {  // round 0 on the IV: everything but X0 is constant
+    const __m512i t1 = ZADD(ZC(p.r0_t1), X[q][0]);
+    D[q] = ZADD(D[q], t1);
+    H[q] = ZADD(t1, ZC(p.r0_t2));
+  }
 #pragma GCC unroll 64
   for (int t = 0; t < 56; t += 8) {
-    ZROUND(A, B, Cc, D, E, F, Gg, H, ZADD(ZC(kSha256K[t]), X[q][t]));
+    if (t != 0) ZROUND(A, B, Cc, D, E, F, Gg, H, ZADD(ZC(kSha256K[t]), X[q][t]));
     ZROUND(H, A, B, Cc, D, E, F, Gg, ZADD(ZC(kSha256K[t + 1]), X[q][t + 1]));
     ZROUND(Gg, H, A, B, Cc, D, E, F, ZADD(ZC(kSha256K[t + 2]), X[q][t + 2]));
     ZROUND(F, Gg, H, A, B, Cc, D, E, ZADD(ZC(kSha256K[t + 3]), X[q][t + 3]));
@@ -415,6 +456,22 @@ __attribute__((target("avx512f,avx512bw"))) static void sha256d_scan_h7_avx512(i
   auto ss1 = [&](uint32_t x) { return rotr(x, 17) ^ rotr(x, 19) ^ (x >> 10); };
   p.w16 = ss1(0) + 0 + ss0(p.w1) + p.w0;    // W14 = 0, W9 = 0
   p.w17 = ss1(640) + 0 + ss0(p.w2) + p.w1;  // W15 = 640, W10 = 0
+  p.c18 = ss1(p.w16) + p.w2;                // W18 = c18 + s0(W3)      (W11 = 0)
+  p.c19 = ss1(p.w17) + ss0(0x80000000u);    // W19 = c19 + W3          (W12 = 0)
+  p.c30 = ss0(640);                         // W30 = s1(W28) + W23 + c30
+  p.c31 = ss0(p.w16) + 640;                 // W31 = s1(W29) + W24 + c31
+  p.c32 = ss0(p.w17) + p.w16;               // W32 = s1(W30) + W25 + c32
+  auto bs1 = [&](uint32_t x) { return rotr(x, 6) ^ rotr(x, 11) ^ rotr(x, 25); };
+  auto bs0 = [&](uint32_t x) { return rotr(x, 2) ^ rotr(x, 13) ^ rotr(x, 22); };
+  auto ch = [](uint32_t x, uint32_t y, uint32_t z) { return (x & y) ^ (~x & z); };
+  auto maj = [](uint32_t x, uint32_t y, uint32_t z) { return (x & y) ^ (x & z) ^ (y & z); };
+  p.r3_t1 = p.st[7] + bs1(p.st[4]) + ch(p.st[4], p.st[5], p.st[6]);
+  p.r3_t2 = bs0(p.st[0]) + maj(p.st[0], p.st[1], p.st[2]);
+  p.x17 = ss1(256);
+  p.x23 = ss0(0x80000000u);
+  p.x30 = ss0(256);
+  p.r0_t1 = kSha256IV[7] + bs1(kSha256IV[4]) + ch(kSha256IV[4], kSha256IV[5], kSha256IV[6]) + kSha256K[0];
+  p.r0_t2 = bs0(kSha256IV[0]) + maj(kSha256IV[0], kSha256IV[1], kSha256IV[2]);
   uint64_t i = 0;
   if (groups == 4)
     for (; i + 64 <= count; i += 64) sha256d_h7_x16<4>(p, mid, start + uint32_t(i), thi, cands);
