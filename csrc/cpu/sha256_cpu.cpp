@@ -414,11 +414,15 @@ __attribute__((target("avx512f,avx512bw"))) static inline void sha256d_h7_x16(co
     ZROUND(Cc, D, E, F, Gg, H, A, B, ZADD(ZC(kSha256K[t + 6]), X[q][t + 6]));
     ZROUND(B, Cc, D, E, F, Gg, H, A, ZADD(ZC(kSha256K[t + 7]), X[q][t + 7]));
   }
-  // rounds 56-59 in full, round 60 only as far as e61 = d60 + T1
+  // round 56 in full (its a is d at round 60); rounds 57-59 only their e half (the a values they would make never
+  // reach e61); round 60 only as far as e61 = d60 + T1
   ZROUND(A, B, Cc, D, E, F, Gg, H, ZADD(ZC(kSha256K[56]), X[q][56]));
-  ZROUND(H, A, B, Cc, D, E, F, Gg, ZADD(ZC(kSha256K[57]), X[q][57]));
-  ZROUND(Gg, H, A, B, Cc, D, E, F, ZADD(ZC(kSha256K[58]), X[q][58]));
-  ZROUND(F, Gg, H, A, B, Cc, D, E, ZADD(ZC(kSha256K[59]), X[q][59]));
+#define ZROUND_E(d, e, f, g, h, kw)                                                 \
+  for (int q = 0; q < G; ++q) d[q] = ZADD(d[q], ZADD(ZADD(h[q], ZS1(e[q])), ZADD(ZCH(e[q], f[q], g[q]), (kw))));
+  ZROUND_E(Cc, D, E, F, Gg, ZADD(ZC(kSha256K[57]), X[q][57]));
+  ZROUND_E(B, Cc, D, E, F, ZADD(ZC(kSha256K[58]), X[q][58]));
+  ZROUND_E(A, B, Cc, D, E, ZADD(ZC(kSha256K[59]), X[q][59]));
+#undef ZROUND_E
   const __m512i vthi = ZC(thi);
   for (int q = 0; q < G; ++q) {
     // round 60: a = E, b..d = F, G, H, e = A, f..h = B, Cc, D
