@@ -225,14 +225,29 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   // Test hook: the scrypt verifier's bounded queue (BoundedWorkQueue) flooded by a producer that never waits, with
-  // a consumer hashing every item on the host (scrypt_1024_1_1, as the GPU miner's verifier does).
-  m.def("_work_queue_flood", [](size_t cap, size_t n, bool hash_each) {
+  // a consumer hashing every item on the host. batch > 1 takes up to that many items per pop_many and hashes them in
+  // one scrypt_1024_1_1_batch pass, as the GPU miner's verifier does (16); batch 1 pops and hashes one at a time.
+  m.def("_work_queue_flood", [](size_t cap, size_t n, bool hash_each, size_t batch) {
     BoundedWorkQueue<std::array<uint8_t, 80>> q(cap);
     std::atomic<uint64_t> processed{0};
     uint64_t accepted = 0;
     {
       py::gil_scoped_release r;
       std::thread consumer([&] {
+        if (batch > 1) {
+          std::vector<std::array<uint8_t, 80>> items;
+          std::vector<const uint8_t*> ip;
+          std::vector<std::array<uint8_t, 32>> outs(batch);
+          std::vector<uint8_t*> op;
+          for (auto& o : outs) op.push_back(o.data());
+          while (items.clear(), q.pop_many(&items, batch) > 0) {
+            ip.clear();
+            for (const auto& it : items) ip.push_back(it.data());
+            if (hash_each) scrypt_1024_1_1_batch(int(items.size()), ip.data(), op.data());
+            processed.fetch_add(items.size());
+          }
+          return;
+        }
         std::array<uint8_t, 80> h;
         uint8_t out[32];
         while (q.pop(&h)) {
@@ -254,7 +269,7 @@ PYBIND11_MODULE(_native, m) {
     d["peak"] = q.peak();
     d["processed"] = processed.load();
     return d;
-  }, py::arg("cap"), py::arg("n"), py::arg("hash_each") = true);
+  }, py::arg("cap"), py::arg("n"), py::arg("hash_each") = true, py::arg("batch") = 1);
   m.attr("X11_STAGES") = kX11StageCount;
   m.def("x11", [](const py::bytes& msg) {
     std::string s = msg; uint8_t o[32];

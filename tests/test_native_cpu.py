@@ -303,6 +303,13 @@ def test_scrypt_verifier_queue_is_bounded_under_a_flood():
         assert r["accepted"] + r["refused"] == n and r["processed"] == r["accepted"], r
     r = N._work_queue_flood(64, 50, False)  # below the cap nothing is refused
     assert r == {"accepted": 50, "refused": 0, "peak": r["peak"], "processed": 50} and r["peak"] <= 50
+    # the verifier's batched consumer (pop_many of up to 16, one scrypt pass per batch): bounded the same way,
+    # every accepted item hashed exactly once
+    r = N._work_queue_flood(64, 3000, True, 16)
+    assert r["peak"] <= 64 and r["refused"] > 0 and r["accepted"] + r["refused"] == 3000, r
+    assert r["processed"] == r["accepted"], r
+    r = N._work_queue_flood(4096, 300, True, 16)
+    assert r["processed"] == r["accepted"] == 300 and r["refused"] == 0, r
 
 
 def test_clock_bounds_track_the_window_minimum():
