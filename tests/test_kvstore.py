@@ -205,3 +205,28 @@ def test_garbage_from_one_peer_never_disturbs_another():
 
         one()
         assert srv._thread.is_alive()
+
+
+def test_supervisor_counts_gpus_from_sysfs_without_torch(tmp_path):
+    """`otedama node` checks --gpus against the KFD topology (parallel/launch.py visible_gpus), so the supervisor never
+    imports torch; *_VISIBLE_DEVICES re-numbering applies as for the engine. Fixture topology: a CPU node and two
+    gfx950 GPUs."""
+    code = (
+        "import sys, json; from otedama_amd import hal; hal.KFD_TOPOLOGY_PATH = sys.argv[1]; "
+        "from otedama_amd.parallel.launch import visible_gpus; "
+        "print(json.dumps([visible_gpus(), 'torch' in sys.modules]))")
+    for n, text in {0: "simd_count 0\ngfx_target_version 0\n",
+                    1: "simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n",
+                    2: "simd_count 1024\nsimd_per_cu 4\ngfx_target_version 90500\n"}.items():
+        (tmp_path / str(n)).mkdir()
+        (tmp_path / str(n) / "properties").write_text(text)
+    env = {k: v for k, v in os.environ.items() if not k.endswith("VISIBLE_DEVICES")}
+    env["PYTHONPATH"] = ROOT
+    out = subprocess.run([sys.executable, "-c", code, str(tmp_path)], env=env, capture_output=True, text=True,
+                         timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "[2, false]"
+    env["HIP_VISIBLE_DEVICES"] = "1"
+    out = subprocess.run([sys.executable, "-c", code, str(tmp_path)], env=env, capture_output=True, text=True,
+                         timeout=60)
+    assert out.stdout.strip() == "[1, false]", out.stderr
