@@ -10,6 +10,20 @@ spawns the N ranks itself (otedama_amd/parallel/launch.py: fresh interpreters,
 the parent never touches the GPU) and exits non-zero when fewer than N GPUs
 are visible; under torchrun (WORLD_SIZE set) ``--gpus`` must equal WORLD_SIZE.
 
+Every run reports (otedama_amd/parallel/guard.py). Each rank runs its sections
+under deadlines watched by a thread that never waits on the main thread:
+  preflight  rendezvous + one tiny all_reduce (the first RCCL traffic) under
+             --preflight-timeout; on failure rank 0 prints an error JSON with
+             the ranks that checked in, each rank's phase, the tail of its
+             stderr and of its RCCL log (NCCL_DEBUG=WARN), and exits non-zero;
+  sha256d    the headline (below);
+  single, scrypt, x11, miner   all ranks; cpu, latency, node, pool   rank 0.
+A section that overruns its budget (or the run's --deadline) is recorded as
+{"error": "timeout after X s"} and the JSON is printed with everything measured
+so far; a SIGTERM (torchrun tearing the job down, the driver's timeout) makes
+rank 0 print it too. The ``summary`` key comes LAST so a tail of the output
+always carries every headline.
+
 One timed step on each rank =
   R1  control broadcast from rank 0 when the variant group changes (the job
       blob itself went out once, before timing),
@@ -29,9 +43,10 @@ expectation (z-score). Weak scaling: per-GPU work is fixed as N grows.
 Then BASELINE config 2 verbatim (one fixed midstate, full 2^32 nonces, the
 single-header kernel), scrypt(1024,1,1) (HBM-resident scratchpads; hits re-
 verified with hashlib.scrypt), X11 (nonce ranges partitioned across ranks; hits
-re-verified with the C++ chain), the share-latency probe (engine on this GPU,
-pool in a separate process; device hit -> accept from the kernel's own clock)
-and the job-switch probe (set_job -> new work running, SHA-256d and scrypt).
+re-verified with the C++ chain), scrypt and X11 through the production miner,
+BASELINE config 1 (the CPU miner), the share-latency and job-switch probes, the
+production node (``otedama node --gpus N``) per algorithm with its node-wide job
+switch, and BASELINE config 5 (mixed pool, vardiff, steady state).
 
 ``--cpu-rehearsal`` runs the same rank/launcher/collective code with gloo and
 the native CPU scanner in place of the kernels (tests/test_bench_launcher.py);
@@ -52,6 +67,7 @@ import time
 
 BASELINE_HPS = 75e6  # BENCHMARKS.md:46 (whole 7950X, SHA-256d)
 METRIC = "hashes/sec (whole node) SHA-256d + scrypt at 1/2/4/8 MI355X; p50 share latency"
+DEFAULT_DEADLINE_S = 500.0  # the driver's run limit is 600 s: report well inside it
 
 
 def synthetic_job(seed: int = 1) -> dict:
@@ -96,14 +112,25 @@ def parse_args(argv=None):
                     help="synthetic header seed: the hit count of a seed is one Poisson draw, repeated on every run")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--node-seconds", type=float, default=-1.0,
-                    help="production node section (otedama node --gpus N + local pool): recorded seconds "
-                         "(-1 = 10 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+                    help="production node section (otedama node --gpus N + local pool): recorded seconds per "
+                         "algorithm (-1 = 8 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
     ap.add_argument("--node-warmup", type=float, default=3.0)
+    ap.add_argument("--node-algorithms", default="sha256d,x11,scrypt",
+                    help="algorithms the node section runs, each against a pool of its own (BASELINE config 4: x11)")
+    ap.add_argument("--node-switches", type=int, default=8,
+                    help="forced new blocks (SetNewPrevHash) per node run for the node-wide job switch (0 = none)")
     ap.add_argument("--pool-seconds", type=float, default=-1.0,
-                    help="BASELINE config 5 (mixed SHA-256d + scrypt pool, vardiff on): recorded seconds "
-                         "(-1 = 12 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+                    help="BASELINE config 5 (mixed SHA-256d + scrypt pool, vardiff on): recorded seconds after every "
+                         "worker settled (-1 = 25 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="BASELINE config 1 (native CPU miner, single thread and all cores): seconds each (0 = skip)")
+    ap.add_argument("--deadline", type=float, default=DEFAULT_DEADLINE_S,
+                    help="seconds from start by which rank 0 prints its JSON, whatever is still running")
+    ap.add_argument("--preflight-timeout", type=float, default=180.0,
+                    help="seconds from start for the rendezvous and the first collective (cold `import torch` "
+                         "included)")
+    ap.add_argument("--section-timeouts", default="",
+                    help="override section budgets, e.g. node=60,pool=90 (seconds)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="gloo + native CPU scanner instead of the GPU kernels (launcher / collective tests)")
     ap.add_argument("--cpu-nonces", type=int, default=1 << 12, help="rehearsal: nonces per variant per step")
@@ -112,7 +139,8 @@ def parse_args(argv=None):
 
 # The benchmark is not the fault-tolerant node: a rank that is slow to start (a cold first `import torch` on a fresh
 # node can take a minute) or busy re-verifying hits must not trip the node's 30 s collective bound. Set before
-# otedama_amd.parallel is imported (it reads the bound at import); spawned ranks inherit it.
+# otedama_amd.parallel is imported (it reads the bound at import); spawned ranks inherit it. The rank guard's section
+# deadlines (parallel/guard.py) are what bounds a hang.
 BENCH_PG_TIMEOUT_S = "600"
 
 
@@ -133,8 +161,13 @@ def main(argv=None) -> int:
 
 
 def launch(args, argv: list[str]) -> int:
-    """No torchrun env and N > 1: spawn the N ranks here (never exec; this process stays GPU-free)."""
-    from otedama_amd.parallel.launch import run_ranks, visible_gpus
+    """No torchrun env and N > 1: spawn the N ranks here (never exec; this process stays GPU-free). The launcher
+    has a deadline of its own past the ranks' (SIGTERM, then SIGKILL) and prints an error JSON itself when rank 0
+    never printed one (e.g. it was killed)."""
+    import shutil
+
+    from otedama_amd.parallel.guard import diagnose_run_dir, run_dir_for
+    from otedama_amd.parallel.launch import free_port, run_ranks, visible_gpus
 
     if not args.cpu_rehearsal and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
         n = visible_gpus()
@@ -142,7 +175,20 @@ def launch(args, argv: list[str]) -> int:
             print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this host has {n}; "
                   "refusing to report a smaller node as N GPUs", file=sys.stderr)
             return 2
-    return run_ranks([sys.executable, os.path.abspath(__file__), *argv], args.gpus)
+    port = free_port()
+    run_dir = run_dir_for({"MASTER_PORT": str(port)})
+    shutil.rmtree(run_dir, ignore_errors=True)
+    os.makedirs(run_dir, exist_ok=True)
+    seen = []
+    t0 = time.time()
+    rc = run_ranks([sys.executable, os.path.abspath(__file__), *argv], args.gpus, port=port,
+                   deadline=args.deadline + 60.0, on_rank0_line=lambda ln: seen.append(ln.startswith('{"metric"')))
+    if not any(seen):
+        out = error_output(args, args.gpus, f"rank 0 printed no result (launcher exit code {rc})",
+                           {"launcher": f"exit code {rc}"}, diagnose_run_dir(run_dir, args.gpus, t0))
+        print(json.dumps(out), flush=True)
+        return rc or 1
+    return rc
 
 
 # --------------------------------------------------------------------------- search back-ends
@@ -185,225 +231,422 @@ def _poisson(found: int, hashes: int, target_int: int) -> tuple[float, float]:
     return exp, ((found - exp) / math.sqrt(exp) if exp > 0 else 0.0)
 
 
-def run_rank(args) -> int:
-    import torch
+def _r(x, digits: int = 4):
+    """Compact number for the summary (4 significant digits)."""
+    if x is None or isinstance(x, bool) or not isinstance(x, (int, float)):
+        return x
+    if x == 0 or not math.isfinite(x):
+        return x
+    return float(f"{x:.{digits}g}")
 
-    from otedama_amd.ops import native
-    from otedama_amd.parallel import NodeComm, barrier, init_from_env, shutdown, stripe_for
-    from otedama_amd.utils.trace import span
 
-    cpu = args.cpu_rehearsal
-    if not cpu and not torch.cuda.is_available():
-        print("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU config "
-              "(or --cpu-rehearsal for the launcher/collective rehearsal)", file=sys.stderr)
-        return 2
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if not cpu and world_env > 1 and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
-        local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
-        if local >= torch.cuda.device_count():
-            print(f"bench.py: rank with LOCAL_RANK={local} has no GPU ({torch.cuda.device_count()} visible)",
-                  file=sys.stderr)
-            return 2
-    N = native.require_native()
-    info = init_from_env(backend="gloo" if cpu else None, use_gpu=not cpu)
-    comm = NodeComm(info)
-    dev = info.device
-    world = info.world_size
+def _base_config(args) -> dict:
+    return {"model": "sha256d", "seq_len": 80}
 
-    def sync():
-        if not cpu:
-            torch.cuda.synchronize(dev)
 
-    job = comm.broadcast_job(synthetic_job(args.seed) if info.is_primary else None)  # R1: the job blob, once
-    if cpu:
-        from otedama_amd.models.header import int_to_hash
+def error_output(args, world: int, error: str, errors: dict, diagnosis: dict | None) -> dict:
+    """The JSON line of a run that has no headline (the pre-flight failed, or rank 0 never reported)."""
+    return {
+        "metric": METRIC, "value": None, "unit": "hashes/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic 80-byte block headers", "config": _base_config(args),
+        "error": error, "errors": errors, "diagnosis": diagnosis,
+        "summary": {"world_size": world, "error": error, "errors": errors,
+                    "ranks_checked_in": (diagnosis or {}).get("ranks_checked_in"),
+                    "rank_phases": (diagnosis or {}).get("phases")},
+    }
 
-        job["target"] = int_to_hash((1 << 244) - 1)  # ~1 hit per 4096 hashes: the rehearsal exercises R2
-    target_int = int.from_bytes(job["target"], "little")
-    stripe = stripe_for(info.rank, info.world_size)
-    use_v = args.sha_kernel == "v" or cpu
-    if cpu:
-        K, V_COUNT = 4, max(1, args.cpu_nonces)
-        steps_per_group = 2
-        search = _CpuSearch(N, K)
-    elif use_v:
-        # One step = 64 x chains version variants (chains per lane of a wave) x 2^35 / that many nonces = 2^35
-        # hashes, the same work as the K=8 step (8 x 2^32); 8 x chains consecutive steps tile the full 2^32 nonces
-        # of one variant group. Two chains run the 4-waves/SIMD build at 128 blocks/CU (profiles/r2/sha_v2).
-        from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, Sha256dSearchV, default_grid
 
-        K = N.SHA256D_V_GROUP * args.sha_chains
-        V_COUNT = (1 << 35) // K
-        steps_per_group = (1 << 32) // V_COUNT
-        SUB_LAUNCHES = 8  # 2^32 hashes per launch
-        s1 = torch.cuda.Stream(dev)
-        if args.sha_chains == 2:
-            search = Sha256dSearchV(dev, grid=args.grid or default_grid(dev, SHA256D_V2_BLOCKS_PER_CU), chains=2,
-                                    occupancy8=False)
+# --------------------------------------------------------------------------- the run
+class Bench:
+    """One rank of the benchmark. Sections fill ``R``; ``output()`` turns whatever is in it into the JSON line."""
+
+    def __init__(self, args, rank: int, world: int):
+        self.args = args
+        self.rank, self.world = rank, world
+        self.cpu = args.cpu_rehearsal
+        self.R: dict = {}
+        self.guard = None
+        self.info = self.comm = self.N = self.dev = None
+        self.budgets = self._budgets()
+
+    # ------------------------------------------------------------------ budgets
+    def _budgets(self) -> dict[str, float]:
+        a = self.args
+        ssteps = a.steps if a.scrypt_steps < 0 else a.scrypt_steps
+        xsteps = a.steps if a.x11_steps < 0 else a.x11_steps
+        miner_s = self.miner_seconds()
+        node_s, pool_s = self.node_seconds(), self.pool_seconds()
+        algos = max(1, len(self.node_algorithms()))
+        b = {"sha256d": 120.0 + 5.0 * (a.steps + a.warmup), "single": 90.0, "scrypt": 90.0 + 3.0 * ssteps,
+             "x11": 90.0 + 2.0 * xsteps, "miner": 2 * (miner_s + 60.0), "cpu": 40.0 + 3.0 * a.cpu_seconds,
+             "latency": 180.0, "node": algos * (150.0 + node_s + a.node_warmup + 4.0 * a.node_switches),
+             "pool": 240.0 + pool_s}
+        for item in filter(None, (s.strip() for s in a.section_timeouts.split(","))):
+            k, _, v = item.partition("=")
+            b[k.strip()] = float(v)
+        return b
+
+    def miner_seconds(self) -> float:
+        return self.args.miner_seconds if self.args.miner_seconds >= 0 else (0.0 if self.cpu else 8.0)
+
+    def node_seconds(self) -> float:
+        return self.args.node_seconds if self.args.node_seconds >= 0 else (0.0 if self.cpu else 8.0)
+
+    def pool_seconds(self) -> float:
+        return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 25.0)
+
+    def node_algorithms(self) -> list[str]:
+        return [x.strip() for x in self.args.node_algorithms.split(",") if x.strip()]
+
+    # ------------------------------------------------------------------ driver
+    def run(self) -> int:
+        g = self.guard
+        try:
+            with g.section("preflight", max(10.0, self.args.preflight_timeout - g.elapsed()), critical=True):
+                self.preflight()
+        except Exception as exc:  # noqa: BLE001 - a start that failed outright (not a hang): report it
+            return self.fail("preflight", f"{type(exc).__name__}: {exc}")
+        try:
+            with g.section("sha256d", self.budgets["sha256d"], critical=True):
+                self.sha256d()
+        except Exception as exc:  # noqa: BLE001
+            return self.fail("sha256d", f"{type(exc).__name__}: {exc}")
+        # sections every rank takes part in (collectives): rank 0 decides whether there is time and tells the rest
+        need = {"single": 15.0, "scrypt": 30.0, "x11": 20.0, "miner": 2 * (self.miner_seconds() + 20.0)}
+        for name, fn in (("single", self.single), ("scrypt", self.scrypt), ("x11", self.x11),
+                         ("miner", self.miner)):
+            if not self.wanted(name):
+                continue
+            go = g.remaining() >= need[name] if self.rank == 0 else True
+            if self.world > 1:
+                go = bool(self.comm.broadcast_control([int(go)])[0])
+            if not go:
+                g.skip(name, f"bench deadline: {g.remaining():.0f} s left")
+                continue
+            with g.section(name, self.budgets[name]):
+                fn()
+        if self.rank != 0:
+            g.finish()
+            self.shutdown()
+            return 0
+        need0 = {"cpu": 2.5 * self.args.cpu_seconds + 5, "latency": 60.0,
+                 "node": 40.0 + self.node_seconds() + self.args.node_warmup, "pool": 60.0 + self.pool_seconds()}
+        for name, fn in (("cpu", self.cpu_miner), ("latency", self.latency), ("node", self.node),
+                         ("pool", self.pool)):
+            if not self.wanted(name):
+                continue
+            if g.remaining() < need0[name]:
+                g.skip(name, f"bench deadline: {g.remaining():.0f} s left")
+                continue
+            with g.section(name, self.budgets[name]):
+                fn()
+        if not g.finish():
+            while True:  # the watchdog fired meanwhile and is printing / exiting
+                time.sleep(1)
+        print(json.dumps(self.output(dict(g.errors))), flush=True)
+        self.shutdown()
+        return 0
+
+    def wanted(self, name: str) -> bool:
+        a, cpu = self.args, self.cpu
+        return {
+            "single": a.single_midstate_headers > 0 and not cpu,
+            "scrypt": (a.steps if a.scrypt_steps < 0 else a.scrypt_steps) > 0 and not cpu,
+            "x11": (a.x11_steps if a.x11_steps >= 0 else a.steps) > 0 and not cpu,
+            "miner": self.miner_seconds() > 0,
+            "cpu": a.cpu_seconds > 0,
+            "latency": not a.no_latency and not cpu,
+            "node": self.node_seconds() > 0 and bool(self.node_algorithms()),
+            "pool": self.pool_seconds() > 0,
+        }[name]
+
+    def fail(self, section: str, error: str) -> int:
+        """A critical section failed with an exception: rank 0 reports, every rank leaves non-zero."""
+        g = self.guard
+        g.errors.setdefault(section, error)
+        if self.rank == 0 and g.finish():
+            print(json.dumps(self.output(dict(g.errors), fatal=error)), flush=True)
+            g.stop_peers()
         else:
-            search = Sha256dSearchV(dev, grid=args.grid or None)
-    else:
-        from otedama_amd.ops.search import Sha256dSearch, Sha256dSearchK
+            g.finish()
+        return 1
 
-        V_COUNT, steps_per_group = 1 << 32, 1
-        K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
-        search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else Sha256dSearch(dev, grid=args.grid or None)
-    slot_words = 1 + (2 if K > 1 else 1) * search.cap
-    # double-buffered hit slots: step i writes outs[i % 2] while R2 of step i-1 reads the other one
-    outs = [torch.zeros(slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
-    gathered = [torch.zeros(world, slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
-    r2_seen = torch.zeros(1, dtype=torch.int64, device=dev)  # hits of every rank that arrived through R2
-    r2_done: list = [None, None]
-    ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+    def emit(self, errors: dict, reason: str) -> int:
+        """Watchdog path (rank 0): print the JSON with what finished; exit code 0 when the headline was measured."""
+        out = self.output(errors, fatal=None if "sha" in self.R else reason)
+        os.write(1, (json.dumps(out) + "\n").encode())
+        return 0 if "sha" in self.R else 1
 
-    def variant_params(step: int) -> tuple[list[bytes], bytes]:
-        hdrs = [N.variant_header(job, stripe.start + (step * K + j) * stripe.stride)[0] for j in range(K)]
-        if K > 1:
-            return hdrs, N.sha256d_prepare_k(hdrs, job["target"])
-        return hdrs, N.sha256d_prepare(hdrs[0], job["target"])
+    def shutdown(self) -> None:
+        if self.info is not None:
+            from otedama_amd.parallel import shutdown
 
-    v_groups: dict[int, tuple[list[bytes], object]] = {}
+            with contextlib.suppress(Exception):
+                shutdown(self.info)
 
-    def v_group(q: int):
-        # variant group q of this rank: stripe positions Kq .. Kq+K-1; the table is uploaded once, before timing
-        if q not in v_groups:
-            hdrs = [N.variant_header(job, stripe.start + (q * K + j) * stripe.stride)[0] for j in range(K)]
-            v_groups[q] = (hdrs, search.prepare(hdrs, job["target"]))
-        return v_groups[q]
+    # ------------------------------------------------------------------ sections
+    def preflight(self) -> None:
+        t0 = time.monotonic()
+        self.guard.set_phase("import")
+        import torch
 
-    hits_log: list[tuple[list[bytes], torch.Tensor]] = []
-    last_group = [-1]
+        from otedama_amd.ops import native
+        from otedama_amd.parallel import NodeComm, init_from_env
 
-    def step(i: int, record: bool) -> None:
-        with span("otd.bench.sha256d_step"):
-            _step(i, record)
+        cpu = self.cpu
+        if not cpu and not torch.cuda.is_available():
+            raise RuntimeError("bench.py requires a GPU (HIP); run `python -m otedama_amd.cli bench-cpu` for the CPU "
+                               "config (or --cpu-rehearsal for the launcher/collective rehearsal)")
+        if not cpu and self.world > 1 and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
+            local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+            if local >= torch.cuda.device_count():
+                raise RuntimeError(f"rank with LOCAL_RANK={local} has no GPU ({torch.cuda.device_count()} visible)")
+        self.N = native.require_native()
+        t_import = time.monotonic()
+        self.guard.set_phase("rendezvous")
+        self.info = init_from_env(backend="gloo" if cpu else None, use_gpu=not cpu)
+        self.comm = NodeComm(self.info)
+        self.dev = self.info.device
+        t_pg = time.monotonic()
+        self.guard.set_phase("first-collective")
+        total = self.comm.allreduce_counters(1)[0]  # the first collective on the data plane (RCCL on GPUs)
+        rows = self.comm.gather_counters([self.info.rank, os.getpid(), 0, 0])
+        if self.world > 1:
+            torch.distributed.barrier()
+        t1 = time.monotonic()
+        if total != self.world:
+            raise RuntimeError(f"pre-flight all_reduce summed {total}, expected {self.world}")
+        self.R["preflight"] = {"ok": True, "ranks": sorted(int(r[0]) for r in rows),
+                               "import_s": round(t_import - t0, 2), "rendezvous_s": round(t_pg - t_import, 2),
+                               "first_collectives_ms": round((t1 - t_pg) * 1e3, 2),
+                               "since_start_s": round(self.guard.elapsed(), 2), "backend": self.info.backend}
 
-    def _step(i: int, record: bool) -> None:
-        b = i % 2
-        q = i // steps_per_group
-        if world > 1 and q != last_group[0]:  # R1 on change: rank 0 announces the next variant group
-            if info.is_primary:
-                ctl.fill_(q)
-            comm.run_async(lambda: torch.distributed.broadcast(ctl, src=0))
-            last_group[0] = q
-        if r2_done[b] is not None:  # the gather that read this slot two steps ago must be done before reuse
-            torch.cuda.current_stream(dev).wait_event(r2_done[b])
-        out = outs[b]
-        if use_v:  # K1: 128 variants x 1/16 of the nonce space (W3 window)
-            hdr, prep = v_group(q)
-            if cpu:
-                search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT, out)
+    def sync(self) -> None:
+        if not self.cpu:
+            import torch
+
+            torch.cuda.synchronize(self.dev)
+
+    def barrier(self) -> None:
+        from otedama_amd.parallel import barrier
+
+        barrier(self.info)
+
+    def sha256d(self) -> None:
+        import torch
+
+        from otedama_amd.parallel import stripe_for
+        from otedama_amd.utils.trace import span
+
+        args, N, comm, info, dev, cpu = self.args, self.N, self.comm, self.info, self.dev, self.cpu
+        world = info.world_size
+        sync = self.sync
+        job = comm.broadcast_job(synthetic_job(args.seed) if info.is_primary else None)  # R1: the job blob, once
+        if cpu:
+            from otedama_amd.models.header import int_to_hash
+
+            job["target"] = int_to_hash((1 << 244) - 1)  # ~1 hit per 4096 hashes: the rehearsal exercises R2
+        self.job = job
+        target_int = int.from_bytes(job["target"], "little")
+        stripe = stripe_for(info.rank, info.world_size)
+        self.stripe = stripe
+        use_v = args.sha_kernel == "v" or cpu
+        s1 = None
+        if cpu:
+            K, V_COUNT = 4, max(1, args.cpu_nonces)
+            steps_per_group = 2
+            search = _CpuSearch(N, K)
+        elif use_v:
+            # One step = 64 x chains version variants (chains per lane of a wave) x 2^35 / that many nonces = 2^35
+            # hashes, the same work as the K=8 step (8 x 2^32); 8 x chains consecutive steps tile the full 2^32 nonces
+            # of one variant group. Two chains run the 4-waves/SIMD build at 128 blocks/CU (profiles/r2/sha_v2).
+            from otedama_amd.ops.search import SHA256D_V2_BLOCKS_PER_CU, Sha256dSearchV, default_grid
+
+            K = N.SHA256D_V_GROUP * args.sha_chains
+            V_COUNT = (1 << 35) // K
+            steps_per_group = (1 << 32) // V_COUNT
+            s1 = torch.cuda.Stream(dev)
+            if args.sha_chains == 2:
+                search = Sha256dSearchV(dev, grid=args.grid or default_grid(dev, SHA256D_V2_BLOCKS_PER_CU), chains=2,
+                                        occupancy8=False)
             else:
-                # the step's window as SUB_LAUNCHES launches of 2^32 hashes alternating over two streams, as the
-                # production miner issues them (a launch's last waves overlap the next launch's first); on three
-                # boxes this measured -0.2% .. +0.35% against one 2^35-hash launch (profiles/r3/s_paths)
-                s0 = torch.cuda.current_stream(dev)
-                out[:1].zero_()
-                s1.wait_stream(s0)
-                sub = V_COUNT // SUB_LAUNCHES
-                lo = (i % steps_per_group) * V_COUNT
-                for j in range(SUB_LAUNCHES):
-                    search.launch_into(prep, lo + j * sub, sub, out, s0 if j % 2 == 0 else s1)
-                # The step's consumers (the hit copy, R2) go behind its last launch on s1, which waits for s0's last
-                # launch only: s0 starts the next step at once and that launch overlaps this step's tail, as the
-                # production miner's two streams never join.
-                s1.wait_stream(s0)
+                search = Sha256dSearchV(dev, grid=args.grid or None)
         else:
-            hdr, params = variant_params(i)
-            search.launch(params, 0, 1 << 32, out=out)  # K1: full 2^32 nonce space
-        tail = s1 if (use_v and not cpu) else None
-        with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
-            if record:  # with the nonce window the step covered (W3 = bswap(nonce) for the v kernel)
-                lo = (i % steps_per_group) * V_COUNT if use_v else 0
-                hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
+            from otedama_amd.ops.search import Sha256dSearch, Sha256dSearchK
 
-            def r2(o=out, g=gathered[b]):
-                if world > 1:
-                    torch.distributed.all_gather_into_tensor(g.view(-1), o)
+            V_COUNT, steps_per_group = 1 << 32, 1
+            K = max(k for k in (1, *N.SHA256D_K_VALUES) if k <= max(1, args.sha_variants))
+            search = Sha256dSearchK(dev, k=K, grid=args.grid or None) if K > 1 else \
+                Sha256dSearch(dev, grid=args.grid or None)
+        SUB_LAUNCHES = 8  # 2^32 hashes per launch
+        slot_words = 1 + (2 if K > 1 else 1) * search.cap
+        # double-buffered hit slots: step i writes outs[i % 2] while R2 of step i-1 reads the other one
+        outs = [torch.zeros(slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
+        gathered = [torch.zeros(world, slot_words, dtype=torch.int32, device=dev) for _ in range(2)]
+        r2_seen = torch.zeros(1, dtype=torch.int64, device=dev)  # hits of every rank that arrived through R2
+        r2_done: list = [None, None]
+        ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+
+        def variant_params(step: int) -> tuple[list[bytes], bytes]:
+            hdrs = [N.variant_header(job, stripe.start + (step * K + j) * stripe.stride)[0] for j in range(K)]
+            if K > 1:
+                return hdrs, N.sha256d_prepare_k(hdrs, job["target"])
+            return hdrs, N.sha256d_prepare(hdrs[0], job["target"])
+
+        v_groups: dict[int, tuple[list[bytes], object]] = {}
+
+        def v_group(q: int):
+            # variant group q of this rank: stripe positions Kq .. Kq+K-1; the table is uploaded once, before timing
+            if q not in v_groups:
+                hdrs = [N.variant_header(job, stripe.start + (q * K + j) * stripe.stride)[0] for j in range(K)]
+                v_groups[q] = (hdrs, search.prepare(hdrs, job["target"]))
+            return v_groups[q]
+
+        hits_log: list = []
+        last_group = [-1]
+
+        def step(i: int, record: bool) -> None:
+            with span("otd.bench.sha256d_step"):
+                _step(i, record)
+
+        def _step(i: int, record: bool) -> None:
+            b = i % 2
+            q = i // steps_per_group
+            if world > 1 and q != last_group[0]:  # R1 on change: rank 0 announces the next variant group
+                if info.is_primary:
+                    ctl.fill_(q)
+                comm.run_async(lambda: torch.distributed.broadcast(ctl, src=0))
+                last_group[0] = q
+            if r2_done[b] is not None:  # the gather that read this slot two steps ago must be done before reuse
+                torch.cuda.current_stream(dev).wait_event(r2_done[b])
+            out = outs[b]
+            if use_v:  # K1: 128 variants x 1/16 of the nonce space (W3 window)
+                hdr, prep = v_group(q)
+                if cpu:
+                    search.launch(prep, (i % steps_per_group) * V_COUNT, V_COUNT, out)
                 else:
-                    g[0].copy_(o)
-                r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
+                    # the step's window as SUB_LAUNCHES launches of 2^32 hashes alternating over two streams, as the
+                    # production miner issues them (a launch's last waves overlap the next launch's first); on three
+                    # boxes this measured -0.2% .. +0.35% against one 2^35-hash launch (profiles/r3/s_paths)
+                    s0 = torch.cuda.current_stream(dev)
+                    out[:1].zero_()
+                    s1.wait_stream(s0)
+                    sub = V_COUNT // SUB_LAUNCHES
+                    lo = (i % steps_per_group) * V_COUNT
+                    for j in range(SUB_LAUNCHES):
+                        search.launch_into(prep, lo + j * sub, sub, out, s0 if j % 2 == 0 else s1)
+                    # The step's consumers (the hit copy, R2) go behind its last launch on s1, which waits for s0's
+                    # last launch only: s0 starts the next step at once and that launch overlaps this step's tail, as
+                    # the production miner's two streams never join.
+                    s1.wait_stream(s0)
+            else:
+                hdr, params = variant_params(i)
+                search.launch(params, 0, 1 << 32, out=out)  # K1: full 2^32 nonce space
+            tail = s1 if (use_v and not cpu) else None
+            with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+                if record:  # with the nonce window the step covered (W3 = bswap(nonce) for the v kernel)
+                    lo = (i % steps_per_group) * V_COUNT if use_v else 0
+                    hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
 
-            r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
+                def r2(o=out, g=gathered[b]):
+                    if world > 1:
+                        torch.distributed.all_gather_into_tensor(g.view(-1), o)
+                    else:
+                        g[0].copy_(o)
+                    r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
 
-    # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
-    # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
-    positions = ((args.steps + args.warmup + steps_per_group - 1) // steps_per_group + 1) * K if use_v \
-        else (args.steps + args.warmup) * K
-    if positions * world > 1 << 16:
-        raise SystemExit("bench.py: (steps + warmup) x variants x GPUs exceeds the 2^16 version-rolling space")
-    if use_v:  # variant tables for every step, timed and warmup, built and uploaded before the timed region
-        for i in range(args.steps + args.warmup):
-            v_group(i // steps_per_group)
-    for i in range(args.warmup):
-        step(args.steps + i, False)
-    sync()
-    barrier(info)
-    sync()
-    r2_seen.zero_()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, True)
-    step_hashes = K * (V_COUNT if use_v else 1 << 32)
-    total = comm.allreduce_counters(args.steps * step_hashes)[0] if world > 1 else args.steps * step_hashes  # R3
-    sync()
-    barrier(info)
-    sync()
-    t_local = time.perf_counter() - t0
-    elapsed = comm.allreduce_max(t_local)
-    sha_hps = total / elapsed
-    # per-rank rates + which ranks actually took part in the collectives (RCCL world check)
-    rows = comm.gather_counters([info.rank, args.steps * step_hashes, int(t_local * 1e6), int(r2_seen.item())])
-    ranks_seen = sorted(int(r[0]) for r in rows)
-    per_rank_hps = [r[1] / max(r[2] * 1e-6, 1e-9) for r in sorted(rows)]
+                r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
 
-    # Re-verify every hit of the timed region on the CPU (full 256-bit compare), de-duplicated by (variant, nonce).
-    found = verified = dups = outside = 0
-    seen: set = set()
-    for hdrs, buf, lo, cnt in hits_log:
-        host = buf.cpu().tolist()
-        n = min(host[0] & 0xFFFFFFFF, search.cap)
-        pairs = [(host[1 + 2 * i], host[2 + 2 * i]) for i in range(n)] if K > 1 else [(x, 0) for x in host[1 : 1 + n]]
-        for nonce, vi in pairs:
-            nonce &= 0xFFFFFFFF
-            found += 1
-            w = nonce if cpu or not use_v else int.from_bytes(nonce.to_bytes(4, "little"), "big")
-            outside += not lo <= w < lo + cnt  # a hit outside the window the step was asked to search
-            if not 0 <= vi < K:
-                continue
-            hdr = hdrs[vi]
-            key = (hdr[:76], nonce)
-            if key in seen:
-                dups += 1
-                continue
-            seen.add(key)
-            h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
-            if int.from_bytes(h, "little") <= target_int:
-                verified += 1
-    found, verified, dups, outside = comm.allreduce_counters(found, verified, dups, outside)
-    expected, z = _poisson(verified, total, target_int)
-    r2_hits = rows[0][3] if rows else 0  # rank 0's R2 view of every rank's hit counts
+        # Warmup steps take the stripe positions right after the timed ones (steps .. steps+W-1), so every position
+        # used stays inside the 2^16 BIP320 variant space: (steps + W) * K * world <= 65536.
+        positions = ((args.steps + args.warmup + steps_per_group - 1) // steps_per_group + 1) * K if use_v \
+            else (args.steps + args.warmup) * K
+        if positions * world > 1 << 16:
+            raise SystemExit("bench.py: (steps + warmup) x variants x GPUs exceeds the 2^16 version-rolling space")
+        self.positions = positions
+        if use_v:  # variant tables for every step, timed and warmup, built and uploaded before the timed region
+            for i in range(args.steps + args.warmup):
+                v_group(i // steps_per_group)
+        for i in range(args.warmup):
+            step(args.steps + i, False)
+        sync()
+        self.barrier()
+        sync()
+        r2_seen.zero_()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, True)
+        step_hashes = K * (V_COUNT if use_v else 1 << 32)
+        total = comm.allreduce_counters(args.steps * step_hashes)[0] if world > 1 else args.steps * step_hashes  # R3
+        sync()
+        self.barrier()
+        sync()
+        t_local = time.perf_counter() - t0
+        elapsed = comm.allreduce_max(t_local)
+        sha_hps = total / elapsed
+        # per-rank rates + which ranks actually took part in the collectives (RCCL world check)
+        rows = comm.gather_counters([info.rank, args.steps * step_hashes, int(t_local * 1e6), int(r2_seen.item())])
+        ranks_seen = sorted(int(r[0]) for r in rows)
+        per_rank_hps = [r[1] / max(r[2] * 1e-6, 1e-9) for r in sorted(rows)]
 
-    # ------------------------------------------- BASELINE config 2 verbatim: one fixed midstate, full 2^32
-    single = {}
-    if args.single_midstate_headers > 0 and not cpu:
+        # Re-verify every hit of the timed region on the CPU (full 256-bit compare), de-duplicated by (variant, nonce).
+        found = verified = dups = outside = 0
+        seen: set = set()
+        for hdrs, buf, lo, cnt in hits_log:
+            host = buf.cpu().tolist()
+            n = min(host[0] & 0xFFFFFFFF, search.cap)
+            pairs = [(host[1 + 2 * i], host[2 + 2 * i]) for i in range(n)] if K > 1 else \
+                [(x, 0) for x in host[1 : 1 + n]]
+            for nonce, vi in pairs:
+                nonce &= 0xFFFFFFFF
+                found += 1
+                w = nonce if cpu or not use_v else int.from_bytes(nonce.to_bytes(4, "little"), "big")
+                outside += not lo <= w < lo + cnt  # a hit outside the window the step was asked to search
+                if not 0 <= vi < K:
+                    continue
+                hdr = hdrs[vi]
+                key = (hdr[:76], nonce)
+                if key in seen:
+                    dups += 1
+                    continue
+                seen.add(key)
+                h = hashlib.sha256(hashlib.sha256(hdr[:76] + nonce.to_bytes(4, "little")).digest()).digest()
+                if int.from_bytes(h, "little") <= target_int:
+                    verified += 1
+        found, verified, dups, outside = comm.allreduce_counters(found, verified, dups, outside)
+        expected, z = _poisson(verified, total, target_int)
+        self.R["sha"] = {
+            "hps": sha_hps, "elapsed": elapsed, "K": K, "V_COUNT": V_COUNT, "use_v": use_v,
+            "steps_per_group": steps_per_group, "step_hashes": step_hashes, "grid": search.grid,
+            "ranks_seen": ranks_seen, "per_rank_hps": per_rank_hps, "found": found, "verified": verified,
+            "dups": dups, "outside": outside, "expected": expected, "z": z,
+            "r2_hits": rows[0][3] if rows else 0,  # rank 0's R2 view of every rank's hit counts
+        }
+
+    def single(self) -> None:
+        """BASELINE config 2 verbatim: one fixed midstate, full 2^32 nonces per header."""
+        import torch
+
         from otedama_amd.ops.search import Sha256dSearch
 
-        ss = Sha256dSearch(dev)
-        heads = [N.variant_header(job, stripe.start + (positions + j) * stripe.stride)[0]
-                 for j in range(args.single_midstate_headers)]
+        N, job, stripe, comm, world = self.N, self.job, self.stripe, self.comm, self.info.world_size
+        target_int = int.from_bytes(job["target"], "little")
+        ss = Sha256dSearch(self.dev)
+        heads = [N.variant_header(job, stripe.start + (self.positions + j) * stripe.stride)[0]
+                 for j in range(self.args.single_midstate_headers)]
         params = [N.sha256d_prepare(h, job["target"]) for h in heads]
         ss.launch(params[0], 0, 1 << 24)  # warm the kernel
-        sync()
-        barrier(info)
-        sync()
+        self.sync()
+        self.barrier()
+        self.sync()
         souts = []
         t0 = time.perf_counter()
         for p in params:
             souts.append(ss.launch(p, 0, 1 << 32, out=torch.zeros_like(ss.out)).buf)
-        sync()
-        barrier(info)
-        sync()
+        self.sync()
+        self.barrier()
+        self.sync()
         s_el = comm.allreduce_max(time.perf_counter() - t0)
         s_total = len(params) * (1 << 32) * world
         s_found = s_ok = 0
@@ -415,40 +658,41 @@ def run_rank(args) -> int:
                 d = hashlib.sha256(hashlib.sha256(h[:76] + nonce.to_bytes(4, "little")).digest()).digest()
                 s_ok += int.from_bytes(d, "little") <= target_int
         s_found, s_ok, _, _ = comm.allreduce_counters(s_found, s_ok)
-        single = {"hashes_per_sec": s_total / s_el, "kernel": "otd_sha256d_search", "headers_per_rank": len(params),
-                  "nonces_per_header": 1 << 32, "grid": ss.grid, "hits_found": s_found, "hits_verified": s_ok,
-                  "hits_expected": _poisson(s_ok, s_total, target_int)[0]}
+        self.R["single"] = {"hashes_per_sec": s_total / s_el, "kernel": "otd_sha256d_search",
+                            "headers_per_rank": len(params), "nonces_per_header": 1 << 32, "grid": ss.grid,
+                            "hits_found": s_found, "hits_verified": s_ok,
+                            "hits_expected": _poisson(s_ok, s_total, target_int)[0]}
         del ss
 
-    # ---------------------------------------------------------------- scrypt
-    scrypt_hps = None
-    ssteps = args.steps if args.scrypt_steps < 0 else args.scrypt_steps
-    scrypt_info = {}
-    if ssteps > 0 and not cpu:
+    def scrypt(self) -> None:
+        import torch
+
         from otedama_amd.models.algorithms import ALGORITHMS
         from otedama_amd.models.header import int_to_hash
         from otedama_amd.ops.search import ScryptSearch
 
-        sc = ScryptSearch(dev, gap=args.scrypt_gap, kernel=args.scrypt_kernel)
+        args, N, comm, info = self.args, self.N, self.comm, self.info
+        world = info.world_size
+        ssteps = args.steps if args.scrypt_steps < 0 else args.scrypt_steps
+        sc = ScryptSearch(self.dev, gap=args.scrypt_gap, kernel=args.scrypt_kernel)
         s_int = ALGORITHMS["scrypt"].diff1
         starget = int_to_hash(s_int)
-        hdr, _, _, _ = N.variant_header(job, stripe.start)
+        hdr, _, _, _ = N.variant_header(self.job, self.stripe.start)
         sparams = N.scrypt_prepare(hdr, starget)
         sc.launch(sparams, 0)
-        sync()
-        barrier(info)
-        sync()
+        self.sync()
+        self.barrier()
+        self.sync()
         sbufs = []
         t0 = time.perf_counter()
         for i in range(ssteps):
             base = ((i * world + info.rank) * sc.batch) & 0xFFFFFFFF  # ranks partition the nonce range
             sbufs.append(sc.launch(sparams, base).buf.clone())
-        sync()
-        barrier(info)
-        sync()
+        self.sync()
+        self.barrier()
+        self.sync()
         selapsed = comm.allreduce_max(time.perf_counter() - t0)
         stotal = comm.allreduce_counters(ssteps * sc.batch)[0] if world > 1 else ssteps * sc.batch
-        scrypt_hps = stotal / selapsed
         # re-verify up to 64 hits per rank with hashlib.scrypt (CPU, ~1 ms each)
         sfound = sver = schecked = 0
         for buf in sbufs:
@@ -462,43 +706,44 @@ def run_rank(args) -> int:
                 d = hashlib.scrypt(h80, salt=h80, n=1024, r=1, p=1, dklen=32)
                 sver += int.from_bytes(d, "little") <= s_int
         sfound, sver, schecked, _ = comm.allreduce_counters(sfound, sver, schecked)
-        scrypt_info = {"kernel": sc.kernel, "lookup_gap": 1 if sc.kernel == "coop" else sc.gap, "lanes": sc.batch,
-                       "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2), "hits_found": sfound,
-                       "hits_checked": schecked, "hits_verified": sver,
-                       "hits_expected": _poisson(sfound, stotal, s_int)[0], "hit_target": "scrypt diff 1 (0xFFFF<<224)"}
+        self.R["scrypt_hps"] = self.R["scrypt_kernel_hps"] = stotal / selapsed
+        self.R["scrypt"] = {"kernel": sc.kernel, "lookup_gap": 1 if sc.kernel == "coop" else sc.gap,
+                            "lanes": sc.batch, "scratch_gib_per_gpu": round(sc.scratch_bytes / 2**30, 2),
+                            "hits_found": sfound, "hits_checked": schecked, "hits_verified": sver,
+                            "hits_expected": _poisson(sfound, stotal, s_int)[0],
+                            "hit_target": "scrypt diff 1 (0xFFFF<<224)", "kernel_path_hashes_per_sec": stotal / selapsed}
         del sc
         torch.cuda.empty_cache()
 
-    # ------------------------------------------------------------------ X11
-    # BASELINE config 4: X11 with the nonce range partitioned across ranks (rank r takes batches
-    # r, r + N, r + 2N, ...). Target 2^-20 so every step yields hits that are re-verified on the CPU.
-    x11_hps = None
-    x11_info = {}
-    xsteps = args.steps if args.x11_steps < 0 else args.x11_steps
-    if xsteps > 0 and not cpu:
+    def x11(self) -> None:
+        """BASELINE config 4: X11 with the nonce range partitioned across ranks (rank r takes batches r, r + N, ...).
+        Target 2^-20 so every step yields hits that are re-verified on the CPU."""
+        import torch
+
         from otedama_amd.models.header import int_to_hash
         from otedama_amd.ops.search import X11Search
 
-        xs = X11Search(dev, cap=4096)
+        args, N, comm, info = self.args, self.N, self.comm, self.info
+        world = info.world_size
+        xsteps = args.steps if args.x11_steps < 0 else args.x11_steps
+        xs = X11Search(self.dev, cap=4096)
         xtarget_int = (1 << 236) - 1
-        hdr, _, _, _ = N.variant_header(job, stripe.start)
+        hdr, _, _, _ = N.variant_header(self.job, self.stripe.start)
         xparams = N.x11_prepare(hdr, int_to_hash(xtarget_int))
         xs.launch(xparams, 0)
-        sync()
-        barrier(info)
-        sync()
+        self.sync()
+        self.barrier()
+        self.sync()
         xhits: list = []
         t0 = time.perf_counter()
         for i in range(xsteps):
             base = ((i * world + info.rank) * xs.batch) & 0xFFFFFFFF
-            r = xs.launch(xparams, base)
-            xhits.append(r.buf.clone())
-        sync()
-        barrier(info)
-        sync()
+            xhits.append(xs.launch(xparams, base).buf.clone())
+        self.sync()
+        self.barrier()
+        self.sync()
         xelapsed = comm.allreduce_max(time.perf_counter() - t0)
         xtotal = comm.allreduce_counters(xsteps * xs.batch)[0] if world > 1 else xsteps * xs.batch
-        x11_hps = xtotal / xelapsed
         xfound = xver = 0
         for buf in xhits:
             host = buf.cpu().tolist()
@@ -507,31 +752,34 @@ def run_rank(args) -> int:
                 h = N.x11(hdr[:76] + (nonce & 0xFFFFFFFF).to_bytes(4, "little"))
                 xver += int.from_bytes(h, "little") <= xtarget_int
         xfound, xver, _, _ = comm.allreduce_counters(xfound, xver)
-        x11_info = {"batch_per_launch": xs.batch, "kernels": "11 stage kernels per batch (tools/bench_x11.py)",
-                    "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20",
-                    "hits_expected": _poisson(xfound, xtotal, xtarget_int)[0]}
+        self.R["x11_hps"] = self.R["x11_kernel_hps"] = xtotal / xelapsed
+        self.R["x11"] = {"batch_per_launch": xs.batch, "kernels": "11 stage kernels per batch (tools/bench_x11.py)",
+                         "hits_found": xfound, "hits_verified": xver, "hit_target": "2^-20",
+                         "hits_expected": _poisson(xfound, xtotal, xtarget_int)[0],
+                         "kernel_path_hashes_per_sec": xtotal / xelapsed}
         del xs
         torch.cuda.empty_cache()
 
-    # ------------------------------------------------- scrypt and X11 through the production miner
-    # The kernel sections above time the ops-API launches one after another. The production miner runs scrypt as two
-    # half-grid batches side by side and X11 with a digest plane per slot, in a device process of its own; its exact
-    # rate over whole launches there, with every share re-verified, is the scrypt / X11 figure (the kernel-path rate
-    # stays beside it). In this torch process the same miner measured 16.2-16.4 MH/s against 17.2-17.5 in fresh
-    # processes, with no section of this script responsible (profiles/r4/h_bench_sections, i_bisect).
-    scrypt_kernel_hps, x11_kernel_hps = scrypt_hps, x11_hps
-    miner_s = args.miner_seconds if args.miner_seconds >= 0 else (0.0 if cpu else 8.0)
-    if miner_s > 0:
+    def miner(self) -> None:
+        """scrypt and X11 through the production miner. The kernel sections above time the ops-API launches one
+        after another. The production miner runs scrypt as two half-grid batches side by side and X11 with a digest
+        plane per slot, in a device process of its own; its exact rate over whole launches there, with every share
+        re-verified, is the scrypt / X11 figure (the kernel-path rate stays beside it). In this torch process the same
+        miner measured 16.2-16.4 MH/s against 17.2-17.5 in fresh processes (profiles/r4/h_bench_sections, i_bisect)."""
+        import torch
+
         from otedama_amd.engine.miner_probe import measure_miner
         from otedama_amd.models.algorithms import ALGORITHMS
 
+        comm, info = self.comm, self.info
+        miner_s = self.miner_seconds()
         for algo, tgt in (("scrypt", ALGORITHMS["scrypt"].diff1), ("x11", (1 << 236) - 1)):
-            if (algo == "scrypt" and ssteps <= 0) or (algo == "x11" and xsteps <= 0):
+            if algo not in self.R:  # its kernel section was skipped or failed
                 continue
-            barrier(info)
+            self.barrier()
             try:
-                r = measure_miner(N, dev.index or 0, algo, tgt, seconds=miner_s, rank=info.rank, world=world,
-                                  seed=args.seed, process=True)
+                r = measure_miner(self.N, self.dev.index or 0, algo, tgt, seconds=miner_s, rank=info.rank,
+                                  world=info.world_size, seed=self.args.seed, process=True)
                 err = ""
             except Exception as exc:  # noqa: BLE001 - auxiliary: the kernel-path figure stays
                 r, err = {"hashes_per_sec": 0.0, "shares": 0, "shares_rechecked": 0, "shares_recheck_ok": 0,
@@ -539,103 +787,118 @@ def run_rank(args) -> int:
             tot, shares_n, chk, chk_ok = comm.allreduce_counters(int(r["hashes_per_sec"]), r["shares"],
                                                                  r["shares_rechecked"], r["shares_recheck_ok"])
             faults = comm.allreduce_counters(int(bool(r.get("faulted")) or bool(err)))[0]
-            info_d = scrypt_info if algo == "scrypt" else x11_info
             miner = dict(r, node_hashes_per_sec=float(tot), node_shares=shares_n, node_shares_rechecked=chk,
                          node_shares_recheck_ok=chk_ok, ranks_faulted=faults, window_seconds=miner_s)
             if err:
                 miner["error"] = err
+            info_d = self.R[algo]
             info_d["miner"] = miner
             used = not faults and chk == chk_ok and tot > 0  # every re-hashed share held and no rank faulted
-            if used and algo == "scrypt":
-                scrypt_hps = float(tot)
-            elif used:
-                x11_hps = float(tot)
+            if used:
+                self.R[f"{algo}_hps"] = float(tot)
             info_d["rate_source"] = "production miner (see miner)" if used else "kernel path"
-        if scrypt_info:
-            scrypt_info["kernel_path_hashes_per_sec"] = scrypt_kernel_hps
-        if x11_info:
-            x11_info["kernel_path_hashes_per_sec"] = x11_kernel_hps
-        torch.cuda.empty_cache()
+        if not self.cpu:
+            torch.cuda.empty_cache()
 
-    # ------------------------------------------------------------ BASELINE config 1: the CPU miner
-    cpu_cfg = None
-    if args.cpu_seconds > 0 and info.is_primary:
+    def cpu_miner(self) -> None:
+        """BASELINE config 1: the native CPU miner, single thread and all cores of this box's CPU share."""
         from otedama_amd.cli.bench_cmd import bench_cpu, cpu_share
 
-        try:
-            cpu_cfg = bench_cpu(args.cpu_seconds, cpu_share(), single_seconds=args.cpu_seconds)
-        except Exception as exc:  # noqa: BLE001 - auxiliary: never fail the headline
-            cpu_cfg = {"error": f"{type(exc).__name__}: {exc}"}
+        self.R["cpu"] = bench_cpu(self.args.cpu_seconds, cpu_share(), single_seconds=self.args.cpu_seconds)
 
-    # ---------------------------------------------------------- share latency
-    # End-to-end share latency against the local pool in a separate process (default 2^29-nonce batches), then the
-    # job-switch time of the native miner for SHA-256d, scrypt and X11 (set_job -> first batch of the new work running).
-    latency = None
-    switch: dict = {}
-    startup = None
-    if not args.no_latency and info.is_primary and not cpu:
+    def latency(self) -> None:
+        """End-to-end share latency against the local pool in a separate process (2^32-nonce batches), then the
+        job-switch time of the device process for SHA-256d, scrypt and X11 (set_job -> new work running)."""
         from otedama_amd.engine.latency_probe import (measure_device_startup, measure_job_switch,
                                                       measure_share_latency)
 
+        idx = self.dev.index or 0
         try:
-            latency = measure_share_latency(device_index=dev.index or 0, seconds=6.0)
-        except Exception as exc:  # noqa: BLE001 - latency is auxiliary; never fail the headline
-            latency = {"error": f"{type(exc).__name__}: {exc}"}
+            self.R["latency"] = measure_share_latency(device_index=idx, seconds=6.0)
+        except Exception as exc:  # noqa: BLE001 - each probe is reported on its own
+            self.R["latency"] = {"error": f"{type(exc).__name__}: {exc}"}
+        switch = {}
         for algo in ("sha256d", "scrypt", "x11"):
             try:
-                switch[algo] = measure_job_switch(device_index=dev.index or 0, algorithm=algo)
+                switch[algo] = measure_job_switch(device_index=idx, algorithm=algo)
             except Exception as exc:  # noqa: BLE001
                 switch[algo] = {"error": f"{type(exc).__name__}: {exc}"}
+        self.R["switch"] = switch
         try:
-            startup = measure_device_startup(device_index=dev.index or 0)
+            self.R["startup"] = measure_device_startup(device_index=idx)
         except Exception as exc:  # noqa: BLE001
-            startup = {"error": f"{type(exc).__name__}: {exc}"}
+            self.R["startup"] = {"error": f"{type(exc).__name__}: {exc}"}
 
-    # ------------------------------------------------ the production node, and BASELINE config 5
-    # Both run after every other rank has finished its kernel sections (they exit after X11): `otedama node --gpus N`
-    # starts its own N ranks (RCCL) with a device process per GPU, and the pool section its own miners.
-    node_res = pool_res = None
-    node_s = args.node_seconds if args.node_seconds >= 0 else (0.0 if cpu else 10.0)
-    pool_s = args.pool_seconds if args.pool_seconds >= 0 else (0.0 if cpu else 12.0)
-    if info.is_primary and node_s > 0:
+    def node(self) -> None:
+        """The production node (`otedama node --gpus N`: supervisor, N RCCL ranks, a device process per GPU, rank 0
+        on the pool session), once per algorithm against a pool of that algorithm, with forced new blocks for the
+        node-wide job switch. Runs after every other rank has left its kernel sections."""
         from otedama_amd.parallel.node_probe import measure_node
 
-        try:
-            node_res = measure_node(world, seconds=node_s, warmup=args.node_warmup, cpu=cpu,
-                                    expected_per_gpu=8e6 if cpu else 19e9, shares_per_gpu=4.0 if cpu else 25.0)
-        except Exception as exc:  # noqa: BLE001
-            node_res = {"error": f"{type(exc).__name__}: {exc}"}
-    if info.is_primary and pool_s > 0:
+        algos = self.node_algorithms()
+        per_algo: dict = {}
+        self.R["node"] = {"algorithms": per_algo}
+        each = self.budgets["node"] / max(1, len(algos))
+        for algo in algos:
+            if self.guard.remaining() < 40.0 + self.node_seconds():
+                per_algo[algo] = {"skipped": f"bench deadline: {self.guard.remaining():.0f} s left"}
+                continue
+            try:
+                per_algo[algo] = measure_node(self.world, seconds=self.node_seconds(), warmup=self.args.node_warmup,
+                                              cpu=self.cpu, algorithm=algo, switches=self.args.node_switches,
+                                              startup_timeout=min(150.0, each - 20.0))
+            except Exception as exc:  # noqa: BLE001
+                per_algo[algo] = {"error": f"{type(exc).__name__}: {exc}"}
+        if "sha256d" in per_algo:  # the SHA-256d run is the node headline (its keys at the top of "node")
+            self.R["node"] = dict(per_algo["sha256d"], algorithms=per_algo)
+
+    def pool(self) -> None:
         from otedama_amd.pool.pool_probe import measure_pool
 
-        try:
-            pool_res = measure_pool(world, seconds=pool_s, cpu=cpu, difficulty=0.001 if cpu else 1.0)
-        except Exception as exc:  # noqa: BLE001
-            pool_res = {"error": f"{type(exc).__name__}: {exc}"}
+        self.R["pool"] = measure_pool(self.world, seconds=self.pool_seconds(), cpu=self.cpu,
+                                      difficulty=0.001 if self.cpu else 1.0)
 
-    if info.is_primary:
+    # ------------------------------------------------------------------ output
+    def output(self, errors: dict, fatal: str | None = None) -> dict:
+        args, R, cpu = self.args, dict(self.R), self.cpu
+        world = self.info.world_size if self.info is not None else self.world
+        backend = self.info.backend if self.info is not None else None
+        sha = R.get("sha")
+        g = self.guard
+        if sha is None:
+            out = error_output(args, world, fatal or "no headline", errors,
+                               g.diagnose() if g is not None and world > 1 or self.world > 1 else None)
+            out["preflight"] = R.get("preflight")
+            out["sections"] = g.sections if g is not None else None
+            out["summary"] = dict(out.pop("summary"), backend=backend, sections_s=self._section_times())
+            return out
+        K, V_COUNT, use_v = sha["K"], sha["V_COUNT"], sha["use_v"]
+        latency = R.get("latency") if isinstance(R.get("latency"), dict) else {}
+        switch = R.get("switch") or {}
+        node = R.get("node")
+        single = R.get("single") or {}
         out = {
             "metric": METRIC,
-            "value": sha_hps,
+            "value": sha["hps"],
             "unit": "hashes/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": sha["elapsed"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": sha_hps / BASELINE_HPS,
+            "vs_baseline": sha["hps"] / BASELINE_HPS,
             "dtype": "u32",
             "data": ("synthetic 80-byte block headers (random prev-hash/merkle root), share target = difficulty 1"
                      if not cpu else "CPU REHEARSAL (gloo + native CPU scanner, share target 2^-12): not a GPU "
                                      "measurement"),
             "config": {
                 "model": "sha256d",
-                "global_batch": step_hashes * world,
+                "global_batch": sha["step_hashes"] * world,
                 "seq_len": 80,
                 "parallelism": (f"dp{world} (nonce-space: per-rank variant stripe; "
-                                + (f"{K} variants x 2^{(V_COUNT).bit_length() - 1} nonces per step, {steps_per_group} "
-                                   "steps tile 2^32 per variant)" if use_v
+                                + (f"{K} variants x 2^{(V_COUNT).bit_length() - 1} nonces per step, "
+                                   f"{sha['steps_per_group']} steps tile 2^32 per variant)" if use_v
                                    else "full 2^32 nonces per variant per step)")),
                 "algorithm": ("SHA-256d nonce search, fixed midstate per variant; " + (
                     f"{K} BIP320 version variants per wave ({max(K // 64, 1)} per lane) share the block-2 message "
@@ -643,51 +906,106 @@ def run_rank(args) -> int:
                     f"{K} BIP320 version variants per launch share the block-2 message schedule")),
                 "sha_kernel": _sha_name(args, K, use_v),
                 "variants_per_step": K,
-                "grid": search.grid,
+                "grid": sha["grid"],
             },
             "world_size": world,
-            "dist_backend": info.backend,
-            "rccl_ranks_seen": ranks_seen,
-            "per_rank_hashes_per_sec": per_rank_hps,
+            "dist_backend": backend,
+            "rccl_ranks_seen": sha["ranks_seen"],
+            "per_rank_hashes_per_sec": sha["per_rank_hps"],
             "rehearsal": "cpu-gloo" if cpu else (
                 "gloo-shared-gpu" if os.environ.get("OTEDAMA_DIST_BACKEND") == "gloo" and world > 1 else None),
-            "sha256d_hashes_per_sec": sha_hps,
-            "sha256d_per_gpu_hashes_per_sec": sha_hps / world,
+            "preflight": R.get("preflight"),
+            "sha256d_hashes_per_sec": sha["hps"],
+            "sha256d_per_gpu_hashes_per_sec": sha["hps"] / world,
             "sha256d_single_midstate_hashes_per_sec": single.get("hashes_per_sec"),
             "sha256d_single_midstate": single,
-            "hits_found": found,
-            "hits_verified": verified,
-            "hits_duplicate": dups,
-            "hits_outside_window": outside,
-            "hits_expected": expected,
-            "hits_z": z,
+            "hits_found": sha["found"],
+            "hits_verified": sha["verified"],
+            "hits_duplicate": sha["dups"],
+            "hits_outside_window": sha["outside"],
+            "hits_expected": sha["expected"],
+            "hits_z": sha["z"],
             "hits_seed": args.seed,  # fixed synthetic headers: every run of this seed draws the same hits
-            "hits_r2_gathered": r2_hits,
-            "scrypt_hashes_per_sec": scrypt_hps,
-            "scrypt": scrypt_info,
-            "x11_hashes_per_sec": x11_hps,
-            "x11": x11_info,
-            "p50_share_latency_ms": (latency or {}).get("p50_ms") if isinstance(latency, dict) else None,
-            "device_hit_to_accept_p50_ms": (latency or {}).get("device_hit_to_accept_p50_ms"),
-            "device_hit_to_accept_p95_ms": (latency or {}).get("device_hit_to_accept_p95_ms"),
-            "share_latency": latency,
+            "hits_r2_gathered": sha["r2_hits"],
+            "scrypt_hashes_per_sec": R.get("scrypt_hps"),
+            "scrypt": R.get("scrypt") or {},
+            "x11_hashes_per_sec": R.get("x11_hps"),
+            "x11": R.get("x11") or {},
+            "p50_share_latency_ms": latency.get("p50_ms"),
+            "device_hit_to_accept_p50_ms": latency.get("device_hit_to_accept_p50_ms"),
+            "device_hit_to_accept_p95_ms": latency.get("device_hit_to_accept_p95_ms"),
+            "share_latency": R.get("latency"),
             "job_switch_ms": {a: v.get("p50_ms") for a, v in switch.items()} or None,
             "job_switch": switch or None,
-            "device_process_startup_s": (startup or {}).get("spawn_to_first_batch_s"),
-            "device_process_startup": startup,
+            "device_process_startup_s": (R.get("startup") or {}).get("spawn_to_first_batch_s"),
+            "device_process_startup": R.get("startup"),
             # the production node (otedama node: supervisor + N RCCL ranks + device processes + local pool)
-            "node_hashes_per_sec": (node_res or {}).get("total_hashes_per_sec"),
-            "node": node_res,
+            "node_hashes_per_sec": (node or {}).get("total_hashes_per_sec"),
+            "node": node,
             # BASELINE config 1 (reference: ~2.5 MH/s single thread, ~75 MH/s whole 7950X; BENCHMARKS.md:25-28,44-49)
-            "cpu_single_thread_hashes_per_sec": (cpu_cfg or {}).get("sha256d_single_thread_hps"),
-            "cpu_all_cores_hashes_per_sec": (cpu_cfg or {}).get("sha256d_all_threads_hps"),
-            "cpu": cpu_cfg,
-            # BASELINE config 5: mixed SHA-256d + scrypt pool with vardiff
-            "pool": pool_res,
+            "cpu_single_thread_hashes_per_sec": (R.get("cpu") or {}).get("sha256d_single_thread_hps"),
+            "cpu_all_cores_hashes_per_sec": (R.get("cpu") or {}).get("sha256d_all_threads_hps"),
+            "cpu": R.get("cpu"),
+            # BASELINE config 5: mixed SHA-256d + scrypt pool with vardiff, windowed in steady state
+            "pool": R.get("pool"),
+            "sections": g.sections if g is not None else None,
+            "errors": errors or None,
         }
-        print(json.dumps(out), flush=True)
-    shutdown(info)
-    return 0
+        out["summary"] = self.summary(out, errors)  # LAST: the driver keeps only the tail of stdout
+        return out
+
+    def _section_times(self) -> dict:
+        g = self.guard
+        return {k: v.get("s") for k, v in (g.sections if g is not None else {}).items()}
+
+    def summary(self, out: dict, errors: dict) -> dict:
+        node = out.get("node") or {}
+        pool = (out.get("pool") or {}).get("algorithms") or {}
+        lat = out.get("share_latency") or {}
+        cpu = out.get("cpu") or {}
+        nalg = node.get("algorithms") or {}
+        js = node.get("job_switch") or {}
+        return {
+            "sha256d_hps": _r(out["value"]),
+            "sha256d_single_midstate_hps": _r(out.get("sha256d_single_midstate_hashes_per_sec")),
+            "scrypt_hps": _r(out.get("scrypt_hashes_per_sec")),
+            "x11_hps": _r(out.get("x11_hashes_per_sec")),
+            "node_hps": _r(node.get("total_hashes_per_sec")),
+            "node_hps_by_algorithm": {a: _r(v.get("total_hashes_per_sec")) for a, v in nalg.items()} or None,
+            "node_rejected_by_algorithm": {a: v.get("pool_rejected") for a, v in nalg.items()} or None,
+            "node_remote_hit_to_accept_p50_ms": _r((node.get("hit_to_accept_remote") or {}).get("p50_ms")),
+            "node_job_switch_worst_rank_p50_ms": _r(js.get("worst_rank_p50_ms")),
+            "node_job_switch_worst_rank_max_ms": _r(js.get("worst_rank_max_ms")),
+            "node_job_switch_stale_rejects": js.get("stale_rejects"),
+            "share_latency_p50_ms": _r(lat.get("p50_ms")),
+            "device_hit_to_accept_p50_ms": _r(lat.get("device_hit_to_accept_p50_ms")),
+            "job_switch_p50_ms": {a: _r(v) for a, v in (out.get("job_switch_ms") or {}).items()} or None,
+            "cpu_1t_hps": _r(cpu.get("sha256d_single_thread_hps")),
+            "cpu_all_hps": _r(cpu.get("sha256d_all_threads_hps")),
+            "pool_validated_per_s": {a: _r(v.get("validated_shares_per_sec")) for a, v in pool.items()} or None,
+            "pool_validate_p50_ms": {a: _r((v.get("validate_ms") or {}).get("p50")) for a, v in pool.items()} or None,
+            "pool_validations": {a: (v.get("validate_ms") or {}).get("samples") for a, v in pool.items()} or None,
+            "world_size": out["world_size"],
+            "backend": out["dist_backend"],
+            "rccl_ranks_seen": out["rccl_ranks_seen"],
+            "sections_s": self._section_times(),
+            "errors": errors or None,
+        }
+
+
+def run_rank(args) -> int:
+    from otedama_amd.parallel.guard import RankGuard, run_dir_for
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    run_dir = run_dir_for()
+    if world > 1:  # RCCL warnings into the run directory, where an error JSON reads them back
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
+        os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(run_dir, "rccl.%h.%p.log"))
+    bench = Bench(args, rank, world)
+    bench.guard = RankGuard(rank, world, args.deadline, emit=bench.emit if rank == 0 else None, run_dir=run_dir)
+    bench.guard.start(tee_stderr=world > 1)
+    return bench.run()
 
 
 if __name__ == "__main__":

@@ -133,6 +133,7 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["job_switches"] = s.job_switches;
   d["last_job_switch_ms"] = s.last_job_switch_ms;
   d["job_switch_ms"] = s.job_switch_ms;
+  d["work_started"] = s.work_started;
   d["ring_overflow"] = s.ring_overflow;
   d["verify_dropped"] = s.verify_dropped;
   d["verify_queue_peak"] = s.verify_queue_peak;

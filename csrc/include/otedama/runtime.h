@@ -87,6 +87,9 @@ struct MinerStats {
   uint64_t job_switches = 0;
   double last_job_switch_ms = 0;
   std::vector<double> job_switch_ms;  // most recent samples (<= 64)
+  // (control-plane epoch, CLOCK_MONOTONIC seconds) at which the first batch of each new work started running on the
+  // device (CPU: the first chunk claimed), most recent <= 64: a node correlates them with the pool's new-block time.
+  std::vector<std::pair<uint64_t, double>> work_started;
   uint64_t aborted_launches = 0;      // batches stopped early by the device abort word
   uint64_t ring_hits = 0;             // hits consumed from the host-coherent ring while their launch was running
   // Candidates lost on the way to the share queue, each counted (the reference counts every dropped share,

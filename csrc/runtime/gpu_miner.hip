@@ -772,6 +772,8 @@ void GpuMiner::loop() {
         stats_.last_job_switch_ms = ms;
         stats_.job_switch_ms.push_back(ms);
         if (stats_.job_switch_ms.size() > 64) stats_.job_switch_ms.erase(stats_.job_switch_ms.begin());
+        stats_.work_started.emplace_back(job ? job->epoch : 0, switch_t0 + ms * 1e-3);
+        if (stats_.work_started.size() > 64) stats_.work_started.erase(stats_.work_started.begin());
         break;
       }
     }

@@ -614,6 +614,7 @@ void CpuMiner::loop(int /*tid*/) {
     const bool sha = job->algo == Algo::kSha256d;
     const uint64_t kChunk = sha ? (1ull << 16) : 256;
     uint64_t claim;
+    double fresh_at = 0;  // this thread opened a new work generation: when its first chunk was claimed
 #ifdef OTEDAMA_STRESS_HOOKS
     // tools/sanitize: widen the snapshot -> claim window so job switches land inside it.
     std::this_thread::sleep_for(std::chrono::microseconds(std::hash<std::thread::id>{}(
@@ -626,7 +627,7 @@ void CpuMiner::loop(int /*tid*/) {
       // old work already searched and emit duplicate shares.
       const uint64_t cg = cursor_gen_.load();
       if (gen < cg) continue;
-      if (gen > cg) { cursor_gen_.store(gen); cursor_.store(0); }
+      if (gen > cg) { cursor_gen_.store(gen); cursor_.store(0); fresh_at = monotonic_seconds(); }
       claim = cursor_.fetch_add(kChunk);
     }
     // claim indexes (variant-stripe slot k, nonce chunk)
@@ -683,6 +684,10 @@ void CpuMiner::loop(int /*tid*/) {
       queue_.push(std::move(s));
     }
     std::lock_guard<std::mutex> g(stats_mu_);
+    if (fresh_at > 0) {
+      stats_.work_started.emplace_back(job->epoch, fresh_at);
+      if (stats_.work_started.size() > 64) stats_.work_started.erase(stats_.work_started.begin());
+    }
     if (stats_.variant_epoch != job->epoch) { stats_.variant_epoch = job->epoch; stats_.variant_next = 0; }
     if (v + job->variant_stride > stats_.variant_next) stats_.variant_next = v + job->variant_stride;
     stats_.hashes += kChunk;

@@ -152,6 +152,10 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
             loop.add_signal_handler(sig, stop.set)
         except (NotImplementedError, RuntimeError):
             pass
+    try:  # SIGUSR1: a new network block now, on every algorithm (operators and probes test stale-work handling)
+        loop.add_signal_handler(signal.SIGUSR1, lambda: [p.new_block() for p in pools])
+    except (NotImplementedError, RuntimeError, AttributeError):
+        pass
     if fs["duration"] > 0:
         loop.call_later(fs["duration"], stop.set)
     await stop.wait()

@@ -417,7 +417,17 @@ class Engine:
                 "follower_pending": {f"rank{r}": int(hb.get("pending", 0)) for r, hb in hbs.items()},
                 "ops": link.ops_run, "reforms": link.reforms, "lost_ranks": list(ms.lost_ranks),
                 "leader_incarnation": ms.incarnation, "remote_stale": ms.remote_stale,
-                "op_p50_ms": link.tick_quantile(0.5) * 1e3, "op_p99_ms": link.tick_quantile(0.99) * 1e3})
+                "op_p50_ms": link.tick_quantile(0.5) * 1e3, "op_p99_ms": link.tick_quantile(0.99) * 1e3,
+                "job_set_at": list(ms.job_set_at), "job_bcast_at": list(ms.job_bcast_at)})
+        # (epoch, CLOCK_MONOTONIC) of each new work's first batch running: rank 0's devices and every follower's
+        # heartbeat (the node job-switch probe, parallel/node_probe.py)
+        local = getattr(ms, "local", ms)
+        ws = {"rank0": sorted(tuple(x) for st in (local.device_stats().values() if local is not None else [])
+                              for x in (st.get("work_started") or []))[-32:]}
+        if link is not None:
+            for r, hb in hbs.items():
+                ws[f"rank{r}"] = [tuple(x) for x in hb.get("ws", [])]
+        rep["work_started"] = ws
         return rep
 
     async def _report_loop(self, path: str, period: float = 0.5) -> None:

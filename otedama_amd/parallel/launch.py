@@ -74,26 +74,54 @@ def _stop_all(procs: list[subprocess.Popen], grace: float = 10.0) -> None:
 
 
 def run_ranks(cmd: Sequence[str], world: int, port: int | None = None, env: dict | None = None,
-              stdout_rank0_only: bool = True, poll: float = 0.1, **extra: str) -> int:
+              stdout_rank0_only: bool = True, poll: float = 0.1, deadline: float | None = None,
+              on_rank0_line=None, **extra: str) -> int:
     """Run ``cmd`` as ``world`` ranks and wait. The first rank to fail stops the others; returns its exit code
-    (0 when every rank succeeded). Only rank 0's stdout is kept when ``stdout_rank0_only`` (one JSON line)."""
+    (0 when every rank succeeded). Only rank 0's stdout is kept when ``stdout_rank0_only`` (one JSON line).
+
+    ``deadline`` (seconds): past it every rank gets SIGTERM, then SIGKILL after a grace period, and the return code
+    is 124 (timeout(1)'s). ``on_rank0_line(line)``: rank 0's stdout is read through this process (and still
+    forwarded to ours) so the caller can tell whether rank 0 reported before it ended."""
+    import threading
+
     port = port or free_port()
     procs: list[subprocess.Popen] = []
     prev = {}
+    readers: list[threading.Thread] = []
 
     def forward(sig, _frame):  # the driver's timeout / Ctrl-C reaches every rank
         _stop_all(procs, grace=5.0)
         sys.exit(128 + sig)
+
+    def pump(stream) -> None:
+        for raw in iter(stream.readline, b""):
+            try:
+                sys.stdout.buffer.write(raw)
+                sys.stdout.flush()
+            except (OSError, ValueError):
+                pass
+            try:
+                on_rank0_line(raw.decode("utf-8", "replace"))
+            except Exception:  # noqa: BLE001 - observing must never break forwarding
+                pass
+        stream.close()
 
     for sig in (signal.SIGTERM, signal.SIGINT):
         try:
             prev[sig] = signal.signal(sig, forward)
         except ValueError:  # not the main thread
             pass
+    end = time.monotonic() + deadline if deadline else None
     try:
         for r in range(world):
             out = None if (r == 0 or not stdout_rank0_only) else subprocess.DEVNULL
+            if r == 0 and on_rank0_line is not None:
+                out = subprocess.PIPE
             procs.append(subprocess.Popen(list(cmd), env=rank_env(r, world, port, env, **extra), stdout=out))
+            if out is subprocess.PIPE:
+                th = threading.Thread(target=pump, args=(procs[-1].stdout,), daemon=True)
+                th.start()
+                readers.append(th)
         while True:
             codes = [p.poll() for p in procs]
             bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
@@ -104,9 +132,16 @@ def run_ranks(cmd: Sequence[str], world: int, port: int | None = None, env: dict
                 return c if c > 0 else 128 - c
             if all(c == 0 for c in codes):
                 return 0
+            if end is not None and time.monotonic() > end:
+                print(f"launch: ranks still running after the {deadline:.0f} s deadline; stopping them",
+                      file=sys.stderr)
+                _stop_all(procs)
+                return 124
             time.sleep(poll)
     finally:
         _stop_all(procs, grace=5.0)
+        for th in readers:
+            th.join(timeout=5)
         for sig, h in prev.items():
             signal.signal(sig, h)
 

@@ -212,6 +212,8 @@ class _Heartbeat:
                 # device-timeline completion time of the counted hashes (one GPU per rank): exact rate windows
                 "done": st[0].get("hashes_done_at_s", 0.0) if len(st) == 1 else 0.0,
                 "coll": self.comm.collectives if self.comm is not None else 0,
+                # (epoch, CLOCK_MONOTONIC) of the latest new work's first batch running on this rank's device(s)
+                "ws": sorted(tuple(x) for s in st for x in (s.get("work_started") or []))[-8:],
                 "gen": self.comm.info.generation if self.comm is not None else 0,
                 "pid": os.getpid(), **self.extra}
 
@@ -342,6 +344,10 @@ class NodeMinerSet:
         self._remote_idle: dict[int, int] = {}
         self.lost_ranks: list[int] = []
         self._hb = _Heartbeat(self.store, comm.info.orig_rank, local, comm) if self.store is not None else None
+        # node-wide job switch accounting (CLOCK_MONOTONIC): when the engine handed rank 0 each new job, and when the
+        # R1 broadcast carrying it completed on rank 0
+        self.job_set_at: collections.deque = collections.deque(maxlen=64)
+        self.job_bcast_at: collections.deque = collections.deque(maxlen=64)
 
     # MinerSet API ------------------------------------------------------------
     @property
@@ -403,6 +409,7 @@ class NodeMinerSet:
                 self._work_key = _work_key(template)
             ep = self.local.set_job(self._with_base(self._template))
             self._epoch = ep
+            self.job_set_at.append((ep, time.monotonic()))
             if template is not None:
                 self._jobs[ep] = {"job_id": template.get("job_id", ""), "channel_id": template.get("channel_id", 0),
                                   "extranonce2_size": int(template.get("extranonce2_size", 0) or 0)}
@@ -729,6 +736,8 @@ class NodeMinerSet:
                         self._post({"op": "job"})
                         self.link.run_op({"op": "job"}, blob, [])
                         self._sent_seq = seq
+                        job = (blob or {}).get("job") or {}
+                        self.job_bcast_at.append((int(job.get("epoch", 0) or 0), time.monotonic()))
                     if info.world_size > 1 and self._gather_wanted:
                         self._gather_wanted = False
                         self._post({"op": "gather"})

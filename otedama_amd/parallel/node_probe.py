@@ -102,21 +102,76 @@ def process_rss(sup_pid: int) -> dict:
     return out
 
 
+# Expected per-GPU (per-rank CPU thread in the rehearsal) rates: the pinned share difficulty gives ~shares_per_gpu
+# accepted shares per second per rank at these rates (MI355X: BASELINE.md; CPU: one native miner thread).
+EXPECTED_RATE = {"gpu": {"sha256d": 19e9, "x11": 3.9e8, "scrypt": 1.7e7},
+                 "cpu": {"sha256d": 8e6, "x11": 4e3, "scrypt": 1.2e4}}
+HASHES_PER_DIFF1 = {"sha256d": 2.0 ** 32, "x11": 2.0 ** 32, "scrypt": 2.0 ** 16}  # scrypt diff1 = 0xFFFF << 224
+
+
+def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks: int,
+                     job_set_at: list | None = None, window: float = 2.0) -> dict:
+    """Node-wide job switch from the pool's forced new blocks: for each block sent at t_b (CLOCK_MONOTONIC, which
+    every process of the host shares) and each rank, the first (epoch, t) in that rank's work-start record with
+    t_b < t <= t_b + window is the moment the rank's device was running the new block's work. Reported per rank and
+    for the worst rank: p50 / max in ms, and how many block x rank pairs never showed a start (``missing``)."""
+    per_rank: dict[str, list[float]] = {f"rank{r}": [] for r in range(ranks)}
+    missing = 0
+    worst_each: list[float] = []
+    leader_each: list[float] = []
+    for tb in block_at:
+        worst = None
+        for r in range(ranks):
+            ts = sorted(t for _e, t in (work_started.get(f"rank{r}") or []) if tb < t <= tb + window)
+            if not ts:
+                missing += 1
+                continue
+            ms = (ts[0] - tb) * 1e3
+            per_rank[f"rank{r}"].append(ms)
+            worst = ms if worst is None else max(worst, ms)
+        if worst is not None:
+            worst_each.append(worst)
+        sets = sorted(t for _e, t in (job_set_at or []) if tb < t <= tb + window)
+        if sets:
+            leader_each.append((sets[0] - tb) * 1e3)
+
+    def med(xs):
+        xs = sorted(xs)
+        return xs[len(xs) // 2] if xs else None
+
+    rows = {r: {"p50_ms": med(v), "max_ms": max(v) if v else None, "samples": len(v)} for r, v in per_rank.items()}
+    p50s = [v["p50_ms"] for v in rows.values() if v["p50_ms"] is not None]
+    maxs = [v["max_ms"] for v in rows.values() if v["max_ms"] is not None]
+    return {"blocks": len(block_at), "per_rank": rows,
+            "worst_rank_p50_ms": max(p50s) if p50s else None, "worst_rank_max_ms": max(maxs) if maxs else None,
+            "node_p50_ms": med(worst_each), "missing": missing,
+            "pool_to_leader_p50_ms": med(leader_each),
+            "definition": ("pool's new block (forced SetNewPrevHash, CLOCK_MONOTONIC at send) -> each rank's device "
+                           "process running the first batch of the new work; node_p50 = median over blocks of the "
+                           "slowest rank")}
+
+
 def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_per_gpu: float = 25.0,
-                 expected_per_gpu: float = 19e9, startup_timeout: float = 150.0, cpu: bool = False,
-                 log_path: str | None = None) -> dict:
-    """Run ``otedama node --gpus N`` against a pinned-difficulty pool for ``warmup`` + ``seconds`` and measure it.
-    ``cpu``: a CPU rehearsal (gloo ranks, one CPU miner thread per rank) of the same processes."""
-    hashes_per_diff1 = 2.0 ** 32
-    diff = expected_per_gpu / (shares_per_gpu * hashes_per_diff1)
+                 expected_per_gpu: float | None = None, startup_timeout: float = 150.0, cpu: bool = False,
+                 log_path: str | None = None, algorithm: str = "sha256d", switches: int = 0,
+                 switch_interval: float | None = None) -> dict:
+    """Run ``otedama node --gpus N`` mining ``algorithm`` against a pinned-difficulty pool for ``warmup`` + ``seconds``
+    and measure it; then force ``switches`` new blocks at the pool (SIGUSR1) and time how fast each rank's device
+    runs the new work (``job_switch``). ``cpu``: a CPU rehearsal (gloo ranks, one CPU miner thread per rank) of the
+    same processes."""
+    kind = "cpu" if cpu else "gpu"
+    if expected_per_gpu is None:
+        expected_per_gpu = EXPECTED_RATE[kind][algorithm]
+        shares_per_gpu = 4.0 if cpu else shares_per_gpu
+    diff = expected_per_gpu / (shares_per_gpu * HASHES_PER_DIFF1[algorithm])
     tmp = tempfile.mkdtemp(prefix="otedama-node-")
     report = os.path.join(tmp, "report.json")
     log_path = log_path or os.path.join(tmp, "node.log")
-    pool, addr = spawn_pool("sha256d", diff, fixed=True)
+    pool, addr = spawn_pool(algorithm, diff, fixed=True)
     cfg = os.path.join(tmp, "config.yaml")
     with open(cfg, "w") as f:
         f.write(f"bitcoin_address: {PROBE_ADDR}\npools:\n  - url: stratum+v2://{addr}\n"
-                + ("mining:\n  cpu_threads: 1\n" if cpu else ""))
+                f"mining:\n  algorithm: {algorithm}\n" + ("  cpu_threads: 1\n" if cpu else ""))
     env = {k: v for k, v in os.environ.items() if k not in _DROP_ENV}
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     env["OTEDAMA_NODE_REPORT"] = report
@@ -127,9 +182,11 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
     out = open(log_path, "w")
     sup = subprocess.Popen([sys.executable, "-m", "otedama_amd", "node", "--gpus", str(gpus), "--config", cfg,
                             "--no-tui"], env=env, cwd=ROOT, stdout=out, stderr=subprocess.STDOUT)
-    res: dict = {"n_ranks": gpus, "share_difficulty_requested": diff, "recorded_seconds": seconds,
-                 "warmup_seconds": warmup, "log": log_path}
+    res: dict = {"algorithm": algorithm, "n_ranks": gpus, "share_difficulty_requested": diff,
+                 "recorded_seconds": seconds, "warmup_seconds": warmup, "log": log_path}
     rep: dict = {}
+    forced: list[float] = []
+    pst: dict = {}
     try:
         # ready: every rank of the node is a member and has counted hashes on its device timeline
         end = time.monotonic() + startup_timeout
@@ -154,6 +211,19 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
             time.sleep(0.1)
         rep = _read(report)
         res["rss_mib"] = process_rss(sup.pid)
+        # node-wide job switch: new blocks forced at the pool, spaced so every rank's heartbeat (2 Hz, the last 8
+        # starts) carries each one
+        gap = switch_interval or (1.5 if algorithm == "scrypt" else 1.0)
+        rej0 = int(rep.get("rejected", 0) or 0)
+        for _ in range(max(0, switches)):
+            pool.send_signal(signal.SIGUSR1)
+            forced.append(time.monotonic())
+            time.sleep(gap)
+        if switches > 0:
+            time.sleep(1.2)  # the last start reaches the report through a heartbeat and a report tick
+            rep_sw = _read(report)
+            res["_switch_report"] = rep_sw
+            res["_rej_during_switches"] = int(rep_sw.get("rejected", 0) or 0) - rej0
     finally:
         sup.send_signal(signal.SIGTERM)
         try:
@@ -196,4 +266,14 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
                        "own device process, rank 0 holding the SV2 session) against otedama pool (separate process, "
                        "pinned difficulty); rates and latencies over the recorded window after the warm-up"),
     })
+    rep_sw = res.pop("_switch_report", None)
+    rej_sw = res.pop("_rej_during_switches", None)
+    if rep_sw is not None:
+        # the pool's own send times of the forced blocks (its first block is the one the node started on)
+        sent = [t for t in pst.get("new_block_at", []) if t >= (forced[0] - 0.5 if forced else 0)]
+        js = job_switch_stats(sent or forced, rep_sw.get("work_started", {}), gpus, rep_sw.get("job_set_at"))
+        stale = (pst.get("reject_reasons") or {}).get("stale-job", 0)
+        js.update({"forced_blocks": len(forced), "stale_rejects": stale, "engine_rejects_during_switches": rej_sw,
+                   "interval_s": switch_interval or (1.5 if algorithm == "scrypt" else 1.0)})
+        res["job_switch"] = js
     return res

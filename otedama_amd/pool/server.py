@@ -181,6 +181,9 @@ class PoolServer:
         self.reject_reasons: dict[str, int] = {}
         self.started_at = time.monotonic()
         self._validate_ms: deque = deque(maxlen=8192)  # submit received -> verdict, per share
+        # CLOCK_MONOTONIC time each new block's clean job was handed to every connection (a node's job-switch probe
+        # times each rank's device from here: parallel/node_probe.py)
+        self.new_block_at: deque = deque(maxlen=256)
         self._init_metrics(registry)
 
     # ------------------------------------------------------------ metrics
@@ -260,6 +263,7 @@ class PoolServer:
         self.jobs.clear()
         self._seen.clear()
         job = self._make_job(clean=True)
+        self.new_block_at.append(time.monotonic())
         self.log("info", f"pool[{self.algo.name}]: new block height={self.block.height}")
         return job
 
@@ -467,6 +471,7 @@ class PoolServer:
             "validate_ms": {"p50": self.validation_ms(0.5), "p95": self.validation_ms(0.95),
                             "p99": self.validation_ms(0.99), "samples": len(self._validate_ms)},
             "fixed_difficulty": self.opts.fixed_difficulty,
+            "new_block_at": list(self.new_block_at)[-64:],
             # per live connection: the difficulty in force, how often vardiff moved it, and when it last moved
             # (seconds after the channel opened: the time vardiff took to reach the difficulty it holds)
             "workers": [{"name": w.name, "difficulty": w.vd.difficulty, "accepted": w.accepted,

@@ -1,0 +1,186 @@
+"""bench.py always reports: a stuck rank, a stuck section or a dead rank 0 must still
+end in one well-formed JSON line inside the deadline, never in a silent timeout.
+
+The CPU rehearsal (gloo + the native CPU scanner) runs the real launcher, rank guard and sections; the fault hook
+OTEDAMA_BENCH_FAULT=stuck:<rank>:<section> hangs one rank at the start of one section (parallel/guard.py).
+Reference rule: nothing in the engine waits without a deadline (internal/engine/run.go:1251).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**extra):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "OTEDAMA_BENCH_FAULT"):
+        e.pop(k, None)
+    e.update(extra)
+    return e
+
+
+def _bench(*args, env=None, timeout=240):
+    t0 = time.monotonic()
+    res = subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout,
+                         env=_env(**(env or {})), cwd=ROOT)
+    return res, time.monotonic() - t0
+
+
+def _json(res) -> dict:
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (res.stdout[-3000:], res.stderr[-3000:])
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(300)
+def test_world8_stuck_rank_in_preflight_prints_an_error_json():
+    """A rank that never reaches the rendezvous: rank 0 reports at the pre-flight deadline with every rank's phase
+    and stderr tail, stops the others, and exits non-zero."""
+    res, took = _bench("--gpus", "8", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
+                       "--preflight-timeout", "25", env={"OTEDAMA_BENCH_FAULT": "stuck:3:preflight"}, timeout=200)
+    assert res.returncode != 0
+    d = _json(res)
+    assert d["value"] is None and d["n_gpus"] == 8
+    assert "preflight" in d["error"] or "preflight" in json.dumps(d["errors"])
+    diag = d["diagnosis"]
+    assert diag["world_size"] == 8 and set(diag["ranks_checked_in"]) == set(range(8))
+    assert diag["ranks"]["3"]["phase"] == "section:preflight"  # never got past the start of the pre-flight
+    assert all(diag["ranks"][str(r)]["phase"] in ("rendezvous", "first-collective", "exit:stopped by rank 0")
+               or diag["ranks"][str(r)]["phase"].startswith("exit") for r in (1, 2, 4, 5, 6, 7))
+    assert d["summary"]["error"] == d["error"] and list(d)[-1] == "summary"
+    assert took < 120, took
+
+
+@pytest.mark.timeout(300)
+def test_stuck_node_section_keeps_the_full_json():
+    """Rank 0 hangs in the node section: the section records its timeout and every earlier result is printed."""
+    res, took = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0.3",
+                       "--node-seconds", "3", "--section-timeouts", "node=12",
+                       env={"OTEDAMA_BENCH_FAULT": "stuck:0:node"}, timeout=200)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d["value"] > 0 and d["n_gpus"] == 2 and d["rccl_ranks_seen"] == [0, 1]
+    assert d["errors"]["node"] == "timeout after 12 s"
+    assert d["sections"]["node"]["status"] == "timeout" and d["sections"]["cpu"]["status"] == "ok"
+    assert d["cpu_single_thread_hashes_per_sec"] > 0
+    s = d["summary"]
+    assert list(d)[-1] == "summary" and s["errors"]["node"] == "timeout after 12 s" and s["sha256d_hps"] > 0
+    assert took < 100, took
+
+
+@pytest.mark.timeout(300)
+def test_dead_rank0_still_gets_a_json_from_the_launcher():
+    """Rank 0 dies before it can print: the launcher prints the error JSON with the ranks' diagnosis."""
+    res, _ = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", "--cpu-rehearsal", "--cpu-seconds", "0",
+                    env={"OTEDAMA_BENCH_FAULT": "exit:0:sha256d"}, timeout=200)
+    assert res.returncode != 0
+    d = _json(res)
+    assert d["value"] is None and "rank 0 printed no result" in d["error"]
+    assert d["diagnosis"]["ranks_checked_in"] == [0, 1]
+
+
+@pytest.mark.timeout(300)
+def test_torchrun_stuck_follower_in_the_headline():
+    """The driver's torchrun command line with a follower stuck in the headline section: rank 0 (blocked in a
+    collective with it) reports at the section deadline, and torchrun's job ends instead of hanging."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    t0 = time.monotonic()
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2",
+                          "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
+                          "--section-timeouts", "sha256d=15"],
+                         capture_output=True, text=True, timeout=240, env=_env(OTEDAMA_BENCH_FAULT="stuck:1:sha256d"),
+                         cwd=ROOT)
+    took = time.monotonic() - t0
+    d = _json(res)
+    assert d["value"] is None and "sha256d" in json.dumps(d["errors"])
+    assert d["diagnosis"]["ranks"]["1"]["phase"] == "section:sha256d"
+    assert took < 120, took
+
+
+def test_run_ranks_deadline_stops_hung_ranks():
+    from otedama_amd.parallel.launch import run_ranks
+
+    t0 = time.monotonic()
+    rc = run_ranks([sys.executable, "-c", "import time; time.sleep(120)"], 2, deadline=2.0)
+    assert rc == 124 and time.monotonic() - t0 < 30
+
+
+def test_run_ranks_forwards_rank0_lines():
+    from otedama_amd.parallel.launch import run_ranks
+
+    seen = []
+    rc = run_ranks([sys.executable, "-c", "import os; print('{\"metric\": %s}' % os.environ['RANK'])"], 2,
+                   on_rank0_line=seen.append)
+    assert rc == 0 and seen == ['{"metric": 0}\n']
+
+
+# ------------------------------------------------------------------ unit level
+def test_fault_spec_parsing():
+    from otedama_amd.parallel.guard import fault_for
+
+    env = {"OTEDAMA_BENCH_FAULT": "stuck:3:preflight, exit:0:node,bogus,stuck:x:y"}
+    assert fault_for(3, "preflight", env) == "stuck"
+    assert fault_for(0, "node", env) == "exit"
+    assert fault_for(1, "preflight", env) is None and fault_for(3, "node", env) is None
+
+
+def test_guard_section_timeout_emits_once(tmp_path):
+    """In-process: a section that overruns calls emit with the section's error (the exit is stubbed out)."""
+    from otedama_amd.parallel import guard as G
+
+    calls = []
+
+    class Stop(Exception):
+        pass
+
+    g = G.RankGuard(0, 1, deadline_s=60, emit=lambda errors, reason: calls.append((errors, reason)) or 0,
+                    run_dir=str(tmp_path), poll_s=0.05)
+    left = []
+    g._leave = lambda code, why: left.append(code)
+    g.stop_children = lambda grace=5.0: None
+    g.start()
+    with g.section("fast", 5):
+        pass
+    with g.section("slow", 0.2):
+        time.sleep(1.0)
+    assert len(calls) == 1 and calls[0][0]["slow"] == "timeout after 0 s" and left == [0]
+    assert g.sections["fast"]["status"] == "ok" and g.sections["slow"]["status"] == "timeout"
+    assert g.finish() is False  # fired first: the main thread must not print a second line
+
+
+def test_guard_records_section_errors_and_finish_blocks_firing(tmp_path):
+    from otedama_amd.parallel import guard as G
+
+    g = G.RankGuard(0, 1, deadline_s=60, emit=lambda e, r: 0, run_dir=str(tmp_path), poll_s=0.05)
+    with g.section("broken", 5):
+        raise ValueError("boom")
+    assert g.errors["broken"] == "ValueError: boom" and g.sections["broken"]["status"] == "error"
+    with pytest.raises(KeyError):
+        with g.section("critical", 5, critical=True):
+            raise KeyError("x")
+    assert g.finish() is True
+    st = json.loads((tmp_path / "rank0.json").read_text())
+    assert st["exited"] is True and st["phase"] == "done"
+
+
+def test_diagnose_ignores_stale_status_files(tmp_path):
+    from otedama_amd.parallel import guard as G
+
+    (tmp_path / "rank1.json").write_text(json.dumps({"rank": 1, "t_start": time.time() - 3600, "pid": 1}))
+    (tmp_path / "rank0.json").write_text(json.dumps({"rank": 0, "t_start": time.time(), "pid": os.getpid(),
+                                                     "phase": "rendezvous", "t_wall": time.time()}))
+    (tmp_path / "rank0.stderr").write_text("x" * 2000 + "the last words")
+    d = G.diagnose_run_dir(str(tmp_path), 2, time.time())
+    assert d["ranks_checked_in"] == [0] and d["ranks"]["1"]["checked_in"] is False
+    assert d["ranks"]["0"]["stderr_tail"].endswith("the last words") and len(d["ranks"]["0"]["stderr_tail"]) <= 600
