@@ -159,8 +159,8 @@ async def _serve(fs, algos: list[str], stdout: TextIO) -> int:
     if fs["duration"] > 0:
         loop.call_later(fs["duration"], stop.set)
     await stop.wait()
-    for p in pools:
-        stdout.write(json.dumps(p.stats()) + "\n")
+    for p in pools:  # the exit line carries the timed validation log too (windowed quantiles for probes)
+        stdout.write(json.dumps(dict(p.stats(), validate_log=p.validate_log())) + "\n")
         await p.stop()
     if srv:
         srv.stop()

@@ -57,6 +57,10 @@ class PoolConfig:
     pool_pubkey: str = ""               # SV2 only: pinned authority key (64 hex chars, x-only secp256k1)
     noise_suite: str = "ellswift"       # SV2 Noise: "ellswift" (Noise_NX_Secp256k1+EllSwift_ChaChaPoly_SHA256, the
                                         # current spec) or "legacy" (32-byte x-only keys, rounds 1-2 wire format)
+    target_grace: float = 0.0           # seconds after a difficulty raise during which shares found under the
+                                        # previous, easier target are still submitted. Only for pools known to credit
+                                        # them (otedama pool: RETARGET_GRACE 10 s); 0 = off, every share below the
+                                        # target in force is dropped locally instead of being rejected by the pool
 
 
 @dataclass
@@ -143,6 +147,8 @@ class Config:
                     issues.append(f"pools[{i}].url invalid: {err}")
             if (p.noise or p.pool_pubkey) and p.url and not p.url.startswith(("stratum+v2://", "stratum+v2tls://")):
                 issues.append(f"pools[{i}]: noise / pool_pubkey apply to stratum+v2 URLs only")
+            if not 0.0 <= float(p.target_grace) <= 60.0:
+                issues.append(f"pools[{i}].target_grace {p.target_grace!r} must be within 0..60 seconds")
             if p.noise_suite not in ("ellswift", "legacy"):
                 issues.append(f"pools[{i}].noise_suite {p.noise_suite!r} is not one of ellswift, legacy")
             if p.pool_pubkey and not _is_xonly_hex(p.pool_pubkey):

@@ -68,8 +68,8 @@ DEFAULT_HYSTERESIS = 0.05
 SHARE_POLL_INTERVAL = 0.005  # share-queue poll for miner sets without wake-up fds (test fakes)
 SHARE_WAKE_FALLBACK = 0.25   # with eventfds: safety re-poll interval (a missed wake-up costs at most this)
 SUBMIT_KEYS_CAP = 1024  # unacked-submit map bound (internal/engine/run.go:726)
-TARGET_GRACE = 10.0     # seconds a raised share target still lets shares found under the previous one through (the
-                        # local pool credits them for the same window, pool/server.py RETARGET_GRACE)
+TARGET_GRACE = 10.0     # the local pool's window (pool/server.py RETARGET_GRACE): the most a pools[].target_grace may
+                        # usefully be; the engine applies the grace of the pool it is connected to (default 0 = off)
 
 
 @dataclass
@@ -180,6 +180,7 @@ class Engine:
         # job id -> (the easier target in force before the last raise, monotonic time of the raise): a share found
         # against it and still queued is submitted within TARGET_GRACE (pools credit such in-flight shares)
         self._prev_targets: dict[str, tuple[int, float]] = {}
+        self._target_grace = 0.0  # the connected pool's pools[].target_grace
         self._submitted = BoundedSet(SUBMIT_KEYS_CAP)  # run.go:720-726: cap 1024, oldest half dropped
         self._session = None
         self._providers: list = []
@@ -701,6 +702,7 @@ class Engine:
                             noise=bool(pc.noise) if pc is not None else False,
                             pool_pubkey=bytes.fromhex(pc.pool_pubkey) if pc is not None and pc.pool_pubkey else b"",
                             noise_suite=pc.noise_suite if pc is not None else "ellswift")
+        self._target_grace = min(float(pc.target_grace), TARGET_GRACE) if pc is not None else 0.0
         self._mark("pool_dial")
         session = await self._dial(url, creds)
         self._mark("pool_connected")
@@ -816,7 +818,7 @@ class Engine:
                 if tgt is not None and h and int.from_bytes(h, "little") > tgt:
                     prev = self._prev_targets.get(s["job_id"])
                     hv = int.from_bytes(h, "little")
-                    if prev is None or hv > prev[0] or time.monotonic() - prev[1] > TARGET_GRACE:
+                    if prev is None or hv > prev[0] or time.monotonic() - prev[1] > self._target_grace:
                         self.m.below_target_skipped.inc()
                         continue
                 en2 = extranonce2_bytes(s["extranonce2"], s["extranonce2_size"])

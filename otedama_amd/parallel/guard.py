@@ -95,8 +95,10 @@ def fault_for(rank: int, section: str, env=None) -> str | None:
 class RankGuard:
     """Per-rank section deadlines and the always-report exit path (module docstring)."""
 
+    PROGRESS_EVERY = 30.0  # rank 0: a "still in section X" line at least this often (a silent run looks hung)
+
     def __init__(self, rank: int, world: int, deadline_s: float, emit=None, run_dir: str | None = None,
-                 margin_s: float = 30.0, marker: str = "bench.py", poll_s: float = 0.25):
+                 margin_s: float = 30.0, marker: str = "bench.py", poll_s: float = 0.25, progress: bool = True):
         self.rank, self.world = rank, world
         self.t0 = time.monotonic()
         self.t_start_wall = time.time()
@@ -118,6 +120,19 @@ class RankGuard:
         self._tee: subprocess.Popen | None = None
         self.status_path = os.path.join(self.run_dir, f"rank{rank}.json")
         self.phase = "start"
+        self.progress_on = progress and rank == 0
+        self._last_progress = time.monotonic()
+
+    def progress(self, msg: str) -> None:
+        """One line on stderr from rank 0: section starts / ends and a periodic heartbeat, so a watcher that kills
+        silent commands (and a human reading the log) sees the run is alive and where it is."""
+        if not self.progress_on:
+            return
+        self._last_progress = time.monotonic()
+        try:
+            os.write(2, f"[bench +{self.elapsed():.1f}s] {msg}\n".encode())
+        except OSError:
+            pass
 
     # ------------------------------------------------------------------ set-up
     def start(self, tee_stderr: bool = False) -> "RankGuard":
@@ -185,6 +200,7 @@ class RankGuard:
             self.section_end = min(t + budget_s + self.margin, self.end)
             self.phase = f"section:{name}"
         self._write_status()
+        self.progress(f"section {name}: start (budget {budget_s:.0f} s)")
         fault = fault_for(self.rank, name)
         if fault == "stuck":
             while True:
@@ -199,6 +215,7 @@ class RankGuard:
                 self.sections[name] = {"s": round(time.monotonic() - t, 2), "status": "error"}
                 self.current = self.section_end = None
             self._write_status()
+            self.progress(f"section {name}: FAILED {self.errors[name]}")
             if critical:
                 raise
             return
@@ -207,11 +224,13 @@ class RankGuard:
                 self.sections[name] = {"s": round(time.monotonic() - t, 2), "status": "ok"}  # stands
             self.current = self.section_end = None
         self._write_status()
+        self.progress(f"section {name}: done in {time.monotonic() - t:.1f} s")
 
     def skip(self, name: str, why: str) -> None:
         with self._lock:
             self.sections[name] = {"s": 0.0, "status": "skipped", "why": why}
         self._write_status()
+        self.progress(f"section {name}: skipped ({why})")
 
     def finish(self) -> bool:
         """The run is complete: nothing may fire after this, and the caller prints its own JSON. False when the
@@ -246,6 +265,8 @@ class RankGuard:
             now = time.monotonic()
             with self._lock:
                 sec, send, budget = self.current, self.section_end, self.section_budget
+            if self.progress_on and now - self._last_progress >= self.PROGRESS_EVERY:
+                self.progress(f"still in {self._where()}")
             if sec is not None and send is not None and now > send:
                 if now >= self.end:
                     self.fire(f"bench deadline ({self.deadline_s:.0f} s) passed in section {sec}", section=sec)

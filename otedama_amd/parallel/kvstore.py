@@ -31,6 +31,7 @@ READY, NOT_READY = 0, 1
 STOP_WAITING, WAIT_CANCELED = 0, 1
 
 _U8, _U32, _U64, _I64 = struct.Struct("<B"), struct.Struct("<I"), struct.Struct("<Q"), struct.Struct("<q")
+TX_CAP = 16 << 20  # replies queued for one peer that is not reading; past this the peer is dropped
 
 
 class _Incomplete(Exception):
@@ -193,6 +194,8 @@ class StoreServer:
                     c = key.data
                     if ev & selectors.EVENT_READ:
                         self._read(c, conns)
+                    if ev & selectors.EVENT_WRITE and c.sock.fileno() in conns:
+                        self._flush(c, conns)  # a slow reader's socket drained: send the rest
             if self._dirty:
                 with self._lock:
                     dirty, self._dirty = self._dirty, set()
@@ -258,25 +261,33 @@ class StoreServer:
             self._drop(c, conns)
 
     def _flush(self, c: _Conn, conns: dict) -> None:
-        # under the data lock: an in-process set() on the supervisor's thread appends WAIT replies to c.tx
+        """Send what the connection has queued without ever blocking: the bytes are taken out under the data lock
+        (an in-process set() on the supervisor's thread appends WAIT replies to c.tx), sent outside it, and what the
+        socket did not take goes back in front and waits for EVENT_WRITE. A peer that stops reading (a process frozen
+        after a GPU fault) can therefore never stall this thread, the supervisor's set('otd/dead/r') or any other
+        rank's heartbeat; one whose backlog passes TX_CAP is dropped."""
         with self._lock:
-            ok = True
+            data, c.tx = bytes(c.tx), bytearray()
+        ok, n = True, 0
+        try:
+            n = c.sock.send(data) if data else 0
+        except (BlockingIOError, InterruptedError):
+            n = 0
+        except OSError:
+            ok = False
+        if ok and n < len(data):
+            with self._lock:
+                c.tx[:0] = data[n:]
+                backlog = len(c.tx)
+            ok = backlog <= TX_CAP
+        if ok:
+            want = selectors.EVENT_READ | (selectors.EVENT_WRITE if c.tx else 0)
             try:
-                n = c.sock.send(c.tx)
-                del c.tx[:n]
-            except (BlockingIOError, InterruptedError):
+                if self._sel.get_key(c.sock).events != want:
+                    self._sel.modify(c.sock, want, c)
+            except (KeyError, ValueError):
                 pass
-            except OSError:
-                ok = False
-            if ok and c.tx:  # a slow reader: block briefly rather than grow an event mask (replies are tiny)
-                try:
-                    c.sock.settimeout(5.0)
-                    c.sock.sendall(c.tx)
-                    c.tx.clear()
-                    c.sock.setblocking(False)
-                except OSError:
-                    ok = False
-        if not ok:
+        else:
             self._drop(c, conns)
 
     def _handle(self, c: _Conn, r: _Reader) -> bool:

@@ -24,6 +24,11 @@ from typing import Sequence
 
 MASTER_ADDR = "127.0.0.1"  # the container hostname may not resolve
 FINAL_EXIT_CODES = (0, 64, 78)  # rank 0 exit codes that end a node: clean stop, usage error, configuration error
+# A rank 0 that keeps dying young (an unhandled exception, a pool that always refuses the credentials) is not
+# restarted forever: after this many consecutive restarts that each lived less than QUICK_EXIT_S the node stops with
+# rank 0's code, so an outer service manager sees the failure.
+RANK0_MAX_QUICK_RESTARTS = 5
+QUICK_EXIT_S = 60.0
 
 
 def free_port() -> int:
@@ -160,7 +165,8 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
     Rank 0 (the leader: pool session + job fan-out) that dies is restarted the same way, as a leader that takes the
     running node over (parallel/node.py ``NodeMinerSet._take_over``); the followers keep hashing meanwhile. Only a
     clean exit (0), a usage / configuration error (64 / 78, which a restart cannot fix) or ``respawn=False`` ends
-    the node with rank 0's exit code."""
+    the node with rank 0's exit code; so does a rank 0 that died RANK0_MAX_QUICK_RESTARTS times in a row, each time
+    within QUICK_EXIT_S of its start."""
     from .kvstore import StoreServer
 
     log = log or (lambda msg: print(f"[node] {msg}", file=sys.stderr, flush=True))
@@ -170,6 +176,7 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
     backoff = {r: backoff_initial for r in range(world)}
     respawn_at: dict[int, float] = {}
     started: dict[int, float] = {}
+    quick_exits = 0  # consecutive rank-0 exits within QUICK_EXIT_S of its start
 
     def spawn(r: int, join: bool) -> None:
         extra = {"OTEDAMA_STORE_HOSTED": "1"}
@@ -205,6 +212,13 @@ def supervise_node(cmd: Sequence[str], world: int, port: int | None = None, env:
             if rc0 is not None and (not respawn or rc0 in FINAL_EXIT_CODES):
                 log(f"rank 0 exited with code {rc0}; stopping the node")
                 return rc0
+            if rc0 is not None:
+                lived = time.monotonic() - started.get(0, time.monotonic())
+                quick_exits = quick_exits + 1 if lived < QUICK_EXIT_S else 0
+                if quick_exits >= RANK0_MAX_QUICK_RESTARTS:
+                    log(f"rank 0 exited with code {rc0} after {lived:.0f}s, {quick_exits} times in a row within "
+                        f"{QUICK_EXIT_S:.0f}s of starting; stopping the node")
+                    return rc0
             now = time.monotonic()
             for r in range(world):
                 p = procs.get(r)

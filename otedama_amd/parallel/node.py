@@ -86,11 +86,24 @@ def _k(*parts) -> str:
     return PREFIX + "/".join(str(p) for p in parts)
 
 
-def _store_get(store, key: str):
+def _store_get(store, key: str, timeout: float | None = None):
+    """The key's value, or None when it is absent or the store failed. ``timeout`` bounds the get itself: a key
+    deleted between the check and the get (the leader trimming the op log) would otherwise block the caller for the
+    store's whole timeout."""
     try:
         if not store.check([key]):
             return None
-        return store.get(key)
+        if timeout is None or not hasattr(store, "set_timeout"):
+            return store.get(key)
+        import datetime
+
+        prev = getattr(store, "timeout", None)
+        store.set_timeout(datetime.timedelta(seconds=timeout))
+        try:
+            return store.get(key)
+        finally:
+            if prev is not None:
+                store.set_timeout(prev)
     except Exception:  # noqa: BLE001
         return None
 
@@ -876,14 +889,20 @@ class NodeWorker:
                 op = inline.pop(k, None)
                 if op is None:
                     key = _k("op", k)
-                    if not self.store.check([key]):
+                    raw = None
+                    if self.store.check([key]):
+                        raw = _store_get(self.store, key, timeout=2.0)  # None: trimmed since the check
+                    else:
                         msgs = self._bell.wait(BELL_FALLBACK)
                         for msg in msgs:
                             got = parse_op_msg(msg)
                             if got is not None and got[0] >= k and len(inline) < 4096:
                                 inline[got[0]] = got[1]
+                    if raw is None:
+                        # Behind the trimmed log? Checked on a timer whether or not datagrams arrive: on a busy node
+                        # the doorbell rings often, and op k may be gone for good.
                         now = time.monotonic()
-                        if not msgs and now - lag_checked >= 1.0:
+                        if now - lag_checked >= 1.0:
                             lag_checked = now
                             nxt = int(_store_get(self.store, _k("next")) or 0)
                             if nxt - k > retain:  # op k was trimmed from the log: re-join from the current end
@@ -893,7 +912,7 @@ class NodeWorker:
                                 self.comm.abort()
                                 self.store.set(_k("join", info.orig_rank), "1")
                         continue
-                    op = json.loads(self.store.get(key))
+                    op = json.loads(raw)
                 k += 1
                 kind = op["op"]
                 if kind == "stop":

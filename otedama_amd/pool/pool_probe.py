@@ -10,6 +10,14 @@ pool's native hash workers), rejects by reason, the pool's validation time (subm
 each worker's difficulty in force / retarget count / time from channel open to its last retarget, and the miners'
 device-timeline hashrates.
 
+Steady state: the recorded window opens only once every worker has converged, i.e. no retarget
+larger than SETTLE_BAND (25%) for two retarget periods; convergence time is reported on its own. The vardiff target
+is a 0.1 s share interval, so every algorithm collects a few hundred validations in the window. Each worker's share
+interval over the window is reported against that target (the reference's relation interval = D * 2^32 / H,
+internal/engine/stats.go:502-513), and validation quantiles are computed from the pool's timed log over the window
+only. A short flood (pool/load.py: SV2 clients submitting valid shares as fast as the pool acknowledges) gives the
+pool's validated-shares-per-second ceiling per algorithm.
+
 [NO REFERENCE CODE]: v3 removed the pool; BASELINE.json names this config without a number.
 """
 from __future__ import annotations
@@ -86,9 +94,39 @@ def layout(gpus: int) -> list[tuple[int, str]]:
     return [(i, "sha256d" if i < half else "scrypt") for i in range(gpus)]
 
 
-def measure_pool(gpus: int = 1, seconds: float = 12.0, warmup: float = 2.0, share_seconds: float = 1.0,
-                 retarget_seconds: float = 4.0, difficulty: float = 1.0, cpu: bool = False,
-                 startup_timeout: float = 180.0) -> dict:
+def _window_quantiles(log: list, t0: float, t1: float) -> dict:
+    xs = sorted(ms for t, ms in log if t0 <= t <= t1)
+    n = len(xs)
+
+    def q(p: float):
+        return xs[min(max(int(p * n + 0.5) - 1, 0), n - 1)] if n else None  # nearest rank
+
+    return {"p50": q(0.5), "p95": q(0.95), "p99": q(0.99), "max": xs[-1] if n else None, "samples": n}
+
+
+def flood(algorithms: list[str], seconds: float = 3.0, miners: int = 8, timeout: float = 90.0) -> dict:
+    """The pool's validated-shares/s ceiling per algorithm: pool/load.py in its own process (the pool and SV2 flood
+    clients, every share valid at the clamped minimum difficulty, fully validated and journaled)."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    out = subprocess.run([sys.executable, "-m", "otedama_amd.pool.load", "--algo", ",".join(algorithms),
+                          "--miners", str(miners * len(algorithms)), "--seconds", repr(seconds)],
+                         capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    res = {}
+    for line in out.stdout.splitlines():
+        if line.startswith("{"):
+            r = json.loads(line)
+            res[r["pool"]] = {"validated_shares_per_sec": r["validated_shares_per_sec"], "rejected": r["rejected"],
+                              "ack_p50_ms": r["ack_latency_ms"]["p50"], "ack_p99_ms": r["ack_latency_ms"]["p99"],
+                              "miners": r["miners"], "seconds": r["seconds"]}
+    if not res:
+        raise RuntimeError(f"flood produced no result: {out.stderr[-500:]}")
+    return res
+
+
+def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.1, retarget_seconds: float = 5.0,
+                 difficulty: float = 1.0, cpu: bool = False, startup_timeout: float = 180.0,
+                 settle_timeout: float = 60.0, steady_periods: float = 2.0, flood_seconds: float = 3.0) -> dict:
     streams = layout(gpus)
     algos = sorted({a for _, a in streams}, key=["sha256d", "scrypt"].index)
     http = f"127.0.0.1:{free_port()}"
@@ -99,12 +137,15 @@ def measure_pool(gpus: int = 1, seconds: float = 12.0, warmup: float = 2.0, shar
     if cpu:
         env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     miners = []
+    final: dict = {}
+    t_open = time.monotonic()
     try:
         for gpu, algo in streams:
             name = f"{'cpu' if cpu else 'gpu'}{gpu}-{algo}"
             cfg = os.path.join(tmp, f"{name}.yaml")
             with open(cfg, "w") as f:
                 f.write(f"bitcoin_address: {PROBE_ADDR}\npools:\n  - url: stratum+v2://{addrs[algo]}\n"
+                        "    target_grace: 10\n"  # otedama pool credits in-flight shares for RETARGET_GRACE
                         f"workers:\n  name: {name}\nmining:\n  algorithm: {algo}\n"
                         + ("  cpu_threads: 1\n  gpus: none\n" if cpu else f"  gpus: '{gpu}'\n"))
             rep = os.path.join(tmp, f"{name}.json")
@@ -124,7 +165,19 @@ def measure_pool(gpus: int = 1, seconds: float = 12.0, warmup: float = 2.0, shar
             time.sleep(0.25)
         else:
             raise RuntimeError(f"miners not accepted within {startup_timeout:.0f} s")
-        time.sleep(warmup)
+        t_first = time.monotonic()
+        # steady state: every worker connected and without a retarget larger than SETTLE_BAND for steady_periods
+        # retarget windows
+        need = steady_periods * retarget_seconds
+        end = time.monotonic() + settle_timeout
+        settled = False
+        while time.monotonic() < end:
+            ws = [w for s in _pool_api(http) for w in s.get("workers", [])]
+            if len(ws) >= len(miners) and all(w["steady_for_s"] >= need and w["accepted"] > 0 for w in ws):
+                settled = True
+                break
+            time.sleep(0.25)
+        t_settled = time.monotonic()
         a0, t0 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
         time.sleep(seconds)
         a1, t1 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
@@ -158,20 +211,34 @@ def measure_pool(gpus: int = 1, seconds: float = 12.0, warmup: float = 2.0, shar
             got = sum(1 for v in s1.get("workers", []) if v["name"] == w["name"])
             prev = next((v for v in s0.get("workers", []) if v["name"] == w["name"]), {})
             n = w["accepted"] - prev.get("accepted", 0)
+            interval = dt / n if n else None
             workers.append({"name": w["name"], "difficulty": w["difficulty"], "retargets": w["retargets"],
-                            "settled_after_s": w["settled_after_s"], "connections": got,
-                            "share_interval_s": dt / n if n else None})
+                            "converged_after_s": w["converged_after_s"], "settled_after_s": w["settled_after_s"],
+                            "window_opened_after_s": w.get("age_s", 0.0) - (t1 - t0),
+                            "connections": got, "accepted_in_window": n,
+                            "share_interval_s": interval,
+                            "interval_vs_target": interval / share_seconds if interval else None})
         out[algo] = {
             "validated_shares_per_sec": acc / dt, "accepted": acc, "rejected": rej,
             "reject_reasons": fin.get("reject_reasons", {}), "accepted_total": fin.get("accepted"),
-            "rejected_total": fin.get("rejected"), "validate_ms": fin.get("validate_ms"),
+            "rejected_total": fin.get("rejected"),
+            "validate_ms": _window_quantiles(fin.get("validate_log", []), t0, t1),
+            "validate_ms_whole_run": fin.get("validate_ms"),
             "target_share_seconds": share_seconds, "workers": workers,
             "miner_hashes_per_sec": rates, "miners": [{"name": m["name"], "gpu": m["gpu"], "exit_code": m["exit_code"]}
                                                       for m in ms],
         }
-    return {"algorithms": out, "layout": [f"{'cpu' if cpu else 'gpu'}{g}:{a}" for g, a in streams],
-            "recorded_seconds": dt, "warmup_seconds": warmup, "initial_difficulty": difficulty,
-            "retarget_seconds": retarget_seconds, "vardiff": True,
-            "definition": ("otedama pool --algorithms sha256d,scrypt (one process) + one `otedama run` per "
-                           "(GPU, algorithm) stream over SV2; every accepted share re-hashed by the pool; windowed "
-                           "after the warm-up")}
+    res = {"algorithms": out, "layout": [f"{'cpu' if cpu else 'gpu'}{g}:{a}" for g, a in streams],
+           "recorded_seconds": dt, "initial_difficulty": difficulty, "retarget_seconds": retarget_seconds,
+           "vardiff": True, "steady_state": settled, "time_to_first_accept_s": t_first - t_open,
+           "time_to_steady_s": t_settled - t_open,
+           "steady_rule": f"no retarget > 25% for {need:.0f} s on every worker",
+           "definition": ("otedama pool --algorithms sha256d,scrypt (one process) + one `otedama run` per "
+                          "(GPU, algorithm) stream over SV2; every accepted share re-hashed by the pool; window opened "
+                          "once every worker's vardiff converged; validation quantiles over the window only")}
+    if flood_seconds > 0:
+        try:
+            res["flood"] = flood(algos, seconds=flood_seconds)
+        except Exception as exc:  # noqa: BLE001 - the flood figure is auxiliary
+            res["flood"] = {"error": f"{type(exc).__name__}: {exc}"}
+    return res

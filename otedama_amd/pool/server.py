@@ -45,6 +45,7 @@ EN1_SIZE = 4
 EN2_SIZE = 4
 MAX_NTIME_FUTURE = 7200
 RETARGET_GRACE = 10.0
+SETTLE_BAND = 0.25  # a retarget that moves the difficulty by more than this fraction means the worker is converging
 MAX_SHARES_PER_JOB = 1 << 20  # credited headers kept per live job before the job is retired
 
 
@@ -116,8 +117,11 @@ class _Worker:
         self.opened_at = time.monotonic()
         self.retargets = 0
         self.last_retarget_at = 0.0  # monotonic time of the last difficulty change (0 = never moved)
+        # monotonic time of the last retarget larger than SETTLE_BAND (0 = none): after it the worker is in steady
+        # state, where vardiff only follows the Poisson noise of its window (~1/sqrt(shares per window))
+        self.last_big_retarget_at = 0.0
 
-    def retargeted(self, old: float) -> None:
+    def retargeted(self, old: float, new: float | None = None) -> None:
         """The worker's difficulty just moved away from `old`. Shares already in flight were found against some
         difficulty of the last RETARGET_GRACE seconds: the grace honours the lowest of them, not only the one
         before this retarget (vardiff ramps through several steps in its first second at a high share rate)."""
@@ -127,6 +131,8 @@ class _Worker:
         self.retarget_at = now
         self.retargets += 1
         self.last_retarget_at = now
+        if new is None or old <= 0 or abs(new / old - 1.0) > SETTLE_BAND:
+            self.last_big_retarget_at = now
 
 
 class PoolServer:
@@ -181,6 +187,7 @@ class PoolServer:
         self.reject_reasons: dict[str, int] = {}
         self.started_at = time.monotonic()
         self._validate_ms: deque = deque(maxlen=8192)  # submit received -> verdict, per share
+        self._validate_log: deque = deque(maxlen=8192)  # (CLOCK_MONOTONIC at the verdict, ms): windowed quantiles
         # CLOCK_MONOTONIC time each new block's clean job was handed to every connection (a node's job-switch probe
         # times each rank's device from here: parallel/node_probe.py)
         self.new_block_at: deque = deque(maxlen=256)
@@ -328,7 +335,9 @@ class PoolServer:
             else:
                 h = await asyncio.get_running_loop().run_in_executor(self._hash_pool, self._slow_hash, hdr)
             v = self._finish(worker, job_id, job, key, h)
-        self._validate_ms.append((time.perf_counter() - t0) * 1e3)
+        ms = (time.perf_counter() - t0) * 1e3
+        self._validate_ms.append(ms)
+        self._validate_log.append((time.monotonic(), ms))
         return v
 
     def share_target(self, difficulty: float) -> bytes:
@@ -427,7 +436,7 @@ class PoolServer:
         old = w.vd.difficulty
         new = self.vardiff.on_share(w.vd)
         if new is not None:
-            w.retargeted(old)
+            w.retargeted(old, new)
             self.journal.save_worker(w.name, new)
         return new
 
@@ -453,6 +462,11 @@ class PoolServer:
     def blocks(self, limit: int = 20) -> list[dict]:
         return [dict(b, algorithm=self.algo.name) for b in self.journal.recent_blocks(limit)]
 
+    def validate_log(self) -> list:
+        """(CLOCK_MONOTONIC, submit -> verdict ms) of the most recent validations: a caller windows them itself
+        (the exit stats line of `otedama pool`; pool/pool_probe.py)."""
+        return [(round(t, 6), round(ms, 4)) for t, ms in self._validate_log]
+
     def validation_ms(self, q: float) -> float | None:
         """Nearest-rank quantile of submit-received -> verdict (header rebuild, PoW hash, duplicate check)."""
         xs = sorted(self._validate_ms)
@@ -476,7 +490,11 @@ class PoolServer:
             # (seconds after the channel opened: the time vardiff took to reach the difficulty it holds)
             "workers": [{"name": w.name, "difficulty": w.vd.difficulty, "accepted": w.accepted,
                          "rejected": w.rejected, "retargets": w.retargets, "age_s": now - w.opened_at,
-                         "settled_after_s": (w.last_retarget_at - w.opened_at) if w.retargets else 0.0}
+                         "settled_after_s": (w.last_retarget_at - w.opened_at) if w.retargets else 0.0,
+                         # steady state: seconds from the channel's open to its last retarget of more than
+                         # SETTLE_BAND, and how long ago that was
+                         "converged_after_s": (w.last_big_retarget_at - w.opened_at) if w.last_big_retarget_at else 0.0,
+                         "steady_for_s": now - (w.last_big_retarget_at or w.opened_at)}
                         for w in live],
         }
 
@@ -757,8 +775,9 @@ class _V2Conn:
             ent = self.channels.get(msg.channel_id)
             if ent is not None and msg.nominal_hashrate > 0 and not self.pool.opts.fixed_difficulty:
                 w = ent[0]
-                w.retargeted(w.vd.difficulty)
+                old = w.vd.difficulty
                 w.vd.difficulty = self.pool.vardiff.difficulty_for_hashrate(msg.nominal_hashrate)
+                w.retargeted(old, w.vd.difficulty)
                 self._send(M.SetTarget(msg.channel_id, self.pool.share_target(w.vd.difficulty)))
         elif isinstance(msg, M.CloseChannel):
             self.channels.pop(msg.channel_id, None)

@@ -20,7 +20,11 @@ class VardiffConfig:
     max_difficulty: float = 1e15
     max_step: float = 4.0
     dead_band: float = 0.10
-    min_shares: int = 4             # retarget early once this many shares arrived faster than target
+    min_shares: int = 4             # retarget early once this many shares arrived early_factor x faster than target
+    # A burst of shares at the right rate is common (Poisson), so an early retarget needs strong evidence: at 2x, a
+    # worker already at its target retargeted on noise several times a minute at a 0.1 s share interval (each a
+    # difficulty doubling and a correction back); at 4x the chance of a spurious one after min_shares is ~2%.
+    early_factor: float = 4.0
 
 
 @dataclass
@@ -58,7 +62,7 @@ class Vardiff:
         now = self.clock()
         elapsed = now - st.window_start
         c = self.cfg
-        early = st.shares >= c.min_shares and elapsed < c.target_share_seconds * st.shares / 2
+        early = st.shares >= c.min_shares and elapsed < c.target_share_seconds * st.shares / c.early_factor
         if elapsed < c.retarget_seconds and not early:
             return None
         if st.shares == 0:

@@ -811,14 +811,16 @@ def test_share_pump_skips_stale_job_shares():
 
 
 def test_share_pump_drops_shares_below_a_raised_target():
-    """SV2 SetTarget re-issues the job with a higher difficulty. A queued share the device verified against the
-    previous target is still submitted for TARGET_GRACE seconds after the raise (the pool credits in-flight shares
-    at the previous difficulty for that long); after the grace, or below even the previous target, it
-    would be rejected as low-difficulty, so it is dropped (counted) instead."""
+    """SV2 SetTarget re-issues the job with a higher difficulty. With the pool's target_grace on (a pool that credits
+    in-flight shares at the previous difficulty, as otedama pool does for RETARGET_GRACE), a queued share
+    the device verified against the previous target is still submitted for that long after the raise; after the
+    grace, or below even the previous target, it would be rejected as low-difficulty, so it is dropped (counted)
+    instead."""
     from otedama_amd.engine import run as run_mod
 
     async def go():
         eng, _ = make_engine()
+        eng._target_grace = run_mod.TARGET_GRACE  # pools[].target_grace: 10
         sess = FakeSession()
         easy, hard = (1 << 250).to_bytes(32, "little"), (1 << 240).to_bytes(32, "little")
         await sess.jobs.put(Job("j1", clean_jobs=True, target=easy))
@@ -838,6 +840,36 @@ def test_share_pump_drops_shares_below_a_raised_target():
         assert sorted(s.nonce for s in sess.submitted) == [1, 2, 3, 6]
         assert eng.m.below_target_skipped.value() == 2
     asyncio.run(go())
+
+
+def test_share_pump_grace_is_off_by_default():
+    """an external pool that applies SetTarget at once would reject shares found under the previous
+    target as low-difficulty (counted against the miner, and rate-limited by some pools): without pools[].target_grace
+    they are dropped locally right after the raise."""
+    async def go():
+        eng, _ = make_engine()
+        assert eng._target_grace == 0.0
+        sess = FakeSession()
+        easy, hard = (1 << 250).to_bytes(32, "little"), (1 << 240).to_bytes(32, "little")
+        await sess.jobs.put(Job("j1", clean_jobs=True, target=easy))
+        await sess.jobs.put(Job("j1", clean_jobs=True, target=hard))
+        await run_pump_until(eng._job_pump(sess), lambda: len(eng.miners.jobs) == 2)
+        weak, strong = (1 << 245).to_bytes(32, "little"), (1 << 230).to_bytes(32, "little")
+        eng.miners.queue = [share(nonce=1, digest=weak), share(nonce=2, digest=strong)]
+        await run_pump_until(eng._share_pump(sess), lambda: len(sess.submitted) == 1)
+        assert [s.nonce for s in sess.submitted] == [2] and eng.m.below_target_skipped.value() == 1
+    asyncio.run(go())
+
+
+def test_pool_target_grace_config_is_validated():
+    from otedama_amd.config import Config, ConfigError, PoolConfig
+
+    Config(bitcoin_address="bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq",
+           pools=[PoolConfig(url="stratum+v2://127.0.0.1:3336", target_grace=10)]).validate()
+    bad = Config(bitcoin_address="bc1qar0srrr7xfkvy5l643lydnw9re59gtzzwf5mdq",
+                 pools=[PoolConfig(url="stratum+v2://127.0.0.1:3336", target_grace=-1)])
+    with pytest.raises(ConfigError, match="target_grace"):
+        bad.validate()
 
 
 def test_share_pump_never_submits_a_duplicate():

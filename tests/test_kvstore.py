@@ -230,3 +230,35 @@ def test_supervisor_counts_gpus_from_sysfs_without_torch(tmp_path):
     out = subprocess.run([sys.executable, "-c", code, str(tmp_path)], env=env, capture_output=True, text=True,
                          timeout=60)
     assert out.stdout.strip() == "[1, false]", out.stderr
+
+
+def test_a_peer_that_stops_reading_never_stalls_the_store():
+    """a client whose socket buffer is full (a rank frozen after a GPU fault) must not block the server
+    thread: other clients and the supervisor's in-process calls stay served at once, and the stalled peer is dropped
+    when its backlog passes TX_CAP."""
+    import socket
+    import struct
+
+    from otedama_amd.parallel import kvstore as K
+
+    with StoreServer() as srv:
+        srv.set("big", b"x" * (1 << 20))
+        raw = socket.create_connection(("127.0.0.1", srv.port))
+        key = b"/big"
+        get = bytes([K.GET]) + struct.pack("<Q", len(key)) + key
+        raw.sendall(bytes([K.VALIDATE]) + struct.pack("<I", K.MAGIC) + get * 40)  # 40 MiB of replies, never read
+        time.sleep(0.5)
+        c = _client(srv.port)
+        t0 = time.monotonic()
+        for i in range(20):
+            c.set(f"k{i}", str(i))
+            assert c.get(f"k{i}") == str(i).encode()
+        srv.set("otd/dead/3", "137")  # the supervisor's in-process call
+        assert time.monotonic() - t0 < 2.0
+        # the stalled peer was dropped once its backlog passed TX_CAP: only the listener, the wake-up pipe and the
+        # torch client are still registered
+        end = time.monotonic() + 5
+        while len(srv._sel.get_map()) > 3 and time.monotonic() < end:
+            time.sleep(0.05)
+        assert len(srv._sel.get_map()) == 3
+        raw.close()

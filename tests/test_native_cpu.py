@@ -390,3 +390,20 @@ def test_avx512_scan_groups_agree(groups):
                          env=dict(os.environ, OTEDAMA_CPU_SCAN_GROUPS=groups))
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.strip() == f"avx512 16 lanes x {groups} groups"
+
+
+def test_maps_check_requires_read_write_permissions():
+    """the CPU-stored abort word is used only when its range is mapped rw in /proc/self/maps; a
+    PROT_NONE reservation of the GPU address range (libhsakmt, small BAR) must not pass."""
+    from otedama_amd.ops.native import require_native
+
+    N = require_native()
+    maps = ("7f0000000000-7f0000100000 ---p 00000000 00:00 0 \n"
+            "7f0000100000-7f0000200000 rw-s 00000000 00:05 12 /dev/dri/renderD128\n"
+            "7f0000200000-7f0000300000 r--p 00000000 00:00 0\n"
+            "garbage line\n")
+    assert not N.maps_range_writable(maps, 0x7F0000000100, 0x7F0000000200)  # PROT_NONE reservation
+    assert N.maps_range_writable(maps, 0x7F0000100100, 0x7F0000100200)       # rw mapping of the BAR
+    assert not N.maps_range_writable(maps, 0x7F0000200100, 0x7F0000200200)  # read-only
+    assert not N.maps_range_writable(maps, 0x7F00000FFFF0, 0x7F0000100010)  # straddles two lines
+    assert not N.maps_range_writable("", 0x1000, 0x1100)

@@ -128,3 +128,20 @@ def test_leader_failover_keeps_the_node_mining(tmp_path, world):
             raise AssertionError("node did not stop within 60 s")
         finally:
             stop_pool(pool)
+
+
+def test_a_rank0_that_keeps_dying_young_stops_the_node():
+    """rank 0 is restarted after a crash, but not forever: five exits in a row, each within a minute of
+    its start (an unhandled exception, credentials the pool always refuses), end the node with rank 0's code."""
+    import sys
+    import time
+
+    from otedama_amd.parallel import launch
+
+    lines = []
+    t0 = time.monotonic()
+    rc = launch.supervise_node([sys.executable, "-c", "import sys; sys.exit(3)"], 1, backoff_initial=0.02,
+                               backoff_max=0.05, log=lines.append)
+    assert rc == 3 and time.monotonic() - t0 < 30
+    assert sum("restarting" in ln for ln in lines) == launch.RANK0_MAX_QUICK_RESTARTS - 1
+    assert "times in a row" in lines[-1]
