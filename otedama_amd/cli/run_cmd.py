@@ -162,7 +162,11 @@ def _run_node_worker(cfg, info, comm, stdout, joining: bool = False) -> int:
     stdout.write(f"[info] node: rank {info.orig_rank} {'joining' if joining else f'of {info.world_size}'} mining on "
                  f"GPU {gpu} ({len(local)} device(s))\n")
     try:
-        NodeWorker(local, comm, log=lambda lvl, msg: stdout.write(f"[{lvl}] {msg}\n"), joining=joining).run()
+        def wlog(lvl: str, msg: str) -> None:  # flushed: a follower's log must survive its SIGKILL
+            stdout.write(f"[{lvl}] {msg}\n")
+            stdout.flush()
+
+        NodeWorker(local, comm, log=wlog, joining=joining).run()
     finally:
         shutdown(info)
     return EXIT_OK

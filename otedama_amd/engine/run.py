@@ -428,6 +428,7 @@ class Engine:
         if link is not None:
             for r, hb in hbs.items():
                 ws[f"rank{r}"] = [tuple(x) for x in hb.get("ws", [])]
+            rep["job_applied"] = {f"rank{r}": [tuple(x) for x in hb.get("ja", [])] for r, hb in hbs.items()}
         rep["work_started"] = ws
         return rep
 

@@ -164,10 +164,15 @@ class NodeComm:
     over gloo, a CPU transport: with device buffers every gloo collective adds device<->host staging and stream
     syncs (a 2-rank R2 gather took 4.7 ms p50 on the MI355X that way)."""
 
-    def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0, host_buffers: bool = False):
+    def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0, host_buffers: bool = False,
+                 force: bool = False, stream_priority: int | None = None):
+        """``force``: issue the collectives at world 1 too (a one-rank process group must exist): the comm-under-load
+        probe (parallel/comm_probe.py) measures the data plane's own path on a single GPU that way.
+        ``stream_priority``: priority of the comm stream (None = normal; lower = higher priority, as HIP's)."""
         self.info = info
         self.bounded = bounded
         self.deadline = deadline
+        self.force = force
         self.collectives = 0  # device collectives issued by this rank (node tick accounting)
         dev = torch.device("cpu") if host_buffers else info.device
         self.dev = dev
@@ -176,7 +181,17 @@ class NodeComm:
         self._counters = torch.zeros(COUNTER_WORDS, dtype=torch.int64, device=dev)
         self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)
         self._alloc_world(max(info.world_size, 1))
-        self.stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        if dev.type != "cuda":
+            self.stream = None
+        elif stream_priority is None:
+            self.stream = torch.cuda.Stream(dev)
+        else:
+            self.stream = torch.cuda.Stream(dev, priority=stream_priority)
+
+    @property
+    def multi(self) -> bool:
+        """Collectives are issued: more than one rank, or forced at world 1."""
+        return self.info.world_size > 1 or self.force
 
     def _alloc_world(self, world: int) -> None:
         dev = self.dev
@@ -254,7 +269,7 @@ class NodeComm:
             host = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8)
             host[: len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
             self._job.copy_(host)
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.broadcast(self._job, src=0, async_op=a))
         host = self._job.cpu().numpy().tobytes()
         n = int.from_bytes(host[:4], "little")
@@ -273,7 +288,7 @@ class NodeComm:
                        en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
                        int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6))
         self._slots.copy_(torch.from_numpy(rows))
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
                                                                 async_op=a))
         else:
@@ -294,7 +309,7 @@ class NodeComm:
     # ---------------------------------------------------------------- R3
     def allreduce_counters(self, hashes: int, shares: int = 0, dropped: int = 0, faults: int = 0) -> tuple:
         self._counters.copy_(torch.tensor([hashes, shares, dropped, faults], dtype=torch.int64))
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM, async_op=a))
         return tuple(int(x) for x in self._counters.cpu().tolist())
 
@@ -302,7 +317,7 @@ class NodeComm:
         """R3 variant for per-device stats: every rank's COUNTER_WORDS counters (all_gather, 32 B/rank)."""
         mine = torch.tensor(list(values)[:COUNTER_WORDS] + [0] * (COUNTER_WORDS - len(values)), dtype=torch.int64)
         self._counters.copy_(mine)
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters,
                                                                 async_op=a))
         else:
@@ -313,13 +328,13 @@ class NodeComm:
         """R1 control word (seq, stop, ...): 4 int64, every tick; the job blob follows only on change."""
         if self.info.is_primary:
             self._ctl.copy_(torch.tensor(list(words)[:4] + [0] * (4 - len(words)), dtype=torch.int64))
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.broadcast(self._ctl, src=0, async_op=a))
         return self._ctl.cpu().tolist()
 
     def allreduce_max(self, value: float) -> float:
         t = torch.tensor([value], dtype=torch.float64, device=self.dev)
-        if self.info.world_size > 1:
+        if self.multi:
             self._collect(lambda a: dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=a))
         return float(t.item())
 

@@ -1,0 +1,187 @@
+"""The node's data plane under a saturating miner, measured on one GPU.
+
+In the node every rank process issues R1 / R2 / R3 on its comm stream while its sibling device process keeps every
+CU of the same GPU busy with an oversubscribed grid (128 blocks per CU for SHA-256d; the scrypt kernel at full HBM
+load). Two questions, each answered with numbers:
+
+1. Do the data-plane operations wait behind that grid? Each op is timed from the rank's call to its result on the
+   host (what the node's op loop sees: the H2D staging copy, the collective on the comm stream, the D2H read), idle
+   and with the miner running, at node cadence (R2 share gathers at ``cadence_hz``, an R1 64 KiB job blob every 10th
+   op, R3 counters every 25th). A one-rank RCCL group is forced (``NodeComm(force=True)``): RCCL runs its one-rank
+   path (copies), so the collective itself is cheap and what is measured is whether any GPU work of this process
+   is scheduled promptly. A tiny elementwise kernel on the comm stream (``kernel_probe``) measures the scheduling of
+   a KERNEL from another process directly: at world > 1, RCCL's collectives are kernels that need CU slots too.
+2. Does the data plane cost hash rate? The miner's exact device-timeline rate (the device process's counter pairs)
+   over alternating windows without and with the ops.
+
+Each configuration is run with the comm stream at normal and at high priority. The reference's rule is that the
+fan-in never stalls a producer (internal/engine/fanin.go:22-58); SURVEY §5.8 puts RCCL on a dedicated stream so the
+kernels keep running while R2/R3 move.
+"""
+from __future__ import annotations
+
+import statistics
+import time
+
+
+def _q(xs: list[float]) -> dict:
+    xs = sorted(xs)
+    n = len(xs)
+
+    def at(p):
+        return xs[min(max(int(p * n + 0.5) - 1, 0), n - 1)] if n else None
+
+    return {"p50_ms": at(0.5), "p99_ms": at(0.99), "max_ms": xs[-1] if n else None, "samples": n}
+
+
+def _miner_rate(dp, t0: tuple[int, float], t1: tuple[int, float]) -> float | None:
+    (h0, d0), (h1, d1) = t0, t1
+    return (h1 - h0) / (d1 - d0) if d1 > d0 > 0 and h1 > h0 else None
+
+
+def _counter(dp) -> tuple[int, float]:
+    st = dp.stats()
+    return int(st.get("hashes", 0)), float(st.get("hashes_done_at_s", 0.0) or 0.0)
+
+
+def run_ops(comm, seconds: float, cadence_hz: float = 50.0, probe_kernel: bool = True) -> dict:
+    """Issue R2 gathers at ``cadence_hz`` (an R1 job blob every 10th op, R3 counters every 25th) for ``seconds``;
+    return per-op latency quantiles and the comm-stream kernel probe's."""
+    import torch
+
+    lat: dict[str, list[float]] = {"R1_job": [], "R2_gather": [], "R3_counters": [], "kernel": []}
+    job = {"job_id": "probe", "header": bytes(80), "coinb1": bytes(2000), "coinb2": bytes(2000),
+           "merkle_branches": [bytes(32)] * 12, "epoch": 1}
+    shares = [{"epoch": 1, "nonce": i, "ntime": 1, "version": 2, "extranonce2": 3, "found_at": time.monotonic()}
+              for i in range(4)]
+    x = torch.zeros(1 << 12, dtype=torch.float32, device=comm.dev) if comm.stream is not None else None
+    period = 1.0 / cadence_hz
+    end = time.monotonic() + seconds
+    k = 0
+    nxt = time.monotonic()
+    while time.monotonic() < end:
+        k += 1
+        t = time.perf_counter()
+        if k % 10 == 0:
+            comm.broadcast_job(job)
+            lat["R1_job"].append((time.perf_counter() - t) * 1e3)
+        elif k % 25 == 0:
+            comm.gather_counters([1, 2, 3, 4])
+            lat["R3_counters"].append((time.perf_counter() - t) * 1e3)
+        else:
+            comm.gather_shares(shares)
+            lat["R2_gather"].append((time.perf_counter() - t) * 1e3)
+        if probe_kernel and x is not None and k % 5 == 0:
+            t = time.perf_counter()
+            with torch.cuda.stream(comm.stream):
+                x.add_(1.0)
+            comm.stream.synchronize()
+            lat["kernel"].append((time.perf_counter() - t) * 1e3)
+        nxt += period
+        time.sleep(max(0.0, nxt - time.monotonic()))
+    return {k: _q(v) for k, v in lat.items() if v}
+
+
+def _one_rank_group(device) -> bool:
+    """A one-rank RCCL group as the default group; True when this call created it (the caller destroys it)."""
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return False
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=device)
+    return True
+
+
+def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scrypt"), seconds: float = 4.0,
+                            cadence_hz: float = 50.0, windows: int = 2) -> dict:
+    """See the module docstring. Per algorithm: op latency idle / loaded at normal and high comm-stream priority,
+    and the miner's rate over alternating windows without / with the ops."""
+    import torch
+
+    dev = torch.device(f"cuda:{device_index}")
+    torch.cuda.set_device(dev)
+    created = _one_rank_group(dev)
+    try:
+        return _measure(dev, device_index, algorithms, seconds, cadence_hz, windows)
+    finally:
+        if created:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+
+
+def _measure(dev, device_index: int, algorithms, seconds: float, cadence_hz: float, windows: int) -> dict:
+    import torch
+
+    from otedama_amd import hal
+    from otedama_amd.engine.latency_probe import _switch_job
+    from otedama_amd.engine.miners import MinerSet
+    from otedama_amd.parallel.comm import DistInfo, NodeComm
+
+    info = DistInfo(0, 1, device_index, "nccl", dev)
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    comms = {"normal": NodeComm(info, bounded=True, deadline=10.0, force=True),
+             "high": NodeComm(info, bounded=True, deadline=10.0, force=True, stream_priority=min(lo, hi))}
+    for c in comms.values():  # warm: RCCL communicator, allocator, kernels
+        run_ops(c, 0.3, cadence_hz)
+    out: dict = {"idle": {p: run_ops(c, seconds, cadence_hz) for p, c in comms.items()},
+                 "rccl_world": 1, "cadence_hz": cadence_hz,
+                 "definition": ("rank-process call -> result on the host for R1 (64 KiB job blob), R2 (share slots "
+                                "all_gather) and R3 (counters all_gather) on the comm stream of a forced one-rank RCCL "
+                                "group; 'kernel' = a 16 KiB elementwise kernel on the comm stream, enqueue -> done")}
+    devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
+    if not devs:
+        raise RuntimeError(f"no KFD GPU node for device {device_index}")
+    for algo in algorithms:
+        ms = MinerSet(devs, algo, 1 << 32, 0, isolation="process")
+        dp = ms.miners[0].native
+        ms.start()
+        try:
+            end = time.monotonic() + 60
+            while not dp.ready_at and dp.alive and time.monotonic() < end:
+                time.sleep(0.01)
+            ms.set_job(_switch_job(0, algo))
+            time.sleep(3.0 if algo == "scrypt" else 1.5)  # allocations, first launches
+            res: dict = {"loaded": {}, "rate_alone": [], "rate_with_ops": {p: [] for p in comms}}
+            for w in range(windows):
+                a = _counter(dp)
+                time.sleep(seconds)
+                res["rate_alone"].append(_miner_rate(dp, a, _counter(dp)))
+                for p, c in comms.items():
+                    a = _counter(dp)
+                    r = run_ops(c, seconds, cadence_hz)
+                    res["rate_with_ops"][p].append(_miner_rate(dp, a, _counter(dp)))
+                    if w == 0:
+                        res["loaded"][p] = r
+            st = dp.stats()
+            if st.get("faulted"):
+                raise RuntimeError(st.get("error"))
+        finally:
+            ms.stop()
+        alone = [r for r in res["rate_alone"] if r]
+        base = statistics.fmean(alone) if alone else None
+        res["rate_alone_hps"] = base
+        res["rate_loss_pct"] = {p: (100.0 * (1.0 - statistics.fmean([r for r in v if r]) / base)
+                                    if base and any(v) else None) for p, v in res["rate_with_ops"].items()}
+        out[algo] = res
+    return out
+
+
+def main(argv=None) -> int:
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser(prog="otedama_amd.parallel.comm_probe")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--algorithms", default="sha256d,scrypt")
+    ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--cadence", type=float, default=50.0)
+    ap.add_argument("--windows", type=int, default=2)
+    a = ap.parse_args(argv)
+    r = measure_comm_under_load(a.device, [x for x in a.algorithms.split(",") if x], a.seconds, a.cadence, a.windows)
+    print(json.dumps(r))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

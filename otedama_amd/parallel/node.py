@@ -71,6 +71,7 @@ PENDING_CAP = 8192         # shares a follower holds for the leader (drop-oldest
 OP_RETAIN = 4096           # op log entries kept in the store (~1 h at the quiet node's ~1 op/s); older ones deleted
 EPOCH_SHIFT = 40           # leader incarnation i numbers its job epochs from (i - 1) << EPOCH_SHIFT
 PREFIX = "otd/"
+PREVIEW_MAX = 60000        # largest job-preview datagram (loopback UDP allows 65507 bytes); bigger jobs go by R1 only
 
 
 def op_retain() -> int:
@@ -341,6 +342,9 @@ class NodeMinerSet:
         self.takeover = comm.info.generation < 0
         self.incarnation = int(self.store.add(_k("leader_inc"), 1)) if self.store is not None else 1
         self._epoch = (self.incarnation - 1) << EPOCH_SHIFT
+        # blob seqs live in the incarnation's namespace too: a restarted leader's first blob must order after every
+        # blob of its predecessor (followers apply only newer seqs)
+        self._seq = (self.incarnation - 1) << EPOCH_SHIFT
         local._epoch = max(local._epoch, self._epoch)
         self.remote_stale = 0  # remote shares of a job the leader no longer knows (e.g. a previous incarnation's)
         self._rows_by_orig: dict[int, list[int]] = {}
@@ -356,6 +360,7 @@ class NodeMinerSet:
         self._remote_faults: dict[int, int] = {}
         self._remote_idle: dict[int, int] = {}
         self.lost_ranks: list[int] = []
+        self._fail_at = 0.0  # monotonic time of the last failed collective (re-forms wait for its stragglers)
         self._hb = _Heartbeat(self.store, comm.info.orig_rank, local, comm) if self.store is not None else None
         # node-wide job switch accounting (CLOCK_MONOTONIC): when the engine handed rank 0 each new job, and when the
         # R1 broadcast carrying it completed on rank 0
@@ -429,8 +434,28 @@ class NodeMinerSet:
                 for old in [e for e in self._jobs if e < ep - 64]:
                     del self._jobs[old]
             self._publish()
+            preview = self._blob if template is not None else None
         self._poke()
+        if preview is not None:
+            self._preview(preview)
         return ep
+
+    def _preview(self, blob: dict) -> None:
+        """Job preview: ring every follower with the new job itself, from the engine's thread, before the leader
+        loop logs the job op and runs its R1 broadcast. A follower starts the work from the datagram at once; the
+        R1 that follows is the consistent delivery (it also covers a lost datagram, and a job too big for one).
+        Ordering is by the blob's seq, so a preview never rolls a follower back, and a preview of an older process
+        group generation is ignored."""
+        if self._bell is None or self.comm.info.world_size <= 1:
+            return
+        from otedama_amd.parallel.comm import _encode
+
+        msg = b"j" + json.dumps({"gen": self._gen, "blob": _encode(blob)}).encode()
+        if len(msg) > PREVIEW_MAX:
+            return
+        for r in list(self.comm.info.members):
+            if r != self.comm.info.orig_rank:
+                self._bell.ring(r, msg)
 
     def _with_base(self, template: dict | None) -> dict | None:
         if template is None or not self._variant_base:
@@ -444,8 +469,10 @@ class NodeMinerSet:
             blob["epoch"] = self._epoch
             if self._variant_base:
                 blob["variant_base"] = self._variant_base
-        self._blob = {"job": blob, "paused": sorted(self._paused)}
         self._seq += 1
+        # seq orders the leader's blobs: a follower never goes back to an older one (a preview can overtake the op
+        # log, parallel/node.py NodeWorker._apply)
+        self._blob = {"job": blob, "paused": sorted(self._paused), "seq": self._seq}
 
     def pause_device(self, device_id: str, paused: bool = True) -> bool:
         if self.local.pause_device(device_id, paused):
@@ -631,12 +658,34 @@ class NodeMinerSet:
                 joiners.append(r)
         return dead, joiners
 
+    def _await_left(self, members: list[int], timeout: float) -> list[int]:
+        """Wait until no member of ``members`` is still tearing down a failed group (heartbeat ``broken`` newer than
+        its ``left``), at most ``timeout`` s; returns the members still busy at the end. Members whose collective
+        is about to time out publish ``broken`` within the bounded deadline of the failure, so the wait starts no
+        earlier than that (``_fail_at``)."""
+        settle = self._fail_at + self.comm.deadline + HB_INTERVAL
+        end = time.monotonic() + timeout
+        busy: list[int] = []
+        while True:
+            now = time.monotonic()
+            hbs = self._heartbeats()
+            busy = [r for r in members if r != self.comm.info.orig_rank and r in hbs
+                    and int(hbs[r].get("broken", -1)) > int(hbs[r].get("left", -1))]
+            if (not busy and now >= settle) or now >= end:
+                return busy
+            time.sleep(0.05)
+
     def _reform(self, dead: list[int], joiners: list[int], why: str, members: list[int] | None = None) -> None:
         info = self.comm.info
         old_world = info.world_size
         if members is None:
             members = [r for r in info.members if r not in dead] + sorted(joiners)
         members = [0] + sorted(r for r in members if r != 0)
+        from otedama_amd.parallel.comm import PG_TIMEOUT_S
+
+        busy = self._await_left(members, PG_TIMEOUT_S + 5.0)
+        if busy:
+            self.log("warn", f"node: ranks {busy} still leaving the failed group; re-forming anyway")
         # every cursor of the current work: the survivors' heartbeats and this rank's own devices
         hw = self.local.high_water()
         for r, hb in self._heartbeats().items():
@@ -738,6 +787,14 @@ class NodeMinerSet:
                     return
                 now = time.monotonic()
                 try:
+                    # a new job goes out first (the switch latency of every follower waits on it); the liveness check
+                    # (a store round trip per rank) after
+                    if info.world_size > 1 and seq != self._sent_seq:
+                        self._post({"op": "job"})
+                        self.link.run_op({"op": "job"}, blob, [])
+                        self._sent_seq = seq
+                        job = (blob or {}).get("job") or {}
+                        self.job_bcast_at.append((int(job.get("epoch", 0) or 0), time.monotonic()))
                     if now >= next_live and self.store is not None:
                         next_live = now + LIVENESS_EVERY
                         dead, joiners = self._dead_and_joiners()
@@ -745,12 +802,6 @@ class NodeMinerSet:
                             why = ", ".join([f"rank {r} lost" for r in dead] + [f"rank {r} joins" for r in joiners])
                             self._try_reform(dead, joiners, why)
                             continue
-                    if info.world_size > 1 and seq != self._sent_seq:
-                        self._post({"op": "job"})
-                        self.link.run_op({"op": "job"}, blob, [])
-                        self._sent_seq = seq
-                        job = (blob or {}).get("job") or {}
-                        self.job_bcast_at.append((int(job.get("epoch", 0) or 0), time.monotonic()))
                     if info.world_size > 1 and self._gather_wanted:
                         self._gather_wanted = False
                         self._post({"op": "gather"})
@@ -771,6 +822,8 @@ class NodeMinerSet:
                         return
                     self.log("warn", f"node: collective failed ({type(exc).__name__}: {exc}); checking ranks")
                     self.link.error = exc
+                    self._fail_at = time.monotonic()
+                    self.comm.abort()  # tear down now (gloo waits out its op timeout), in parallel with the followers
                     # the peer that broke it shows up as dead within one heartbeat timeout (its process exited, or
                     # it stopped heartbeating); re-form without it, or with everyone if it was transient
                     end = time.monotonic() + self.hb_timeout + 1.0
@@ -833,7 +886,12 @@ class NodeWorker:
         self._bell = _Bell(self.store, comm.info.orig_rank)
         self._pending: list[dict] = []
         self._hb.extra["pending"] = 0  # before the heartbeat thread starts: the share thread only updates it
+        # (epoch, CLOCK_MONOTONIC) of the latest jobs this rank handed its devices (node job-switch breakdown)
+        self._applied: collections.deque = collections.deque(maxlen=8)
+        self._hb.extra["ja"] = []
         self.pending_dropped = 0  # shares dropped past PENDING_CAP (a leader that stays away)
+        self.previews = 0  # jobs started from a preview datagram ahead of their R1 broadcast
+        self._seq_applied = 0  # seq of the leader blob this rank runs (previews and R1 only move it forward)
         self._plock = threading.Lock()
         self._stop = threading.Event()
 
@@ -895,6 +953,9 @@ class NodeWorker:
                     else:
                         msgs = self._bell.wait(BELL_FALLBACK)
                         for msg in msgs:
+                            if msg[:1] == b"j":
+                                self._take_preview(msg, broken)
+                                continue
                             got = parse_op_msg(msg)
                             if got is not None and got[0] >= k and len(inline) < 4096:
                                 inline[got[0]] = got[1]
@@ -909,7 +970,7 @@ class NodeWorker:
                                 self.log("warn", f"node: {self.rank_id} fell {nxt - k} ops behind the log; re-joining")
                                 k, broken = nxt, True
                                 inline.clear()
-                                self.comm.abort()
+                                self._leave_group()
                                 self.store.set(_k("join", info.orig_rank), "1")
                         continue
                     op = json.loads(raw)
@@ -918,6 +979,13 @@ class NodeWorker:
                 if kind == "stop":
                     return
                 if kind == "reform":
+                    cur = _store_get(self.store, _k("gen"), timeout=2.0)
+                    if cur is not None and int(cur) > int(op["gen"]):
+                        # superseded: the leader gave up on this generation (a member joined too late, e.g. one
+                        # stuck tearing down a gloo group) and posted a newer one further down the log; joining it now
+                        # would only wait out the rendezvous timeout while the leader waits in the next one
+                        broken = True
+                        continue
                     if info.orig_rank in op["members"]:
                         try:
                             self.link.run_op(op, None, [])
@@ -937,7 +1005,7 @@ class NodeWorker:
                     if kind == "job":
                         blob, _ = self.link.run_op(op, None, [])
                         if blob is not None:
-                            self._apply(blob)
+                            self._apply(blob)  # a no-op when its preview was applied already (same seq)
                     elif kind == "gather":
                         with self._plock:
                             out, self._pending = self._pending[:SHARE_SLOTS], self._pending[SHARE_SLOTS:]
@@ -956,7 +1024,7 @@ class NodeWorker:
                         self.local.retire_faulted()  # survivors re-split this rank's class at once
                 except Exception as exc:  # noqa: BLE001 - leave this group; the leader re-forms
                     self.log("warn", f"node: {self.rank_id}: collective failed ({type(exc).__name__}: {exc})")
-                    self.comm.abort()
+                    self._leave_group()
                     broken = True
         finally:
             self._stop.set()
@@ -965,10 +1033,46 @@ class NodeWorker:
             self.local.stop()
             self._bell.close()
 
-    def _apply(self, blob: dict) -> None:
+    def _leave_group(self) -> None:
+        """Abort the current group, telling the leader through the heartbeat: ``broken`` = the generation whose
+        collective failed, ``left`` = the generation whose teardown finished. Tearing a gloo group down waits out
+        its op timeout (RCCL aborts at once); the leader posts the next re-form only once every broken member has
+        left (NodeMinerSet._await_left), so nobody reaches the rendezvous after the leader gave up on it."""
+        gen = self.comm.info.generation
+        self._hb.extra["broken"] = gen
+        try:
+            self.comm.abort()
+        finally:
+            self._hb.extra["left"] = gen
+
+    def _take_preview(self, msg: bytes, broken: bool) -> None:
+        """A job preview from the leader (NodeMinerSet._preview): start it if it belongs to this rank's current
+        generation and is newer than what runs."""
+        try:
+            d = json.loads(msg[1:])
+        except ValueError:
+            return
+        info = self.comm.info
+        if broken or info.generation < 0 or d.get("gen") != info.generation:
+            return
+        from otedama_amd.parallel.comm import _decode
+
+        if self._apply(_decode(d.get("blob") or {})):
+            self.previews += 1
+
+    def _apply(self, blob: dict) -> bool:
+        """Hand the leader's blob to the local devices; False when it is not newer than the one running (by seq)."""
+        seq = int(blob.get("seq", 0) or 0)
+        if seq and seq <= self._seq_applied:
+            return False
+        if seq:
+            self._seq_applied = seq
         job = blob.get("job")
         paused = self.rank_id in set(blob.get("paused", []))
         if job is None or paused:
             self.local.set_job(None)
-            return
+            return True
         self.local.set_job(job, epoch=int(job["epoch"]))
+        self._applied.append((int(job["epoch"]), time.monotonic()))
+        self._hb.extra["ja"] = list(self._applied)
+        return True

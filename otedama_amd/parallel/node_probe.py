@@ -110,7 +110,8 @@ HASHES_PER_DIFF1 = {"sha256d": 2.0 ** 32, "x11": 2.0 ** 32, "scrypt": 2.0 ** 16}
 
 
 def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks: int,
-                     job_set_at: list | None = None, window: float = 2.0) -> dict:
+                     job_set_at: list | None = None, window: float = 2.0, job_bcast_at: list | None = None,
+                     job_applied: dict[str, list] | None = None) -> dict:
     """Node-wide job switch from the pool's forced new blocks: for each block sent at t_b (CLOCK_MONOTONIC, which
     every process of the host shares) and each rank, the first (epoch, t) in that rank's work-start record with
     t_b < t <= t_b + window is the moment the rank's device was running the new block's work. Reported per rank and
@@ -119,6 +120,8 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
     missing = 0
     worst_each: list[float] = []
     leader_each: list[float] = []
+    bcast_each: list[float] = []
+    applied_each: dict[str, list[float]] = {}
     for tb in block_at:
         worst = None
         for r in range(ranks):
@@ -134,6 +137,13 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
         sets = sorted(t for _e, t in (job_set_at or []) if tb < t <= tb + window)
         if sets:
             leader_each.append((sets[0] - tb) * 1e3)
+        bc = sorted(t for _e, t in (job_bcast_at or []) if tb < t <= tb + window)
+        if bc:
+            bcast_each.append((bc[0] - tb) * 1e3)
+        for r in range(1, ranks):
+            ap = sorted(t for _e, t in ((job_applied or {}).get(f"rank{r}") or []) if tb < t <= tb + window)
+            if ap:
+                applied_each.setdefault(f"rank{r}", []).append((ap[0] - tb) * 1e3)
 
     def med(xs):
         xs = sorted(xs)
@@ -146,6 +156,10 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
             "worst_rank_p50_ms": max(p50s) if p50s else None, "worst_rank_max_ms": max(maxs) if maxs else None,
             "node_p50_ms": med(worst_each), "missing": missing,
             "pool_to_leader_p50_ms": med(leader_each),
+            # where the time goes (medians, ms after the pool's send): the leader's R1 broadcast completing, and each
+            # follower handing the job to its device process
+            "pool_to_r1_done_p50_ms": med(bcast_each),
+            "pool_to_follower_apply_p50_ms": {r: med(v) for r, v in applied_each.items()} or None,
             "definition": ("pool's new block (forced SetNewPrevHash, CLOCK_MONOTONIC at send) -> each rank's device "
                            "process running the first batch of the new work; node_p50 = median over blocks of the "
                            "slowest rank")}
@@ -271,7 +285,8 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
     if rep_sw is not None:
         # the pool's own send times of the forced blocks (its first block is the one the node started on)
         sent = [t for t in pst.get("new_block_at", []) if t >= (forced[0] - 0.5 if forced else 0)]
-        js = job_switch_stats(sent or forced, rep_sw.get("work_started", {}), gpus, rep_sw.get("job_set_at"))
+        js = job_switch_stats(sent or forced, rep_sw.get("work_started", {}), gpus, rep_sw.get("job_set_at"),
+                              job_bcast_at=rep_sw.get("job_bcast_at"), job_applied=rep_sw.get("job_applied"))
         stale = (pst.get("reject_reasons") or {}).get("stale-job", 0)
         js.update({"forced_blocks": len(forced), "stale_rejects": stale, "engine_rejects_during_switches": rej_sw,
                    "interval_s": switch_interval or (1.5 if algorithm == "scrypt" else 1.0)})

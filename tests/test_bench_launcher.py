@@ -121,7 +121,7 @@ def test_driver_torchrun_invocation_with_the_node_section():
     assert "error" not in node, node
     assert node["n_ranks"] == 4 and node["ranks_seen"] == [0, 1, 2, 3] and node["exit_code"] == 0
     assert all(r > 0 for r in node["per_rank_hashes_per_sec"]) and node["accepted_remote_in_window"] > 0
-    assert node["rejected"] == 0 and node["pool_rejected"] == 0
+    assert node["rejected"] == 0 and node["pool_rejected"] == node["job_switch"]["stale_rejects"]
 
 
 def test_bench_ranks_get_a_long_collective_bound(monkeypatch):
@@ -163,7 +163,12 @@ def test_node_section_json_contract(n):
     assert len(node["per_rank_hashes_per_sec"]) == n and all(r > 0 for r in node["per_rank_hashes_per_sec"])
     assert node["total_hashes_per_sec"] == pytest.approx(sum(node["per_rank_hashes_per_sec"]))
     assert d["node_hashes_per_sec"] == node["total_hashes_per_sec"]
-    assert node["rejected"] == 0 and node["pool_rejected"] == 0 and node["pool_accepted"] > 0
+    # no reject while mining; the forced new blocks of the job-switch phase may catch a share in flight (stale only)
+    assert node["rejected"] == 0 and node["pool_accepted"] > 0
+    assert set(node["pool_reject_reasons"] or {}) <= {"stale-job"}
+    js = node["job_switch"]
+    assert node["pool_rejected"] == js["stale_rejects"]
+    assert js["missing"] == 0 and all(v["samples"] == js["blocks"] for v in js["per_rank"].values())
     assert set(node["collectives"]) == {"rank0", *(f"rank{r}" for r in range(1, n))}
     assert all(c > 0 for c in node["collectives"].values())
     # remote ranks' shares crossed R2 and were accepted; CPU miners carry no kernel clock, so the host timeline is used
@@ -175,7 +180,8 @@ def test_node_section_json_contract(n):
 @pytest.mark.timeout(300)
 def test_pool_and_cpu_sections_json_contract():
     """BASELINE configs 1 and 5 in the bench JSON: the native CPU miner (single thread, all cores) and the mixed
-    SHA-256d + scrypt pool with vardiff (here CPU miners for both algorithms)."""
+    SHA-256d + scrypt pool with vardiff (here CPU miners for both algorithms), windowed once every worker converged
+    (VERDICT r4 item 5), with the pool's flood capacity beside it."""
     res = _bench("--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--pool-seconds", "3", "--cpu-seconds", "0.5",
                  timeout=280)
     assert res.returncode == 0, res.stderr[-3000:]
@@ -187,6 +193,13 @@ def test_pool_and_cpu_sections_json_contract():
     assert set(pool["algorithms"]) == {"sha256d", "scrypt"}
     for algo, a in pool["algorithms"].items():
         assert a["accepted_total"] > 0 and a["rejected_total"] == 0, (algo, a)
-        assert a["validate_ms"]["p50"] is not None and a["validate_ms"]["samples"] == a["accepted_total"]
+        # validation quantiles over the window only (the pool's timed log), the whole run's beside them
+        assert a["validate_ms"]["p50"] is not None and abs(a["validate_ms"]["samples"] - a["accepted"]) <= 3
+        assert a["validate_ms_whole_run"]["samples"] == a["accepted_total"]
         assert a["workers"] and all(w["difficulty"] > 0 for w in a["workers"])
+        for w in a["workers"]:  # the window opened after the worker's last large retarget
+            assert w["converged_after_s"] <= w["window_opened_after_s"] or not pool["steady_state"], w
+            assert w["share_interval_s"] and w["interval_vs_target"] > 0
         assert all(m["exit_code"] == 0 for m in a["miners"])
+        assert pool["flood"][algo]["validated_shares_per_sec"] > 100 and pool["flood"][algo]["rejected"] == 0
+    assert pool["time_to_steady_s"] >= pool["time_to_first_accept_s"] > 0
