@@ -106,12 +106,18 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # node mode (otedama node / torchrun): one rank per GPU; rank 0 is the pool-facing engine. A rank the
         # supervisor restarted after a loss joins the running node instead of forming it.
+        from otedama_amd.engine.run import mark_early
+
+        mark_early("torch_import")
         from otedama_amd.parallel.comm import NodeComm, init_from_env, join_from_env
+
+        mark_early("torch_imported")
 
         # a replacement process: followers join the running node; rank 0 restarted by the supervisor takes the
         # node over as its leader (parallel/node.py NodeMinerSet._take_over)
         joining = os.environ.get("OTEDAMA_NODE_JOIN") == "1"
         info = join_from_env() if joining else init_from_env()
+        mark_early("process_group_ready")
         # the rank's HIP ordinal (init_from_env maps local ranks onto the visible GPUs; on an 8-GPU node it is the
         # local rank, on a 1-GPU rehearsal over gloo every rank shares GPU 0)
         cfg.mining.gpus = str(info.device.index if info.device.type == "cuda" else info.local_rank)

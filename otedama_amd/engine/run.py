@@ -130,6 +130,15 @@ def mask_addr(a: str) -> str:
 
 
 
+# Start-up marks taken before the engine exists (otedama run in node mode: torch import, the process group's
+# rendezvous); the engine starts its own marks from these (startup phases in /debug/stats and the node report).
+EARLY_MARKS: dict[str, float] = {}
+
+
+def mark_early(name: str) -> None:
+    EARLY_MARKS.setdefault(name, time.time())
+
+
 def _process_start_wall() -> float:
     """Wall-clock time this process started, to ~10 ms: its start in clock ticks after boot (/proc/self/stat
     field 22) against the uptime now (/proc/uptime); 0.0 where /proc is unavailable."""
@@ -153,7 +162,7 @@ class Engine:
         self.registry.register_collector(runtime_collector())
         self.algorithm = get_algorithm(self.cfg.mining.algorithm)
         self.start_time = opts.clock.now()
-        self._marks: dict[str, float] = {}
+        self._marks: dict[str, float] = dict(EARLY_MARKS)
         self.devices: list = []
         self.miners: MinerSet | None = None
         self.curtailed = False
@@ -422,6 +431,19 @@ class Engine:
                 "job_set_at": list(ms.job_set_at), "job_bcast_at": list(ms.job_bcast_at)})
         # (epoch, CLOCK_MONOTONIC) of each new work's first batch running: rank 0's devices and every follower's
         # heartbeat (the node job-switch probe, parallel/node_probe.py)
+        # start-up of this rank, seconds after its process started: torch imported, process group formed, engine
+        # phases (devices, miners, pool connect, first job), and the device process's first batch
+        t0 = getattr(self, "_t0_wall", None)
+        if t0 is None:
+            t0 = self._t0_wall = _process_start_wall()
+        if t0:
+            ph = {k: round(v - t0, 3) for k, v in self._marks.items()}
+            for m in getattr(getattr(ms, "local", ms), "miners", []) or []:
+                wall = float(getattr(m.native, "first_hash_wall", 0.0) or 0.0)
+                if wall:
+                    ph.setdefault("first_batch_running", round(wall - t0, 3))
+            rep["startup_phases_s"] = ph
+            rep["process_start_wall"] = t0
         local = getattr(ms, "local", ms)
         ws = {"rank0": sorted(tuple(x) for st in (local.device_stats().values() if local is not None else [])
                               for x in (st.get("work_started") or []))[-32:]}

@@ -115,7 +115,7 @@ def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> Di
     store = None
     if not dist.is_initialized():
         store = _connect_store(rank, world)
-        kw = {"device_id": device} if backend == "nccl" else {}
+        kw = {"device_id": device, "pg_options": rccl_pg_options()} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 store=dist.PrefixStore("otd-g0", store),
                                 timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
@@ -162,31 +162,54 @@ class NodeComm:
 
     ``host_buffers=True``: the buffers live in host memory and there is no comm stream. That is the node's layout
     over gloo, a CPU transport: with device buffers every gloo collective adds device<->host staging and stream
-    syncs (a 2-rank R2 gather took 4.7 ms p50 on the MI355X that way)."""
+    syncs (a 2-rank R2 gather took 4.7 ms p50 on the MI355X that way).
+
+    On a GPU every op keeps ALL of its device work on the comm stream, a high-priority stream: the staged inputs
+    (pinned host -> device), the collective (RCCL's own stream waits on it; the process group is created with
+    high-priority RCCL streams, ``rccl_pg_options``) and the results (device -> pinned host). The GPU is saturated by
+    the sibling device process's mining grid, and any kernel or blit of this process on a normal-priority queue waits
+    behind it for a CU slot: an R2 gather with its copies on the default stream took 5.3 ms p50 under a SHA-256d miner
+    against 0.16 ms idle (profiles/r5/c_comm_load). ``staging="legacy"`` keeps that old layout for the A/B."""
 
     def __init__(self, info: DistInfo, bounded: bool = False, deadline: float = 3.0, host_buffers: bool = False,
-                 force: bool = False, stream_priority: int | None = None):
+                 force: bool = False, stream_priority: int | str | None = "high", staging: str = "stream"):
         """``force``: issue the collectives at world 1 too (a one-rank process group must exist): the comm-under-load
         probe (parallel/comm_probe.py) measures the data plane's own path on a single GPU that way.
-        ``stream_priority``: priority of the comm stream (None = normal; lower = higher priority, as HIP's)."""
+        ``stream_priority``: "high" (default), None (normal) or a HIP priority (lower = higher).
+        ``staging``: "stream" (copies on the comm stream through pinned host buffers) or "legacy"."""
+        if staging not in ("stream", "legacy"):
+            raise ValueError("staging must be 'stream' or 'legacy'")
         self.info = info
         self.bounded = bounded
         self.deadline = deadline
         self.force = force
+        self.staging = staging
         self.collectives = 0  # device collectives issued by this rank (node tick accounting)
         dev = torch.device("cpu") if host_buffers else info.device
         self.dev = dev
-        self._job = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8, device=dev)
-        self._slots = torch.zeros(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
-        self._counters = torch.zeros(COUNTER_WORDS, dtype=torch.int64, device=dev)
-        self._ctl = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.cuda = dev.type == "cuda"
+        self._job, self._job_h = self._pair(JOB_BLOB_BYTES, dtype=torch.uint8)
+        self._slots, self._slots_h = self._pair(SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64)
+        self._counters, self._counters_h = self._pair(COUNTER_WORDS, dtype=torch.int64)
+        self._ctl, self._ctl_h = self._pair(4, dtype=torch.int64)
+        self._max, self._max_h = self._pair(1, dtype=torch.float64)
         self._alloc_world(max(info.world_size, 1))
-        if dev.type != "cuda":
+        if not self.cuda:
             self.stream = None
-        elif stream_priority is None:
-            self.stream = torch.cuda.Stream(dev)
         else:
-            self.stream = torch.cuda.Stream(dev, priority=stream_priority)
+            if stream_priority == "high":
+                lo, hi = torch.cuda.Stream.priority_range()
+                stream_priority = min(lo, hi)
+            self.stream = torch.cuda.Stream(dev) if stream_priority is None else \
+                torch.cuda.Stream(dev, priority=int(stream_priority))
+
+    def _pair(self, *shape, dtype):
+        """(device buffer, host mirror): the mirror is pinned on a GPU (async copies on the comm stream) and is the
+        buffer itself on the CPU."""
+        d = torch.zeros(*shape, dtype=dtype, device=self.dev)
+        if not self.cuda:
+            return d, d
+        return d, torch.zeros(*shape, dtype=dtype, pin_memory=True)
 
     @property
     def multi(self) -> bool:
@@ -194,9 +217,8 @@ class NodeComm:
         return self.info.world_size > 1 or self.force
 
     def _alloc_world(self, world: int) -> None:
-        dev = self.dev
-        self._gathered = torch.zeros(world, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64, device=dev)
-        self._counter_rows = torch.zeros(world, COUNTER_WORDS, dtype=torch.int64, device=dev)
+        self._gathered, self._gathered_h = self._pair(world, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64)
+        self._counter_rows, self._counter_rows_h = self._pair(world, COUNTER_WORDS, dtype=torch.int64)
 
     # ---------------------------------------------------------------- group generations
     def abort(self) -> None:
@@ -225,15 +247,65 @@ class NodeComm:
         self.abort()
         rank, world = members.index(info.orig_rank), len(members)
         if world > 1:
-            kw = {"device_id": info.device} if info.backend == "nccl" else {}
+            kw = {"device_id": info.device, "pg_options": rccl_pg_options()} if info.backend == "nccl" else {}
             dist.init_process_group(backend=info.backend, rank=rank, world_size=world,
                                     store=dist.PrefixStore(f"otd-g{generation}", info.store),
                                     timeout=datetime.timedelta(seconds=PG_TIMEOUT_S), **kw)
         info.rank, info.world_size, info.generation, info.members = rank, world, generation, list(members)
         self._alloc_world(world)
 
+    # ---------------------------------------------------------------- one op
+    def _poll(self, done) -> None:
+        """Wait for ``done()`` against the deadline: yield-only for the first 2 ms (a gather of the share slots
+        completes in ~0.2 ms once every rank is in it), then 0.2 ms sleeps."""
+        now = time.monotonic()
+        end, spin_until = now + self.deadline, now + 0.002
+        while not done():
+            now = time.monotonic()
+            if now > end:
+                raise CollectiveTimeout(f"collective did not finish in {self.deadline:.1f} s")
+            time.sleep(0.0 if now < spin_until else 0.0002)
+
+    def _op(self, h2d: list, start, d2h: list) -> None:
+        """One data-plane op: inputs staged host -> device, the collective ``start(async_op)``, results device ->
+        host. ``h2d`` / ``d2h`` are (destination, source) pairs. Without a collective (world 1) the result is the
+        input, copied on the host."""
+        if not self.cuda:
+            if self.multi:
+                self._collect(start)
+            return
+        if self.staging == "legacy":  # copies on the caller's stream, the collective on the comm stream
+            for d, h in h2d:
+                d.copy_(h)
+            if self.multi:
+                self._collect(start)
+            for h, d in d2h:
+                h.copy_(d)
+            return
+        s = self.stream
+        with torch.cuda.stream(s):
+            for d, h in h2d:
+                d.copy_(h, non_blocking=True)
+            if self.multi:
+                self.collectives += 1
+                if self.bounded:
+                    work = start(True)
+                    self._poll(work.is_completed)
+                    work.wait()  # re-raises a failed collective; the comm stream waits on RCCL's
+                else:
+                    start(False)
+            for h, d in d2h:
+                h.copy_(d, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(s)
+        if self.bounded:
+            self._poll(ev.query)
+        else:
+            ev.synchronize()
+
     def _collect(self, start) -> None:
-        """Run one collective. ``start(async_op)`` issues it; bounded mode polls the Work against the deadline."""
+        """Run one collective (CPU buffers, or the legacy staging). ``start(async_op)`` issues it; bounded mode polls
+        the Work against the deadline."""
         self.collectives += 1
         if not self.bounded:
             self._run(lambda: start(False))
@@ -245,15 +317,7 @@ class NodeComm:
                 work = start(True)
         else:
             work = start(True)
-        # poll: yield-only for the first 2 ms (a gather of the share slots completes in ~0.2 ms once every rank is
-        # in it), then 0.2 ms sleeps up to the deadline
-        now = time.monotonic()
-        end, spin_until = now + self.deadline, now + 0.002
-        while not work.is_completed():
-            now = time.monotonic()
-            if now > end:
-                raise CollectiveTimeout(f"collective did not finish in {self.deadline:.1f} s")
-            time.sleep(0.0 if now < spin_until else 0.0002)
+        self._poll(work.is_completed)
         work.wait()  # re-raises a failed collective (gloo: a peer's connection closed)
         if self.stream is not None:
             self.stream.synchronize()
@@ -266,12 +330,12 @@ class NodeComm:
             if len(payload) + 4 > JOB_BLOB_BYTES:
                 raise ValueError(f"job blob too large for broadcast ({len(payload)} bytes)")
             buf = len(payload).to_bytes(4, "little") + payload
-            host = torch.zeros(JOB_BLOB_BYTES, dtype=torch.uint8)
-            host[: len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
-            self._job.copy_(host)
+            self._job_h.zero_()
+            self._job_h[: len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
         if self.multi:
-            self._collect(lambda a: dist.broadcast(self._job, src=0, async_op=a))
-        host = self._job.cpu().numpy().tobytes()
+            self._op([(self._job, self._job_h)], lambda a: dist.broadcast(self._job, src=0, async_op=a),
+                     [(self._job_h, self._job)])
+        host = self._job_h.numpy().tobytes()
         n = int.from_bytes(host[:4], "little")
         if n == 0:
             return None
@@ -287,14 +351,16 @@ class NodeComm:
             rows[i] = (e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
                        en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
                        int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6))
-        self._slots.copy_(torch.from_numpy(rows))
+        self._slots_h.copy_(torch.from_numpy(rows))
         if self.multi:
-            self._collect(lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
-                                                                async_op=a))
+            self._op([(self._slots, self._slots_h)],
+                     lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
+                                                           async_op=a),
+                     [(self._gathered_h, self._gathered)])
         else:
-            self._gathered[0].copy_(self._slots)
+            self._gathered_h[0].copy_(self._slots_h)
         out = []
-        g = self._gathered.cpu().numpy()
+        g = self._gathered_h.numpy()
         for r, i in zip(*np.nonzero(g[:, :, 1] >> 31)):  # valid records only, in rank then slot order
             r, rec = int(r), g[r, i].tolist()
             out.append({
@@ -308,35 +374,41 @@ class NodeComm:
 
     # ---------------------------------------------------------------- R3
     def allreduce_counters(self, hashes: int, shares: int = 0, dropped: int = 0, faults: int = 0) -> tuple:
-        self._counters.copy_(torch.tensor([hashes, shares, dropped, faults], dtype=torch.int64))
+        self._counters_h.copy_(torch.tensor([hashes, shares, dropped, faults], dtype=torch.int64))
         if self.multi:
-            self._collect(lambda a: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM, async_op=a))
-        return tuple(int(x) for x in self._counters.cpu().tolist())
+            self._op([(self._counters, self._counters_h)],
+                     lambda a: dist.all_reduce(self._counters, op=dist.ReduceOp.SUM, async_op=a),
+                     [(self._counters_h, self._counters)])
+        return tuple(int(x) for x in self._counters_h.tolist())
 
     def gather_counters(self, values: list[int]) -> list[list[int]]:
         """R3 variant for per-device stats: every rank's COUNTER_WORDS counters (all_gather, 32 B/rank)."""
         mine = torch.tensor(list(values)[:COUNTER_WORDS] + [0] * (COUNTER_WORDS - len(values)), dtype=torch.int64)
-        self._counters.copy_(mine)
+        self._counters_h.copy_(mine)
         if self.multi:
-            self._collect(lambda a: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters,
-                                                                async_op=a))
+            self._op([(self._counters, self._counters_h)],
+                     lambda a: dist.all_gather_into_tensor(self._counter_rows.view(-1), self._counters, async_op=a),
+                     [(self._counter_rows_h, self._counter_rows)])
         else:
-            self._counter_rows[0].copy_(self._counters)
-        return self._counter_rows.cpu().tolist()
+            self._counter_rows_h[0].copy_(self._counters_h)
+        return self._counter_rows_h.tolist()
 
     def broadcast_control(self, words: list[int]) -> list[int]:
         """R1 control word (seq, stop, ...): 4 int64, every tick; the job blob follows only on change."""
         if self.info.is_primary:
-            self._ctl.copy_(torch.tensor(list(words)[:4] + [0] * (4 - len(words)), dtype=torch.int64))
+            self._ctl_h.copy_(torch.tensor(list(words)[:4] + [0] * (4 - len(words)), dtype=torch.int64))
         if self.multi:
-            self._collect(lambda a: dist.broadcast(self._ctl, src=0, async_op=a))
-        return self._ctl.cpu().tolist()
+            self._op([(self._ctl, self._ctl_h)], lambda a: dist.broadcast(self._ctl, src=0, async_op=a),
+                     [(self._ctl_h, self._ctl)])
+        return self._ctl_h.tolist()
 
     def allreduce_max(self, value: float) -> float:
-        t = torch.tensor([value], dtype=torch.float64, device=self.dev)
+        self._max_h.fill_(value)
         if self.multi:
-            self._collect(lambda a: dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=a))
-        return float(t.item())
+            self._op([(self._max, self._max_h)],
+                     lambda a: dist.all_reduce(self._max, op=dist.ReduceOp.MAX, async_op=a),
+                     [(self._max_h, self._max)])
+        return float(self._max_h.item())
 
     def _run(self, fn) -> None:
         """Blocking form: the collective runs on the comm stream and the current stream waits for it (used where
@@ -365,6 +437,20 @@ class NodeComm:
         ev = torch.cuda.Event()
         ev.record(self.stream)
         return ev
+
+
+def rccl_pg_options():
+    """ProcessGroupNCCL options for the node's groups: RCCL's internal streams at high priority, so a collective's
+    kernel is dispatched ahead of the mining grid of the sibling device process (OTEDAMA_RCCL_HIGH_PRIORITY=0 turns
+    it off)."""
+    if os.environ.get("OTEDAMA_RCCL_HIGH_PRIORITY", "1") == "0":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except Exception:  # noqa: BLE001 - a torch without the NCCL backend
+        return None
 
 
 def _encode(obj):

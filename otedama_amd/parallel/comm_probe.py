@@ -21,7 +21,12 @@ kernels keep running while R2/R3 move.
 from __future__ import annotations
 
 import statistics
+import sys
 import time
+
+
+def _say(msg: str) -> None:
+    print(f"[comm_probe] {msg}", file=sys.stderr, flush=True)
 
 
 def _q(xs: list[float]) -> dict:
@@ -82,57 +87,69 @@ def run_ops(comm, seconds: float, cadence_hz: float = 50.0, probe_kernel: bool =
     return {k: _q(v) for k, v in lat.items() if v}
 
 
-def _one_rank_group(device) -> bool:
-    """A one-rank RCCL group as the default group; True when this call created it (the caller destroys it)."""
+# The A/B: "legacy" is the round-4 layout (staging copies on the caller's stream, RCCL's streams and the comm stream
+# at normal priority); "node" is the node's layout now (every copy on a high-priority comm stream through pinned
+# buffers, RCCL's streams at high priority: comm.rccl_pg_options).
+CONFIGS = {"legacy": {"pg_high": False, "staging": "legacy", "stream_priority": None},
+           "node": {"pg_high": True, "staging": "stream", "stream_priority": "high"}}
+
+
+def _one_rank_group(device, high: bool) -> None:
+    """A one-rank RCCL group as the default group (the probe's own: it is destroyed after each window)."""
     import torch.distributed as dist
 
-    if dist.is_initialized():
-        return False
-    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=device)
-    return True
+    opts = None
+    if high:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=device,
+                            pg_options=opts)
+
+
+def _with_config(dev, device_index: int, name: str, fn):
+    """Run ``fn(comm)`` with config ``name``'s process group and NodeComm, then tear the group down."""
+    import torch.distributed as dist
+
+    from otedama_amd.parallel.comm import DistInfo, NodeComm
+
+    cfg = CONFIGS[name]
+    _one_rank_group(dev, cfg["pg_high"])
+    try:
+        comm = NodeComm(DistInfo(0, 1, device_index, "nccl", dev), bounded=True, deadline=10.0, force=True,
+                        stream_priority=cfg["stream_priority"], staging=cfg["staging"])
+        run_ops(comm, 0.3)  # warm: RCCL communicator, allocator, kernels
+        return fn(comm)
+    finally:
+        dist.destroy_process_group()
 
 
 def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scrypt"), seconds: float = 4.0,
                             cadence_hz: float = 50.0, windows: int = 2) -> dict:
-    """See the module docstring. Per algorithm: op latency idle / loaded at normal and high comm-stream priority,
-    and the miner's rate over alternating windows without / with the ops."""
+    """See the module docstring. Per configuration (CONFIGS) and algorithm: op latency idle / loaded, and the
+    miner's rate over alternating windows without / with the ops."""
     import torch
-
-    dev = torch.device(f"cuda:{device_index}")
-    torch.cuda.set_device(dev)
-    created = _one_rank_group(dev)
-    try:
-        return _measure(dev, device_index, algorithms, seconds, cadence_hz, windows)
-    finally:
-        if created:
-            import torch.distributed as dist
-
-            dist.destroy_process_group()
-
-
-def _measure(dev, device_index: int, algorithms, seconds: float, cadence_hz: float, windows: int) -> dict:
-    import torch
+    import torch.distributed as dist
 
     from otedama_amd import hal
     from otedama_amd.engine.latency_probe import _switch_job
     from otedama_amd.engine.miners import MinerSet
-    from otedama_amd.parallel.comm import DistInfo, NodeComm
 
-    info = DistInfo(0, 1, device_index, "nccl", dev)
-    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
-    comms = {"normal": NodeComm(info, bounded=True, deadline=10.0, force=True),
-             "high": NodeComm(info, bounded=True, deadline=10.0, force=True, stream_priority=min(lo, hi))}
-    for c in comms.values():  # warm: RCCL communicator, allocator, kernels
-        run_ops(c, 0.3, cadence_hz)
-    out: dict = {"idle": {p: run_ops(c, seconds, cadence_hz) for p, c in comms.items()},
-                 "rccl_world": 1, "cadence_hz": cadence_hz,
+    if dist.is_initialized():
+        raise RuntimeError("the comm probe needs the default process group to itself")
+    dev = torch.device(f"cuda:{device_index}")
+    torch.cuda.set_device(dev)
+    _say("idle phase")
+    out: dict = {"idle": {c: _with_config(dev, device_index, c, lambda comm: run_ops(comm, seconds, cadence_hz))
+                          for c in CONFIGS},
+                 "configs": CONFIGS, "rccl_world": 1, "cadence_hz": cadence_hz,
                  "definition": ("rank-process call -> result on the host for R1 (64 KiB job blob), R2 (share slots "
-                                "all_gather) and R3 (counters all_gather) on the comm stream of a forced one-rank RCCL "
-                                "group; 'kernel' = a 16 KiB elementwise kernel on the comm stream, enqueue -> done")}
+                                "all_gather) and R3 (counters all_gather) of a forced one-rank RCCL group; 'kernel' = "
+                                "a 16 KiB elementwise kernel on the comm stream, enqueue -> done")}
     devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
     if not devs:
         raise RuntimeError(f"no KFD GPU node for device {device_index}")
     for algo in algorithms:
+        _say(f"{algo}: miner up, alternating windows")
         ms = MinerSet(devs, algo, 1 << 32, 0, isolation="process")
         dp = ms.miners[0].native
         ms.start()
@@ -142,17 +159,20 @@ def _measure(dev, device_index: int, algorithms, seconds: float, cadence_hz: flo
                 time.sleep(0.01)
             ms.set_job(_switch_job(0, algo))
             time.sleep(3.0 if algo == "scrypt" else 1.5)  # allocations, first launches
-            res: dict = {"loaded": {}, "rate_alone": [], "rate_with_ops": {p: [] for p in comms}}
+            res: dict = {"loaded": {}, "rate_alone": [], "rate_with_ops": {c: [] for c in CONFIGS}}
             for w in range(windows):
                 a = _counter(dp)
                 time.sleep(seconds)
                 res["rate_alone"].append(_miner_rate(dp, a, _counter(dp)))
-                for p, c in comms.items():
-                    a = _counter(dp)
-                    r = run_ops(c, seconds, cadence_hz)
-                    res["rate_with_ops"][p].append(_miner_rate(dp, a, _counter(dp)))
-                    if w == 0:
-                        res["loaded"][p] = r
+                for c in CONFIGS:
+                    def window(comm, c=c, w=w):
+                        a = _counter(dp)
+                        r = run_ops(comm, seconds, cadence_hz)
+                        res["rate_with_ops"][c].append(_miner_rate(dp, a, _counter(dp)))
+                        if w == 0:
+                            res["loaded"][c] = r
+
+                    _with_config(dev, device_index, c, window)
             st = dp.stats()
             if st.get("faulted"):
                 raise RuntimeError(st.get("error"))
@@ -161,8 +181,8 @@ def _measure(dev, device_index: int, algorithms, seconds: float, cadence_hz: flo
         alone = [r for r in res["rate_alone"] if r]
         base = statistics.fmean(alone) if alone else None
         res["rate_alone_hps"] = base
-        res["rate_loss_pct"] = {p: (100.0 * (1.0 - statistics.fmean([r for r in v if r]) / base)
-                                    if base and any(v) else None) for p, v in res["rate_with_ops"].items()}
+        res["rate_loss_pct"] = {c: (100.0 * (1.0 - statistics.fmean([r for r in v if r]) / base)
+                                    if base and any(v) else None) for c, v in res["rate_with_ops"].items()}
         out[algo] = res
     return out
 

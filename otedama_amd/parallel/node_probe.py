@@ -192,7 +192,7 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
     env["OTEDAMA_PG_TIMEOUT"] = "60"
     if cpu:
         env.update(OTEDAMA_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    t_spawn = time.monotonic()
+    t_spawn, t_spawn_wall = time.monotonic(), time.time()
     out = open(log_path, "w")
     sup = subprocess.Popen([sys.executable, "-m", "otedama_amd", "node", "--gpus", str(gpus), "--config", cfg,
                             "--no-tui"], env=env, cwd=ROOT, stdout=out, stderr=subprocess.STDOUT)
@@ -217,6 +217,11 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
         else:
             raise RuntimeError(f"node not ready within {startup_timeout:.0f} s")
         res["startup_s"] = time.monotonic() - t_spawn
+        # where the start-up goes: seconds after rank 0's process started (torch import, rendezvous, engine phases,
+        # the device process's first batch), and the supervisor's spawn -> rank 0's process start
+        res["startup_phases_s"] = rep.get("startup_phases_s")
+        if rep.get("process_start_wall"):
+            res["supervisor_to_rank0_start_s"] = round(rep["process_start_wall"] - t_spawn_wall, 3)
         time.sleep(warmup)
         t0 = time.monotonic()
         time.sleep(seconds)
