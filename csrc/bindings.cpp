@@ -134,6 +134,7 @@ py::dict stats_to_dict(const MinerStats& s) {
   d["last_job_switch_ms"] = s.last_job_switch_ms;
   d["job_switch_ms"] = s.job_switch_ms;
   d["work_started"] = s.work_started;
+  d["reserved_cus"] = s.reserved_cus;
   d["ring_overflow"] = s.ring_overflow;
   d["verify_dropped"] = s.verify_dropped;
   d["verify_queue_peak"] = s.verify_queue_peak;
@@ -411,6 +412,10 @@ PYBIND11_MODULE(_native, m) {
   m.def("gpu_arch_name", &gpu_arch_name);
   m.def("gpu_cu_count", &gpu_cu_count);
   m.def("scrypt_scratch_bytes", &scrypt_scratch_bytes);
+  // test hook: the /proc/self/maps check behind the CPU-stored abort word (GpuMiner host_abort)
+  m.def("maps_range_writable", [](const std::string& maps, uint64_t lo, uint64_t hi) {
+    return maps_range_writable(maps, uintptr_t(lo), uintptr_t(hi));
+  });
   m.def("launch_sha256d", [](const py::bytes& params, uint32_t base, uint64_t count, uintptr_t out, uint32_t cap,
                              int grid, uintptr_t stream) {
     std::string ps = need(params, sizeof(Sha256dParams), "params");

@@ -102,6 +102,7 @@ struct MinerStats {
   double clock_calib_rtt_us = 0;      // round trip of the start-up device-clock calibration
   uint64_t clock_samples = 0;         // per-launch clock stamps folded into the device -> host clock mapping
   bool host_abort = false;            // the abort word is stored by the CPU through the BAR (no control stream)
+  uint64_t reserved_cus = 0;          // CUs left out of the search streams' CU mask (OTEDAMA_RESERVE_CUS)
   // Device-timeline time (s, from the miner's start) at which the batches counted in `hashes` had completed: a
   // rate over two samples, (hashes1 - hashes0) / (done_at1 - done_at0), is exact instead of quantized by launches.
   double hashes_done_at_s = 0;
@@ -225,5 +226,9 @@ std::vector<uint32_t> cpu_scan_sha256d_lanes(int lanes, const uint8_t header80[8
 
 // Seconds on CLOCK_MONOTONIC (same clock as Python time.monotonic()).
 double monotonic_seconds();
+
+// True when [lo, hi) lies inside one line of a /proc/<pid>/maps text whose permissions are read AND write. A range the
+// GPU runtime reserved with PROT_NONE ("---p") does not qualify: the CPU would fault on its first store.
+bool maps_range_writable(const std::string& maps, uintptr_t lo, uintptr_t hi);
 
 }  // namespace otedama

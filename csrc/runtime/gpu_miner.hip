@@ -110,8 +110,10 @@ constexpr auto kIdlePoll = std::chrono::microseconds(100);
 constexpr double kClockWindowS = 2.0;  // per-launch clock bounds kept for the device -> host mapping
 
 // Let the CPU store to a device allocation directly: grant the CPU agent access (the allocation is VRAM, reachable
-// through the PCIe BAR when the runtime exposes it) and confirm that the range is now mapped in this process before
-// anything touches it. False leaves the word device-only (stores then go through a stream).
+// through the PCIe BAR when the runtime exposes it) and confirm that the range is now mapped READ-WRITE in this process
+// before anything touches it. libhsakmt reserves the GPU virtual-address range with PROT_NONE, so a mapping line alone
+// proves nothing (small BAR, a VF without a mapped BAR): maps_range_writable requires the rw permissions. False leaves
+// the word device-only (stores then go through a stream). The caller still verifies a store by reading it back.
 bool cpu_store_map(void* p, size_t n) {
   hsa_agent_t cpu{};
   auto pick = [](hsa_agent_t a, void* data) -> hsa_status_t {
@@ -126,15 +128,13 @@ bool cpu_store_map(void* p, size_t n) {
   if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS) return false;
   FILE* f = std::fopen("/proc/self/maps", "r");
   if (!f) return false;
-  const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + n;
-  char line[512];
-  bool mapped = false;
-  while (!mapped && std::fgets(line, sizeof line, f)) {
-    unsigned long a = 0, b = 0;
-    mapped = std::sscanf(line, "%lx-%lx", &a, &b) == 2 && a <= lo && hi <= b;
-  }
+  std::string maps;
+  char buf[4096];
+  size_t got;
+  while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) maps.append(buf, got);
   std::fclose(f);
-  return mapped;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  return maps_range_writable(maps, lo, lo + n);
 }
 
 // Header variants of one stripe group (up to 128 consecutive positions sharing block 2). Built once per
@@ -276,9 +276,35 @@ void GpuMiner::loop() {
   // OTEDAMA_SEARCH_STREAMS=1 the batches share one stream (one hardware queue less, 173 MiB of host memory).
   const char* ss_env = std::getenv("OTEDAMA_SEARCH_STREAMS");
   const bool one_stream = ss_env && std::atoi(ss_env) == 1;
+  // OTEDAMA_RESERVE_CUS=<cu>,<cu>,...: the search streams get a CU mask without these CUs, so a kernel of another
+  // process on the same GPU (a node rank's RCCL collective) finds a free slot at once instead of waiting for a
+  // mining workgroup to finish (parallel/comm_probe.py measures the trade: the reserved CUs' share of the rate).
+  std::vector<uint32_t> cu_mask;
+  int reserved = 0;
+  if (const char* rc_env = std::getenv("OTEDAMA_RESERVE_CUS")) {
+    const int ncu = gpu_cu_count(device_) > 0 ? gpu_cu_count(device_) : 256;
+    cu_mask.assign((ncu + 31) / 32, 0xFFFFFFFFu);
+    if (ncu % 32) cu_mask.back() = (1u << (ncu % 32)) - 1u;
+    for (const char* q = rc_env; *q;) {
+      char* end = nullptr;
+      const long cu = std::strtol(q, &end, 10);
+      if (end == q) break;
+      if (cu >= 0 && cu < ncu && (cu_mask[cu / 32] >> (cu % 32) & 1u)) {
+        cu_mask[cu / 32] &= ~(1u << (cu % 32));
+        ++reserved;
+      }
+      q = (*end == ',') ? end + 1 : end;
+    }
+  }
   for (int i = 0; i < kInflight; ++i) {
     if (one_stream && i > 0) slots[i].stream = slots[0].stream;
+    else if (reserved > 0)
+      OTD_HIP(hipExtStreamCreateWithCUMask(&slots[i].stream, uint32_t(cu_mask.size()), cu_mask.data()));
     else OTD_HIP(hipStreamCreateWithFlags(&slots[i].stream, hipStreamNonBlocking));
+  }
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.reserved_cus = uint64_t(reserved);
   }
   // The abort word must never wait behind a search kernel. The CPU stores it itself when it can map the word
   // (OTEDAMA_HOST_ABORT=0 forces the stream form). Otherwise the store goes on a high-priority stream: HIP
@@ -293,6 +319,22 @@ void GpuMiner::loop() {
   OTD_HIP(hipStreamSynchronize(slots[0].stream));
   const char* ha_env = std::getenv("OTEDAMA_HOST_ABORT");
   host_abort = !(ha_env && ha_env[0] == '0') && cpu_store_map(d_abort, 256);
+  if (host_abort) {
+    // Prove the path before trusting it: a CPU store must land in VRAM where the device (a copy on a search stream)
+    // reads it back. Anything else (a mapping that swallows writes) falls back to the control stream.
+    for (uint32_t probe : {0xA5C3E10Fu, 0u}) {
+      __atomic_store_n(d_abort, probe, __ATOMIC_RELEASE);
+      _mm_sfence();
+      uint32_t back = ~probe;
+      OTD_HIP(hipMemcpyAsync(&back, d_abort, sizeof back, hipMemcpyDeviceToHost, slots[0].stream));
+      OTD_HIP(hipStreamSynchronize(slots[0].stream));
+      if (back != probe) { host_abort = false; break; }
+    }
+    if (!host_abort) {  // the word must read 0 whichever path stores it from now on
+      OTD_HIP(hipMemsetAsync(d_abort, 0, 256, slots[0].stream));
+      OTD_HIP(hipStreamSynchronize(slots[0].stream));
+    }
+  }
   if (!host_abort) {
     int prio_lo = 0, prio_hi = 0;
     OTD_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -700,6 +701,21 @@ void CpuMiner::loop(int /*tid*/) {
 }  // namespace otedama
 
 namespace otedama {
+bool maps_range_writable(const std::string& maps, uintptr_t lo, uintptr_t hi) {
+  size_t pos = 0;
+  while (pos < maps.size()) {
+    size_t eol = maps.find('\n', pos);
+    if (eol == std::string::npos) eol = maps.size();
+    const std::string line = maps.substr(pos, eol - pos);
+    pos = eol + 1;
+    unsigned long a = 0, b = 0;
+    char perms[8] = {0};
+    if (std::sscanf(line.c_str(), "%lx-%lx %7s", &a, &b, perms) != 3) continue;
+    if (a <= lo && hi <= b) return perms[0] == 'r' && perms[1] == 'w';
+  }
+  return false;
+}
+
 double monotonic_seconds() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);

@@ -124,9 +124,11 @@ def _with_config(dev, device_index: int, name: str, fn):
 
 
 def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scrypt"), seconds: float = 4.0,
-                            cadence_hz: float = 50.0, windows: int = 2) -> dict:
+                            cadence_hz: float = 50.0, windows: int = 2, reserves=("",)) -> dict:
     """See the module docstring. Per configuration (CONFIGS) and algorithm: op latency idle / loaded, and the
-    miner's rate over alternating windows without / with the ops."""
+    miner's rate over alternating windows without / with the ops. ``reserves``: OTEDAMA_RESERVE_CUS specs to run
+    the miner with ("" = none; e.g. "0" keeps CU 0 out of the mining kernels' CU mask); each non-empty one is
+    reported under "<algo>@reserve:<spec>" with the node configuration only."""
     import torch
     import torch.distributed as dist
 
@@ -148,8 +150,17 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
     devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
     if not devs:
         raise RuntimeError(f"no KFD GPU node for device {device_index}")
-    for algo in algorithms:
-        _say(f"{algo}: miner up, alternating windows")
+    import os
+
+    runs = [(algo, spec) for spec in reserves for algo in algorithms]
+    for algo, spec in runs:
+        key = algo if not spec else f"{algo}@reserve:{spec}"
+        configs = list(CONFIGS) if not spec else ["node"]
+        _say(f"{key}: miner up, alternating windows")
+        if spec:
+            os.environ["OTEDAMA_RESERVE_CUS"] = spec  # inherited by the device process
+        else:
+            os.environ.pop("OTEDAMA_RESERVE_CUS", None)
         ms = MinerSet(devs, algo, 1 << 32, 0, isolation="process")
         dp = ms.miners[0].native
         ms.start()
@@ -159,12 +170,12 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
                 time.sleep(0.01)
             ms.set_job(_switch_job(0, algo))
             time.sleep(3.0 if algo == "scrypt" else 1.5)  # allocations, first launches
-            res: dict = {"loaded": {}, "rate_alone": [], "rate_with_ops": {c: [] for c in CONFIGS}}
+            res: dict = {"loaded": {}, "rate_alone": [], "rate_with_ops": {c: [] for c in configs}}
             for w in range(windows):
                 a = _counter(dp)
                 time.sleep(seconds)
                 res["rate_alone"].append(_miner_rate(dp, a, _counter(dp)))
-                for c in CONFIGS:
+                for c in configs:
                     def window(comm, c=c, w=w):
                         a = _counter(dp)
                         r = run_ops(comm, seconds, cadence_hz)
@@ -176,14 +187,16 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
             st = dp.stats()
             if st.get("faulted"):
                 raise RuntimeError(st.get("error"))
+            res["reserved_cus"] = st.get("reserved_cus", 0)
         finally:
             ms.stop()
+            os.environ.pop("OTEDAMA_RESERVE_CUS", None)
         alone = [r for r in res["rate_alone"] if r]
         base = statistics.fmean(alone) if alone else None
         res["rate_alone_hps"] = base
         res["rate_loss_pct"] = {c: (100.0 * (1.0 - statistics.fmean([r for r in v if r]) / base)
                                     if base and any(v) else None) for c, v in res["rate_with_ops"].items()}
-        out[algo] = res
+        out[key] = res
     return out
 
 
@@ -197,8 +210,11 @@ def main(argv=None) -> int:
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--cadence", type=float, default=50.0)
     ap.add_argument("--windows", type=int, default=2)
+    ap.add_argument("--reserves", default="", help="';'-separated OTEDAMA_RESERVE_CUS specs besides none, e.g. '0;0,32'")
     a = ap.parse_args(argv)
-    r = measure_comm_under_load(a.device, [x for x in a.algorithms.split(",") if x], a.seconds, a.cadence, a.windows)
+    reserves = [""] + [x for x in a.reserves.split(";") if x]
+    r = measure_comm_under_load(a.device, [x for x in a.algorithms.split(",") if x], a.seconds, a.cadence, a.windows,
+                                reserves)
     print(json.dumps(r))
     return 0
 
