@@ -1,0 +1,283 @@
+// Native RCCL data plane of the multi-GPU node: R1 (job broadcast), R2 (share gather), R3 (counters), SURVEY §7.1
+// ("the RCCL comm layer (R1-R3)" in C++) and §5.8 (one comm stream per GPU, pinned host buffers on the pool side).
+//
+// One RcclComm per rank process and process-group generation (otedama_amd/parallel/rcclcomm.py owns the unique-id
+// exchange through the node's store and the generations). Design points, each measured on the MI355X
+// (profiles/r5/d_comm_ab):
+//   * every op is ONE chain on one high-priority HIP stream: pinned host staging -> device, the RCCL collective,
+//     device -> pinned host, an event. The GPU is saturated by the sibling device process's mining grid; a kernel or
+//     blit of this process on a normal-priority queue waited behind it for a CU slot (R2 4.5 ms p50 with the copies
+//     on the default stream, 1.9 ms with everything on high-priority streams);
+//   * the communicator is non-blocking (ncclConfig_t.blocking = 0): init and every op are polled against a deadline
+//     with the GIL released, so a dead peer never hangs the caller; ncclCommAbort tears a broken group down at once;
+//   * no torch in the process: the node's rank processes import only this module and the native miner bindings
+//     (start-up: `import torch` was ~1.45 s of a rank's 1.8 s to its process group, profiles/r5/c_node_rehearsal).
+//
+// The reference has no collective layer; its fan-out / fan-in are Go channels
+// (internal/engine/fanin.go:22-58), which never block a producer: the deadlines here keep that property.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <pybind11/pybind11.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+namespace py = pybind11;
+
+namespace {
+
+struct RcclTimeout : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Poll-wait: yield for the first 2 ms (a small collective completes in ~0.1-0.2 ms once every rank is in it), then
+// 100 us sleeps up to the deadline. `ready` returns 1 (done), 0 (not yet) or throws.
+template <class F>
+void wait_until(F ready, double timeout_s, const char* what) {
+  const double t0 = now_s(), end = t0 + timeout_s, spin_until = t0 + 0.002;
+  for (;;) {
+    if (ready()) return;
+    const double t = now_s();
+    if (t > end) throw RcclTimeout(std::string(what) + " did not finish in " + std::to_string(timeout_s) + " s");
+    if (t < spin_until) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
+
+class RcclComm {
+ public:
+  RcclComm(int device, int nranks, int rank, const std::string& uid, double timeout_s)
+      : device_(device), nranks_(nranks), rank_(rank) {
+    if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("unique id must be 128 bytes");
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("bad rank / nranks");
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    int lo = 0, hi = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+    hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "hipEventCreate");
+    ncclUniqueId id;
+    std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;
+      r = ncclCommInitRankConfig(&comm_, nranks_, id, rank_, &cfg);
+      if (r == ncclSuccess || r == ncclInProgress) {
+        try {
+          wait_until([&] { return settled(); }, timeout_s, "ncclCommInitRankConfig");
+          r = ncclSuccess;
+        } catch (...) {
+          abort_nogil();
+          release();
+          throw;
+        }
+      }
+    }
+    if (r != ncclSuccess) {
+      release();
+      throw std::runtime_error(std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+    }
+  }
+  ~RcclComm() {
+    abort_nogil();
+    release();
+  }
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int nranks() const { return nranks_; }
+  int rank() const { return rank_; }
+  bool alive() const { return comm_ != nullptr; }
+  uint64_t ops() const { return ops_; }
+
+  // R1: root's `data` (nbytes) to every rank; returns the nbytes every rank now holds.
+  py::bytes broadcast(const std::string& data, size_t nbytes, int root, double timeout_s) {
+    if (rank_ == root && data.size() != nbytes) throw std::invalid_argument("root's data must be nbytes long");
+    ensure(nbytes, nbytes);
+    std::string out(nbytes, '\0');
+    {
+      py::gil_scoped_release nogil;
+      if (rank_ == root) std::memcpy(host_, data.data(), nbytes);
+      run(nbytes, nbytes, timeout_s, "broadcast",
+          [&] { return ncclBroadcast(dev_, dev_, nbytes, ncclUint8, root, comm_, stream_); });
+      std::memcpy(out.data(), host_, nbytes);
+    }
+    return py::bytes(out);
+  }
+
+  // R2 / R3: every rank's `mine` (same length everywhere), concatenated in rank order.
+  py::bytes all_gather(const std::string& mine, double timeout_s) {
+    const size_t n = mine.size(), total = n * size_t(nranks_);
+    ensure(n, total);
+    std::string out(total, '\0');
+    {
+      py::gil_scoped_release nogil;
+      // in place: rank r's contribution sits at offset r * n of the receive buffer
+      std::memcpy(static_cast<char*>(host_) + size_t(rank_) * n, mine.data(), n);
+      run(n, total, timeout_s, "all_gather", [&] {
+        return ncclAllGather(static_cast<char*>(dev_) + size_t(rank_) * n, dev_, n, ncclUint8, comm_, stream_);
+      }, size_t(rank_) * n);
+      std::memcpy(out.data(), host_, total);
+    }
+    return py::bytes(out);
+  }
+
+  // R3: element-wise sum (or max) of `data` across ranks; dtype "i64" or "f64".
+  py::bytes all_reduce(const std::string& data, const std::string& dtype, const std::string& op, double timeout_s) {
+    const ncclDataType_t t = dtype == "f64" ? ncclFloat64 : ncclInt64;
+    if (dtype != "f64" && dtype != "i64") throw std::invalid_argument("dtype must be i64 or f64");
+    const ncclRedOp_t o = op == "max" ? ncclMax : ncclSum;
+    if (op != "max" && op != "sum") throw std::invalid_argument("op must be sum or max");
+    if (data.size() % 8) throw std::invalid_argument("data must be whole 8-byte elements");
+    const size_t n = data.size();
+    ensure(n, n);
+    std::string out(n, '\0');
+    {
+      py::gil_scoped_release nogil;
+      std::memcpy(host_, data.data(), n);
+      run(n, n, timeout_s, "all_reduce",
+          [&] { return ncclAllReduce(dev_, dev_, n / 8, t, o, comm_, stream_); });
+      std::memcpy(out.data(), host_, n);
+    }
+    return py::bytes(out);
+  }
+
+  // Tear the communicator down at once (a peer died, or a new generation is formed): ncclCommAbort never waits for
+  // the peers. Idempotent.
+  void abort() {
+    py::gil_scoped_release nogil;
+    abort_nogil();
+  }
+
+ private:
+  void abort_nogil() {
+    if (comm_ == nullptr) return;
+    (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+
+  // The communicator's asynchronous state: 1 = settled, 0 = in progress; throws on an error.
+  int settled() {
+    ncclResult_t st = ncclSuccess;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) throw std::runtime_error(std::string("ncclCommGetAsyncError: ") + ncclGetErrorString(q));
+    if (st == ncclInProgress) return 0;
+    if (st != ncclSuccess) throw std::runtime_error(std::string("rccl: ") + ncclGetErrorString(st));
+    return 1;
+  }
+
+  void ensure(size_t in_bytes, size_t out_bytes) {
+    const size_t need = std::max(in_bytes, out_bytes);
+    if (need <= cap_) return;
+    size_t cap = 64 << 10;
+    while (cap < need) cap *= 2;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    if (dev_) (void)hipFree(dev_);
+    if (host_) (void)hipHostFree(host_);
+    dev_ = nullptr;
+    host_ = nullptr;
+    cap_ = 0;
+    hip_check(hipMalloc(&dev_, cap), "hipMalloc");
+    hip_check(hipHostMalloc(&host_, cap, hipHostMallocDefault), "hipHostMalloc");
+    cap_ = cap;
+  }
+
+  // One op, all on the comm stream: host_[in_off, in_off + in_bytes) (placed there by the caller) -> dev_ at the same
+  // offset, the collective,
+  // dev_[0, out_bytes) -> host_, then the event polled against the deadline (and the communicator's async error).
+  template <class Start>
+  void run(size_t in_bytes, size_t out_bytes, double timeout_s, const char* what, Start start, size_t in_off = 0) {
+    if (comm_ == nullptr) throw std::runtime_error("rccl: communicator aborted");
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    char* h = static_cast<char*>(host_);
+    char* d = static_cast<char*>(dev_);
+    hip_check(hipMemcpyAsync(d + in_off, h + in_off, in_bytes, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync H2D");
+    ncclResult_t r = start();
+    if (r != ncclSuccess && r != ncclInProgress)
+      throw std::runtime_error(std::string("rccl ") + what + ": " + ncclGetErrorString(r));
+    if (r == ncclInProgress) wait_until([&] { return settled(); }, timeout_s, what);  // enqueue of a non-blocking comm
+    hip_check(hipMemcpyAsync(h, d, out_bytes, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync D2H");
+    hip_check(hipEventRecord(done_, stream_), "hipEventRecord");
+    wait_until([&] {
+      const hipError_t q = hipEventQuery(done_);
+      if (q == hipSuccess) return 1;
+      if (q != hipErrorNotReady) hip_check(q, "hipEventQuery");
+      settled();  // a failed peer surfaces here while the event never completes
+      return 0;
+    }, timeout_s, what);
+    ++ops_;
+  }
+
+  void release() {
+    if (dev_) (void)hipFree(dev_);
+    if (host_) (void)hipHostFree(host_);
+    if (done_) (void)hipEventDestroy(done_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+    dev_ = host_ = nullptr;
+    done_ = nullptr;
+    stream_ = nullptr;
+    cap_ = 0;
+  }
+
+  int device_, nranks_, rank_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t done_ = nullptr;
+  void* dev_ = nullptr;
+  void* host_ = nullptr;
+  size_t cap_ = 0;
+  uint64_t ops_ = 0;
+};
+
+py::bytes unique_id() {
+  ncclUniqueId id;
+  ncclResult_t r;
+  {
+    py::gil_scoped_release nogil;
+    r = ncclGetUniqueId(&id);
+  }
+  if (r != ncclSuccess) throw std::runtime_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  return py::bytes(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+std::string version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return std::to_string(v);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_rccl, m) {
+  m.doc() = "Native RCCL data plane of the otedama node (R1/R2/R3 on a high-priority HIP stream)";
+  py::register_exception<RcclTimeout>(m, "RcclTimeout", PyExc_TimeoutError);
+  m.def("unique_id", &unique_id, "ncclGetUniqueId: 128 bytes for the group's rank 0 to publish");
+  m.def("version", &version);
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init<int, int, int, const std::string&, double>(), py::arg("device"), py::arg("nranks"),
+           py::arg("rank"), py::arg("unique_id"), py::arg("timeout_s"))
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("alive", &RcclComm::alive)
+      .def_property_readonly("ops", &RcclComm::ops)
+      .def("broadcast", &RcclComm::broadcast, py::arg("data"), py::arg("nbytes"), py::arg("root"),
+           py::arg("timeout_s"))
+      .def("all_gather", &RcclComm::all_gather, py::arg("mine"), py::arg("timeout_s"))
+      .def("all_reduce", &RcclComm::all_reduce, py::arg("data"), py::arg("dtype"), py::arg("op"),
+           py::arg("timeout_s"))
+      .def("abort", &RcclComm::abort);
+}

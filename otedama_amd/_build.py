@@ -42,9 +42,14 @@ CXX_SOURCES = [
 ]
 
 
-def ext_path() -> Path:
+# The node's native RCCL data plane is a module of its own (``otedama_amd._rccl``): only a node rank loads it, so
+# librccl is never mapped into the engine, the device processes or the pool.
+RCCL_SOURCES = ["runtime/rccl_comm.cpp"]
+
+
+def ext_path(name: str = "_native") -> Path:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return ROOT / "otedama_amd" / f"_native{suffix}"
+    return ROOT / "otedama_amd" / f"{name}{suffix}"
 
 
 def _hipcc() -> str:
@@ -122,6 +127,30 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-lpthread", "-lcrypto",
                 "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lhsa-runtime64"]
         _compile(link, verbose)
+        os.replace(tmp, out)
+    build_rccl(verbose, force, hipcc, common, py_inc, pybind11.get_include())
+    return out
+
+
+def build_rccl(verbose: bool, force: bool, hipcc: str, common: list[str], py_inc: str, pyb_inc: str) -> Path:
+    """``otedama_amd._rccl``: host code only (RCCL + the HIP runtime API, no kernels), compiled as HIP for gfx950 like
+    the miner runtime, linked to librccl."""
+    out = ext_path("_rccl")
+    objs, tasks = [], []
+    deps = _headers()
+    for rel in RCCL_SOURCES:
+        src = CSRC / rel
+        obj = BUILD / (rel.replace("/", "_") + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src, deps):
+            tasks.append([hipcc, f"--offload-arch={ARCH}", *common, "-I/opt/rocm/include", f"-I{py_inc}",
+                          f"-I{pyb_inc}", "-fvisibility=hidden", "-x", "hip", "-c", str(src), "-o", str(obj)])
+    for t in tasks:
+        _compile(t, verbose)
+    if force or tasks or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+        tmp = out.with_suffix(".tmp.so")
+        _compile([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp), "-L/opt/rocm/lib", "-lrccl",
+                  "-lamdhip64"], verbose)
         os.replace(tmp, out)
     return out
 

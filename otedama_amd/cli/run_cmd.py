@@ -107,16 +107,18 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         # node mode (otedama node / torchrun): one rank per GPU; rank 0 is the pool-facing engine. A rank the
         # supervisor restarted after a loss joins the running node instead of forming it.
         from otedama_amd.engine.run import mark_early
+        from otedama_amd.parallel.rcclcomm import native_wanted, open_node_comm
 
-        mark_early("torch_import")
-        from otedama_amd.parallel.comm import NodeComm, init_from_env, join_from_env
-
-        mark_early("torch_imported")
-
+        # On GPUs the ranks run the native RCCL data plane and never import torch (parallel/rcclcomm.py); gloo
+        # rehearsals and CPU hosts use torch.distributed.
+        if native_wanted():
+            os.environ.setdefault("OTEDAMA_NO_TORCH", "1")
+        mark_early("comm_open")
         # a replacement process: followers join the running node; rank 0 restarted by the supervisor takes the
         # node over as its leader (parallel/node.py NodeMinerSet._take_over)
         joining = os.environ.get("OTEDAMA_NODE_JOIN") == "1"
-        info = join_from_env() if joining else init_from_env()
+        info, comm = open_node_comm(joining, host_buffers=not native_wanted(),
+                                    log=lambda m: (stdout.write(f"[warn] {m}\n"), stdout.flush()))
         mark_early("process_group_ready")
         # the rank's HIP ordinal (init_from_env maps local ranks onto the visible GPUs; on an 8-GPU node it is the
         # local rank, on a 1-GPU rehearsal over gloo every rank shares GPU 0)
@@ -124,11 +126,9 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         # equal device count per rank keeps the stripes disjoint: the rank's GPU, or (a CPU-only rehearsal node over
         # gloo) one CPU miner per rank
         cfg.mining.cpu_threads = 0 if info.device.type == "cuda" else max(1, cfg.mining.cpu_threads)
-        # gloo is a CPU transport: its node buffers stay in host memory (RCCL's live on the rank's GPU)
-        host_buffers = info.backend == "gloo"
         if info.orig_rank > 0:
-            return _run_node_worker(cfg, info, NodeComm(info, host_buffers=host_buffers), stdout, joining)
-        node = NodeComm(info, host_buffers=host_buffers)
+            return _run_node_worker(cfg, info, comm, stdout, joining)
+        node = comm
         no_tui = True
     logln("info", i18n.STARTUP_READY)
     pool_url = cfg.pools[0].url if cfg.pools else C.DEFAULT_POOL_URL
@@ -140,16 +140,13 @@ def cmd_run(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
     finally:
         close_log()
         if node is not None:
-            from otedama_amd.parallel.comm import shutdown
-
-            shutdown(node.info)
+            node.close()
 
 
 def _run_node_worker(cfg, info, comm, stdout, joining: bool = False) -> int:
     """Ranks > 0 of a node: mine rank 0's jobs on the local GPU until rank 0 stops."""
     from otedama_amd import hal
     from otedama_amd.engine.miners import MinerSet
-    from otedama_amd.parallel.comm import shutdown
     from otedama_amd.parallel.node import NodeWorker
 
     on_gpu = info.device.type == "cuda"
@@ -174,7 +171,7 @@ def _run_node_worker(cfg, info, comm, stdout, joining: bool = False) -> int:
 
         NodeWorker(local, comm, log=wlog, joining=joining).run()
     finally:
-        shutdown(info)
+        comm.close()
     return EXIT_OK
 
 

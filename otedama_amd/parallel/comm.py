@@ -30,52 +30,14 @@ import datetime
 import json
 import os
 import time
-from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-JOB_BLOB_BYTES = 64 << 10  # a real V1 job (coinbase parts + 12 merkle branches, hex in JSON) can pass 4 KiB
-SHARE_SLOTS = 64
-# epoch_lo, epoch_hi|valid, nonce, ntime, version, en2_lo, en2_hi, rank|device, found_at_us, device_found_at_us
-# (both times CLOCK_MONOTONIC, which every process of the host shares: the leader computes the kernel-hit -> accept
-# latency of a remote rank's share directly)
-SHARE_WORDS = 10
-COUNTER_WORDS = 4  # hashes, shares, dropped, faulted
-
-
-PG_TIMEOUT_S = float(os.environ.get("OTEDAMA_PG_TIMEOUT", "30"))
-
-
-class CollectiveTimeout(RuntimeError):
-    """A bounded collective did not finish in time (a peer is dead or stuck)."""
-
-
-@dataclass
-class DistInfo:
-    rank: int = 0            # rank in the current process group
-    world_size: int = 1
-    local_rank: int = 0
-    backend: str = "none"
-    device: torch.device = torch.device("cpu")
-    orig_rank: int = -1      # launcher-assigned identity (RANK at start); stable across re-forms
-    generation: int = 0      # process-group generation (store prefix otd-g<gen>)
-    members: list = field(default_factory=list)  # orig ranks of the current group, in group-rank order
-    store: object = None     # the rendezvous TCPStore (node control plane)
-    capacity: int = 0        # ranks the node was launched with (WORLD_SIZE at start; orig ranks 0..capacity-1)
-
-    def __post_init__(self):
-        if self.orig_rank < 0:
-            self.orig_rank = self.rank
-        if not self.members:
-            self.members = list(range(self.world_size))
-        if self.capacity <= 0:
-            self.capacity = max(self.world_size, 1)
-
-    @property
-    def is_primary(self) -> bool:
-        return self.rank == 0
+from otedama_amd.parallel.commbase import (COUNTER_WORDS, JOB_BLOB_BYTES, PG_TIMEOUT_S, SHARE_SLOTS,  # noqa: F401
+                                           SHARE_WORDS, CollectiveTimeout, DistInfo, _decode, _encode,
+                                           job_from_payload, job_payload, pack_shares, unpack_shares)
 
 
 def _connect_store(rank: int, world: int):
@@ -185,6 +147,8 @@ class NodeComm:
         self.force = force
         self.staging = staging
         self.collectives = 0  # device collectives issued by this rank (node tick accounting)
+        if not isinstance(info.device, torch.device):  # a torch-free Device (commbase): its torch twin
+            info.device = torch.device(info.device.type, info.device.index)
         dev = torch.device("cpu") if host_buffers else info.device
         self.dev = dev
         self.cuda = dev.type == "cuda"
@@ -215,6 +179,15 @@ class NodeComm:
     def multi(self) -> bool:
         """Collectives are issued: more than one rank, or forced at world 1."""
         return self.info.world_size > 1 or self.force
+
+    def close(self) -> None:
+        """Leave the process group at the end of the rank's life."""
+        shutdown(self.info)
+
+    def bind_thread(self) -> None:
+        """Make the comm's GPU the calling thread's current device (the node's leader loop runs in a thread)."""
+        if self.cuda:
+            torch.cuda.set_device(self.info.device)
 
     def _alloc_world(self, world: int) -> None:
         self._gathered, self._gathered_h = self._pair(world, SHARE_SLOTS, SHARE_WORDS, dtype=torch.int64)
@@ -326,32 +299,16 @@ class NodeComm:
     def broadcast_job(self, job: dict | None) -> dict | None:
         """Rank 0 passes the job dict (bytes values hex-encoded); all ranks get it back."""
         if self.info.is_primary:
-            payload = json.dumps(_encode(job)).encode() if job is not None else b""
-            if len(payload) + 4 > JOB_BLOB_BYTES:
-                raise ValueError(f"job blob too large for broadcast ({len(payload)} bytes)")
-            buf = len(payload).to_bytes(4, "little") + payload
-            self._job_h.zero_()
-            self._job_h[: len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+            self._job_h.copy_(torch.frombuffer(bytearray(job_payload(job)), dtype=torch.uint8))
         if self.multi:
             self._op([(self._job, self._job_h)], lambda a: dist.broadcast(self._job, src=0, async_op=a),
                      [(self._job_h, self._job)])
-        host = self._job_h.numpy().tobytes()
-        n = int.from_bytes(host[:4], "little")
-        if n == 0:
-            return None
-        return _decode(json.loads(host[4 : 4 + n].decode()))
+        return job_from_payload(self._job_h.numpy().tobytes())
 
     # ---------------------------------------------------------------- R2
     def gather_shares(self, shares: list[dict], device_index: int = 0) -> list[dict]:
         """All-gather up to SHARE_SLOTS share records per rank; returns every rank's shares."""
-        rows = np.zeros((SHARE_SLOTS, SHARE_WORDS), dtype=np.int64)
-        for i, s in enumerate(shares[:SHARE_SLOTS]):
-            e = int(s.get("epoch", 0))
-            en2 = int(s.get("extranonce2", 0))
-            rows[i] = (e & 0xFFFFFFFF, (e >> 32) | (1 << 31), s["nonce"], s.get("ntime", 0), s.get("version", 0),
-                       en2 & 0xFFFFFFFF, en2 >> 32, (self.info.rank << 16) | device_index,
-                       int(s.get("found_at", 0.0) * 1e6), int((s.get("device_found_at", 0.0) or 0.0) * 1e6))
-        self._slots_h.copy_(torch.from_numpy(rows))
+        self._slots_h.copy_(torch.from_numpy(pack_shares(shares, self.info.rank, device_index)))
         if self.multi:
             self._op([(self._slots, self._slots_h)],
                      lambda a: dist.all_gather_into_tensor(self._gathered.view(-1, SHARE_WORDS), self._slots,
@@ -359,18 +316,7 @@ class NodeComm:
                      [(self._gathered_h, self._gathered)])
         else:
             self._gathered_h[0].copy_(self._slots_h)
-        out = []
-        g = self._gathered_h.numpy()
-        for r, i in zip(*np.nonzero(g[:, :, 1] >> 31)):  # valid records only, in rank then slot order
-            r, rec = int(r), g[r, i].tolist()
-            out.append({
-                "epoch": rec[0] | ((rec[1] & 0x7FFFFFFF) << 32), "nonce": rec[2] & 0xFFFFFFFF,
-                "ntime": rec[3] & 0xFFFFFFFF, "version": rec[4] & 0xFFFFFFFF,
-                "extranonce2": (rec[5] & 0xFFFFFFFF) | (rec[6] << 32), "rank": rec[7] >> 16,
-                "device_index": rec[7] & 0xFFFF, "found_at": rec[8] / 1e6, "device_found_at": rec[9] / 1e6,
-                "orig_rank": self.info.members[r] if r < len(self.info.members) else r,
-            })
-        return out
+        return unpack_shares(self._gathered_h.numpy(), self.info.members)
 
     # ---------------------------------------------------------------- R3
     def allreduce_counters(self, hashes: int, shares: int = 0, dropped: int = 0, faults: int = 0) -> tuple:
@@ -451,23 +397,3 @@ def rccl_pg_options():
         return opts
     except Exception:  # noqa: BLE001 - a torch without the NCCL backend
         return None
-
-
-def _encode(obj):
-    if isinstance(obj, bytes):
-        return {"__b": obj.hex()}
-    if isinstance(obj, dict):
-        return {k: _encode(v) for k, v in obj.items()}
-    if isinstance(obj, (list, tuple)):
-        return [_encode(v) for v in obj]
-    return obj
-
-
-def _decode(obj):
-    if isinstance(obj, dict):
-        if set(obj) == {"__b"}:
-            return bytes.fromhex(obj["__b"])
-        return {k: _decode(v) for k, v in obj.items()}
-    if isinstance(obj, list):
-        return [_decode(v) for v in obj]
-    return obj

@@ -39,6 +39,19 @@ def free_port() -> int:
     return port
 
 
+def visible_gpus_kfd() -> int:
+    """GPUs in the KFD topology that a child may use (honours HIP/ROCR/CUDA_VISIBLE_DEVICES); 0 without a KFD
+    topology. Never imports torch."""
+    from otedama_amd.hal import KFD_TOPOLOGY_PATH, KFDDriver
+
+    if not os.path.isdir(KFD_TOPOLOGY_PATH):
+        return 0
+    try:
+        return len(KFDDriver().enumerate())
+    except Exception:  # noqa: BLE001 - an unreadable topology: no GPUs
+        return 0
+
+
 def visible_gpus() -> int:
     """HIP devices visible to a child (honours HIP/ROCR/CUDA_VISIBLE_DEVICES) without initialising HIP here: from
     the KFD topology in sysfs (no torch import, so the supervisor stays small), else torch's device count."""

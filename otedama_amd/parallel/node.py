@@ -58,7 +58,7 @@ import threading
 import time
 
 from otedama_amd.engine.miners import GROUP, RESPLIT_GROUPS, MinerSet
-from otedama_amd.parallel.comm import SHARE_SLOTS, NodeComm
+from otedama_amd.parallel.commbase import SHARE_SLOTS
 from otedama_amd.utils.trace import span
 
 DEFAULT_TICK = 0.005       # reported control-loop granularity (the loop itself waits on its doorbell)
@@ -448,7 +448,7 @@ class NodeMinerSet:
         group generation is ignored."""
         if self._bell is None or self.comm.info.world_size <= 1:
             return
-        from otedama_amd.parallel.comm import _encode
+        from otedama_amd.parallel.commbase import _encode
 
         msg = b"j" + json.dumps({"gen": self._gen, "blob": _encode(blob)}).encode()
         if len(msg) > PREVIEW_MAX:
@@ -681,7 +681,7 @@ class NodeMinerSet:
         if members is None:
             members = [r for r in info.members if r not in dead] + sorted(joiners)
         members = [0] + sorted(r for r in members if r != 0)
-        from otedama_amd.parallel.comm import PG_TIMEOUT_S
+        from otedama_amd.parallel.commbase import PG_TIMEOUT_S
 
         busy = self._await_left(members, PG_TIMEOUT_S + 5.0)
         if busy:
@@ -769,10 +769,7 @@ class NodeMinerSet:
 
     def _loop(self) -> None:
         info = self.comm.info
-        if info.device.type == "cuda":
-            import torch
-
-            torch.cuda.set_device(info.device)
+        self.comm.bind_thread()  # the comm's device is this thread's (HIP device state is per thread)
         next_live = next_stats = time.monotonic()
         try:
             if self.takeover and self.store is not None:
@@ -1055,7 +1052,7 @@ class NodeWorker:
         info = self.comm.info
         if broken or info.generation < 0 or d.get("gen") != info.generation:
             return
-        from otedama_amd.parallel.comm import _decode
+        from otedama_amd.parallel.commbase import _decode
 
         if self._apply(_decode(d.get("blob") or {})):
             self.previews += 1
