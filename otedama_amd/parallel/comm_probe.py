@@ -91,7 +91,10 @@ def run_ops(comm, seconds: float, cadence_hz: float = 50.0, probe_kernel: bool =
 # at normal priority); "node" is the node's layout now (every copy on a high-priority comm stream through pinned
 # buffers, RCCL's streams at high priority: comm.rccl_pg_options).
 CONFIGS = {"legacy": {"pg_high": False, "staging": "legacy", "stream_priority": None},
-           "node": {"pg_high": True, "staging": "stream", "stream_priority": "high"}}
+           "node": {"pg_high": True, "staging": "stream", "stream_priority": "high"},
+           # the node's data plane on GPUs from round 5 on: the native RCCL module (parallel/rcclcomm.py), the whole
+           # op one chain on its own high-priority stream, no torch in the rank
+           "native": {"native": True}}
 
 
 def _one_rank_group(device, high: bool) -> None:
@@ -113,6 +116,8 @@ def _with_config(dev, device_index: int, name: str, fn):
     from otedama_amd.parallel.comm import DistInfo, NodeComm
 
     cfg = CONFIGS[name]
+    if cfg.get("native"):
+        return _with_native(device_index, fn)
     _one_rank_group(dev, cfg["pg_high"])
     try:
         comm = NodeComm(DistInfo(0, 1, device_index, "nccl", dev), bounded=True, deadline=10.0, force=True,
@@ -123,12 +128,34 @@ def _with_config(dev, device_index: int, name: str, fn):
         dist.destroy_process_group()
 
 
+_NATIVE_GEN = [0]
+
+
+def _with_native(device_index: int, fn):
+    from otedama_amd.parallel.commbase import Device, DistInfo
+    from otedama_amd.parallel.kvclient import StoreClient
+    from otedama_amd.parallel.kvstore import StoreServer
+    from otedama_amd.parallel.rcclcomm import NativeNodeComm
+
+    with StoreServer() as srv:
+        info = DistInfo(0, 1, device_index, "rccl", Device("cuda", device_index),
+                        store=StoreClient("127.0.0.1", srv.port, timeout=30))
+        comm = NativeNodeComm(info, bounded=True, deadline=10.0, force=True)
+        _NATIVE_GEN[0] += 1
+        comm.reform([0], _NATIVE_GEN[0])
+        try:
+            run_ops(comm, 0.3)
+            return fn(comm)
+        finally:
+            comm.close()
+
+
 def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scrypt"), seconds: float = 4.0,
                             cadence_hz: float = 50.0, windows: int = 2, reserves=("",)) -> dict:
     """See the module docstring. Per configuration (CONFIGS) and algorithm: op latency idle / loaded, and the
     miner's rate over alternating windows without / with the ops. ``reserves``: OTEDAMA_RESERVE_CUS specs to run
     the miner with ("" = none; e.g. "0" keeps CU 0 out of the mining kernels' CU mask); each non-empty one is
-    reported under "<algo>@reserve:<spec>" with the node configuration only."""
+    reported under "<algo>@reserve:<spec>" with the native configuration only."""
     import torch
     import torch.distributed as dist
 
@@ -155,7 +182,7 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
     runs = [(algo, spec) for spec in reserves for algo in algorithms]
     for algo, spec in runs:
         key = algo if not spec else f"{algo}@reserve:{spec}"
-        configs = list(CONFIGS) if not spec else ["node"]
+        configs = list(CONFIGS) if not spec else ["native"]
         _say(f"{key}: miner up, alternating windows")
         if spec:
             os.environ["OTEDAMA_RESERVE_CUS"] = spec  # inherited by the device process

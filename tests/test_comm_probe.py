@@ -55,6 +55,7 @@ def test_comm_under_load_on_the_gpu():
 
     r = measure_comm_under_load(0, ["sha256d"], seconds=1.0, cadence_hz=50.0, windows=1)
     assert r["idle"]["node"]["R2_gather"]["samples"] > 20 and r["idle"]["legacy"]["R2_gather"]["samples"] > 20
+    assert r["idle"]["native"]["R2_gather"]["samples"] > 20 and r["sha256d"]["loaded"]["native"]["R1_job"]["samples"]
     s = r["sha256d"]
     assert s["rate_alone_hps"] > 1e10
     assert s["loaded"]["node"]["R2_gather"]["samples"] > 20 and s["loaded"]["legacy"]["kernel"]["samples"] > 0
