@@ -977,6 +977,8 @@ class Bench:
             "node_job_switch_worst_rank_p50_ms": _r(js.get("worst_rank_p50_ms")),
             "node_job_switch_worst_rank_max_ms": _r(js.get("worst_rank_max_ms")),
             "node_job_switch_stale_rejects": js.get("stale_rejects"),
+            "node_backend": node.get("dist_backend"),
+            "node_ranks_seen": node.get("ranks_seen"),
             "share_latency_p50_ms": _r(lat.get("p50_ms")),
             "device_hit_to_accept_p50_ms": _r(lat.get("device_hit_to_accept_p50_ms")),
             "job_switch_p50_ms": {a: _r(v) for a, v in (out.get("job_switch_ms") or {}).items()} or None,
