@@ -122,10 +122,13 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
     leader_each: list[float] = []
     bcast_each: list[float] = []
     applied_each: dict[str, list[float]] = {}
-    for tb in block_at:
+    blocks = sorted(block_at)
+    for bi, tb in enumerate(blocks):
+        # a start belongs to this block only before the next block was sent
+        end = min(tb + window, blocks[bi + 1]) if bi + 1 < len(blocks) else tb + window
         worst = None
         for r in range(ranks):
-            ts = sorted(t for _e, t in (work_started.get(f"rank{r}") or []) if tb < t <= tb + window)
+            ts = sorted(t for _e, t in (work_started.get(f"rank{r}") or []) if tb < t <= end)
             if not ts:
                 missing += 1
                 continue
@@ -134,14 +137,14 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
             worst = ms if worst is None else max(worst, ms)
         if worst is not None:
             worst_each.append(worst)
-        sets = sorted(t for _e, t in (job_set_at or []) if tb < t <= tb + window)
+        sets = sorted(t for _e, t in (job_set_at or []) if tb < t <= end)
         if sets:
             leader_each.append((sets[0] - tb) * 1e3)
-        bc = sorted(t for _e, t in (job_bcast_at or []) if tb < t <= tb + window)
+        bc = sorted(t for _e, t in (job_bcast_at or []) if tb < t <= end)
         if bc:
             bcast_each.append((bc[0] - tb) * 1e3)
         for r in range(1, ranks):
-            ap = sorted(t for _e, t in ((job_applied or {}).get(f"rank{r}") or []) if tb < t <= tb + window)
+            ap = sorted(t for _e, t in ((job_applied or {}).get(f"rank{r}") or []) if tb < t <= end)
             if ap:
                 applied_each.setdefault(f"rank{r}", []).append((ap[0] - tb) * 1e3)
 
@@ -152,7 +155,7 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
     rows = {r: {"p50_ms": med(v), "max_ms": max(v) if v else None, "samples": len(v)} for r, v in per_rank.items()}
     p50s = [v["p50_ms"] for v in rows.values() if v["p50_ms"] is not None]
     maxs = [v["max_ms"] for v in rows.values() if v["max_ms"] is not None]
-    return {"blocks": len(block_at), "per_rank": rows,
+    return {"blocks": len(blocks), "per_rank": rows,
             "worst_rank_p50_ms": max(p50s) if p50s else None, "worst_rank_max_ms": max(maxs) if maxs else None,
             "node_p50_ms": med(worst_each), "missing": missing,
             "pool_to_leader_p50_ms": med(leader_each),

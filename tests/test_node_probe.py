@@ -52,3 +52,27 @@ def test_mixed_pool_layout(gpus, want):
     from otedama_amd.pool.pool_probe import layout
 
     assert layout(gpus) == want
+
+
+def test_job_switch_stats_per_rank_and_worst():
+    """Node-wide job switch: for each forced block, each rank's first work start after the pool's
+    send within the window; worst-rank p50 / max, the node's per-block slowest rank, and missing starts."""
+    from otedama_amd.parallel.node_probe import job_switch_stats
+
+    blocks = [10.0, 11.0, 12.0]
+    ws = {"rank0": [(1, 10.0005), (2, 11.0004), (3, 12.0006)],
+          "rank1": [(1, 10.0020), (2, 11.0030), (3, 12.0010)],
+          "rank2": [(1, 10.0010), (3, 12.0200)]}  # missed block 2 (e.g. a lost heartbeat sample)
+    js = job_switch_stats(blocks, ws, 3, job_set_at=[(1, 10.0002), (2, 11.0002), (3, 12.0003)],
+                          job_bcast_at=[(1, 10.0008)], job_applied={"rank1": [(1, 10.0011)]})
+    assert js["blocks"] == 3 and js["missing"] == 1
+    r = js["per_rank"]
+    assert r["rank0"]["samples"] == 3 and r["rank2"]["samples"] == 2
+    assert abs(r["rank1"]["p50_ms"] - 2.0) < 1e-6 and abs(r["rank2"]["max_ms"] - 20.0) < 1e-6
+    assert abs(js["worst_rank_max_ms"] - 20.0) < 1e-6 and abs(js["worst_rank_p50_ms"] - 20.0) < 1e-6
+    assert abs(js["node_p50_ms"] - 3.0) < 1e-6  # per block slowest: 2.0, 3.0, 20.0
+    assert abs(js["pool_to_leader_p50_ms"] - 0.2) < 1e-6 and abs(js["pool_to_r1_done_p50_ms"] - 0.8) < 1e-6
+    assert abs(js["pool_to_follower_apply_p50_ms"]["rank1"] - 1.1) < 1e-6
+    # a start before the block or after the window is not this block's
+    js2 = job_switch_stats([10.0], {"rank0": [(1, 9.9), (2, 13.0)]}, 1)
+    assert js2["missing"] == 1 and js2["worst_rank_p50_ms"] is None
