@@ -94,7 +94,7 @@ def test_native_node_comm_generations_through_the_store():
         assert comm.broadcast_control([9, 8]) == [9, 8, 0, 0] and comm.allreduce_max(3.5) == 3.5
         comm.reform([0], 1)  # the next generation: a fresh id and communicator
         assert info.generation == 1 and srv.get("otd-g1/rcclid") != srv.get("otd-g0/rcclid")
-        assert comm.allreduce_counters(1)[0] == 1 and comm.collectives == 8
+        assert comm.allreduce_counters(1)[0] == 1 and comm.collectives == 7
         comm.close()
 
 
