@@ -979,6 +979,7 @@ class Bench:
             "node_job_switch_stale_rejects": js.get("stale_rejects"),
             "node_backend": node.get("dist_backend"),
             "node_ranks_seen": node.get("ranks_seen"),
+            "node_time_to_hashing_s": node.get("time_to_hashing_s"),
             "share_latency_p50_ms": _r(lat.get("p50_ms")),
             "device_hit_to_accept_p50_ms": _r(lat.get("device_hit_to_accept_p50_ms")),
             "job_switch_p50_ms": {a: _r(v) for a, v in (out.get("job_switch_ms") or {}).items()} or None,
@@ -987,6 +988,11 @@ class Bench:
             "pool_validated_per_s": {a: _r(v.get("validated_shares_per_sec")) for a, v in pool.items()} or None,
             "pool_validate_p50_ms": {a: _r((v.get("validate_ms") or {}).get("p50")) for a, v in pool.items()} or None,
             "pool_validations": {a: (v.get("validate_ms") or {}).get("samples") for a, v in pool.items()} or None,
+            # every worker's last >25% retarget came before the measurement window opened
+            "pool_steady_in_window": all(w.get("converged_after_s") is not None
+                                         and w.get("window_opened_after_s") is not None
+                                         and w["converged_after_s"] <= w["window_opened_after_s"]
+                                         for v in pool.values() for w in v.get("workers") or []) if pool else None,
             "world_size": out["world_size"],
             "backend": out["dist_backend"],
             "rccl_ranks_seen": out["rccl_ranks_seen"],

@@ -464,6 +464,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
+// Segmented cooperative ROMix: iterations [it0, it1) of the hash's 2048 (0..1023 write the pad, 1024..2047 look it
+// up), X carried across launches in xbuf. The ROMix of one batch becomes `segments` launches of ~T/segments each
+// (T ~ 32-64 ms with every wave slot of the chip held), so a kernel of another process -- the node's RCCL
+// collective on its high-priority stream -- finds a free slot within one segment instead of one whole ROMix
+// (parallel/comm_probe.py measures both the wait and the rate it costs: 2 x 128 B of X per lane per segment).
+// Same residency rule as the split kernel: one hash per lane slot (count <= grid * 256).
+template <int LCPOL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void otd_scrypt_romix_coop_seg(
+    uint32_t count, uint4* __restrict__ xbuf, uint4* __restrict__ V, uint32_t it0, uint32_t it1,
+    const otedama::HitSink sink) {
+  __shared__ uint4 tiles[4 * 256];
+  const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t lane = uint32_t(slot & 63u);
+  const uint64_t wave = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot >> 32))) << 26) |
+                        uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot) >> 6));
+  uint4* Vw = V + wave * (1024ull * 64u * 8u);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Vw, (short)0, 1024 * 64 * 128, 0x00020000);
+  uint4* tile = tiles + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256;
+  if (slot >= count) return;  // count is a multiple of 64: whole waves leave together
+  if (abort_newer(abort_peek(sink), sink.epoch)) return;  // stale work: pbkdf_out publishes nothing either
+  uint32_t X[32];
+  load_entry(xbuf + (slot << 3), X);
+  const uint32_t w1 = it1 < 1024u ? it1 : 1024u;
+  for (uint32_t i = it0; i < w1; ++i) {
+    coop_store_entry(X, rs, tile, lane, i);
+    blockmix(X);
+  }
+  for (uint32_t i = it0 > 1024u ? it0 : 1024u; i < it1; ++i) {
+    coop_v4u R[4];
+    coop_issue<LCPOL>(X, rs, tile, lane, R);
+    coop_consume(X, tile, lane, R);
+    blockmix(X);
+  }
+  store_entry(xbuf + (slot << 3), X);
+}
+
 // Two-stream cooperative ROMix: wave w owns hashes [128w, 128w+128) (lane l: 128w+l and 128w+64+l) and a
 // 16 MiB pad region (8 MiB per stream). count is a multiple of 128 (launcher rounds up).
 template <int LCPOL>
@@ -543,6 +579,15 @@ static bool scrypt_write_polls() {
   return on;
 }
 
+// OTEDAMA_SCRYPT_SEGMENTS=S (1..64, default 1): the cooperative ROMix of a batch as S launches
+// (otd_scrypt_romix_coop_seg) when every lane slot holds one hash; 1 = one launch with in-loop abort polls.
+// Read at every launch (one environ scan per ~30 ms batch) so a test can switch it within one process.
+static uint32_t scrypt_segments() {
+  const char* v = std::getenv("OTEDAMA_SCRYPT_SEGMENTS");
+  const long x = v ? std::strtol(v, nullptr, 10) : 1;
+  return uint32_t(x < 1 ? 1 : (x > 64 ? 64 : x));
+}
+
 // xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
 // gap: 1/2/4 = per-lane ROMix with that lookup gap; kScryptCoop = lane-cooperative ROMix (gap 1).
 hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t count, void* xbuf, void* scratch,
@@ -558,7 +603,12 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
     case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
-      if (scrypt_write_polls())
+      if (scrypt_segments() > 1 && uint64_t(count64) <= uint64_t(grid) * 256u) {
+        const uint32_t S = scrypt_segments();
+        for (uint32_t k = 0; k < S; ++k)
+          hipLaunchKernelGGL(otd_scrypt_romix_coop_seg<2>, dim3(grid), dim3(256), 0, stream, count64, X, V,
+                             2048u * k / S, 2048u * (k + 1) / S, sink);
+      } else if (scrypt_write_polls())
         hipLaunchKernelGGL((otd_scrypt_romix_coop<2, 64>), dim3(grid), dim3(256), 0, stream, count64, X, V, sink);
       else
         hipLaunchKernelGGL((otd_scrypt_romix_coop<2, 1024>), dim3(grid), dim3(256), 0, stream, count64, X, V, sink);

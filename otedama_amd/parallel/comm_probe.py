@@ -151,11 +151,13 @@ def _with_native(device_index: int, fn):
 
 
 def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scrypt"), seconds: float = 4.0,
-                            cadence_hz: float = 50.0, windows: int = 2, reserves=("",)) -> dict:
+                            cadence_hz: float = 50.0, windows: int = 2, reserves=("",), variants=()) -> dict:
     """See the module docstring. Per configuration (CONFIGS) and algorithm: op latency idle / loaded, and the
     miner's rate over alternating windows without / with the ops. ``reserves``: OTEDAMA_RESERVE_CUS specs to run
     the miner with ("" = none; e.g. "0" keeps CU 0 out of the mining kernels' CU mask); each non-empty one is
-    reported under "<algo>@reserve:<spec>" with the native configuration only."""
+    reported under "<algo>@reserve:<spec>" with the native configuration only. ``variants``: further miner
+    environments ("NAME=VALUE[&NAME=VALUE]", e.g. "OTEDAMA_SCRYPT_SEGMENTS=8"), reported as "<algo>@<variant>" with
+    the native configuration only."""
     import torch
     import torch.distributed as dist
 
@@ -179,15 +181,15 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
         raise RuntimeError(f"no KFD GPU node for device {device_index}")
     import os
 
-    runs = [(algo, spec) for spec in reserves for algo in algorithms]
-    for algo, spec in runs:
-        key = algo if not spec else f"{algo}@reserve:{spec}"
-        configs = list(CONFIGS) if not spec else ["native"]
+    runs = [(algo, f"reserve:{spec}" if spec else "", {"OTEDAMA_RESERVE_CUS": spec} if spec else {})
+            for spec in reserves for algo in algorithms]
+    runs += [(algo, v, dict(kv.split("=", 1) for kv in v.split("&"))) for v in variants for algo in algorithms]
+    for algo, tag, env in runs:
+        key = algo if not tag else f"{algo}@{tag}"
+        configs = list(CONFIGS) if not tag else ["native"]
         _say(f"{key}: miner up, alternating windows")
-        if spec:
-            os.environ["OTEDAMA_RESERVE_CUS"] = spec  # inherited by the device process
-        else:
-            os.environ.pop("OTEDAMA_RESERVE_CUS", None)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)  # inherited by the device process
         ms = MinerSet(devs, algo, 1 << 32, 0, isolation="process")
         dp = ms.miners[0].native
         ms.start()
@@ -217,7 +219,11 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
             res["reserved_cus"] = st.get("reserved_cus", 0)
         finally:
             ms.stop()
-            os.environ.pop("OTEDAMA_RESERVE_CUS", None)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         alone = [r for r in res["rate_alone"] if r]
         base = statistics.fmean(alone) if alone else None
         res["rate_alone_hps"] = base
@@ -238,10 +244,12 @@ def main(argv=None) -> int:
     ap.add_argument("--cadence", type=float, default=50.0)
     ap.add_argument("--windows", type=int, default=2)
     ap.add_argument("--reserves", default="", help="';'-separated OTEDAMA_RESERVE_CUS specs besides none, e.g. '0;0,32'")
+    ap.add_argument("--variants", default="",
+                    help="';'-separated miner environments, e.g. 'OTEDAMA_SCRYPT_SEGMENTS=8;OTEDAMA_SCRYPT_SEGMENTS=16'")
     a = ap.parse_args(argv)
     reserves = [""] + [x for x in a.reserves.split(";") if x]
     r = measure_comm_under_load(a.device, [x for x in a.algorithms.split(",") if x], a.seconds, a.cadence, a.windows,
-                                reserves)
+                                reserves, [x for x in a.variants.split(";") if x])
     print(json.dumps(r))
     return 0
 

@@ -5,9 +5,17 @@ The only related reference code is the share-interval estimate
 vardiff inverts it: every retarget window the observed share interval moves the
 difficulty toward ``target_share_seconds``, bounded per step (x4 / /4) and
 globally (min/max), with a 10% dead band so it does not flap.
+
+A window's interval estimate from n shares is itself noisy (Poisson: relative spread ~1/sqrt(n)), so a retarget also
+needs the deviation to be significant, |ln ratio| >= noise_z / sqrt(n), judged once per retarget period (a test at
+every share finds a noise excursion sooner or later). A window that is not significant keeps accumulating shares, up
+to max_window_factor retarget periods, instead of being thrown away: a miner on target is left alone, and a real 2x
+mismatch is corrected at the first look. At a 0.1 s share target the pool bench saw >25% retargets on noise alone
+after vardiff had settled (profiles/r5/g_bench), and the window must open on steady workers only.
 """
 from __future__ import annotations
 
+import math
 import time
 from dataclasses import dataclass, field
 
@@ -20,11 +28,14 @@ class VardiffConfig:
     max_difficulty: float = 1e15
     max_step: float = 4.0
     dead_band: float = 0.10
-    min_shares: int = 4             # retarget early once this many shares arrived early_factor x faster than target
+    min_shares: int = 16            # retarget early once this many shares arrived early_factor x faster than target
     # A burst of shares at the right rate is common (Poisson), so an early retarget needs strong evidence: at 2x, a
     # worker already at its target retargeted on noise several times a minute at a 0.1 s share interval (each a
-    # difficulty doubling and a correction back); at 4x the chance of a spurious one after min_shares is ~2%.
+    # difficulty doubling and a correction back). At 4x after 16 shares a worker on target never fires early, one at
+    # 2x in ~1-2% of windows; a new worker at 1000x its difficulty still reaches its level in a few dozen shares.
     early_factor: float = 4.0
+    noise_z: float = 3.0            # significance of a window's deviation, in standard errors of its estimate
+    max_window_factor: float = 8.0  # an insignificant window accumulates up to this many retarget periods
 
 
 @dataclass
@@ -34,6 +45,7 @@ class VardiffState:
     shares: int = 0
     accepted_work: float = 0.0      # sum of share difficulties in the window
     total_shares: int = 0
+    looks: int = 0                  # retarget periods of this window already judged insignificant
 
     def hashes_per_diff1(self, diff1_hashes: float) -> float:
         return diff1_hashes
@@ -63,15 +75,21 @@ class Vardiff:
         elapsed = now - st.window_start
         c = self.cfg
         early = st.shares >= c.min_shares and elapsed < c.target_share_seconds * st.shares / c.early_factor
-        if elapsed < c.retarget_seconds and not early:
+        # the window is looked at once per retarget period (a test at every share would find a noise excursion)
+        due = elapsed >= c.retarget_seconds * (st.looks + 1)
+        if not due and not early:
             return None
         if st.shares == 0:
             ratio = 1.0 / c.max_step if elapsed >= 2 * c.retarget_seconds else 0.5
         else:
             observed = elapsed / st.shares
             ratio = c.target_share_seconds / max(observed, 1e-9)
+            young = elapsed < c.max_window_factor * c.retarget_seconds
+            if not early and young and abs(math.log(max(ratio, 1e-300))) < c.noise_z / math.sqrt(st.shares):
+                st.looks = int(elapsed // c.retarget_seconds)  # within the estimate's own noise: let it sharpen
+                return None
         ratio = min(max(ratio, 1.0 / c.max_step), c.max_step)
-        st.window_start, st.shares, st.accepted_work = now, 0, 0.0
+        st.window_start, st.shares, st.accepted_work, st.looks = now, 0, 0.0, 0
         new = self.clamp(st.difficulty * ratio)
         if abs(new - st.difficulty) <= c.dead_band * st.difficulty:
             return None

@@ -132,6 +132,25 @@ def test_scrypt_more_lanes_than_slots(kernel):
     assert got == ref and 100 < len(ref) < 412
 
 
+@pytest.mark.parametrize("segments,n,lanes_per_slot", [(3, 200, 1), (8, 192, 1), (16, 256, 1), (4, 512, 2)])
+def test_scrypt_segmented_romix_matches_hashlib(monkeypatch, segments, n, lanes_per_slot):
+    """OTEDAMA_SCRYPT_SEGMENTS: the cooperative ROMix as S launches with X carried in xbuf (segment bounds that do
+    and do not fall on the write/read boundary); with more lanes than slots the launcher keeps the one-launch
+    kernel (a pad cannot be shared between two hashes across launches)."""
+    from otedama_amd.models.header import int_to_hash
+    from otedama_amd.ops.search import ScryptSearch
+
+    monkeypatch.setenv("OTEDAMA_SCRYPT_SEGMENTS", str(segments))
+    hdr = os.urandom(76) + bytes(4)
+    sc = ScryptSearch("cuda:0", grid=1, lanes_per_slot=lanes_per_slot, cap=1024, kernel="coop")
+    target_int = (1 << 254) - 1
+    got = sorted(sc.search(hdr, int_to_hash(target_int), 7000, n))
+    ref = [x for x in range(7000, 7000 + n) if int.from_bytes(hashlib.scrypt(
+        hdr[:76] + struct.pack("<I", x), salt=hdr[:76] + struct.pack("<I", x), n=1024, r=1, p=1, dklen=32),
+        "little") <= target_int]
+    assert got == ref and 0 < len(ref) < n
+
+
 def test_scrypt_split_refuses_more_lanes_than_slots():
     """The split kernel keeps one hash per lane slot across its two launches: a batch larger than the grid's slots
     is refused rather than silently reusing a pad between the launches."""

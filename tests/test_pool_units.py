@@ -57,6 +57,33 @@ def test_vardiff_converges_on_a_steady_miner():
     assert vd.difficulty_for_hashrate(hashrate) == pytest.approx(hashrate * 10.0 / 2.0 ** 32)
 
 
+def test_vardiff_leaves_a_poisson_miner_on_target_alone_and_corrects_a_real_mismatch():
+    """Noise is not a retarget: a miner exactly on target (exponential share gaps, 0.1 s target, 5 s windows as the
+    pool bench runs it) sees no retarget beyond SETTLE_BAND over 2000 shares; a miner at 2x is corrected at the
+    window's first look (one retarget period, ~100 shares here)."""
+    import random
+
+    rng = random.Random(5)
+    clk = FakeClock()
+    cfg = VardiffConfig(target_share_seconds=0.1, retarget_seconds=5.0)
+    vd = Vardiff(cfg, diff1_hashes=1.0, clock=clk)
+    hashrate = 1000.0
+    s = vd.new_state(hashrate * 0.1)  # on target
+    big = 0
+    for _ in range(2000):
+        clk.t += rng.expovariate(hashrate / s.difficulty)
+        old = s.difficulty
+        new = vd.on_share(s)
+        big += new is not None and abs(new / old - 1.0) > 0.25
+    assert big == 0
+    s = vd.new_state(hashrate * 0.05)  # shares twice as fast as the target
+    for n in range(1, 200):
+        clk.t += rng.expovariate(hashrate / s.difficulty)
+        if vd.on_share(s) is not None:
+            break
+    assert n <= 140 and s.difficulty == pytest.approx(hashrate * 0.1, rel=0.25)
+
+
 def test_vardiff_lowers_difficulty_when_shares_stop():
     clk = FakeClock()
     cfg = VardiffConfig(retarget_seconds=30.0)

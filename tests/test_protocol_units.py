@@ -180,9 +180,9 @@ def test_vardiff_converges_and_bounds():
     now = [0.0]
     vd = Vardiff(VardiffConfig(target_share_seconds=10, retarget_seconds=30), clock=lambda: now[0])
     s = vd.new_state(1.0)
-    # shares every 1 s at difficulty 1 -> should raise difficulty (bounded x4 per step)
+    # shares every 1 s at difficulty 1 -> should raise difficulty (bounded x4 per step) once min_shares arrived
     new = None
-    for _ in range(4):
+    for _ in range(16):
         now[0] += 1.0
         new = vd.on_share(s) or new
     assert new == 4.0 and s.difficulty == 4.0
