@@ -43,7 +43,9 @@ def cmd_node(args: list[str], stdout: TextIO, stderr: TextIO) -> int:
         return EXIT_USAGE
     from otedama_amd.parallel.launch import supervise_node, visible_gpus
 
-    if os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo":
+    from otedama_amd.parallel.rcclcomm import cpu_standin
+
+    if os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo" and not cpu_standin():
         n = visible_gpus()
         if n < gpus:
             stderr.write(f"otedama node: --gpus {gpus} needs {gpus} visible GPUs, this host has {n}\n")

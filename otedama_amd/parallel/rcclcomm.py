@@ -12,9 +12,13 @@ if any rank fails (the RCCL bootstrap, a missing library, a deadline), every ran
 (RCCL through ProcessGroupNCCL) together, and the choice is recorded at ``otd/comm`` for replacement ranks. CPU hosts
 and rehearsals (``OTEDAMA_DIST_BACKEND=gloo``) use torch.distributed over gloo as before; ``OTEDAMA_NODE_COMM=torch``
 forces torch.distributed on GPUs too.
+
+``OTEDAMA_RCCL_MODULE`` names a module with ``_rccl``'s API to load instead (tests/loopback_rccl.py: the collectives
+over the store, so this protocol runs at world 4 / 8 on CPUs, where the one-GPU box cannot run RCCL at world > 1).
 """
 from __future__ import annotations
 
+import importlib
 import os
 import time
 
@@ -34,9 +38,7 @@ class NativeNodeComm:
     parallel/comm.py NodeComm (the node uses nothing else)."""
 
     def __init__(self, info: DistInfo, bounded: bool = True, deadline: float = 3.0, force: bool = False):
-        from otedama_amd import _rccl
-
-        self._rccl = _rccl
+        self._rccl = rccl_module()
         self.info = info
         self.bounded = bounded
         self.deadline = deadline
@@ -150,6 +152,26 @@ class NativeNodeComm:
         return float(v[0])
 
 
+def rccl_module():
+    """``otedama_amd._rccl``, or the stand-in OTEDAMA_RCCL_MODULE names (see the module docstring)."""
+    name = os.environ.get("OTEDAMA_RCCL_MODULE")
+    if name:
+        return importlib.import_module(name)
+    from otedama_amd import _rccl
+
+    return _rccl
+
+
+def cpu_standin() -> bool:
+    """OTEDAMA_RCCL_MODULE names a stand-in that runs on CPUs (DEVICE_TYPE = "cpu"): the ranks mine on CPUs."""
+    return bool(os.environ.get("OTEDAMA_RCCL_MODULE")) and getattr(rccl_module(), "DEVICE_TYPE", "cuda") == "cpu"
+
+
+def _rank_device(local: int) -> Device:
+    """The rank's device: its GPU, or a CPU under a CPU stand-in module."""
+    return Device("cpu", None) if cpu_standin() else Device("cuda", local)
+
+
 def _wait_get(store, key: str, timeout: float) -> bytes:
     """The key's value once it is set, within ``timeout`` s (TimeoutError otherwise)."""
     end = time.monotonic() + timeout
@@ -210,10 +232,10 @@ def open_node_comm(joining: bool, host_buffers: bool = False, log=None):
         if mode != "rccl":
             store.close()
             return _torch_comm(joining, host_buffers)
-        info = DistInfo(-1, 0, local, "rccl", Device("cuda", local), orig_rank=rank, generation=-1, members=[],
+        info = DistInfo(-1, 0, local, "rccl", _rank_device(local), orig_rank=rank, generation=-1, members=[],
                         store=store, capacity=world)
         return info, NativeNodeComm(info)
-    info = DistInfo(rank, world, local, "rccl", Device("cuda", local), store=store, capacity=world)
+    info = DistInfo(rank, world, local, "rccl", _rank_device(local), store=store, capacity=world)
     comm = None
     err = ""
     try:

@@ -10,4 +10,8 @@ timeout -k 10 500 python -m otedama_amd.parallel.comm_probe --algorithms scrypt 
   --variants "OTEDAMA_SCRYPT_SEGMENTS=4;OTEDAMA_SCRYPT_SEGMENTS=8;OTEDAMA_SCRYPT_SEGMENTS=16;OTEDAMA_SCRYPT_SEGMENTS=32" \
   > "$out/comm_scrypt.json" 2> "$out/comm_scrypt.err" || exit $?
 timeout -k 10 300 python -m otedama_amd.parallel.comm_probe --algorithms x11 --seconds 4 --windows 2 \
-  > "$out/comm_x11.json" 2> "$out/comm_x11.err"
+  > "$out/comm_x11.json" 2> "$out/comm_x11.err" || exit $?
+timeout -k 10 200 python -c "
+import json
+from otedama_amd.pool.pool_probe import measure_pool
+print(json.dumps(measure_pool(1)))" > "$out/pool.json" 2> "$out/pool.err"
