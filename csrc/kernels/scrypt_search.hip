@@ -21,6 +21,7 @@
 #include "cdna_bitops.h"
 #include "hitsink_dev.h"
 #include <cstdlib>
+#include <cstring>
 
 #include "otedama/job.h"
 
@@ -477,27 +478,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   __shared__ uint4 tiles[4 * 256];
   const uint64_t slot = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint32_t lane = uint32_t(slot & 63u);
-  const uint64_t wave = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot >> 32))) << 26) |
-                        uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(slot) >> 6));
-  uint4* Vw = V + wave * (1024ull * 64u * 8u);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Vw, (short)0, 1024 * 64 * 128, 0x00020000);
   uint4* tile = tiles + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 256;
-  if (slot >= count) return;  // count is a multiple of 64: whole waves leave together
   if (abort_newer(abort_peek(sink), sink.epoch)) return;  // stale work: pbkdf_out publishes nothing either
-  uint32_t X[32];
-  load_entry(xbuf + (slot << 3), X);
-  const uint32_t w1 = it1 < 1024u ? it1 : 1024u;
-  for (uint32_t i = it0; i < w1; ++i) {
-    coop_store_entry(X, rs, tile, lane, i);
-    blockmix(X);
+  // grid-stride over the batch's hashes (count is a multiple of 64: whole waves iterate together); a launch grid of
+  // exactly the chip's resident blocks leaves no second round of blocks to straggle at each segment's end
+  const uint64_t nslots = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t h = slot; h < count; h += nslots) {
+    const uint64_t hw = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(h >> 32))) << 26) |
+                        uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(h) >> 6));
+    const __amdgpu_buffer_rsrc_t rh =
+        __builtin_amdgcn_make_buffer_rsrc(V + hw * (1024ull * 64u * 8u), (short)0, 1024 * 64 * 128, 0x00020000);
+    uint32_t X[32];
+    load_entry(xbuf + (h << 3), X);
+    const uint32_t w1 = it1 < 1024u ? it1 : 1024u;
+    for (uint32_t i = it0; i < w1; ++i) {
+      coop_store_entry(X, rh, tile, lane, i);
+      blockmix(X);
+    }
+    for (uint32_t i = it0 > 1024u ? it0 : 1024u; i < it1; ++i) {
+      coop_v4u R[4];
+      coop_issue<LCPOL>(X, rh, tile, lane, R);
+      coop_consume(X, tile, lane, R);
+      blockmix(X);
+    }
+    store_entry(xbuf + (h << 3), X);
   }
-  for (uint32_t i = it0 > 1024u ? it0 : 1024u; i < it1; ++i) {
-    coop_v4u R[4];
-    coop_issue<LCPOL>(X, rs, tile, lane, R);
-    coop_consume(X, tile, lane, R);
-    blockmix(X);
-  }
-  store_entry(xbuf + (slot << 3), X);
 }
 
 // Two-stream cooperative ROMix: wave w owns hashes [128w, 128w+128) (lane l: 128w+l and 128w+64+l) and a
@@ -579,13 +584,34 @@ static bool scrypt_write_polls() {
   return on;
 }
 
-// OTEDAMA_SCRYPT_SEGMENTS=S (1..64, default 1): the cooperative ROMix of a batch as S launches
-// (otd_scrypt_romix_coop_seg) when every lane slot holds one hash; 1 = one launch with in-loop abort polls.
+// OTEDAMA_SCRYPT_SEGMENTS=S (1..64): the cooperative ROMix of a batch as S launches (otd_scrypt_romix_coop_seg)
+// when every lane slot holds one hash.
 // Read at every launch (one environ scan per ~30 ms batch) so a test can switch it within one process.
+// Unset = 0: the one-launch kernel. Set (1..64): the segmented kernel, S=1 included (its code alone, for the A/B).
 static uint32_t scrypt_segments() {
   const char* v = std::getenv("OTEDAMA_SCRYPT_SEGMENTS");
-  const long x = v ? std::strtol(v, nullptr, 10) : 1;
+  if (!v || !v[0]) return 0;
+  const long x = std::strtol(v, nullptr, 10);
   return uint32_t(x < 1 ? 1 : (x > 64 ? 64 : x));
+}
+
+// OTEDAMA_SCRYPT_SEG_GRID caps the segmented kernel's launch grid: "resident" = the chip's resident blocks (8 per CU
+// at 8 waves/SIMD), N = N blocks; each lane slot then walks several hashes per segment. Unset: the allocation grid
+// (one hash per lane slot).
+static int scrypt_seg_grid(int grid) {
+  const char* v = std::getenv("OTEDAMA_SCRYPT_SEG_GRID");
+  if (!v || !v[0]) return grid;
+  int cap = 0;
+  if (std::strcmp(v, "resident") == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      return grid;
+    cap = cus * 8;
+  } else {
+    cap = int(std::strtol(v, nullptr, 10));
+  }
+  return cap > 0 && cap < grid ? cap : grid;
 }
 
 // xbuf: count * 128 bytes. scratch: scrypt_scratch_bytes(grid, gap).
@@ -603,10 +629,11 @@ hipError_t launch_scrypt_search(const ScryptParams& p, uint32_t base, uint32_t c
   hipLaunchKernelGGL(otd_scrypt_pbkdf_in, dim3(eg), dim3(256), 0, stream, p, base, count, X);
   switch (gap) {
     case kScryptCoop:  // nt lookups: +0.5-1% over default-policy loads (profiles/r1/scrypt_romix_ab.md)
-      if (scrypt_segments() > 1 && uint64_t(count64) <= uint64_t(grid) * 256u) {
+      if (scrypt_segments() > 0 && uint64_t(count64) <= uint64_t(grid) * 256u) {
         const uint32_t S = scrypt_segments();
+        const int sg = scrypt_seg_grid(grid);
         for (uint32_t k = 0; k < S; ++k)
-          hipLaunchKernelGGL(otd_scrypt_romix_coop_seg<2>, dim3(grid), dim3(256), 0, stream, count64, X, V,
+          hipLaunchKernelGGL(otd_scrypt_romix_coop_seg<2>, dim3(sg), dim3(256), 0, stream, count64, X, V,
                              2048u * k / S, 2048u * (k + 1) / S, sink);
       } else if (scrypt_write_polls())
         hipLaunchKernelGGL((otd_scrypt_romix_coop<2, 64>), dim3(grid), dim3(256), 0, stream, count64, X, V, sink);

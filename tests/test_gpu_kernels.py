@@ -132,17 +132,21 @@ def test_scrypt_more_lanes_than_slots(kernel):
     assert got == ref and 100 < len(ref) < 412
 
 
-@pytest.mark.parametrize("segments,n,lanes_per_slot", [(3, 200, 1), (8, 192, 1), (16, 256, 1), (4, 512, 2)])
-def test_scrypt_segmented_romix_matches_hashlib(monkeypatch, segments, n, lanes_per_slot):
+@pytest.mark.parametrize("segments,n,lanes_per_slot,seg_grid", [(1, 128, 1, ""), (3, 200, 1, ""), (8, 192, 1, ""),
+                                                                  (16, 256, 1, ""), (4, 512, 2, ""), (6, 960, 1, "1"),
+                                                                  (32, 256, 1, "resident")])
+def test_scrypt_segmented_romix_matches_hashlib(monkeypatch, segments, n, lanes_per_slot, seg_grid):
     """OTEDAMA_SCRYPT_SEGMENTS: the cooperative ROMix as S launches with X carried in xbuf (segment bounds that do
     and do not fall on the write/read boundary); with more lanes than slots the launcher keeps the one-launch
-    kernel (a pad cannot be shared between two hashes across launches)."""
+    kernel (a pad cannot be shared between two hashes across launches). OTEDAMA_SCRYPT_SEG_GRID=1: one launched
+    block walks the hashes of four allocated blocks (grid-stride, each hash on its own pad)."""
     from otedama_amd.models.header import int_to_hash
     from otedama_amd.ops.search import ScryptSearch
 
     monkeypatch.setenv("OTEDAMA_SCRYPT_SEGMENTS", str(segments))
+    monkeypatch.setenv("OTEDAMA_SCRYPT_SEG_GRID", seg_grid)
     hdr = os.urandom(76) + bytes(4)
-    sc = ScryptSearch("cuda:0", grid=1, lanes_per_slot=lanes_per_slot, cap=1024, kernel="coop")
+    sc = ScryptSearch("cuda:0", grid=4 if seg_grid == "1" else 1, lanes_per_slot=lanes_per_slot, cap=1024, kernel="coop")
     target_int = (1 << 254) - 1
     got = sorted(sc.search(hdr, int_to_hash(target_int), 7000, n))
     ref = [x for x in range(7000, 7000 + n) if int.from_bytes(hashlib.scrypt(
