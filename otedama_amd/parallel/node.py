@@ -26,6 +26,13 @@ trip sits between a follower's wake-up and the collective; the store stays the s
 costs one fallback poll, <= 50 ms; a lost share ring is covered by the pending count in the follower's heartbeat). Share records carry the kernel's own hit time, so the leader records device hit ->
 pool accept for remote ranks' shares the same way as for its own.
 
+Share previews: the R2 gather is a device collective, and on a GPU that the sibling device process saturates it waits
+for a wave slot (~1 ms p50 under SHA-256d, up to ~15 ms p99 under scrypt, profiles/r5/e_reserve_cus). A follower
+therefore also sends each new share record to the leader's preview port (otd/spv, a loopback datagram read by a
+thread of its own), and the leader submits it on arrival. R2 stays the consistent delivery: every share still
+travels in a gather (a lost datagram, a restarted leader), and the leader admits each share once, whichever path
+brings it first (key: rank, epoch, nonce, ntime, version, extranonce2).
+
 Rank loss (reference analogues: the partial-failure-tolerant detector
 internal/hal/registry.go:138-201 and the failover loop internal/engine/run.go:368-521): the leader declares a
 follower dead when the supervisor marks it, its heartbeat is older than HB_TIMEOUT, or a collective with it fails
@@ -58,7 +65,7 @@ import threading
 import time
 
 from otedama_amd.engine.miners import GROUP, RESPLIT_GROUPS, MinerSet
-from otedama_amd.parallel.commbase import SHARE_SLOTS
+from otedama_amd.parallel.commbase import SHARE_SLOTS, SHARE_WORDS, pack_shares, unpack_shares
 from otedama_amd.utils.trace import span
 
 DEFAULT_TICK = 0.005       # reported control-loop granularity (the loop itself waits on its doorbell)
@@ -67,11 +74,39 @@ HB_TIMEOUT = 2.0           # a follower whose heartbeat is older is dead
 LIVENESS_EVERY = 0.25      # leader liveness check period
 STATS_INTERVAL = 10.0      # R3 cadence (the reference's stats tick, internal/engine/run.go:377-380)
 BELL_FALLBACK = 0.05       # doorbell wait ceiling: a lost datagram delays an op or a gather by at most this
+PREVIEW_GRACE = 0.02       # a follower rings for the R2 of previewed shares this long after the first preview
 PENDING_CAP = 8192         # shares a follower holds for the leader (drop-oldest past it, counted)
 OP_RETAIN = 4096           # op log entries kept in the store (~1 h at the quiet node's ~1 op/s); older ones deleted
 EPOCH_SHIFT = 40           # leader incarnation i numbers its job epochs from (i - 1) << EPOCH_SHIFT
 PREFIX = "otd/"
 PREVIEW_MAX = 60000        # largest job-preview datagram (loopback UDP allows 65507 bytes); bigger jobs go by R1 only
+SEEN_MAX = 65536           # share keys the leader remembers to admit each share once (preview and R2 both carry it)
+
+
+def share_preview_msgs(shares: list[dict], orig_rank: int) -> list[bytes]:
+    """Share-preview datagrams: b"p" + the sender's orig rank (2 bytes) + up to SHARE_SLOTS R2 records each."""
+    out = []
+    for i in range(0, len(shares), SHARE_SLOTS):
+        part = shares[i:i + SHARE_SLOTS]
+        rows = pack_shares(part, orig_rank)[: len(part)]
+        out.append(b"p" + orig_rank.to_bytes(2, "little") + rows.tobytes())
+    return out
+
+
+def parse_share_preview(msg: bytes) -> list[dict]:
+    """The share records of a preview datagram (orig_rank set from its header); [] for anything malformed."""
+    body = msg[3:]
+    if msg[:1] != b"p" or not body or len(body) % (8 * SHARE_WORDS):
+        return []
+    import numpy as np
+
+    orig = int.from_bytes(msg[1:3], "little")
+    rows = np.frombuffer(body, dtype=np.int64).reshape(1, -1, SHARE_WORDS)
+    return unpack_shares(rows, [orig])
+
+
+def share_key(s: dict) -> tuple:
+    return (s["orig_rank"], s["epoch"], s["nonce"], s.get("ntime", 0), s.get("version", 0), s.get("extranonce2", 0))
 
 
 def op_retain() -> int:
@@ -132,7 +167,7 @@ class _Bell:
         self.orig = orig_rank
         self.store = _clone(store) if store is not None else None
         self._lock = threading.Lock()
-        self._ports: dict[int, tuple[int, float]] = {}
+        self._ports: dict = {}  # orig rank or store key -> (port, looked up at)
         self.rings = 0
         self.dropped = 0  # fault injection only
         if self.store is not None:
@@ -153,6 +188,21 @@ class _Bell:
             self._ports[orig] = (port, now)
             return port
 
+    def port_at(self, key: str) -> int | None:
+        """A port published at ``key`` (cached for PORT_TTL, like the doorbell ports: a restarted leader has a new
+        one)."""
+        now = time.monotonic()
+        with self._lock:
+            hit = self._ports.get(key)
+            if hit is not None and now - hit[1] < self.PORT_TTL:
+                return hit[0]
+            raw = _store_get(self.store, key) if self.store is not None else None
+            if raw is None:
+                return hit[0] if hit else None
+            port = int(raw)
+            self._ports[key] = (port, now)
+            return port
+
     def ring(self, orig: int, kind: bytes = b"o") -> None:
         port = self._port_of(orig)
         if port is None:
@@ -165,6 +215,17 @@ class _Bell:
             self.rings += 1
         except OSError:
             pass  # the store stays authoritative: the peer's fallback poll picks the work up
+
+    def send_port(self, port: int, msg: bytes) -> bool:
+        """One datagram to a loopback port (the leader's share-preview port); subject to the same fault injection."""
+        if self.DROP and random.random() < self.DROP:
+            self.dropped += 1
+            return False
+        try:
+            self.sock.sendto(msg, ("127.0.0.1", port))
+            return True
+        except OSError:
+            return False
 
     def wait(self, timeout: float) -> list[bytes]:
         got: list[bytes] = []
@@ -331,6 +392,13 @@ class NodeMinerSet:
         self._jobs: dict[int, dict] = {}          # epoch -> job meta for remote shares
         self._remote = collections.deque(maxlen=65536)
         self._remote_efd = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
+        # remote shares are admitted once, from a preview datagram or an R2 gather, whichever comes first
+        self._seen: collections.OrderedDict = collections.OrderedDict()
+        self._take_lock = threading.Lock()
+        self.share_previews = 0        # remote shares first admitted from a preview datagram
+        self.share_gathered_first = 0  # ... first from an R2 gather (a lost or late datagram)
+        self._spv: socket.socket | None = None
+        self._spv_thread: threading.Thread | None = None
         self._thread: threading.Thread | None = None
         self._op_k = 0
         self._retain = op_retain()
@@ -390,6 +458,14 @@ class NodeMinerSet:
         if self.store is not None and not self.takeover:
             self.store.set(_k("next"), "0")
             self.store.set(_k("gen"), str(self._gen))
+        if self.store is not None and self.capacity > 1:
+            self._spv = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            self._spv.bind(("127.0.0.1", 0))
+            self._spv.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+            self._spv.setblocking(False)
+            self.store.set(_k("spv"), str(self._spv.getsockname()[1]))
+            self._spv_thread = threading.Thread(target=self._spv_loop, name="otedama-node-spv", daemon=True)
+            self._spv_thread.start()
         self._thread = threading.Thread(target=self._loop, name="otedama-node-r0", daemon=True)
         self._thread.start()
 
@@ -402,6 +478,12 @@ class NodeMinerSet:
             self._thread = None
         if self._hb is not None:
             self._hb.stop.set()
+        if self._spv_thread is not None:
+            self._spv_thread.join(timeout=2)
+            self._spv_thread = None
+        if self._spv is not None:
+            self._spv.close()
+            self._spv = None
         self.local.stop()
         if self._bell is not None:
             self._bell.close()
@@ -847,22 +929,53 @@ class NodeMinerSet:
         if any(m[:1] == b"s" for m in got):
             self._gather_wanted = True
 
-    def _take(self, shares: list[dict]) -> None:
+    def _spv_loop(self) -> None:
+        """Share previews: submit a follower's shares as their datagram arrives, whatever the leader loop is doing
+        (it may sit in a collective that waits for a wave slot)."""
+        sock = self._spv
+        while not self._stop:
+            try:
+                ready, _, _ = select.select([sock], [], [], 0.25)
+            except (OSError, ValueError):
+                return
+            while ready:
+                try:
+                    msg = sock.recv(65536)
+                except (BlockingIOError, OSError):
+                    break
+                shares = parse_share_preview(msg)
+                if shares:
+                    self._take(shares, preview=True)
+
+    def _take(self, shares: list[dict], preview: bool = False) -> None:
         n = 0
-        for s in shares:
-            if s["orig_rank"] == self.comm.info.orig_rank:
-                continue
-            meta = self._jobs.get(s["epoch"])
-            if meta is None:
-                self.remote_stale += 1  # a job older than the retained window, or a previous leader's
-                continue
-            s.update(meta)
-            s["device_id"] = f"rank{s['orig_rank']}"
-            self._remote.append(s)
-            n += 1
-        per_rank = collections.Counter(s["orig_rank"] for s in shares)
-        if per_rank and max(per_rank.values()) >= SHARE_SLOTS:
-            self._gather_wanted = True  # a rank filled its slot array: it may hold more
+        me = self.comm.info.orig_rank
+        with self._take_lock:
+            for s in shares:
+                if s["orig_rank"] == me:
+                    continue
+                key = share_key(s)
+                if key in self._seen:
+                    continue  # already admitted by the other path
+                self._seen[key] = None
+                if len(self._seen) > SEEN_MAX:
+                    self._seen.popitem(last=False)
+                meta = self._jobs.get(s["epoch"])
+                if meta is None:
+                    self.remote_stale += 1  # a job older than the retained window, or a previous leader's
+                    continue
+                s.update(meta)
+                s["device_id"] = f"rank{s['orig_rank']}"
+                self._remote.append(s)
+                n += 1
+                if preview:
+                    self.share_previews += 1
+                else:
+                    self.share_gathered_first += 1
+        if not preview:
+            per_rank = collections.Counter(s["orig_rank"] for s in shares)
+            if per_rank and max(per_rank.values()) >= SHARE_SLOTS:
+                self._gather_wanted = True  # a rank filled its slot array: it may hold more
         if n:
             os.eventfd_write(self._remote_efd, 1)
 
@@ -888,26 +1001,34 @@ class NodeWorker:
         self._hb.extra["ja"] = []
         self.pending_dropped = 0  # shares dropped past PENDING_CAP (a leader that stays away)
         self.previews = 0  # jobs started from a preview datagram ahead of their R1 broadcast
+        self.previews_sent = 0  # share-preview datagrams sent to the leader
+        # OTEDAMA_NODE_SHARE_PREVIEWS=0: shares travel by R2 only (the A/B baseline)
+        self._share_previews = os.environ.get("OTEDAMA_NODE_SHARE_PREVIEWS", "1") != "0"
         self._seq_applied = 0  # seq of the leader blob this rank runs (previews and R1 only move it forward)
         self._plock = threading.Lock()
         self._stop = threading.Event()
 
     def _share_loop(self) -> None:
-        """Wake on the local miners' share eventfds and ring the leader's doorbell at once; the shares travel with
-        the R2 gather the leader posts in response. While shares are still waiting (a lost datagram, a leader that
-        is being restarted, more than one gather's worth) the bell is rung again every BELL_FALLBACK."""
+        """Wake on the local miners' share eventfds, send the new shares to the leader's preview port and ring its
+        doorbell for the R2 gather that delivers them consistently. With a preview out, the ring waits PREVIEW_GRACE,
+        so the gather (and the collective's device work) stays out of the leader's way while it submits the
+        previewed shares, and the shares of that window share one gather. Without one (previews off, no port yet, a
+        failed send) the ring goes at once. While shares are still waiting (a lost datagram, a leader that is being
+        restarted, more than one gather's worth) the bell is rung again every BELL_FALLBACK."""
         fds = list(self.local.share_fds())
         last_ring = 0.0
+        hold_until = None  # a preview went out: ring for its R2 at this time
         while not self._stop.is_set():
+            wait = BELL_FALLBACK if hold_until is None else max(0.0, min(BELL_FALLBACK, hold_until - time.monotonic()))
             if fds:
-                ready, _, _ = select.select(fds, [], [], BELL_FALLBACK)
+                ready, _, _ = select.select(fds, [], [], wait)
                 for fd in ready:
                     try:
                         os.read(fd, 8)
                     except BlockingIOError:
                         pass
             else:
-                self._stop.wait(0.01)
+                self._stop.wait(min(wait, 0.01))
             new = self.local.poll(256)
             with self._plock:
                 if new:
@@ -919,9 +1040,31 @@ class NodeWorker:
                 waiting = len(self._pending)
             self._hb.extra["pending"] = waiting
             now = time.monotonic()
-            if new or (waiting and now - last_ring >= BELL_FALLBACK):
+            ring = False
+            if new:
+                sent = False
+                if self._share_previews:
+                    port = self._bell.port_at(_k("spv"))
+                    if port is not None:
+                        sent = True
+                        for msg in share_preview_msgs(new, self.comm.info.orig_rank):
+                            if self._bell.send_port(port, msg):
+                                self.previews_sent += 1
+                            else:
+                                sent = False
+                if sent:
+                    hold_until = hold_until or now + PREVIEW_GRACE
+                else:
+                    ring = True
+            if waiting and hold_until is not None and now >= hold_until:
+                ring = True
+            elif waiting and hold_until is None and now - last_ring >= BELL_FALLBACK:
+                ring = True
+            if ring:
                 self._bell.ring(0, b"s")
-                last_ring = now
+                last_ring, hold_until = now, None
+            elif not waiting:
+                hold_until = None
 
     def run(self) -> None:
         self.local.start()

@@ -294,6 +294,8 @@ def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_p
         "collectives_total": rep.get("leader_collectives", 0) + sum(follower_coll.values()),
         "node_ops": rep.get("ops", 0), "op_p50_ms": rep.get("op_p50_ms"), "op_p99_ms": rep.get("op_p99_ms"),
         "remote_stale": rep.get("remote_stale", 0),
+        "share_previews": rep.get("share_previews", 0),
+        "share_gathered_first": rep.get("share_gathered_first", 0),
         "hit_to_accept_rank0": lat["local"], "hit_to_accept_remote": lat["remote"],
         "host_verify_to_accept_rank0": host["local"], "host_verify_to_accept_remote": host["remote"],
         "definition": ("otedama node --gpus N (supervisor + N ranks, RCCL between them, each rank's GPU miner in its "
