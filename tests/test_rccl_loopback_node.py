@@ -150,7 +150,7 @@ def test_native_path_node_survives_a_follower_and_a_leader_loss(tmp_path, world)
     assert pst["accepted"] > 0 and pst["rejected"] == 0, pst
 
 
-def test_loopback_module_collectives_and_timeouts():
+def test_loopback_module_collectives_and_timeouts(monkeypatch):
     """The stand-in itself: RCCL's results for every op at world 3, a deadline when a member never enters the op,
     and an aborted communicator refusing further ops."""
     import threading
@@ -161,7 +161,7 @@ def test_loopback_module_collectives_and_timeouts():
     from otedama_amd.parallel.kvstore import StoreServer
 
     with StoreServer() as srv:
-        os.environ["MASTER_PORT"] = str(srv.port)
+        monkeypatch.setenv("MASTER_PORT", str(srv.port))
         uid = lb.unique_id()
         comms, errs = [None] * 3, []
 
