@@ -75,6 +75,7 @@ def main() -> int:
     ap.add_argument("--difficulty", type=float, default=2.0)
     ap.add_argument("--job-interval", type=float, default=5.0)
     ap.add_argument("--block-interval", type=float, default=45.0)
+    ap.add_argument("--share-seconds", type=float, default=1.0, help="the pool's vardiff target share interval")
     ap.add_argument("--max-rss-growth-mb", type=float, default=64.0)
     ap.add_argument("--workdir", default="gpurun_out/soak")
     ap.add_argument("--bounce-at", type=float, default=0.0,
@@ -97,7 +98,7 @@ def main() -> int:
 
     def make_pool(sv2="127.0.0.1:0", v1="127.0.0.1:0"):
         return PoolServer(PoolOptions(algorithm=a.algorithm, initial_difficulty=a.difficulty, payout_address=ADDR,
-                                      target_share_seconds=1.0, retarget_seconds=15.0, job_interval=a.job_interval,
+                                      target_share_seconds=a.share_seconds, retarget_seconds=15.0, job_interval=a.job_interval,
                                       block_interval=a.block_interval, noise=bool(a.noise), noise_suite=a.noise,
                                       listen_sv2=sv2, listen_v1=v1))
 
