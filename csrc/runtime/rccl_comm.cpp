@@ -202,6 +202,9 @@ class RcclComm {
   template <class Start>
   void run(size_t in_bytes, size_t out_bytes, double timeout_s, const char* what, Start start, size_t in_off = 0) {
     if (comm_ == nullptr) throw std::runtime_error("rccl: communicator aborted");
+    // An op that timed out may still be queued on the stream (its peer never came): the next op would stage into
+    // the buffers it reads and writes. Such a communicator only serves an abort.
+    if (broken_) throw std::runtime_error("rccl: an earlier op timed out; abort this communicator and re-form");
     hip_check(hipSetDevice(device_), "hipSetDevice");
     char* h = static_cast<char*>(host_);
     char* d = static_cast<char*>(dev_);
@@ -209,16 +212,21 @@ class RcclComm {
     ncclResult_t r = start();
     if (r != ncclSuccess && r != ncclInProgress)
       throw std::runtime_error(std::string("rccl ") + what + ": " + ncclGetErrorString(r));
-    if (r == ncclInProgress) wait_until([&] { return settled(); }, timeout_s, what);  // enqueue of a non-blocking comm
-    hip_check(hipMemcpyAsync(h, d, out_bytes, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync D2H");
-    hip_check(hipEventRecord(done_, stream_), "hipEventRecord");
-    wait_until([&] {
-      const hipError_t q = hipEventQuery(done_);
-      if (q == hipSuccess) return 1;
-      if (q != hipErrorNotReady) hip_check(q, "hipEventQuery");
-      settled();  // a failed peer surfaces here while the event never completes
-      return 0;
-    }, timeout_s, what);
+    try {
+      if (r == ncclInProgress) wait_until([&] { return settled(); }, timeout_s, what);  // non-blocking enqueue
+      hip_check(hipMemcpyAsync(h, d, out_bytes, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync D2H");
+      hip_check(hipEventRecord(done_, stream_), "hipEventRecord");
+      wait_until([&] {
+        const hipError_t q = hipEventQuery(done_);
+        if (q == hipSuccess) return 1;
+        if (q != hipErrorNotReady) hip_check(q, "hipEventQuery");
+        settled();  // a failed peer surfaces here while the event never completes
+        return 0;
+      }, timeout_s, what);
+    } catch (...) {
+      broken_ = true;
+      throw;
+    }
     ++ops_;
   }
 
@@ -241,6 +249,7 @@ class RcclComm {
   void* host_ = nullptr;
   size_t cap_ = 0;
   uint64_t ops_ = 0;
+  bool broken_ = false;
 };
 
 py::bytes unique_id() {

@@ -9,6 +9,7 @@ the node's ranks load this module instead, so that protocol runs end to end at w
   * init waits for all ``nranks`` members of the id (RCCL's bootstrap) and fails after ``timeout_s``;
   * an op completes only when every member has entered it; a dead peer makes it raise TimeoutError after its
     deadline (what ``RcclTimeout`` is on the native module);
+  * an op that failed (a timeout) leaves the communicator broken: every later op raises RuntimeError until an abort;
   * ``abort`` is immediate and every later op raises RuntimeError.
 """
 from __future__ import annotations
@@ -45,6 +46,7 @@ class RcclComm:
         self._seq = 0
         self._ops = 0
         self._alive = True
+        self._broken = False
         self._store.set(f"{self._p}/join/{rank}", b"1")
         try:
             self._wait([f"{self._p}/join/{r}" for r in range(nranks)], timeout_s, "init")
@@ -81,6 +83,8 @@ class RcclComm:
     def _exchange(self, mine: bytes | None, senders: list[int], timeout_s: float, what: str) -> list[bytes]:
         if not self._alive:
             raise RuntimeError("rccl: communicator aborted")
+        if self._broken:
+            raise RuntimeError("rccl: an earlier op timed out; abort this communicator and re-form")
         s = self._seq
         self._seq += 1
         # every member has set its op s-1 key before anyone reaches op s+1, so op s-1's keys are read by now
@@ -88,7 +92,11 @@ class RcclComm:
             self._store.delete_key(f"{self._p}/{s - 2}/{self.rank}")
         self._store.set(f"{self._p}/{s}/{self.rank}", mine if mine is not None else b"")
         keys = [f"{self._p}/{s}/{r}" for r in range(self.nranks)]
-        self._wait(keys, timeout_s, what)  # every member entered the op (a barrier, as a collective is)
+        try:
+            self._wait(keys, timeout_s, what)  # every member entered the op (a barrier, as a collective is)
+        except TimeoutError:
+            self._broken = True
+            raise
         self._ops += 1
         return [self._store.get(f"{self._p}/{s}/{r}") for r in senders]
 

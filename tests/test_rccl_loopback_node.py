@@ -195,6 +195,8 @@ def test_loopback_module_collectives_and_timeouts(monkeypatch):
         with pytest.raises(TimeoutError):  # ranks 1 and 2 never enter: a dead peer
             comms[0].all_gather(b"x" * 8, 0.3)
         assert time.monotonic() - t0 < 2.0
+        with pytest.raises(RuntimeError, match="timed out"):  # broken until aborted, as the native module
+            comms[0].all_gather(b"x" * 8, 0.3)
         comms[0].abort()
         assert not comms[0].alive
         with pytest.raises(RuntimeError):

@@ -120,3 +120,21 @@ def test_a_native_rank_process_never_imports_torch():
                          env=dict(os.environ, PYTHONPATH=ROOT))
     assert res.returncode == 0, res.stderr[-3000:]
     assert res.stdout.strip().splitlines()[-1] == "NO-TORCH", res.stdout
+
+
+@pytest.mark.gpu
+def test_an_op_past_its_deadline_leaves_the_communicator_broken_until_aborted():
+    """A timed-out op may still sit in the comm stream (at world > 1: its peer never came), so the next op must not
+    stage into the buffers it uses: the communicator refuses every op until it is aborted, and a new one works."""
+    from otedama_amd import _rccl
+
+    c = _rccl.RcclComm(0, 1, 0, _rccl.unique_id(), 30.0)
+    big = bytes(64 << 20)  # ~ms of staging copies: still in flight at a zero deadline
+    with pytest.raises(TimeoutError):
+        c.all_gather(big, 0.0)
+    with pytest.raises(RuntimeError, match="timed out"):
+        c.all_gather(b"x" * 8, 5.0)
+    c.abort()
+    d = _rccl.RcclComm(0, 1, 0, _rccl.unique_id(), 30.0)
+    assert d.all_gather(b"y" * 8, 5.0) == b"y" * 8
+    d.abort()
