@@ -71,74 +71,97 @@ class StoreClient:
 
     def set_timeout(self, timeout: float | datetime.timedelta) -> None:
         self._timeout = timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout)
-        self._sock.settimeout(self._timeout)
+        if self._sock is not None:
+            self._sock.settimeout(self._timeout)
 
     def clone(self) -> "StoreClient":
         return StoreClient(self.host, self.port, self._timeout)
 
     def set(self, key, value) -> None:
-        with self._lock:
-            self._sock.sendall(_U8.pack(SET) + _vec(_key(key)) + _vec(_b(value)))
+        self._rpc(_U8.pack(SET) + _vec(_key(key)) + _vec(_b(value)), lambda: None)
 
     def get(self, key) -> bytes:
         """The key's value, waiting for it to be set up to the client's timeout (TimeoutError), as torch's get()."""
         self.wait([key])
-        with self._lock:
-            self._sock.sendall(_U8.pack(GET) + _vec(_key(key)))
-            return self._read_vec()
+        return self._rpc(_U8.pack(GET) + _vec(_key(key)), self._read_vec)
 
     def add(self, key, delta: int) -> int:
-        with self._lock:
-            self._sock.sendall(_U8.pack(ADD) + _vec(_key(key)) + _I64.pack(int(delta)))
-            return _I64.unpack(self._read(8))[0]
+        return self._rpc(_U8.pack(ADD) + _vec(_key(key)) + _I64.pack(int(delta)), lambda: _I64.unpack(self._read(8))[0])
 
     def check(self, keys) -> bool:
-        with self._lock:
-            self._sock.sendall(_U8.pack(CHECK) + _U64.pack(len(keys)) + b"".join(_vec(_key(k)) for k in keys))
-            return self._read(1)[0] == READY
+        return self._rpc(_U8.pack(CHECK) + _U64.pack(len(keys)) + b"".join(_vec(_key(k)) for k in keys),
+                         lambda: self._read(1)[0] == READY)
 
     def delete_key(self, key) -> bool:
-        with self._lock:
-            self._sock.sendall(_U8.pack(DELETE_KEY) + _vec(_key(key)))
-            return _I64.unpack(self._read(8))[0] == 1
+        return self._rpc(_U8.pack(DELETE_KEY) + _vec(_key(key)), lambda: _I64.unpack(self._read(8))[0] == 1)
 
     def wait(self, keys, timeout: float | datetime.timedelta | None = None) -> None:
         """Block until every key exists (TimeoutError after ``timeout``, default the client's)."""
         t = self._timeout if timeout is None else (
             timeout.total_seconds() if isinstance(timeout, datetime.timedelta) else float(timeout))
         with self._lock:
-            self._sock.sendall(_U8.pack(WAIT) + _U64.pack(len(keys)) + b"".join(_vec(_key(k)) for k in keys))
-            self._sock.settimeout(t)
+            sock = self._conn()
+            canceled = False  # the wait timed out and was withdrawn: the connection is back in sync
             try:
-                got = self._read(1)[0]
-            except socket.timeout:
-                # withdraw the wait: the server answers WAIT_CANCELED (after a STOP_WAITING that crossed it)
-                self._sock.settimeout(self._timeout)
-                self._sock.sendall(_U8.pack(CANCEL_WAIT))
-                while self._read(1)[0] != WAIT_CANCELED:
-                    pass
-                raise TimeoutError(f"wait timeout after {t:.1f} s, keys: {list(keys)}") from None
-            finally:
-                self._sock.settimeout(self._timeout)
+                sock.sendall(_U8.pack(WAIT) + _U64.pack(len(keys)) + b"".join(_vec(_key(k)) for k in keys))
+                sock.settimeout(t)
+                try:
+                    got = self._read(1)[0]
+                except socket.timeout:
+                    # withdraw the wait: the server answers WAIT_CANCELED (after a STOP_WAITING that crossed it)
+                    sock.settimeout(self._timeout)
+                    sock.sendall(_U8.pack(CANCEL_WAIT))
+                    while self._read(1)[0] != WAIT_CANCELED:
+                        pass
+                    canceled = True
+                    raise TimeoutError(f"wait timeout after {t:.1f} s, keys: {list(keys)}") from None
+                sock.settimeout(self._timeout)
+            except BaseException:
+                if canceled:
+                    sock.settimeout(self._timeout)
+                else:
+                    self._drop()
+                raise
             if got != STOP_WAITING:
+                self._drop()
                 raise RuntimeError(f"store: unexpected WAIT reply {got}")
 
     def ping(self) -> bool:
-        with self._lock:
-            self._sock.sendall(_U8.pack(PING) + _U32.pack(0x0D7E))
-            return _U32.unpack(self._read(4))[0] == 0x0D7E
+        return self._rpc(_U8.pack(PING) + _U32.pack(0x0D7E), lambda: _U32.unpack(self._read(4))[0] == 0x0D7E)
 
     def close(self) -> None:
-        try:
-            self._sock.close()
-        except OSError:
-            pass
+        self._drop()
 
     # ---------------------------------------------------------------- wire
+    def _conn(self) -> socket.socket:
+        if self._sock is None:  # the previous request failed part way: a fresh connection, in protocol sync
+            self._sock = self._connect(self._timeout)
+        return self._sock
+
+    def _drop(self) -> None:
+        sock, self._sock = self._sock, None
+        if sock is not None:
+            try:
+                sock.close()
+            except OSError:
+                pass
+
+    def _rpc(self, payload: bytes, read):
+        """One request and its reply. A request that fails part way (a timeout, a reset) may leave a reply in flight
+        that the next request would read as its own, so the connection is dropped and the next request reconnects."""
+        with self._lock:
+            sock = self._conn()
+            try:
+                sock.sendall(payload)
+                return read()
+            except BaseException:
+                self._drop()
+                raise
+
     def _read(self, n: int) -> bytes:
         buf = bytearray()
         while len(buf) < n:
-            chunk = self._sock.recv(n - len(buf))
+            chunk = self._sock.recv(n - len(buf))  # type: ignore[union-attr]
             if not chunk:
                 raise ConnectionError("store closed the connection")
             buf += chunk

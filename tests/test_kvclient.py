@@ -62,3 +62,30 @@ def test_interleaves_with_torchs_client(server):
     assert mine.get("k2") == b"from-torch"
     assert theirs.add("c", 1) == 1 and mine.add("c", 1) == 2 and theirs.add("c", 0) == 2
     assert theirs.check(["k1", "k2"]) and mine.check(["k1", "k2"])
+
+
+def test_a_request_that_fails_part_way_reconnects_in_sync():
+    """A reply that arrives after its request gave up must not be read as the next request's reply: the client drops
+    the connection on a failed request and the next one reconnects."""
+    import socket as _socket
+
+    from otedama_amd.parallel.kvclient import StoreClient
+    from otedama_amd.parallel.kvstore import StoreServer
+
+    with StoreServer() as srv:
+        c = StoreClient("127.0.0.1", srv.port, timeout=5.0)
+        c.set("a", b"1")
+        real = c._sock
+        c._sock.settimeout(1e-9)  # the next reply cannot arrive in time
+        try:
+            c.check(["a"])
+        except (_socket.timeout, TimeoutError, BlockingIOError, OSError):
+            pass
+        else:  # the reply beat the clock: nothing to test on this host
+            return
+        assert c._sock is None and real.fileno() == -1  # dropped, not reused with a reply in flight
+        assert c.get("a") == b"1" and c.check(["a"]) and c.add("n", 2) == 2
+        with pytest.raises(TimeoutError):
+            c.wait(["missing"], timeout=0.1)
+        assert c._sock is not None and c.get("a") == b"1"  # a withdrawn wait keeps the connection in sync
+        c.close()
