@@ -196,6 +196,7 @@ async def _run_async(cfg, fs, no_tui, wallet_pass, mnemonic_pass, structlog, std
             "stats": lambda: eng_holder["e"].stats() if "e" in eng_holder else {},
             "devices": lambda: eng_holder["e"].device_list() if "e" in eng_holder else [],
             "debug_stats": lambda: eng_holder["e"].debug_stats() if "e" in eng_holder else {},
+            "node": lambda: eng_holder["e"].node_status() if "e" in eng_holder else {},
         })
         try:
             srv.start()

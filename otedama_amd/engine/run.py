@@ -455,6 +455,35 @@ class Engine:
         rep["work_started"] = ws
         return rep
 
+    def node_status(self) -> dict:
+        """GET /api/v1/node: the multi-GPU node as its leader sees it (membership, generation, data plane, each rank's
+        rate and heartbeat, share delivery). A standalone engine reports a one-rank node."""
+        ms = self.miners
+        link = getattr(ms, "link", None)
+        if link is None:
+            return {"world": 1, "members": [0], "backend": "none", "generation": 0, "ranks": {}}
+        info = link.comm.info
+        try:
+            hbs = ms.heartbeats_snapshot()
+        except Exception:  # noqa: BLE001 - store gone: shutting down
+            hbs = {}
+        now = time.time()
+        ranks = {"rank0": {"hashrate": sum(self.device_hashrates.get(d.id, 0.0) for d in ms.local.miners),
+                           "leader": True}}
+        for r, hb in hbs.items():
+            ranks[f"rank{r}"] = {"hashrate": self.device_hashrates.get(f"rank{r}", 0.0),
+                                 "heartbeat_age_s": round(now - float(hb.get("t", 0.0) or 0.0), 3),
+                                 "generation": hb.get("gen"), "pending_shares": int(hb.get("pending", 0)),
+                                 "collectives": int(hb.get("coll", 0)), "pid": hb.get("pid"),
+                                 "member": r in info.members}
+        return {"world": info.world_size, "capacity": ms.capacity, "members": list(info.members),
+                "backend": info.backend, "generation": info.generation, "leader_incarnation": ms.incarnation,
+                "lost_ranks": list(ms.lost_ranks), "reforms": link.reforms, "ops": link.ops_run,
+                "leader_collectives": link.comm.collectives,
+                "op_p50_ms": link.tick_quantile(0.5) * 1e3, "op_p99_ms": link.tick_quantile(0.99) * 1e3,
+                "share_previews": ms.share_previews, "share_gathered_first": ms.share_gathered_first,
+                "remote_stale": ms.remote_stale, "ranks": ranks}
+
     async def _report_loop(self, path: str, period: float = 0.5) -> None:
         """Write node_report() to ``path`` every ``period`` s (atomic rename), with the accepted shares'
         (monotonic, hit -> accept ms, origin) and a bounded series of counter samples."""

@@ -9,7 +9,7 @@ Parity: internal/httpserver/server.go
   * /debug/stats: raw native device counters + stripe/fault/stall state (JSON; MI355X
     addition), served whenever the owner registers a ``debug_stats`` provider
   * timeouts: 5 s header read / 10 s read / 10 s write / 60 s idle
-Additions for the north star's "REST/WS API": GET /api/v1/{stats,devices,pool}
+Additions for the north star's "REST/WS API": GET /api/v1/{stats,devices,pool,node}
 (JSON from provider callbacks) and a minimal RFC 6455 WebSocket at /ws that
 pushes the stats JSON once per second. Unauthenticated: bind to loopback.
 """

@@ -91,8 +91,10 @@ def test_native_path_node_survives_a_follower_and_a_leader_loss(tmp_path, world)
                 OTEDAMA_PG_TIMEOUT="20", OTEDAMA_NODE_REPORT=str(report))
     nenv.pop("OTEDAMA_DIST_BACKEND", None)
     log = tmp_path / "node.out"
+    api = f"127.0.0.1:{free_port()}"
     sup = subprocess.Popen([sys.executable, "-m", "otedama_amd", "node", "--gpus", str(world), "--config", str(cfg),
-                            "--no-tui"], env=nenv, cwd=ROOT, stdout=open(log, "w"), stderr=subprocess.STDOUT)
+                            "--no-tui", "--http-addr", api], env=nenv, cwd=ROOT, stdout=open(log, "w"),
+                           stderr=subprocess.STDOUT)
     try:
         # every follower's shares cross R2 on the native path's collectives
         first = _wait(lambda: (lambda r: r if _remote(r) >= world and r.get("world") == world else None)(
@@ -106,6 +108,13 @@ def test_native_path_node_survives_a_follower_and_a_leader_loss(tmp_path, world)
         for r, p in ranks.items():  # a native rank never loads torch (start-up and RSS)
             maps = open(f"/proc/{p.pid}/maps").read()
             assert "libtorch" not in maps, f"rank {r} mapped libtorch"
+        # the leader's view over HTTP: every rank a member of generation 0 on the native data plane, heartbeating
+        with urllib.request.urlopen(f"http://{api}/api/v1/node", timeout=5) as resp:
+            st = json.loads(resp.read())
+        assert st["world"] == world and st["backend"] == "rccl" and st["members"] == list(range(world)), st
+        assert set(st["ranks"]) == {f"rank{r}" for r in range(world)}, st
+        assert all(v["heartbeat_age_s"] < 2.0 and v["member"] for k, v in st["ranks"].items() if k != "rank0"), st
+        assert st["share_previews"] > 0 and st["remote_stale"] == 0, st
 
         # a follower lost: the leader's collective times out, it aborts and re-forms (without it, or with the
         # supervisor's replacement when that is already back); the replacement is a member of a later generation
