@@ -268,7 +268,9 @@ class _Heartbeat:
     op loop may sit in a bounded collective meanwhile)."""
 
     def __init__(self, store, orig_rank: int, local: MinerSet, comm: NodeComm | None = None):
+        self._origin = store
         self.store = _clone(store)
+        self.failures = 0  # store writes that failed (each retried on a fresh connection)
         self.orig = orig_rank
         self.local = local
         self.comm = comm
@@ -293,11 +295,19 @@ class _Heartbeat:
                 "pid": os.getpid(), **self.extra}
 
     def _loop(self):
+        """One heartbeat per HB_INTERVAL. A failed write (the store stalled past its timeout, a reset connection) is
+        retried on a fresh connection at the next beat: a heartbeat thread that gave up would leave a live rank
+        looking dead to the leader for good (never re-admitted). At shutdown the store is gone and the process with
+        it."""
         while not self.stop.is_set():
             try:
                 self.store.set(_k("hb", self.orig), json.dumps(self.payload()))
-            except Exception:  # noqa: BLE001 - store gone: the node is shutting down
-                return
+            except Exception:  # noqa: BLE001
+                self.failures += 1
+                try:
+                    self.store = _clone(self._origin)
+                except Exception:  # noqa: BLE001 - not reachable now: try again at the next beat
+                    pass
             self.stop.wait(HB_INTERVAL)
 
 
