@@ -953,9 +953,12 @@ class NodeMinerSet:
                     msg = sock.recv(65536)
                 except (BlockingIOError, OSError):
                     break
-                shares = parse_share_preview(msg)
-                if shares:
-                    self._take(shares, preview=True)
+                try:
+                    shares = parse_share_preview(msg)
+                    if shares:
+                        self._take(shares, preview=True)
+                except Exception as exc:  # noqa: BLE001 - one bad datagram must not end the previews (R2 covers it)
+                    self.log("warn", f"node: share preview dropped ({type(exc).__name__}: {exc})")
 
     def _take(self, shares: list[dict], preview: bool = False) -> None:
         n = 0
@@ -1025,6 +1028,15 @@ class NodeWorker:
         previewed shares, and the shares of that window share one gather. Without one (previews off, no port yet, a
         failed send) the ring goes at once. While shares are still waiting (a lost datagram, a leader that is being
         restarted, more than one gather's worth) the bell is rung again every BELL_FALLBACK."""
+        while not self._stop.is_set():
+            try:
+                self._share_pass()
+            except Exception as exc:  # noqa: BLE001 - the share path must outlive one bad pass
+                self.log("warn", f"node: {self.rank_id}: share loop error ({type(exc).__name__}: {exc})")
+                self._stop.wait(BELL_FALLBACK)
+
+    def _share_pass(self) -> None:
+        """The share loop's body (see _share_loop); returns only on stop or an error."""
         fds = list(self.local.share_fds())
         last_ring = 0.0
         hold_until = None  # a preview went out: ring for its R2 at this time
