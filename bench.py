@@ -974,6 +974,7 @@ class Bench:
             "node_hps_by_algorithm": {a: _r(v.get("total_hashes_per_sec")) for a, v in nalg.items()} or None,
             "node_rejected_by_algorithm": {a: v.get("pool_rejected") for a, v in nalg.items()} or None,
             "node_remote_hit_to_accept_p50_ms": _r((node.get("hit_to_accept_remote") or {}).get("p50_ms")),
+            "node_share_previews": node.get("share_previews"),  # remote shares admitted from a preview, not R2
             "node_job_switch_worst_rank_p50_ms": _r(js.get("worst_rank_p50_ms")),
             "node_job_switch_worst_rank_max_ms": _r(js.get("worst_rank_max_ms")),
             "node_job_switch_stale_rejects": js.get("stale_rejects"),
