@@ -134,6 +134,16 @@ class EngineMetrics:
         self.node_ranks = G("otedama_node_ranks", "Multi-GPU node: ranks (one per GPU) in the torchrun job; 1 when "
                                                   "running standalone.")
         self.node_ranks.set(1)
+        self.node_generation = G("otedama_node_generation",
+                                 "Multi-GPU node: process-group generation (each re-form after a lost or rejoining "
+                                 "rank starts the next one); 0 outside node mode.")
+        self.node_lost_ranks = G("otedama_node_lost_ranks",
+                                 "Multi-GPU node: ranks currently out of the node (lost, not yet re-admitted).")
+        self.node_share_previews = G("otedama_node_share_previews",
+                                     "Multi-GPU node: remote shares the leader admitted from a follower's preview "
+                                     "datagram, ahead of the R2 gather, since start.")
+        self.node_remote_stale = G("otedama_node_remote_stale_shares",
+                                   "Multi-GPU node: remote shares of a job the leader no longer knows (dropped).")
         self._lock = threading.Lock()
         self._reject_reason: dict[str, object] = {}
         self._last_reject: dict[str, object] = {}

@@ -954,6 +954,10 @@ class Engine:
             self.m.node_collective_seconds.set(link.tick_quantile(0.5))
             self.m.node_collective_p99.set(link.tick_quantile(0.99))
             self.m.node_collectives.set(link.comm.collectives)
+            self.m.node_generation.set(max(link.comm.info.generation, 0))
+            self.m.node_lost_ranks.set(len(getattr(self.miners, "lost_ranks", []) or []))
+            self.m.node_share_previews.set(getattr(self.miners, "share_previews", 0))
+            self.m.node_remote_stale.set(getattr(self.miners, "remote_stale", 0))
         self.m.devices_faulted.set(sum(1 for s in dstats.values() if s["faulted"]))
         self.m.devices_stalled.set(len(stalled_devs))
         self.m.devices_active.set(len(self.miners.live()) - len(stalled_devs))
