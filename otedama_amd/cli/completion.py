@@ -23,7 +23,8 @@ COMMANDS = {
     "help": "Print help",
     "completion": "Generate shell completion",
 }
-SUBCOMMANDS = {"config": "show validate", "service": "install uninstall status", "completion": "bash zsh fish"}
+SUBCOMMANDS = {"config": "show validate", "service": "install uninstall status", "completion": "bash zsh fish",
+               "node": "status"}
 
 
 def join_or(items) -> str:

@@ -512,3 +512,22 @@ def test_pool_config_errors(monkeypatch, args, needle):
                                          ("127.0.0.1:0", 3, "127.0.0.1:0"), ("", 1, ""), ("[::1]:10", 1, "[::1]:11")])
 def test_pool_port_bump(addr, k, want):
     assert pool_cmd._bump(addr, k) == want
+
+
+def test_node_status_renders_the_leaders_view_and_fails_without_a_node():
+    import io
+
+    from otedama_amd.cli.node_cmd import cmd_node, render_status
+
+    st = {"world": 2, "backend": "rccl", "generation": 3, "leader_incarnation": 2, "members": [0, 1],
+          "lost_ranks": [], "reforms": 3, "op_p50_ms": 0.4, "op_p99_ms": 1.2, "share_previews": 10,
+          "share_gathered_first": 1, "remote_stale": 0,
+          "ranks": {"rank0": {"hashrate": 19.4e9, "leader": True},
+                    "rank1": {"hashrate": 19.3e9, "heartbeat_age_s": 0.3, "generation": 3, "pending_shares": 0,
+                              "collectives": 42, "member": True}}}
+    out = render_status(st)
+    assert "node: 2 ranks over rccl, generation 3, leader incarnation 2" in out
+    assert "19.40 GH/s" in out and "19.30 GH/s" in out and "38.70 GH/s" in out and "10 from previews" in out
+    err = io.StringIO()
+    assert cmd_node(["status", "--http-addr", "127.0.0.1:1"], io.StringIO(), err) == 1
+    assert "no node answering" in err.getvalue()

@@ -115,6 +115,11 @@ def test_native_path_node_survives_a_follower_and_a_leader_loss(tmp_path, world)
         assert set(st["ranks"]) == {f"rank{r}" for r in range(world)}, st
         assert all(v["heartbeat_age_s"] < 2.0 and v["member"] for k, v in st["ranks"].items() if k != "rank0"), st
         assert st["share_previews"] > 0 and st["remote_stale"] == 0, st
+        res = subprocess.run([sys.executable, "-m", "otedama_amd", "node", "status", "--http-addr", api],
+                             capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+        assert res.returncode == 0, res.stderr
+        assert f"node: {world} ranks over rccl, generation 0" in res.stdout, res.stdout
+        assert all(f"rank{r}" in res.stdout for r in range(world)) and "total" in res.stdout, res.stdout
 
         # a follower lost: the leader's collective times out, it aborts and re-forms (without it, or with the
         # supervisor's replacement when that is already back); the replacement is a member of a later generation
