@@ -11,7 +11,6 @@ WORKDIR /src
 COPY csrc csrc
 COPY otedama_amd otedama_amd
 COPY pyproject.toml README.md ./
-ENV OTEDAMA_OFFLOAD_ARCH=gfx950
 RUN python3 -m otedama_amd._build -j 16 && python3 -m compileall -q otedama_amd
 
 FROM ${BASE}

@@ -3,7 +3,6 @@
 # the toolchain is ROCm (hipcc for gfx950) + g++ + Python instead of Go.
 
 PYTHON      ?= python3
-ARCH        ?= gfx950
 JOBS        ?= 8
 GPURUN      ?= /usr/local/graft/bin/gpurun
 IMAGE       ?= otedama-mi355x
@@ -18,10 +17,10 @@ help: ## Display this help message
 	@grep -E '^[a-zA-Z_-]+:.*?## ' $(MAKEFILE_LIST) | awk 'BEGIN {FS = ":.*?## "}; {printf "  %-16s %s\n", $$1, $$2}'
 
 build: ## Compile the gfx950 HIP kernels + C++ runtime into otedama_amd/_native*.so (incremental)
-	OTEDAMA_OFFLOAD_ARCH=$(ARCH) $(PYTHON) -m otedama_amd._build -j $(JOBS)
+	$(PYTHON) -m otedama_amd._build -j $(JOBS)
 
 rebuild: ## Force a full native rebuild
-	OTEDAMA_OFFLOAD_ARCH=$(ARCH) $(PYTHON) -m otedama_amd._build -j $(JOBS) --force
+	$(PYTHON) -m otedama_amd._build -j $(JOBS) --force
 
 test: build ## Run the CPU test suite (what CI runs; GPU tests are skipped without a GPU)
 	$(PYTHON) -m pytest tests -x -q -m "not gpu"

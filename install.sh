@@ -22,7 +22,7 @@ command -v hipcc >/dev/null 2>&1 || [ -x /opt/rocm/bin/hipcc ] || {
   echo "install.sh: ROCm hipcc not found (install ROCm 7.x for gfx950)" >&2; exit 1; }
 "$PY" -c "import torch" 2>/dev/null || { echo "install.sh: PyTorch (ROCm build) is required" >&2; exit 1; }
 
-echo "==> building native extension for ${OTEDAMA_OFFLOAD_ARCH:-gfx950}"
+echo "==> building native extension for gfx950"
 (cd "$SRC" && "$PY" -m otedama_amd._build)
 
 mkdir -p "$PREFIX/bin"

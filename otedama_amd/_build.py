@@ -21,7 +21,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "native"
-ARCH = os.environ.get("OTEDAMA_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X (CDNA4) only: the kernels use gfx950 instructions (v_bitop3, buffer-load-to-LDS)
 
 HIP_SOURCES = [
     "kernels/sha256d_search.hip",
