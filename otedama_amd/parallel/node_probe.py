@@ -171,8 +171,9 @@ def job_switch_stats(block_at: list[float], work_started: dict[str, list], ranks
 def _switch_gap(algorithm: str, cpu: bool) -> float:
     """Seconds between forced blocks: a rank's first batch of block k must start before block k+1 is sent to count.
     CPU rehearsals run N ranks + their miners + the pool on a few shared cores, where a follower's apply can lag a
-    second behind (a tests/test_bench_launcher.py world-4 run missed 4 of 32 starts at 1 s)."""
-    return (1.5 if algorithm == "scrypt" else 1.0) * (2.0 if cpu else 1.0)
+    second behind (a tests/test_bench_launcher.py world-4 run missed 4 of 32 starts at 1 s, and 1 of 32 at 2 s with
+    other node tests running beside it)."""
+    return (1.5 if algorithm == "scrypt" else 1.0) * (3.0 if cpu else 1.0)
 
 
 def measure_node(gpus: int, seconds: float = 10.0, warmup: float = 3.0, shares_per_gpu: float = 25.0,
