@@ -173,7 +173,11 @@ class Engine:
         # share crossed the R2 gather; parallel/node.py)
         self.device_latency_by_origin = {"local": LatencyTracker(4096), "remote": LatencyTracker(4096)}
         # accepted shares: (monotonic, device hit -> accept ms | None, origin, device, host verify -> accept ms | None)
-        self.accept_log: collections.deque = collections.deque(maxlen=16384)
+        # (time, hit -> accept ms, origin, device, host-verify -> accept ms) per accepted share, for the node report
+        # (OTEDAMA_NODE_REPORT) only: a production engine keeps no per-share history (it was ~200 B per share, 3 MB
+        # of RSS growth over a 6500-share soak, profiles/r5/k_node_soak)
+        self.accept_log: collections.deque = collections.deque(
+            maxlen=16384 if os.environ.get("OTEDAMA_NODE_REPORT") else 0)
         self.hash_window = HashrateWindow()
         self.current_hashrate = 0.0
         self.device_hashrates: dict[str, float] = {}
@@ -954,7 +958,7 @@ class Engine:
             self.m.node_collective_seconds.set(link.tick_quantile(0.5))
             self.m.node_collective_p99.set(link.tick_quantile(0.99))
             self.m.node_collectives.set(link.comm.collectives)
-            self.m.node_generation.set(max(link.comm.info.generation, 0))
+            self.m.node_generation.set(max(getattr(getattr(link.comm, "info", None), "generation", 0), 0))
             self.m.node_lost_ranks.set(len(getattr(self.miners, "lost_ranks", []) or []))
             self.m.node_share_previews.set(getattr(self.miners, "share_previews", 0))
             self.m.node_remote_stale.set(getattr(self.miners, "remote_stale", 0))

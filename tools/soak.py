@@ -44,6 +44,40 @@ def rss_mb(pid: int) -> float:
     return 0.0
 
 
+def proc_roles(pid: int) -> dict[int, tuple[str, float]]:
+    """pid -> (role, RSS MB) for ``pid`` and its descendants: "supervisor"/"engine", "rank<r>", "devproc<r>"."""
+    kids: dict[int, list[int]] = {}
+    for d in os.listdir("/proc"):
+        if d.isdigit():
+            try:
+                with open(f"/proc/{d}/stat") as f:
+                    kids.setdefault(int(f.read().rsplit(")", 1)[1].split()[1]), []).append(int(d))
+            except (OSError, IndexError, ValueError):
+                continue
+    out, todo = {}, [(pid, None)]
+    while todo:
+        p, parent_role = todo.pop()
+        try:
+            with open(f"/proc/{p}/cmdline", "rb") as f:
+                cmd = f.read().replace(b"\0", b" ").decode(errors="replace")
+            with open(f"/proc/{p}/environ", "rb") as f:
+                env = dict(kv.split(b"=", 1) for kv in f.read().split(b"\0") if b"=" in kv)
+        except OSError:
+            continue
+        rank = env.get(b"RANK", b"").decode()
+        if "devproc" in cmd:
+            role = "devproc" + (parent_role[4:] if parent_role and parent_role.startswith("rank") else "")
+        elif parent_role is None:
+            role = "top"
+        elif " run " in cmd + " " and rank:
+            role = f"rank{rank}"
+        else:
+            role = "other"
+        out[p] = (role, rss_mb(p))
+        todo += [(c, role) for c in kids.get(p, [])]
+    return out
+
+
 def tree_rss_mb(pid: int) -> tuple[float, float]:
     """(RSS of pid and all its descendants, RSS of the descendants): the engine keeps its GPUs in device processes."""
     kids: dict[int, list[int]] = {}
@@ -153,6 +187,7 @@ def main() -> int:
             return 1
         t0 = time.time()
         base_acc = base_rej = 0.0  # pool counters of the pools before a bounce
+        first_roles = last_roles = None  # per-process RSS at the first steady sample and at the end
         while time.time() - t0 < a.seconds:
             time.sleep(a.every)
             if a.bounce_at and bounce is None and time.time() - t0 >= a.bounce_at:
@@ -189,6 +224,10 @@ def main() -> int:
                  "rss_mb": round(rss_mb(proc.pid), 1)}
             tree, child = tree_rss_mb(proc.pid)
             s["tree_rss_mb"], s["device_procs_rss_mb"] = round(tree, 1), round(child, 1)
+            roles = proc_roles(proc.pid)
+            if first_roles is None and s["t"] >= a.warmup:
+                first_roles = roles
+            last_roles = roles
             samples.append(s)
             print(json.dumps(s), flush=True)
     finally:
@@ -216,6 +255,10 @@ def main() -> int:
                "tree_rss_growth_mb": round((last.get("tree_rss_mb") or 0.0) - (steady[0].get("tree_rss_mb") or 0.0
                                                                                 if steady else 0.0), 1),
                "miner_exit_code": exit_code}
+    if first_roles and last_roles:  # RSS growth per process over the steady window, by role
+        summary["rss_growth_by_process_mb"] = {
+            f"{last_roles[p][0]}:{p}": round(last_roles[p][1] - first_roles[p][1], 1)
+            for p in sorted(last_roles, key=lambda q: last_roles[q][0]) if p in first_roles}
     ok = (rates and min(rates) >= 0.9 * med and (not a.bounce_at or (bounce or {}).get("first_accept_after_restart_s")) and not last.get("rejected") and not last.get("pool_rejected")
           and summary["rss_growth_mb"] <= a.max_rss_growth_mb and summary["tree_rss_growth_mb"] <= a.max_rss_growth_mb
           and exit_code == 0)
