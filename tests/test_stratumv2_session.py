@@ -316,7 +316,11 @@ def test_submit_map_is_bounded():
         s = await _dial(pool)
         tasks = [asyncio.ensure_future(s.submit(B.ShareSubmission("1", i, 2, 3), timeout=10))
                  for i in range(V2.SUBMIT_MAP_CAP + 10)]
-        await asyncio.sleep(0.5)
+        for _ in range(200):  # every submit issued (a loaded host runs the tasks late)
+            await asyncio.sleep(0.05)
+            if s._seq >= V2.SUBMIT_MAP_CAP + 10:
+                break
+        await asyncio.sleep(0.05)
         assert len(s._pending) <= V2.SUBMIT_MAP_CAP
         dropped = [t.result() for t in tasks if t.done()]
         assert dropped and all("overflow" in r.reason for r in dropped)

@@ -225,6 +225,7 @@ def main() -> int:
             tree, child = tree_rss_mb(proc.pid)
             s["tree_rss_mb"], s["device_procs_rss_mb"] = round(tree, 1), round(child, 1)
             roles = proc_roles(proc.pid)
+            s["rss_by_process_mb"] = {f"{r}:{p}": round(m, 1) for p, (r, m) in sorted(roles.items())}
             if first_roles is None and s["t"] >= a.warmup:
                 first_roles = roles
             last_roles = roles
