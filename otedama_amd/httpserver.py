@@ -117,7 +117,7 @@ class _Handler(BaseHTTPRequestHandler):
         name = path[len("/debug/pprof"):].strip("/")
         if name in ("", "index"):
             body = "/debug/pprof/goroutine (thread stacks)\n/debug/pprof/profile?seconds=N (cProfile)\n" \
-                   "/debug/pprof/heap (gc counts)\n/debug/pprof/cmdline\n"
+                   "/debug/pprof/heap (gc counts; live allocations by line under PYTHONTRACEMALLOC=1)\n/debug/pprof/cmdline\n"
             return self._send(200, body.encode(), "text/plain; charset=utf-8")
         if name in ("goroutine", "threads"):
             frames = sys._current_frames()
@@ -134,8 +134,17 @@ class _Handler(BaseHTTPRequestHandler):
         if name == "heap":
             import gc
 
-            body = json.dumps({"gc_counts": gc.get_count(), "gc_stats": gc.get_stats(),
-                               "objects": len(gc.get_objects())})
+            heap = {"gc_counts": gc.get_count(), "gc_stats": gc.get_stats(), "objects": len(gc.get_objects())}
+            import tracemalloc
+
+            if tracemalloc.is_tracing():  # PYTHONTRACEMALLOC=1 at start-up: the live allocations by source line
+                snap = tracemalloc.take_snapshot().filter_traces(
+                    (tracemalloc.Filter(False, tracemalloc.__file__), tracemalloc.Filter(False, "<frozen *>")))
+                stats = snap.statistics("lineno")
+                heap["traced_kib"] = round(sum(st.size for st in stats) / 1024, 1)
+                heap["top"] = [{"where": f"{st.traceback[0].filename}:{st.traceback[0].lineno}",
+                                "kib": round(st.size / 1024, 1), "blocks": st.count} for st in stats[:40]]
+            body = json.dumps(heap)
             return self._send(200, body.encode(), "application/json")
         if name == "profile":
             import cProfile

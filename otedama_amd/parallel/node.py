@@ -81,6 +81,7 @@ EPOCH_SHIFT = 40           # leader incarnation i numbers its job epochs from (i
 PREFIX = "otd/"
 PREVIEW_MAX = 60000        # largest job-preview datagram (loopback UDP allows 65507 bytes); bigger jobs go by R1 only
 SEEN_MAX = 65536           # share keys the leader remembers to admit each share once (preview and R2 both carry it)
+SEEN_TTL = 120.0           # ... for this long: R2 follows a preview within ~20 ms, or after a re-form within seconds
 
 
 def share_preview_msgs(shares: list[dict], orig_rank: int) -> list[bytes]:
@@ -105,8 +106,11 @@ def parse_share_preview(msg: bytes) -> list[dict]:
     return unpack_shares(rows, [orig])
 
 
-def share_key(s: dict) -> tuple:
-    return (s["orig_rank"], s["epoch"], s["nonce"], s.get("ntime", 0), s.get("version", 0), s.get("extranonce2", 0))
+def share_key(s: dict) -> int:
+    """A share's identity for the leader's admit-once check, as one 64-bit hash (a tuple of six ints per remembered
+    share was ~320 B of the leader's heap; tracemalloc, profiles/r5/n_rss)."""
+    return hash((s["orig_rank"], s["epoch"], s["nonce"], s.get("ntime", 0), s.get("version", 0),
+                 s.get("extranonce2", 0)))
 
 
 def op_retain() -> int:
@@ -402,7 +406,8 @@ class NodeMinerSet:
         self._jobs: dict[int, dict] = {}          # epoch -> job meta for remote shares
         self._remote = collections.deque(maxlen=65536)
         self._remote_efd = os.eventfd(0, os.EFD_NONBLOCK | os.EFD_CLOEXEC)
-        # remote shares are admitted once, from a preview datagram or an R2 gather, whichever comes first
+        # remote shares are admitted once, from a preview datagram or an R2 gather, whichever comes first:
+        # share_key -> monotonic time it was first seen, oldest first, pruned past SEEN_TTL and SEEN_MAX
         self._seen: collections.OrderedDict = collections.OrderedDict()
         self._take_lock = threading.Lock()
         self.share_previews = 0        # remote shares first admitted from a preview datagram
@@ -963,16 +968,18 @@ class NodeMinerSet:
     def _take(self, shares: list[dict], preview: bool = False) -> None:
         n = 0
         me = self.comm.info.orig_rank
+        now = time.monotonic()
         with self._take_lock:
+            seen = self._seen
+            while seen and (len(seen) > SEEN_MAX or now - next(iter(seen.values())) > SEEN_TTL):
+                seen.popitem(last=False)
             for s in shares:
                 if s["orig_rank"] == me:
                     continue
                 key = share_key(s)
-                if key in self._seen:
+                if key in seen:
                     continue  # already admitted by the other path
-                self._seen[key] = None
-                if len(self._seen) > SEEN_MAX:
-                    self._seen.popitem(last=False)
+                seen[key] = now
                 meta = self._jobs.get(s["epoch"])
                 if meta is None:
                     self.remote_stale += 1  # a job older than the retained window, or a previous leader's

@@ -53,3 +53,38 @@ def test_node_submits_previews_and_admits_each_share_once(drop, monkeypatch):
     else:
         assert r["share_previews"] > 0, r
         assert r["share_gathered_first"] <= max(2, r["share_previews"] // 20), r  # a datagram is rarely late
+
+
+def test_leader_admits_each_share_once_and_forgets_old_keys(monkeypatch):
+    """NodeMinerSet._take: a share seen from a preview is skipped when its R2 copy arrives; the remembered keys are
+    pruned past SEEN_TTL and capped at SEEN_MAX (the leader's heap stays flat on a long run)."""
+    import collections
+    import os as _os
+    import threading
+    import types
+
+    from otedama_amd.parallel import node as nodemod
+
+    clock = [1000.0]
+    monkeypatch.setattr(nodemod.time, "monotonic", lambda: clock[0])
+    monkeypatch.setattr(nodemod, "SEEN_MAX", 4)
+    ms = types.SimpleNamespace(
+        comm=types.SimpleNamespace(info=types.SimpleNamespace(orig_rank=0)), _take_lock=threading.Lock(),
+        _seen=collections.OrderedDict(), _jobs={(3 << 40) + i: {"job_id": str(i)} for i in range(16)},
+        remote_stale=0, _remote=collections.deque(), share_previews=0, share_gathered_first=0,
+        _remote_efd=_os.eventfd(0, _os.EFD_NONBLOCK), _gather_wanted=False)
+    take = nodemod.NodeMinerSet._take
+
+    def share(i):
+        return dict(_share(i), orig_rank=1)
+
+    take(ms, [share(0)], preview=True)
+    take(ms, [share(0)])  # its R2 copy
+    assert len(ms._remote) == 1 and ms.share_previews == 1 and ms.share_gathered_first == 0
+    for i in range(1, 6):
+        take(ms, [share(i)], preview=True)
+    assert len(ms._seen) <= 5 and len(ms._remote) == 6  # capped (pruned before each batch)
+    clock[0] += nodemod.SEEN_TTL + 1
+    take(ms, [share(7)], preview=True)
+    assert list(ms._seen.values()) == [clock[0]]  # everything older than the TTL is gone
+    _os.close(ms._remote_efd)
