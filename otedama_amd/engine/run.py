@@ -432,6 +432,7 @@ class Engine:
                 "ops": link.ops_run, "reforms": link.reforms, "lost_ranks": list(ms.lost_ranks),
                 "leader_incarnation": ms.incarnation, "remote_stale": ms.remote_stale,
                 "share_previews": ms.share_previews, "share_gathered_first": ms.share_gathered_first,
+                "previews_refused": getattr(ms, "previews_refused", 0),
                 "op_p50_ms": link.tick_quantile(0.5) * 1e3, "op_p99_ms": link.tick_quantile(0.99) * 1e3,
                 "job_set_at": list(ms.job_set_at), "job_bcast_at": list(ms.job_bcast_at)})
         # (epoch, CLOCK_MONOTONIC) of each new work's first batch running: rank 0's devices and every follower's

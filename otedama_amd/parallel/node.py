@@ -412,6 +412,7 @@ class NodeMinerSet:
         self._take_lock = threading.Lock()
         self.share_previews = 0        # remote shares first admitted from a preview datagram
         self.share_gathered_first = 0  # ... first from an R2 gather (a lost or late datagram)
+        self.previews_refused = 0      # preview datagrams not from the sending rank's doorbell socket
         self._spv: socket.socket | None = None
         self._spv_thread: threading.Thread | None = None
         self._thread: threading.Thread | None = None
@@ -955,10 +956,16 @@ class NodeMinerSet:
                 return
             while ready:
                 try:
-                    msg = sock.recv(65536)
+                    msg, src = sock.recvfrom(65536)
                 except (BlockingIOError, OSError):
                     break
                 try:
+                    # a preview comes from its rank's doorbell socket (otd/bell/<rank>): anything else on this
+                    # loopback port (a stale sender of an earlier node on this host) is dropped
+                    if len(msg) < 3 or self._bell is None or \
+                            src[1] != self._bell._port_of(int.from_bytes(msg[1:3], "little")):
+                        self.previews_refused += 1
+                        continue
                     shares = parse_share_preview(msg)
                     if shares:
                         self._take(shares, preview=True)

@@ -88,3 +88,43 @@ def test_leader_admits_each_share_once_and_forgets_old_keys(monkeypatch):
     take(ms, [share(7)], preview=True)
     assert list(ms._seen.values()) == [clock[0]]  # everything older than the TTL is gone
     _os.close(ms._remote_efd)
+
+
+def test_previews_are_taken_only_from_the_ranks_doorbell_socket():
+    """The leader's preview reader accepts a datagram only from the doorbell socket its rank published
+    (otd/bell/<rank>); a datagram from any other local socket is refused and counted."""
+    import socket
+    import threading
+    import time as _time
+    import types
+
+    from otedama_amd.parallel import node as nodemod
+    from otedama_amd.parallel.kvclient import StoreClient
+    from otedama_amd.parallel.kvstore import StoreServer
+
+    with StoreServer() as srv:
+        store = StoreClient("127.0.0.1", srv.port, timeout=10)
+        leader_bell, follower_bell = nodemod._Bell(store, 0), nodemod._Bell(store, 1)
+        spv = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        spv.bind(("127.0.0.1", 0))
+        spv.setblocking(False)
+        taken = []
+        ms = types.SimpleNamespace(_bell=leader_bell, _spv=spv, _stop=False, previews_refused=0,
+                                   log=lambda *a: None, _take=lambda sh, preview: taken.extend(sh))
+        th = threading.Thread(target=nodemod.NodeMinerSet._spv_loop, args=(ms,), daemon=True)
+        th.start()
+        port = spv.getsockname()[1]
+        msg = nodemod.share_preview_msgs([_share(1)], 1)[0]
+        rogue = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        rogue.sendto(msg, ("127.0.0.1", port))            # right format, wrong socket
+        assert follower_bell.send_port(port, msg)          # the rank's own doorbell socket
+        end = _time.monotonic() + 5
+        while (not taken or ms.previews_refused < 1) and _time.monotonic() < end:
+            _time.sleep(0.01)
+        ms._stop = True
+        th.join(timeout=2)
+        assert len(taken) == 1 and taken[0]["orig_rank"] == 1 and ms.previews_refused == 1
+        for sock in (rogue, spv):
+            sock.close()
+        leader_bell.close()
+        follower_bell.close()
