@@ -331,3 +331,30 @@ def test_background_zero_interval_uses_the_default():
 
 def test_default_logger_is_silent():
     R.Fetcher(sources=[]).log("anything")
+
+
+def test_failed_fetches_leave_no_cyclic_garbage():
+    """On a host with no route to the rate APIs every fetch fails. A failure must not leave reference cycles
+    (raised error -> traceback -> frame -> error; the futures' exceptions -> worker frames -> opener, socket): only a
+    full GC frees those, and in a long-running process they piled up as ~2.5 MB of RSS per 5-minute fetch
+    (profiles/r5/n_rss). Before the fix, 10 failed fetches left 2,882 unreachable objects."""
+    import gc
+
+    from otedama_amd import rates
+
+    dead = [rates.Source("Dead", "http://127.0.0.1:1/x", lambda b: 0.0)] * 3
+    f = rates.Fetcher(sources=dead, timeout=2)
+    try:
+        f.fetch()  # the pool's threads and the resolver set-up, once
+    except Exception:  # noqa: BLE001
+        pass
+    gc.collect()
+    gc.disable()
+    try:
+        for _ in range(10):
+            with pytest.raises(RuntimeError, match="all sources failed"):
+                f.fetch()
+        assert gc.collect() == 0
+    finally:
+        gc.enable()
+        f.stop()
