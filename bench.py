@@ -63,6 +63,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 BASELINE_HPS = 75e6  # BENCHMARKS.md:46 (whole 7950X, SHA-256d)
@@ -378,12 +379,28 @@ class Bench:
         os.write(1, (json.dumps(out) + "\n").encode())
         return 0 if "sha" in self.R else 1
 
-    def shutdown(self) -> None:
-        if self.info is not None:
-            from otedama_amd.parallel import shutdown
+    SHUTDOWN_S = 20.0  # bound on tearing the process group down once the JSON is out
 
+    def shutdown(self) -> None:
+        """Tear the process group down, bounded: at world > 1 the peers may already be gone (the other ranks leave
+        after their last collective section while rank 0 runs the node and pool sections), and a teardown that
+        waited on them must not hold this process (and the driver's torchrun) open after the JSON line is out."""
+        if self.info is None:
+            return
+        from otedama_amd.parallel import shutdown
+
+        def run():
             with contextlib.suppress(Exception):
                 shutdown(self.info)
+
+        th = threading.Thread(target=run, name="otedama-bench-shutdown", daemon=True)
+        th.start()
+        th.join(self.SHUTDOWN_S)
+        if th.is_alive():
+            print(f"bench.py: rank {self.rank}: process-group teardown did not finish in {self.SHUTDOWN_S:.0f} s; "
+                  "leaving without it", file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(0)
 
     # ------------------------------------------------------------------ sections
     def preflight(self) -> None:
