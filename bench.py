@@ -422,7 +422,24 @@ class Bench:
         self.N = native.require_native()
         t_import = time.monotonic()
         self.guard.set_phase("rendezvous")
-        self.info = init_from_env(backend="gloo" if cpu else None, use_gpu=not cpu)
+        backend, store, probe = ("gloo" if cpu else None), None, None
+        if self.world > 1 and ((backend or os.environ.get("OTEDAMA_DIST_BACKEND")) != "gloo"
+                               or os.environ.get("OTEDAMA_BENCH_PROBE") == "1"):
+            # Can RCCL form a group of every rank, within a deadline? Checked in child processes first
+            # (parallel/rccl_probe.py): a hang there costs the deadline, not the run. If any rank's check fails,
+            # every rank runs over gloo together and the headline is still measured (kernels on each rank's GPU).
+            from otedama_amd.parallel.comm import connect_store_from_env
+            from otedama_amd.parallel.guard import fault_for
+            from otedama_amd.parallel.rccl_probe import run_probe
+
+            self.guard.set_phase("data-plane probe")
+            store = connect_store_from_env()
+            probe = run_probe(store, self.rank, self.world, fault=fault_for(self.rank, "probe"))
+            if not probe["ok"]:
+                backend = "gloo"
+                os.environ["OTEDAMA_DIST_BACKEND"] = "gloo"  # the node / pool sections' processes follow
+            self.guard.set_phase("rendezvous")
+        self.info = init_from_env(backend=backend, use_gpu=not cpu, store=store)
         self.comm = NodeComm(self.info)
         self.dev = self.info.device
         t_pg = time.monotonic()
@@ -435,6 +452,7 @@ class Bench:
         if total != self.world:
             raise RuntimeError(f"pre-flight all_reduce summed {total}, expected {self.world}")
         self.R["preflight"] = {"ok": True, "ranks": sorted(int(r[0]) for r in rows),
+                               "data_plane": {"backend": self.info.backend, "probe": probe},
                                "import_s": round(t_import - t0, 2), "rendezvous_s": round(t_pg - t_import, 2),
                                "first_collectives_ms": round((t1 - t_pg) * 1e3, 2),
                                "since_start_s": round(self.guard.elapsed(), 2), "backend": self.info.backend}

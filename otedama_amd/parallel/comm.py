@@ -52,7 +52,13 @@ def _connect_store(rank: int, world: int):
                          timeout=datetime.timedelta(seconds=max(PG_TIMEOUT_S, 60.0)), wait_for_workers=False, **kw)
 
 
-def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> DistInfo:
+def connect_store_from_env():
+    """This rank's connection to the job's rendezvous store (torchrun's agent, the supervisor, or hosted here by
+    rank 0), before any process group: the bench's data-plane pre-flight (parallel/rccl_probe.py) uses it first."""
+    return _connect_store(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init_from_env(backend: str | None = None, use_gpu: bool | None = None, store=None) -> DistInfo:
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun).
 
     One rank per GPU (LOCAL_RANK = HIP ordinal) over RCCL. ``OTEDAMA_DIST_BACKEND=gloo`` rehearses the
@@ -74,9 +80,8 @@ def init_from_env(backend: str | None = None, use_gpu: bool | None = None) -> Di
         backend = "nccl" if use_gpu else "gloo"
     # RCCL: no watchdog that tears the process down on a peer's death; node.py aborts and re-forms instead
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
-    store = None
     if not dist.is_initialized():
-        store = _connect_store(rank, world)
+        store = store if store is not None else _connect_store(rank, world)
         kw = {"device_id": device, "pg_options": rccl_pg_options()} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 store=dist.PrefixStore("otd-g0", store),

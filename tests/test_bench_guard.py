@@ -184,3 +184,28 @@ def test_diagnose_ignores_stale_status_files(tmp_path):
     d = G.diagnose_run_dir(str(tmp_path), 2, time.time())
     assert d["ranks_checked_in"] == [0] and d["ranks"]["1"]["checked_in"] is False
     assert d["ranks"]["0"]["stderr_tail"].endswith("the last words") and len(d["ranks"]["0"]["stderr_tail"]) <= 600
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fault", ["", "fail:2:probe", "hang:1:probe"])
+def test_data_plane_probe_falls_back_together_and_still_measures(fault):
+    """The pre-flight's data-plane probe (parallel/rccl_probe.py): every rank checks in a child process that the
+    group forms and an all_reduce completes, under a deadline; if any rank's check fails or hangs, every rank runs
+    the bench over gloo together and the headline is still measured. Rehearsed here with the probe's children on
+    gloo (OTEDAMA_PROBE_BACKEND) and an injected failure or hang in one rank's child."""
+    env = {"OTEDAMA_BENCH_PROBE": "1", "OTEDAMA_PROBE_BACKEND": "gloo", "OTEDAMA_PROBE_TIMEOUT": "8"}
+    if fault:
+        env["OTEDAMA_BENCH_FAULT"] = fault
+    res, took = _bench("--gpus", "4", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
+                       env=env, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    dp = d["preflight"]["data_plane"]
+    assert d["value"] and d["value"] > 0 and dp["backend"] == "gloo"
+    assert dp["probe"]["ok"] is (fault == ""), dp
+    if fault:
+        bad = fault.split(":")[1]
+        assert not dp["probe"]["ranks"][bad]["ok"]
+        assert ("injected" if fault.startswith("fail") else "killed") in dp["probe"]["ranks"][bad]["reason"]
+        # the group needs every rank: the others' children waited for it until their deadline
+        assert all(v["ok"] is False for v in dp["probe"]["ranks"].values()), dp

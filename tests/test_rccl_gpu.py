@@ -87,3 +87,28 @@ def test_rccl_group_rendezvous_through_the_supervisors_store():
                 dist.destroy_process_group()
         assert srv.refused == 0
         assert srv.num_keys() > 0
+
+
+@pytest.mark.gpu
+def test_data_plane_probe_forms_an_rccl_group_at_world_one(monkeypatch):
+    """bench.py's data-plane pre-flight (parallel/rccl_probe.py) on the GPU: the child forms a torch.distributed RCCL
+    group through the job's store, runs its all_reduce, meets its peers at the done barrier and reports ok; an
+    injected hang is killed at the deadline and reported as such."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from otedama_amd.parallel.launch import free_port
+    from otedama_amd.parallel.rccl_probe import run_probe
+
+    port = free_port()
+    store = dist.TCPStore("127.0.0.1", port, is_master=True, timeout=datetime.timedelta(seconds=60),
+                          wait_for_workers=False)
+    for k, v in {"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(port), "TORCHELASTIC_RUN_ID": "probe-ok"}.items():
+        monkeypatch.setenv(k, v)
+    r = run_probe(store, 0, 1, timeout=60)
+    assert r["ok"] and r["ranks"]["0"]["ok"], r
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "probe-hang")
+    r = run_probe(store, 0, 1, timeout=3, fault="hang")
+    assert not r["ok"] and "killed" in r["ranks"]["0"]["reason"], r
