@@ -32,6 +32,18 @@ def _prefix() -> str:
     return f"otd-probe-{run}"
 
 
+def _why(stderr: str) -> str:
+    """The informative line of a failed child's stderr: the last error-looking line that is not a warning (torch
+    prints a destroy_process_group warning at exit after the real error), else the last line."""
+    lines = [ln.strip() for ln in stderr.strip().splitlines() if ln.strip()]
+    for ln in reversed(lines):
+        if "Warning" in ln or "warn(" in ln:
+            continue
+        if any(k in ln for k in ("Error", "error", "Duplicate", "NCCL", "nccl", "Exception", "failure")):
+            return ln[:300]
+    return (lines[-1] if lines else "no output")[:300]
+
+
 def run_probe(store, rank: int, world: int, timeout: float | None = None, fault: str | None = None) -> dict:
     """Run this rank's probe child, publish its verdict, and return every rank's ({"ok", "ranks", "seconds"}).
     ``fault="fail"`` makes this rank's child fail (tests); ``"hang"`` makes it hang past the deadline.
@@ -50,7 +62,7 @@ def run_probe(store, rank: int, world: int, timeout: float | None = None, fault:
         out, err = proc.communicate(timeout=timeout)
         ok = proc.returncode == 0 and "probe ok" in out
         if not ok:
-            reason = (err.strip().splitlines() or [f"exit code {proc.returncode}"])[-1][:300]
+            reason = f"exit code {proc.returncode}: " + _why(err)
     except subprocess.TimeoutExpired:
         proc.kill()
         proc.communicate()
@@ -88,7 +100,9 @@ def _child() -> int:
     kw = {}
     dev = torch.device("cpu")
     if backend == "nccl":
-        dev = torch.device(f"cuda:{local}")
+        # one rank per GPU on a node (local < device count); ranks sharing one GPU (a rehearsal) land on the same
+        # device, where RCCL refuses the group: the real failure the fallback exists for
+        dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
         torch.cuda.set_device(dev)
         kw["device_id"] = dev
     dist.init_process_group(backend, rank=rank, world_size=world,
