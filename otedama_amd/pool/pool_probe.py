@@ -169,11 +169,19 @@ def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.
         # steady state: every worker connected and without a retarget larger than SETTLE_BAND for steady_periods
         # retarget windows
         need = steady_periods * retarget_seconds
+
+        def calm(w: dict) -> bool:
+            # no >25% retarget on its way: vardiff's open window, once it holds enough shares to say, points within
+            # 25% of the difficulty in force (on a slow host a 20% miss was corrected after the window had opened)
+            r, n = w.get("window_ratio"), w.get("window_shares", 0) or 0
+            return r is None or n < 30 or abs(math.log(max(r, 1e-12))) < math.log(1.25)
+
         end = time.monotonic() + settle_timeout
         settled = False
         while time.monotonic() < end:
             ws = [w for s in _pool_api(http) for w in s.get("workers", [])]
-            if len(ws) >= len(miners) and all(w["steady_for_s"] >= need and w["accepted"] > 0 for w in ws):
+            if len(ws) >= len(miners) and all(w["steady_for_s"] >= need and w["accepted"] > 0 and calm(w)
+                                              for w in ws):
                 settled = True
                 break
             time.sleep(0.25)

@@ -494,7 +494,13 @@ class PoolServer:
                          # steady state: seconds from the channel's open to its last retarget of more than
                          # SETTLE_BAND, and how long ago that was
                          "converged_after_s": (w.last_big_retarget_at - w.opened_at) if w.last_big_retarget_at else 0.0,
-                         "steady_for_s": now - (w.last_big_retarget_at or w.opened_at)}
+                         "steady_for_s": now - (w.last_big_retarget_at or w.opened_at),
+                         # vardiff's open window: its shares and the difficulty ratio they point to (target interval
+                         # / observed); far from 1 with many shares = a retarget is on its way
+                         "window_shares": w.vd.shares,
+                         "window_ratio": (self.vardiff.cfg.target_share_seconds * w.vd.shares
+                                          / max(self.vardiff.clock() - w.vd.window_start, 1e-9)) if w.vd.shares
+                         else None}
                         for w in live],
         }
 
