@@ -428,13 +428,16 @@ class PoolServer:
         w.vd.difficulty = self.vardiff.difficulty_for_hashrate(nominal_hashrate)
         w.prev_difficulty = w.vd.difficulty
 
-    def after_accept(self, w: _Worker) -> float | None:
+    def after_accept(self, w: _Worker, credited: float | None = None) -> float | None:
+        """Vardiff's bookkeeping of an accepted share; ``credited``: the difficulty the share was accepted at (lower
+        than the one in force for a grace share after a raise)."""
         if self.opts.fixed_difficulty:
             w.vd.shares += 1
             w.vd.total_shares += 1
             return None
         old = w.vd.difficulty
-        new = self.vardiff.on_share(w.vd)
+        weight = credited / old if credited and old > 0 else 1.0
+        new = self.vardiff.on_share(w.vd, weight)
         if new is not None:
             w.retargeted(old, new)
             self.journal.save_worker(w.name, new)
@@ -652,7 +655,7 @@ class _V1Conn:
             v = await self.pool.validate_async(self.worker, str(job_id), self.en1 + en2, ntime, nonce, version)
             if v.accepted:
                 self._write({"id": mid, "result": True, "error": None})
-                if self.pool.after_accept(self.worker) is not None:
+                if self.pool.after_accept(self.worker, v.difficulty) is not None:
                     self._send_difficulty()
             else:
                 code = {"stale-job": 21, "duplicate-share": 22, "low-difficulty-share": 23}.get(v.reason, 20)
@@ -772,7 +775,7 @@ class _V2Conn:
             v = await self.pool.validate_async(w, f"{msg.job_id:x}", prefix, msg.ntime, msg.nonce, msg.nversion)
             if v.accepted:
                 self._send(M.SubmitSharesSuccess(msg.channel_id, msg.sequence_number, 1, max(int(v.difficulty), 1)))
-                new = self.pool.after_accept(w)
+                new = self.pool.after_accept(w, v.difficulty)
                 if new is not None:
                     self._send(M.SetTarget(msg.channel_id, self.pool.share_target(new)))
             else:

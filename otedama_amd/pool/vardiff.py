@@ -42,7 +42,7 @@ class VardiffConfig:
 class VardiffState:
     difficulty: float
     window_start: float = field(default_factory=time.monotonic)
-    shares: int = 0
+    shares: float = 0           # shares in the window, a grace share counting its credited fraction
     accepted_work: float = 0.0      # sum of share difficulties in the window
     total_shares: int = 0
     looks: int = 0                  # retarget periods of this window already judged insignificant
@@ -63,11 +63,15 @@ class Vardiff:
     def clamp(self, d: float) -> float:
         return min(max(d, self.cfg.min_difficulty), self.cfg.max_difficulty)
 
-    def on_share(self, st: VardiffState) -> float | None:
-        """Record an accepted share; returns a new difficulty when a retarget fires."""
-        st.shares += 1
+    def on_share(self, st: VardiffState, weight: float = 1.0) -> float | None:
+        """Record an accepted share; returns a new difficulty when a retarget fires. ``weight``: the share's credited
+        difficulty over the one in force. A share the pool took at the previous, lower difficulty in the grace after
+        a raise is worth that fraction of a share. Counted whole, the old-rate shares of the grace read as a miner
+        still too fast, and vardiff raised again and then walked back (late >25% retargets in the pool probe)."""
+        w = min(max(weight, 0.0), 1.0)
+        st.shares += w
         st.total_shares += 1
-        st.accepted_work += st.difficulty
+        st.accepted_work += st.difficulty * w
         return self.maybe_retarget(st)
 
     def maybe_retarget(self, st: VardiffState) -> float | None:

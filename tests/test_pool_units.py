@@ -265,3 +265,18 @@ def test_retarget_grace_honours_the_lowest_recent_difficulty(monkeypatch):
     t[0] += srv.RETARGET_GRACE + 1     # a retarget long after: the window starts again from the last difficulty
     w.retargeted(8.0)
     assert w.prev_difficulty == 8.0
+
+
+def test_vardiff_counts_a_grace_share_at_its_credited_fraction():
+    """After a raise, the pool credits in-flight shares at the previous difficulty for a grace period; vardiff counts
+    each such share as old/new of a share, so the old-rate shares of the grace do not read as a miner that is still
+    too fast (which raised again and then walked back: late >25% retargets)."""
+    from otedama_amd.pool.vardiff import Vardiff, VardiffConfig
+
+    vd = Vardiff(VardiffConfig(target_share_seconds=1.0, retarget_seconds=10.0), clock=lambda: 0.0)
+    st = vd.new_state(4.0)
+    vd.on_share(st, 0.25)  # found at difficulty 1 while 4 is in force
+    vd.on_share(st)
+    assert st.shares == 1.25 and st.total_shares == 2 and st.accepted_work == 5.0
+    vd.on_share(st, 7.0)  # clamped: a share is never worth more than one
+    assert st.shares == 2.25
