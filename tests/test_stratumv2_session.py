@@ -328,7 +328,11 @@ def test_submit_map_is_bounded():
         await s.close()
         # every submit still waiting ends with "closed": gathered, so no task's exception goes unretrieved
         results = await asyncio.gather(*pending, return_exceptions=True)
-        bad = [r for r in results if not (isinstance(r, B.PoolProtoError) and "closed" in str(r))]
+        # each ends on the close: "closed before verdict" while waiting for it, "Connection lost" while still
+        # writing (a loaded host), or dropped by the map's bound meanwhile; none hangs, none is accepted
+        bad = [r for r in results if not ((isinstance(r, B.PoolProtoError) and ("closed" in str(r)
+                                                                               or "Connection lost" in str(r)))
+                                           or (isinstance(r, B.ShareResult) and "overflow" in r.reason))]
         assert results and not bad, bad[:3]
         await pool.stop()
     run(go())
