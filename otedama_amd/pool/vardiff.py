@@ -42,13 +42,10 @@ class VardiffConfig:
 class VardiffState:
     difficulty: float
     window_start: float = field(default_factory=time.monotonic)
-    shares: float = 0           # shares in the window, a grace share counting its credited fraction
+    shares: float = 0.0         # shares in the window, a grace share counting its credited fraction
     accepted_work: float = 0.0      # sum of share difficulties in the window
     total_shares: int = 0
     looks: int = 0                  # retarget periods of this window already judged insignificant
-
-    def hashes_per_diff1(self, diff1_hashes: float) -> float:
-        return diff1_hashes
 
 
 class Vardiff:
