@@ -25,6 +25,10 @@ import sys
 import time
 
 PROBE_TIMEOUT_S = 60.0
+# How long a rank at the probe waits for its peers to reach it before starting its child anyway. The ranks' cold
+# `import torch` on a fresh node runs at each rank's own pace (up to a minute or two); a child started before its
+# peers arrive would spend its deadline on their import, and a skew past it would read as an RCCL failure.
+ARRIVE_TIMEOUT_S = 120.0
 
 
 def _prefix() -> str:
@@ -44,13 +48,22 @@ def _why(stderr: str) -> str:
     return (lines[-1] if lines else "no output")[:300]
 
 
-def run_probe(store, rank: int, world: int, timeout: float | None = None, fault: str | None = None) -> dict:
-    """Run this rank's probe child, publish its verdict, and return every rank's ({"ok", "ranks", "seconds"}).
+def run_probe(store, rank: int, world: int, timeout: float | None = None, fault: str | None = None,
+              arrive_timeout: float = ARRIVE_TIMEOUT_S) -> dict:
+    """Run this rank's probe child, publish its verdict, and return every rank's ({"ok", "ranks", "seconds",
+    "arrive_s"}). The child starts once every rank has reached the probe (or after ``arrive_timeout``), so its
+    deadline measures RCCL and not the ranks' start-up skew.
     ``fault="fail"`` makes this rank's child fail (tests); ``"hang"`` makes it hang past the deadline.
     ``timeout``: default OTEDAMA_PROBE_TIMEOUT, else PROBE_TIMEOUT_S."""
     if timeout is None:
         timeout = float(os.environ.get("OTEDAMA_PROBE_TIMEOUT", PROBE_TIMEOUT_S))
     prefix = _prefix()
+    t_arrive = time.monotonic()
+    store.set(f"{prefix}/arrive/{rank}", "1")
+    arrived = [f"{prefix}/arrive/{r}" for r in range(world)]
+    end = t_arrive + arrive_timeout
+    while not store.check(arrived) and time.monotonic() < end:
+        time.sleep(0.05)
     t0 = time.monotonic()
     env = dict(os.environ, OTEDAMA_PROBE_PREFIX=prefix)
     if fault:
@@ -76,7 +89,8 @@ def run_probe(store, rank: int, world: int, timeout: float | None = None, fault:
         while not store.check([key]) and time.monotonic() < end:
             time.sleep(0.05)
         ranks[str(r)] = json.loads(store.get(key)) if store.check([key]) else {"ok": False, "reason": "no verdict"}
-    return {"ok": all(v.get("ok") for v in ranks.values()), "ranks": ranks, "seconds": round(time.monotonic() - t0, 2)}
+    return {"ok": all(v.get("ok") for v in ranks.values()), "ranks": ranks, "seconds": round(time.monotonic() - t0, 2),
+            "arrive_s": round(t0 - t_arrive, 2)}
 
 
 def _child() -> int:
