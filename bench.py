@@ -109,6 +109,12 @@ def parse_args(argv=None):
     ap.add_argument("--x11-steps", type=int, default=-1, help="-1 = same as --steps; 0 = skip")
     ap.add_argument("--miner-seconds", type=float, default=-1.0,
                     help="scrypt / X11 through the production GpuMiner: recorded seconds each (-1 = 8 on GPUs; 0 = skip)")
+    ap.add_argument("--comm-ops", type=int, default=200,
+                    help="comm section: ops of each of R1 / R2 / R3 / R2_dev per phase (0 = skip the section)")
+    ap.add_argument("--comm-hz", type=float, default=100.0, help="comm section: op cadence")
+    ap.add_argument("--comm-load", default="sha256d,scrypt",
+                    help="comm section: algorithms every rank mines while the ops run (after the idle phase)")
+    ap.add_argument("--comm-busbw-mib", type=int, default=256, help="comm section: all_gather size for the bus bandwidth")
     ap.add_argument("--seed", type=int, default=1,
                     help="synthetic header seed: the hit count of a seed is one Poisson draw, repeated on every run")
     ap.add_argument("--no-latency", action="store_true")
@@ -187,7 +193,7 @@ def launch(args, argv: list[str]) -> int:
     if not any(seen):
         out = error_output(args, args.gpus, f"rank 0 printed no result (launcher exit code {rc})",
                            {"launcher": f"exit code {rc}"}, diagnose_run_dir(run_dir, args.gpus, t0))
-        print(json.dumps(out), flush=True)
+        print(finalize(out), flush=True)
         return rc or 1
     return rc
 
@@ -241,21 +247,104 @@ def _r(x, digits: int = 4):
     return float(f"{x:.{digits}g}")
 
 
-def _base_config(args) -> dict:
-    return {"model": "sha256d", "seq_len": 80}
+def _base_config(args, world: int = 1) -> dict:
+    return {"model": "sha256d", "global_batch": None, "seq_len": 80, "parallelism": f"dp{world}"}
+
+
+def _short_errors(errors: dict | None, n: int = 160) -> dict | None:
+    return {str(k)[:40]: str(v)[:n] for k, v in errors.items()} if errors else None
 
 
 def error_output(args, world: int, error: str, errors: dict, diagnosis: dict | None) -> dict:
-    """The JSON line of a run that has no headline (the pre-flight failed, or rank 0 never reported)."""
+    """The result of a run that has no headline (the pre-flight failed, or rank 0 never reported). The diagnosis
+    (every rank's stderr and RCCL log tail) stays in the detail file; the line carries the phases only."""
+    phases = {k[:48]: v for k, v in ((diagnosis or {}).get("phases") or {}).items()}
     return {
         "metric": METRIC, "value": None, "unit": "hashes/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32", "data": "synthetic 80-byte block headers", "config": _base_config(args),
+        "dtype": "u32", "data": "synthetic 80-byte block headers", "config": _base_config(args, world),
         "error": error, "errors": errors, "diagnosis": diagnosis,
-        "summary": {"world_size": world, "error": error, "errors": errors,
+        "summary": {"world_size": world, "error": str(error)[:300], "errors": _short_errors(errors),
                     "ranks_checked_in": (diagnosis or {}).get("ranks_checked_in"),
-                    "rank_phases": (diagnosis or {}).get("phases")},
+                    "rank_phases": phases or None},
     }
+
+
+# ------------------------------------------------------------------------------ the printed line
+# The driver parses the LAST line of stdout and keeps only a tail of it: BENCH_r05's 25 KB line came back unparsed
+# (VERDICT r5, missing #1). The line is the driver contract (CONTRACT_KEYS, a short ``config``), the path of the
+# detail file, and the compact ``summary`` last; every full section object goes to the detail file.
+LINE_CAP = 6144
+CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data")
+CONFIG_KEYS = ("model", "global_batch", "seq_len", "parallelism", "kernel", "variants_per_step")
+# summary keys dropped first when a line would still pass LINE_CAP (long error texts, per-rank lists)
+_DROP_ORDER = ("rank_phases", "sections_s", "ranks_seen", "per_rank_hps", "job_switch_p50_ms", "node_rejected",
+               "cfg5_pool_validate_p50_ms", "errors", "node_hps")
+
+
+def detail_paths() -> list[str]:
+    """Where the full result goes: OTEDAMA_BENCH_DETAIL if set, else ./bench_detail.json and
+    ./gpurun_out/bench_detail.json (the part of a GPU box's tree that comes back)."""
+    p = os.environ.get("OTEDAMA_BENCH_DETAIL")
+    if p:
+        return [p]
+    return [os.path.abspath("bench_detail.json"), os.path.abspath(os.path.join("gpurun_out", "bench_detail.json"))]
+
+
+def write_detail(full: dict) -> str | None:
+    """Write the full result (every section object) to the detail file(s); the first path written, or None."""
+    first = None
+    blob = json.dumps(full, default=str)
+    for p in detail_paths():
+        try:
+            os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+            tmp = f"{p}.{os.getpid()}.tmp"
+            with open(tmp, "w") as f:
+                f.write(blob)
+            os.replace(tmp, p)
+            first = first or p
+        except OSError:
+            continue
+    return first
+
+
+def compact_line(full: dict, detail: str | None) -> str:
+    """The one JSON line rank 0 prints: driver contract keys, a config of <= 6 short fields, the detail path, and
+    ``summary`` last, capped at LINE_CAP bytes (summary keys are dropped in _DROP_ORDER, then strings cut, if a
+    pathological run would pass it)."""
+    line = {k: full.get(k) for k in CONTRACT_KEYS}
+    cfg = full.get("config") or {}
+    line["config"] = {k: (cfg[k][:60] if isinstance(cfg[k], str) else cfg[k]) for k in CONFIG_KEYS if k in cfg}
+    if full.get("error") is not None:
+        line["error"] = str(full["error"])[:300]
+    line["detail"] = os.path.basename(detail) if detail else None
+    summary = dict(full.get("summary") or {})
+    line["summary"] = summary
+    s = json.dumps(line, default=str)
+    for k in _DROP_ORDER:
+        if len(s) <= LINE_CAP:
+            break
+        if k in summary:
+            summary.pop(k)
+            summary.setdefault("dropped", []).append(k)
+            s = json.dumps(line, default=str)
+    if len(s) > LINE_CAP:  # last resort: every summary value as a short string
+        line["summary"] = {k: (v if isinstance(v, (int, float, bool)) or v is None else str(v)[:40])
+                           for k, v in list(summary.items())[:60]}
+        s = json.dumps(line, default=str)
+    return s
+
+
+def finalize(full: dict) -> str:
+    """Write the detail file, say where on stderr, and return the line to print."""
+    detail = write_detail(full)
+    if detail:
+        try:
+            os.write(2, f"bench.py: full result -> {detail}\n".encode())
+        except OSError:
+            pass
+    return compact_line(full, detail)
 
 
 # --------------------------------------------------------------------------- the run
@@ -281,6 +370,7 @@ class Bench:
         algos = max(1, len(self.node_algorithms()))
         b = {"sha256d": 120.0 + 5.0 * (a.steps + a.warmup), "single": 90.0, "scrypt": 90.0 + 3.0 * ssteps,
              "x11": 90.0 + 2.0 * xsteps, "miner": 2 * (miner_s + 60.0), "cpu": 40.0 + 3.0 * a.cpu_seconds,
+             "comm": 60.0 + len(self.comm_phases()) * (30.0 + 4 * a.comm_ops / 100.0),
              "latency": 180.0, "node": algos * (150.0 + node_s + a.node_warmup + 4.0 * a.node_switches),
              "pool": 240.0 + pool_s}
         for item in filter(None, (s.strip() for s in a.section_timeouts.split(","))):
@@ -296,6 +386,12 @@ class Bench:
 
     def pool_seconds(self) -> float:
         return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 25.0)
+
+    def comm_phases(self) -> list[str]:
+        """The comm section's phases: idle, then under each mining algorithm (GPUs only: the CPU rehearsal has no
+        device process to load the data plane with)."""
+        algos = [] if self.cpu else [x.strip() for x in self.args.comm_load.split(",") if x.strip()]
+        return ["idle", *algos]
 
     def node_algorithms(self) -> list[str]:
         return [x.strip() for x in self.args.node_algorithms.split(",") if x.strip()]
@@ -314,9 +410,10 @@ class Bench:
         except Exception as exc:  # noqa: BLE001
             return self.fail("sha256d", f"{type(exc).__name__}: {exc}")
         # sections every rank takes part in (collectives): rank 0 decides whether there is time and tells the rest
-        need = {"single": 15.0, "scrypt": 30.0, "x11": 20.0, "miner": 2 * (self.miner_seconds() + 20.0)}
+        need = {"single": 15.0, "scrypt": 30.0, "x11": 20.0, "miner": 2 * (self.miner_seconds() + 20.0),
+                "comm": 30.0 + 2 * len(self.comm_phases()) * 12.0}
         for name, fn in (("single", self.single), ("scrypt", self.scrypt), ("x11", self.x11),
-                         ("miner", self.miner)):
+                         ("miner", self.miner), ("comm", self.comm_section)):
             if not self.wanted(name):
                 continue
             go = g.remaining() >= need[name] if self.rank == 0 else True
@@ -345,7 +442,7 @@ class Bench:
         if not g.finish():
             while True:  # the watchdog fired meanwhile and is printing / exiting
                 time.sleep(1)
-        print(json.dumps(self.output(dict(g.errors))), flush=True)
+        print(finalize(self.output(dict(g.errors))), flush=True)
         self.shutdown()
         return 0
 
@@ -356,6 +453,7 @@ class Bench:
             "scrypt": (a.steps if a.scrypt_steps < 0 else a.scrypt_steps) > 0 and not cpu,
             "x11": (a.x11_steps if a.x11_steps >= 0 else a.steps) > 0 and not cpu,
             "miner": self.miner_seconds() > 0,
+            "comm": a.comm_ops > 0,
             "cpu": a.cpu_seconds > 0,
             "latency": not a.no_latency and not cpu,
             "node": self.node_seconds() > 0 and bool(self.node_algorithms()),
@@ -367,7 +465,7 @@ class Bench:
         g = self.guard
         g.errors.setdefault(section, error)
         if self.rank == 0 and g.finish():
-            print(json.dumps(self.output(dict(g.errors), fatal=error)), flush=True)
+            print(finalize(self.output(dict(g.errors), fatal=error)), flush=True)
             g.stop_peers()
         else:
             g.finish()
@@ -376,7 +474,7 @@ class Bench:
     def emit(self, errors: dict, reason: str) -> int:
         """Watchdog path (rank 0): print the JSON with what finished; exit code 0 when the headline was measured."""
         out = self.output(errors, fatal=None if "sha" in self.R else reason)
-        os.write(1, (json.dumps(out) + "\n").encode())
+        os.write(1, (finalize(out) + "\n").encode())
         return 0 if "sha" in self.R else 1
 
     SHUTDOWN_S = 20.0  # bound on tearing the process group down once the JSON is out
@@ -385,13 +483,12 @@ class Bench:
         """Tear the process group down, bounded: at world > 1 the peers may already be gone (the other ranks leave
         after their last collective section while rank 0 runs the node and pool sections), and a teardown that
         waited on them must not hold this process (and the driver's torchrun) open after the JSON line is out."""
-        if self.info is None:
+        if self.info is None or self.comm is None:
             return
-        from otedama_amd.parallel import shutdown
 
         def run():
             with contextlib.suppress(Exception):
-                shutdown(self.info)
+                self.comm.close()
 
         th = threading.Thread(target=run, name="otedama-bench-shutdown", daemon=True)
         th.start()
@@ -403,6 +500,56 @@ class Bench:
             os._exit(0)
 
     # ------------------------------------------------------------------ sections
+    PREFLIGHT_RESERVE_S = 40.0  # of the pre-flight budget kept back from the probe for a gloo fallback's init
+
+    def native_wanted(self) -> bool:
+        """The bench's data plane is the node's: the native RCCL module (parallel/rcclcomm.py) on GPUs, or its CPU
+        stand-in when OTEDAMA_RCCL_MODULE names one (the rehearsal of that path). OTEDAMA_BENCH_COMM=torch keeps
+        torch.distributed; OTEDAMA_DIST_BACKEND=gloo (ranks sharing one GPU) and the plain CPU rehearsal use gloo."""
+        mode = os.environ.get("OTEDAMA_BENCH_COMM", "").lower()
+        if mode in ("torch", "native"):
+            return mode == "native"
+        if os.environ.get("OTEDAMA_RCCL_MODULE"):
+            return True
+        return not self.cpu and os.environ.get("OTEDAMA_DIST_BACKEND") != "gloo"
+
+    def open_native(self, store, timeout: float):
+        """(NativeNodeComm, error): every rank forms the native communicator, then all ranks agree through the store;
+        if any rank failed, every rank drops it (error set) and the caller falls back together."""
+        import torch
+
+        from otedama_amd.parallel.commbase import DistInfo
+        from otedama_amd.parallel.rcclcomm import NativeNodeComm, _wait_get, cpu_standin
+
+        local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        dev = torch.device("cpu") if (self.cpu or cpu_standin()) else torch.device(f"cuda:{local}")
+        if dev.type == "cuda":
+            torch.cuda.set_device(dev)
+        info = DistInfo(self.rank, self.world, local, "rccl", dev, store=store)
+        comm, err = None, ""
+        try:
+            from otedama_amd.parallel.guard import fault_for
+
+            if fault_for(self.rank, "native") == "fail":  # tests: this rank's in-process init fails after the probe
+                raise RuntimeError("injected native init failure")
+            comm = NativeNodeComm(info, bounded=False, force=True, device_stream=True)
+            comm.reform(list(range(self.world)), 1, timeout=timeout)
+        except Exception as exc:  # noqa: BLE001 - decided together below
+            comm, err = None, f"{type(exc).__name__}: {exc}"[:300]
+        if self.world > 1:
+            store.set(f"otd-bench/native/{self.rank}", "1" if comm is not None else "0")
+            try:
+                flags = [_wait_get(store, f"otd-bench/native/{r}", timeout + 10.0) for r in range(self.world)]
+            except TimeoutError as exc:
+                flags, err = [], err or str(exc)
+            if len(flags) != self.world or any(f != b"1" for f in flags):
+                bad = [r for r, f in enumerate(flags) if f != b"1"]
+                err = err or f"native communicator failed on rank(s) {bad}"
+                if comm is not None:
+                    comm.close()
+                comm = None
+        return comm, err
+
     def preflight(self) -> None:
         t0 = time.monotonic()
         self.guard.set_phase("import")
@@ -423,36 +570,49 @@ class Bench:
         t_import = time.monotonic()
         self.guard.set_phase("rendezvous")
         backend, store, probe = ("gloo" if cpu else None), None, None
-        if self.world > 1 and ((backend or os.environ.get("OTEDAMA_DIST_BACKEND")) != "gloo"
-                               or os.environ.get("OTEDAMA_BENCH_PROBE") == "1"):
-            # Can RCCL form a group of every rank, within a deadline? Checked in child processes first
-            # (parallel/rccl_probe.py): a hang there costs the deadline, not the run. If any rank's check fails,
-            # every rank runs over gloo together and the headline is still measured (kernels on each rank's GPU).
+        native_on = self.native_wanted()
+        left = lambda: max(20.0, self.args.preflight_timeout - self.guard.elapsed())  # noqa: E731
+        if self.world > 1 and (native_on or os.environ.get("OTEDAMA_BENCH_PROBE") == "1"):
+            # Can the native RCCL module form a group of every rank, within a deadline? Checked in child processes
+            # first (parallel/rccl_probe.py): a hang there costs the deadline, not the run. If any rank's check fails,
+            # every rank runs over gloo together (rank 0's one decision) and the headline is still measured.
             from otedama_amd.parallel.comm import connect_store_from_env
             from otedama_amd.parallel.guard import fault_for
             from otedama_amd.parallel.rccl_probe import run_probe
 
             self.guard.set_phase("data-plane probe")
             store = connect_store_from_env()
-            probe = run_probe(store, self.rank, self.world, fault=fault_for(self.rank, "probe"))
+            probe = run_probe(store, self.rank, self.world, fault=fault_for(self.rank, "probe"),
+                              budget=left() - self.PREFLIGHT_RESERVE_S)
             if not probe["ok"]:
-                backend = "gloo"
-                os.environ["OTEDAMA_DIST_BACKEND"] = "gloo"  # the node / pool sections' processes follow
+                native_on, backend = False, "gloo"
             self.guard.set_phase("rendezvous")
-        self.info = init_from_env(backend=backend, use_gpu=not cpu, store=store)
-        self.comm = NodeComm(self.info)
+        comm, native_err = None, ""
+        if native_on:
+            comm, native_err = self.open_native(store, timeout=min(120.0, max(10.0, left() - 30.0)))
+            if comm is None and self.world > 1:
+                backend = "gloo"
+        if backend == "gloo" and self.world > 1:
+            os.environ["OTEDAMA_DIST_BACKEND"] = "gloo"  # the node / pool sections' processes follow
+        if comm is not None:
+            self.info, impl = comm.info, "rccl-native"
+        else:
+            self.info = init_from_env(backend=backend, use_gpu=not cpu, store=store)
+            comm = NodeComm(self.info)
+            impl = {"nccl": "torch-nccl"}.get(self.info.backend, self.info.backend)
+        self.comm = comm
         self.dev = self.info.device
         t_pg = time.monotonic()
         self.guard.set_phase("first-collective")
         total = self.comm.allreduce_counters(1)[0]  # the first collective on the data plane (RCCL on GPUs)
         rows = self.comm.gather_counters([self.info.rank, os.getpid(), 0, 0])
-        if self.world > 1:
-            torch.distributed.barrier()
+        self.comm.barrier()
         t1 = time.monotonic()
         if total != self.world:
             raise RuntimeError(f"pre-flight all_reduce summed {total}, expected {self.world}")
         self.R["preflight"] = {"ok": True, "ranks": sorted(int(r[0]) for r in rows),
-                               "data_plane": {"backend": self.info.backend, "probe": probe},
+                               "data_plane": {"impl": impl, "backend": self.info.backend, "probe": probe,
+                                              **({"native_error": native_err} if native_err else {})},
                                "import_s": round(t_import - t0, 2), "rendezvous_s": round(t_pg - t_import, 2),
                                "first_collectives_ms": round((t1 - t_pg) * 1e3, 2),
                                "since_start_s": round(self.guard.elapsed(), 2), "backend": self.info.backend}
@@ -464,9 +624,7 @@ class Bench:
             torch.cuda.synchronize(self.dev)
 
     def barrier(self) -> None:
-        from otedama_amd.parallel import barrier
-
-        barrier(self.info)
+        self.comm.barrier()
 
     def sha256d(self) -> None:
         import torch
@@ -551,7 +709,7 @@ class Bench:
             if world > 1 and q != last_group[0]:  # R1 on change: rank 0 announces the next variant group
                 if info.is_primary:
                     ctl.fill_(q)
-                comm.run_async(lambda: torch.distributed.broadcast(ctl, src=0))
+                comm.run_async(lambda: comm.broadcast_tensor(ctl))
                 last_group[0] = q
             if r2_done[b] is not None:  # the gather that read this slot two steps ago must be done before reuse
                 torch.cuda.current_stream(dev).wait_event(r2_done[b])
@@ -585,10 +743,7 @@ class Bench:
                     hits_log.append((hdr, out.clone(), lo, V_COUNT if use_v else 1 << 32))
 
                 def r2(o=out, g=gathered[b]):
-                    if world > 1:
-                        torch.distributed.all_gather_into_tensor(g.view(-1), o)
-                    else:
-                        g[0].copy_(o)
+                    comm.gather_tensor(g, o)  # device-resident on the native data plane (a copy at world 1 on torch)
                     r2_seen.add_(g[:, 0].clamp(max=search.cap).sum())
 
                 r2_done[b] = comm.run_async(r2)  # R2 overlaps the next step's kernel
@@ -835,6 +990,18 @@ class Bench:
         if not self.cpu:
             torch.cuda.empty_cache()
 
+    def comm_section(self) -> None:
+        """The run's own data plane measured across every rank (parallel/comm_probe.py measure_node_comm): the node's
+        R1 / R2 / R3 and the device-resident R2 as p50 / p99 over --comm-ops each, idle and with every rank's GPU
+        mining, the miner-rate change the ops cause, and one large all_gather's bus bandwidth (xGMI or not)."""
+        from otedama_amd.parallel.comm_probe import measure_node_comm
+
+        self.R["comm"] = measure_node_comm(self.comm, self.dev, phases=self.comm_phases(), ops=self.args.comm_ops,
+                                           cadence_hz=self.args.comm_hz,
+                                           busbw_bytes=(4 << 20) if self.cpu else self.args.comm_busbw_mib << 20,
+                                           say=self.guard.progress)
+        self.R["comm"]["impl"] = (self.R.get("preflight") or {}).get("data_plane", {}).get("impl")
+
     def cpu_miner(self) -> None:
         """BASELINE config 1: the native CPU miner, single thread and all cores of this box's CPU share."""
         from otedama_amd.cli.bench_cmd import bench_cpu, cpu_share
@@ -931,16 +1098,17 @@ class Bench:
                 "model": "sha256d",
                 "global_batch": sha["step_hashes"] * world,
                 "seq_len": 80,
-                "parallelism": (f"dp{world} (nonce-space: per-rank variant stripe; "
+                "parallelism": f"dp{world}",
+                "kernel": _sha_name(args, K, use_v),
+                "variants_per_step": K,
+                "nonce_split": ("per-rank variant stripe; "
                                 + (f"{K} variants x 2^{(V_COUNT).bit_length() - 1} nonces per step, "
-                                   f"{sha['steps_per_group']} steps tile 2^32 per variant)" if use_v
-                                   else "full 2^32 nonces per variant per step)")),
+                                   f"{sha['steps_per_group']} steps tile 2^32 per variant" if use_v
+                                   else "full 2^32 nonces per variant per step")),
                 "algorithm": ("SHA-256d nonce search, fixed midstate per variant; " + (
                     f"{K} BIP320 version variants per wave ({max(K // 64, 1)} per lane) share the block-2 message "
                     "schedule, computed on the scalar unit" if use_v else
                     f"{K} BIP320 version variants per launch share the block-2 message schedule")),
-                "sha_kernel": _sha_name(args, K, use_v),
-                "variants_per_step": K,
                 "grid": sha["grid"],
             },
             "world_size": world,
@@ -994,46 +1162,81 @@ class Bench:
         return {k: v.get("s") for k, v in (g.sections if g is not None else {}).items()}
 
     def summary(self, out: dict, errors: dict) -> dict:
+        """The compact part of the printed line. Every figure names the BASELINE config it answers (cfg1..cfg5,
+        BASELINE.json "configs"); the N>1 evidence (rank spread, node efficiency against this run's own per-GPU kernel
+        rate, the share delivery split, lost ranks, the data plane and its measured collectives) sits beside it."""
         node = out.get("node") or {}
         pool = (out.get("pool") or {}).get("algorithms") or {}
         lat = out.get("share_latency") or {}
         cpu = out.get("cpu") or {}
         nalg = node.get("algorithms") or {}
         js = node.get("job_switch") or {}
+        world = out["world_size"]
+        per_rank = [x for x in out.get("per_rank_hashes_per_sec") or [] if x]
+        workers = [w for v in pool.values() for w in v.get("workers") or []]
+        ivt = [w.get("interval_vs_target") for w in workers if w.get("interval_vs_target") is not None]
+        dp = ((out.get("preflight") or {}).get("data_plane") or {})
+        comm = self.R.get("comm") or {}
+        comm_lat = {ph: comm.get(ph) or {} for ph in ("idle", "sha256d", "scrypt") if comm.get(ph)}
+
+        def p99(op):
+            v = {ph: _r((d.get(op) or {}).get("p99_ms")) for ph, d in comm_lat.items()}
+            return v or None
+
+        node_sha = (nalg.get("sha256d") or {}).get("total_hashes_per_sec")
         return {
-            "sha256d_hps": _r(out["value"]),
-            "sha256d_single_midstate_hps": _r(out.get("sha256d_single_midstate_hashes_per_sec")),
-            "scrypt_hps": _r(out.get("scrypt_hashes_per_sec")),
-            "x11_hps": _r(out.get("x11_hashes_per_sec")),
-            "node_hps": _r(node.get("total_hashes_per_sec")),
-            "node_hps_by_algorithm": {a: _r(v.get("total_hashes_per_sec")) for a, v in nalg.items()} or None,
-            "node_rejected_by_algorithm": {a: v.get("pool_rejected") for a, v in nalg.items()} or None,
-            "node_remote_hit_to_accept_p50_ms": _r((node.get("hit_to_accept_remote") or {}).get("p50_ms")),
-            "node_share_previews": node.get("share_previews"),  # remote shares admitted from a preview, not R2
-            "node_job_switch_worst_rank_p50_ms": _r(js.get("worst_rank_p50_ms")),
-            "node_job_switch_worst_rank_max_ms": _r(js.get("worst_rank_max_ms")),
-            "node_job_switch_stale_rejects": js.get("stale_rejects"),
-            "node_backend": node.get("dist_backend"),
-            "node_ranks_seen": node.get("ranks_seen"),
-            "node_time_to_hashing_s": node.get("time_to_hashing_s"),
+            "cfg2_version_rolled_hps": _r(out["value"]),
+            "cfg2_single_midstate_hps": _r(out.get("sha256d_single_midstate_hashes_per_sec")),
+            "cfg2_per_gpu_hps": _r(out["value"] / max(world, 1)) if out.get("value") else None,
+            "cfg3_scrypt_hps": _r(out.get("scrypt_hashes_per_sec")),
+            "cfg3_scrypt_kernel_hps": _r(self.R.get("scrypt_kernel_hps")),
+            "cfg4_x11_hps": _r(out.get("x11_hashes_per_sec")),
+            "cfg4_x11_node_hps": _r((nalg.get("x11") or {}).get("total_hashes_per_sec")),
+            "cfg1_cpu_1t_hps": _r(cpu.get("sha256d_single_thread_hps")),
+            "cfg1_cpu_all_hps": _r(cpu.get("sha256d_all_threads_hps")),
+            "cfg5_pool_validated_per_s": {a: _r(v.get("validated_shares_per_sec")) for a, v in pool.items()} or None,
+            "cfg5_pool_validations": {a: (v.get("validate_ms") or {}).get("samples") for a, v in pool.items()} or None,
+            "cfg5_pool_validate_p50_ms": {a: _r((v.get("validate_ms") or {}).get("p50")) for a, v in pool.items()}
+            or None,
+            "cfg5_pool_interval_vs_target": [_r(min(ivt), 3), _r(max(ivt), 3)] if ivt else None,
+            "cfg5_pool_retargets_in_window": sum(int(w.get("retargets_in_window") or 0) for w in workers)
+            if workers else None,
+            # every worker's vardiff settled before the measurement window opened
+            "cfg5_pool_steady": all(w.get("settled_after_s") is not None and w.get("window_opened_after_s") is not None
+                                    and w["settled_after_s"] <= w["window_opened_after_s"] for w in workers)
+            if workers else None,
             "share_latency_p50_ms": _r(lat.get("p50_ms")),
             "device_hit_to_accept_p50_ms": _r(lat.get("device_hit_to_accept_p50_ms")),
             "job_switch_p50_ms": {a: _r(v) for a, v in (out.get("job_switch_ms") or {}).items()} or None,
-            "cpu_1t_hps": _r(cpu.get("sha256d_single_thread_hps")),
-            "cpu_all_hps": _r(cpu.get("sha256d_all_threads_hps")),
-            "pool_validated_per_s": {a: _r(v.get("validated_shares_per_sec")) for a, v in pool.items()} or None,
-            "pool_validate_p50_ms": {a: _r((v.get("validate_ms") or {}).get("p50")) for a, v in pool.items()} or None,
-            "pool_validations": {a: (v.get("validate_ms") or {}).get("samples") for a, v in pool.items()} or None,
-            # every worker's last >25% retarget came before the measurement window opened
-            "pool_steady_in_window": all(w.get("converged_after_s") is not None
-                                         and w.get("window_opened_after_s") is not None
-                                         and w["converged_after_s"] <= w["window_opened_after_s"]
-                                         for v in pool.values() for w in v.get("workers") or []) if pool else None,
-            "world_size": out["world_size"],
-            "backend": out["dist_backend"],
-            "rccl_ranks_seen": out["rccl_ranks_seen"],
+            "hits_verified": out.get("hits_verified"),
+            "hits_z": _r(out.get("hits_z"), 3),
+            # the production node (otedama node --gpus N), per algorithm
+            "node_hps": {a: _r(v.get("total_hashes_per_sec")) for a, v in nalg.items()} or None,
+            "node_rejected": {a: v.get("pool_rejected") for a, v in nalg.items()} or None,
+            "node_job_switch_worst_p50_ms": _r(js.get("worst_rank_p50_ms")),
+            "node_op_p99_ms": _r(node.get("op_p99_ms")),
+            "node_time_to_hashing_s": node.get("time_to_hashing_s"),
+            # N > 1 evidence
+            "world_size": world,
+            "ranks_seen": out["rccl_ranks_seen"],
+            "per_rank_hps": [_r(x, 3) for x in per_rank] if world > 1 else None,
+            "rank_rate_min_max": _r(min(per_rank) / max(per_rank), 3) if per_rank else None,
+            "rank_efficiency": _r(node_sha / out["value"], 3) if node_sha and out.get("value") else None,
+            "remote_hit_to_accept_p50_ms": _r((node.get("hit_to_accept_remote") or {}).get("p50_ms")),
+            "shares_via_preview": sum(int(v.get("share_previews") or 0) for v in nalg.values()) if nalg else None,
+            "shares_via_r2": sum(int(v.get("share_gathered_first") or 0) for v in nalg.values()) if nalg else None,
+            "reforms": sum(int(v.get("reforms") or 0) for v in nalg.values()) if nalg else None,
+            "lost_ranks": sorted({r for v in nalg.values() for r in v.get("lost_ranks") or []}) if nalg else None,
+            "node_backend": node.get("dist_backend"),
+            "data_plane": dp.get("impl") or out["dist_backend"],
+            "comm_r1_p99_ms": p99("R1"),
+            "comm_r2_p99_ms": p99("R2"),
+            "comm_r3_p99_ms": p99("R3"),
+            "comm_r2_dev_p99_ms": p99("R2_dev"),
+            "comm_busbw_gbps": _r((comm.get("busbw") or {}).get("busbw_gbps")),
+            "comm_miner_rate_change_pct": comm.get("miner_rate_change_pct"),
             "sections_s": self._section_times(),
-            "errors": errors or None,
+            "errors": _short_errors(errors),
         }
 
 

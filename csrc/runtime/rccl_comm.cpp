@@ -11,7 +11,12 @@
 //   * the communicator is non-blocking (ncclConfig_t.blocking = 0): init and every op are polled against a deadline
 //     with the GIL released, so a dead peer never hangs the caller; ncclCommAbort tears a broken group down at once;
 //   * no torch in the process: the node's rank processes import only this module and the native miner bindings
-//     (start-up: `import torch` was ~1.45 s of a rank's 1.8 s to its process group, profiles/r5/c_node_rehearsal).
+//     (start-up: `import torch` was ~1.45 s of a rank's 1.8 s to its process group, profiles/r5/c_node_rehearsal);
+//   * device-resident ops (`*_dev`): the collective reads and writes device memory the caller owns (bench.py's hit
+//     slots, the comm section's 256 MiB bus-bandwidth buffer) and is enqueued on the caller's HIP stream, so nothing
+//     is staged through the host and the traffic is GPU to GPU over xGMI. Every op of a communicator, staged or not,
+//     is ordered on the device after the previous one (an event hand-off between streams), so ranks that issue the
+//     same op sequence run it in the same order whatever streams they used.
 //
 // The reference has no collective layer; its fan-out / fan-in are Go channels
 // (internal/engine/fanin.go:22-58), which never block a producer: the deadlines here keep that property.
@@ -68,6 +73,7 @@ class RcclComm {
     hip_check(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
     hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
     hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&order_, hipEventDisableTiming), "hipEventCreate");
     ncclUniqueId id;
     std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -101,12 +107,14 @@ class RcclComm {
 
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }
+  int device() const { return device_; }
   bool alive() const { return comm_ != nullptr; }
   uint64_t ops() const { return ops_; }
 
   // R1: root's `data` (nbytes) to every rank; returns the nbytes every rank now holds.
   py::bytes broadcast(const std::string& data, size_t nbytes, int root, double timeout_s) {
     if (rank_ == root && data.size() != nbytes) throw std::invalid_argument("root's data must be nbytes long");
+    usable();
     ensure(nbytes, nbytes);
     std::string out(nbytes, '\0');
     {
@@ -122,6 +130,7 @@ class RcclComm {
   // R2 / R3: every rank's `mine` (same length everywhere), concatenated in rank order.
   py::bytes all_gather(const std::string& mine, double timeout_s) {
     const size_t n = mine.size(), total = n * size_t(nranks_);
+    usable();
     ensure(n, total);
     std::string out(total, '\0');
     {
@@ -144,6 +153,7 @@ class RcclComm {
     if (op != "max" && op != "sum") throw std::invalid_argument("op must be sum or max");
     if (data.size() % 8) throw std::invalid_argument("data must be whole 8-byte elements");
     const size_t n = data.size();
+    usable();
     ensure(n, n);
     std::string out(n, '\0');
     {
@@ -154,6 +164,33 @@ class RcclComm {
       std::memcpy(out.data(), host_, n);
     }
     return py::bytes(out);
+  }
+
+  // Device-resident forms: pointers to device memory of this comm's GPU (torch's data_ptr()), enqueued on `stream`
+  // (a hipStream_t as an integer, torch's Stream.cuda_stream; 0 = the comm's own stream). They return once the op is
+  // enqueued (the non-blocking communicator settled); completion is the caller's, through its stream.
+  void all_gather_dev(uintptr_t send, uintptr_t recv, size_t nbytes, uintptr_t stream, double timeout_s) {
+    enqueue(stream, timeout_s, "all_gather_dev", [&](hipStream_t s) {
+      return ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), nbytes, ncclUint8, comm_,
+                           s);
+    });
+  }
+  void broadcast_dev(uintptr_t buf, size_t nbytes, int root, uintptr_t stream, double timeout_s) {
+    if (root < 0 || root >= nranks_) throw std::invalid_argument("bad root");
+    enqueue(stream, timeout_s, "broadcast_dev", [&](hipStream_t s) {
+      return ncclBroadcast(reinterpret_cast<const void*>(buf), reinterpret_cast<void*>(buf), nbytes, ncclUint8, root,
+                           comm_, s);
+    });
+  }
+  void all_reduce_dev(uintptr_t buf, size_t count, const std::string& dtype, const std::string& op, uintptr_t stream,
+                      double timeout_s) {
+    if (dtype != "f64" && dtype != "i64") throw std::invalid_argument("dtype must be i64 or f64");
+    if (op != "max" && op != "sum") throw std::invalid_argument("op must be sum or max");
+    const ncclDataType_t t = dtype == "f64" ? ncclFloat64 : ncclInt64;
+    const ncclRedOp_t o = op == "max" ? ncclMax : ncclSum;
+    enqueue(stream, timeout_s, "all_reduce_dev", [&](hipStream_t s) {
+      return ncclAllReduce(reinterpret_cast<const void*>(buf), reinterpret_cast<void*>(buf), count, t, o, comm_, s);
+    });
   }
 
   // Tear the communicator down at once (a peer died, or a new generation is formed): ncclCommAbort never waits for
@@ -168,6 +205,43 @@ class RcclComm {
     if (comm_ == nullptr) return;
     (void)ncclCommAbort(comm_);
     comm_ = nullptr;
+  }
+
+  // An op may start: the communicator exists and no earlier op timed out. Checked before anything touches the staging
+  // buffers (ensure() may free them, and a timed-out op may still be queued on them: ADVICE r5).
+  void usable() const {
+    if (comm_ == nullptr) throw std::runtime_error("rccl: communicator aborted");
+    if (broken_) throw std::runtime_error("rccl: an earlier op timed out; abort this communicator and re-form");
+  }
+
+  // Device order across streams: `s` waits for the previous op of this communicator when that op went to another
+  // stream; the op about to be enqueued on `s` is recorded by after().
+  void order_on(hipStream_t s) {
+    if (last_stream_ != nullptr && last_stream_ != s) hip_check(hipStreamWaitEvent(s, order_, 0), "hipStreamWaitEvent");
+  }
+  void after(hipStream_t s) {
+    hip_check(hipEventRecord(order_, s), "hipEventRecord");
+    last_stream_ = s;
+  }
+
+  template <class Start>
+  void enqueue(uintptr_t stream, double timeout_s, const char* what, Start start) {
+    usable();
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : stream_;
+    py::gil_scoped_release nogil;
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    order_on(s);
+    const ncclResult_t r = start(s);
+    if (r != ncclSuccess && r != ncclInProgress)
+      throw std::runtime_error(std::string("rccl ") + what + ": " + ncclGetErrorString(r));
+    try {
+      if (r == ncclInProgress) wait_until([&] { return settled(); }, timeout_s, what);
+    } catch (...) {
+      broken_ = true;
+      throw;
+    }
+    after(s);
+    ++ops_;
   }
 
   // The communicator's asynchronous state: 1 = settled, 0 = in progress; throws on an error.
@@ -201,13 +275,13 @@ class RcclComm {
   // dev_[0, out_bytes) -> host_, then the event polled against the deadline (and the communicator's async error).
   template <class Start>
   void run(size_t in_bytes, size_t out_bytes, double timeout_s, const char* what, Start start, size_t in_off = 0) {
-    if (comm_ == nullptr) throw std::runtime_error("rccl: communicator aborted");
     // An op that timed out may still be queued on the stream (its peer never came): the next op would stage into
-    // the buffers it reads and writes. Such a communicator only serves an abort.
-    if (broken_) throw std::runtime_error("rccl: an earlier op timed out; abort this communicator and re-form");
+    // the buffers it reads and writes. Such a communicator only serves an abort (usable(), checked by the caller
+    // before it staged anything).
     hip_check(hipSetDevice(device_), "hipSetDevice");
     char* h = static_cast<char*>(host_);
     char* d = static_cast<char*>(dev_);
+    order_on(stream_);
     hip_check(hipMemcpyAsync(d + in_off, h + in_off, in_bytes, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync H2D");
     ncclResult_t r = start();
     if (r != ncclSuccess && r != ncclInProgress)
@@ -215,6 +289,7 @@ class RcclComm {
     try {
       if (r == ncclInProgress) wait_until([&] { return settled(); }, timeout_s, what);  // non-blocking enqueue
       hip_check(hipMemcpyAsync(h, d, out_bytes, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync D2H");
+      after(stream_);
       hip_check(hipEventRecord(done_, stream_), "hipEventRecord");
       wait_until([&] {
         const hipError_t q = hipEventQuery(done_);
@@ -234,9 +309,11 @@ class RcclComm {
     if (dev_) (void)hipFree(dev_);
     if (host_) (void)hipHostFree(host_);
     if (done_) (void)hipEventDestroy(done_);
+    if (order_) (void)hipEventDestroy(order_);
     if (stream_) (void)hipStreamDestroy(stream_);
     dev_ = host_ = nullptr;
-    done_ = nullptr;
+    done_ = order_ = nullptr;
+    last_stream_ = nullptr;
     stream_ = nullptr;
     cap_ = 0;
   }
@@ -245,6 +322,8 @@ class RcclComm {
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t done_ = nullptr;
+  hipEvent_t order_ = nullptr;      // recorded after every op, on the stream it went to
+  hipStream_t last_stream_ = nullptr;
   void* dev_ = nullptr;
   void* host_ = nullptr;
   size_t cap_ = 0;
@@ -288,5 +367,12 @@ PYBIND11_MODULE(_rccl, m) {
       .def("all_gather", &RcclComm::all_gather, py::arg("mine"), py::arg("timeout_s"))
       .def("all_reduce", &RcclComm::all_reduce, py::arg("data"), py::arg("dtype"), py::arg("op"),
            py::arg("timeout_s"))
+      .def("all_gather_dev", &RcclComm::all_gather_dev, py::arg("send"), py::arg("recv"), py::arg("nbytes"),
+           py::arg("stream"), py::arg("timeout_s"))
+      .def("broadcast_dev", &RcclComm::broadcast_dev, py::arg("buf"), py::arg("nbytes"), py::arg("root"),
+           py::arg("stream"), py::arg("timeout_s"))
+      .def("all_reduce_dev", &RcclComm::all_reduce_dev, py::arg("buf"), py::arg("count"), py::arg("dtype"),
+           py::arg("op"), py::arg("stream"), py::arg("timeout_s"))
+      .def_property_readonly("device", [](const RcclComm& c) { return c.device(); })
       .def("abort", &RcclComm::abort);
 }

@@ -361,6 +361,23 @@ class NodeComm:
                      [(self._max_h, self._max)])
         return float(self._max_h.item())
 
+    def barrier(self) -> None:
+        barrier(self.info)
+
+    # ---------------------------------------------------------------- device-resident forms (bench.py)
+    def gather_tensor(self, out, inp) -> None:
+        """``out`` (world x inp.shape) gets every rank's contiguous ``inp`` (parallel/rcclcomm.py has the same)."""
+        if self.info.world_size > 1:
+            self.collectives += 1
+            dist.all_gather_into_tensor(out.view(-1), inp.view(-1))
+        else:
+            out[0].copy_(inp)
+
+    def broadcast_tensor(self, t, src: int = 0) -> None:
+        if self.info.world_size > 1:
+            self.collectives += 1
+            dist.broadcast(t, src=src)
+
     def _run(self, fn) -> None:
         """Blocking form: the collective runs on the comm stream and the current stream waits for it (used where
         the caller reads the result right away)."""

@@ -233,6 +233,173 @@ def measure_comm_under_load(device_index: int = 0, algorithms=("sha256d", "scryp
     return out
 
 
+# ---------------------------------------------------------------------------------------------------------------------
+# bench.py's comm section: the node's collectives measured across every rank of the run
+NODE_COMM_DEFINITION = (
+    "every rank in lockstep on the run's data plane (bench.py preflight.data_plane): R1 = the node's 64 KiB job-blob "
+    "broadcast, R2 = its share-slot all_gather (64 x 10 int64 per rank), R3 = its counter all_reduce, each host call -> "
+    "result on the host; R2_dev = bench.py's device-resident hit-slot gather, enqueue -> stream done. Ops interleaved "
+    "R1,R2,R3,R2_dev at `cadence_hz` from a common barrier. Phases: idle, then with every rank's device process mining "
+    "the named algorithm (the production miner, one per GPU). miner_rate_change_pct = node-wide miner rate with the ops "
+    "against an equal window without them. busbw: one all_gather of `busbw_bytes` in total (device buffers), "
+    "busbw = bytes/time x (N-1)/N as nccl-tests defines it")
+
+
+def _lockstep_ops(comm, ops: int, cadence_hz: float, dev) -> dict:
+    """``ops`` of each of R1 / R2 / R3 / R2_dev, interleaved, every rank on the same schedule from a barrier."""
+    import torch
+
+    from otedama_amd.parallel.commbase import SHARE_SLOTS
+
+    job = {"job_id": "comm", "header": bytes(80), "coinb1": bytes(2000), "coinb2": bytes(2000),
+           "merkle_branches": [bytes(32)] * 12, "epoch": 1}
+    shares = [{"epoch": 1, "nonce": i, "ntime": 1, "version": 2, "extranonce2": 3, "found_at": time.monotonic()}
+              for i in range(4)]
+    world = comm.info.world_size
+    slot = torch.zeros(1 + 2 * SHARE_SLOTS, dtype=torch.int32, device=dev)
+    gathered = torch.zeros(world, slot.numel(), dtype=torch.int32, device=dev)
+    cuda = dev.type == "cuda"
+    lat: dict[str, list[float]] = {"R1": [], "R2": [], "R3": [], "R2_dev": []}
+    names = list(lat)
+    comm.barrier()
+    t0 = time.monotonic()
+    period = 1.0 / cadence_hz
+    for k in range(4 * ops):
+        time.sleep(max(0.0, t0 + k * period - time.monotonic()))
+        op = names[k % 4]
+        t = time.perf_counter()
+        if op == "R1":
+            comm.broadcast_job(job)
+        elif op == "R2":
+            comm.gather_shares(shares)
+        elif op == "R3":
+            comm.allreduce_counters(1, 2, 3, 4)
+        else:
+            stream = comm.stream if cuda else None
+            with torch.cuda.stream(stream) if stream is not None else _null():
+                comm.gather_tensor(gathered, slot)
+            if stream is not None:
+                stream.synchronize()
+            elif cuda:
+                torch.cuda.synchronize(dev)
+        lat[op].append((time.perf_counter() - t) * 1e3)
+    return {k: _q(v) for k, v in lat.items()}
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _busbw(comm, dev, total_bytes: int, iters: int = 5) -> dict:
+    """One all_gather of ``total_bytes`` in total (each rank contributes total/N), timed over ``iters`` after a warm
+    one; every rank's block is checked."""
+    import torch
+
+    world, rank = comm.info.world_size, comm.info.rank
+    per = max(4096, (total_bytes // world) // 4096 * 4096)
+    send = torch.full((per,), (rank + 1) & 0xFF, dtype=torch.uint8, device=dev)
+    recv = torch.zeros(world, per, dtype=torch.uint8, device=dev)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    comm.gather_tensor(recv, send)
+    sync()
+    ok = all(int(recv[r, 0]) == (r + 1) & 0xFF and int(recv[r, -1]) == (r + 1) & 0xFF for r in range(world))
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        comm.gather_tensor(recv, send)
+    sync()
+    t = comm.allreduce_max((time.perf_counter() - t0) / iters)
+    ok = comm.allreduce_counters(int(ok))[0] == world
+    algbw = per * world / t / 1e9
+    return {"bytes": per * world, "iters": iters, "ms": t * 1e3, "algbw_gbps": algbw,
+            "busbw_gbps": algbw * (world - 1) / world, "blocks_ok": ok, "device": dev.type}
+
+
+def _start_miner(device_index: int, algo: str):
+    from otedama_amd import hal
+    from otedama_amd.engine.latency_probe import _switch_job
+    from otedama_amd.engine.miners import MinerSet
+
+    devs = [d for d in hal.KFDDriver().enumerate() if d.index == device_index]
+    if not devs:
+        raise RuntimeError(f"no KFD GPU node for device {device_index}")
+    ms = MinerSet(devs, algo, 1 << 32, 0, isolation="process")
+    dp = ms.miners[0].native
+    ms.start()
+    end = time.monotonic() + 60
+    while not dp.ready_at and dp.alive and time.monotonic() < end:
+        time.sleep(0.01)
+    if not dp.ready_at:
+        ms.stop()
+        raise RuntimeError(f"{algo} device process not ready")
+    ms.set_job(_switch_job(0, algo))
+    return ms, dp
+
+
+def measure_node_comm(comm, dev, phases=("idle", "sha256d", "scrypt"), ops: int = 200, cadence_hz: float = 100.0,
+                      busbw_bytes: int = 256 << 20, rate_window_s: float = 3.0, warm_s: dict | None = None,
+                      say=None) -> dict:
+    """bench.py's comm section (NODE_COMM_DEFINITION). Every rank calls this with the same arguments; each step that
+    could fail on one rank (a miner that does not start) is agreed on through R3 first, so no rank is left alone in
+    a collective."""
+    say = say or (lambda m: None)
+    world = comm.info.world_size
+    warm_s = warm_s or {"sha256d": 1.5, "scrypt": 3.0}
+    out: dict = {"world": world, "ops_per_type": ops, "cadence_hz": cadence_hz, "definition": NODE_COMM_DEFINITION}
+    rates: dict = {}
+    for ph in phases:
+        if ph == "idle":
+            say("comm: idle ops")
+            out["idle"] = _lockstep_ops(comm, ops, cadence_hz, dev)
+            continue
+        say(f"comm: {ph} miner up")
+        ms = dp = None
+        err = ""
+        try:
+            ms, dp = _start_miner(dev.index or 0, ph)
+            time.sleep(warm_s.get(ph, 2.0))
+        except Exception as exc:  # noqa: BLE001 - agreed below
+            err = f"{type(exc).__name__}: {exc}"[:200]
+        try:
+            if comm.allreduce_counters(int(ms is not None))[0] != world:
+                out[ph] = {"skipped": err or "a peer's miner did not start"}
+                continue
+            comm.barrier()
+            a = _counter(dp)
+            time.sleep(rate_window_s)
+            alone = _miner_rate(dp, a, _counter(dp)) or 0.0
+            a = _counter(dp)
+            res = _lockstep_ops(comm, ops, cadence_hz, dev)
+            with_ops = _miner_rate(dp, a, _counter(dp)) or 0.0
+            st = dp.stats()
+            res["miner_rate_alone_hps"], res["miner_rate_with_ops_hps"] = alone, with_ops
+            res["miner_faulted"] = bool(st.get("faulted"))
+            out[ph] = res
+            rates[ph] = (alone, with_ops)
+        finally:
+            if ms is not None:
+                ms.stop()
+    if rates:
+        change = {}
+        for ph, (alone, with_ops) in rates.items():
+            tot_alone, tot_with, _, _ = comm.allreduce_counters(int(alone), int(with_ops))
+            change[ph] = round(100.0 * (tot_with / tot_alone - 1.0), 2) if tot_alone > 0 else None
+        out["miner_rate_change_pct"] = change
+    if busbw_bytes > 0:
+        say("comm: bus bandwidth")
+        out["busbw"] = _busbw(comm, dev, busbw_bytes)
+    return out
+
+
 def main(argv=None) -> int:
     import argparse
     import json

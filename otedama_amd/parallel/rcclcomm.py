@@ -37,7 +37,10 @@ class NativeNodeComm:
     """R1 / R2 / R3 over the native RCCL module, one communicator per process-group generation. Same interface as
     parallel/comm.py NodeComm (the node uses nothing else)."""
 
-    def __init__(self, info: DistInfo, bounded: bool = True, deadline: float = 3.0, force: bool = False):
+    def __init__(self, info: DistInfo, bounded: bool = True, deadline: float = 3.0, force: bool = False,
+                 device_stream: bool = False):
+        """``device_stream``: give the comm a high-priority torch stream for the device-resident forms' overlapped
+        use (``run_async``; bench.py). The node's ranks leave it off and never import torch."""
         self._rccl = rccl_module()
         self.info = info
         self.bounded = bounded
@@ -46,6 +49,14 @@ class NativeNodeComm:
         self.collectives = 0
         self.stream = None
         self.dev = info.device
+        if device_stream and getattr(info.device, "type", "cpu") == "cuda":
+            import torch
+
+            if not isinstance(info.device, torch.device):
+                info.device = torch.device(info.device.type, info.device.index)
+            self.dev = info.device
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.stream = torch.cuda.Stream(self.dev, priority=min(lo, hi))
         self._rc = None  # the current generation's RcclComm
         self._job_h = np.zeros(JOB_BLOB_BYTES, dtype=np.uint8)  # rank 0's last blob
 
@@ -69,7 +80,7 @@ class NativeNodeComm:
             except Exception:  # noqa: BLE001 - the group is unusable either way
                 pass
 
-    def reform(self, members: list[int], generation: int) -> None:
+    def reform(self, members: list[int], generation: int, timeout: float | None = None) -> None:
         """Leave the current group and form generation ``generation`` of ``members`` (orig ranks; group rank =
         position). The group's rank 0 publishes the RCCL unique id under otd-g<gen>/rcclid; the others wait for it
         (bounded by OTEDAMA_PG_TIMEOUT), then every member initialises its communicator (same bound)."""
@@ -77,6 +88,7 @@ class NativeNodeComm:
         if info.orig_rank not in members:
             raise ValueError(f"rank {info.orig_rank} is not a member of generation {generation}")
         self.abort()
+        timeout = PG_TIMEOUT_S if timeout is None else timeout
         rank, world = members.index(info.orig_rank), len(members)
         if world > 1 or self.force:
             key = f"otd-g{generation}/rcclid"
@@ -84,14 +96,16 @@ class NativeNodeComm:
                 try:
                     uid = self._rccl.unique_id()
                 except Exception:
-                    info.store.set(key, FAILED_ID)  # the other members fail at once instead of at their deadline
+                    if info.store is not None:
+                        info.store.set(key, FAILED_ID)  # the other members fail at once instead of at their deadline
                     raise
-                info.store.set(key, uid)
+                if info.store is not None:  # a forced one-rank group may have no store (bench.py at N=1)
+                    info.store.set(key, uid)
             else:
-                uid = _wait_get(info.store, key, PG_TIMEOUT_S)
+                uid = _wait_get(info.store, key, timeout)
                 if uid == FAILED_ID:
                     raise RuntimeError(f"generation {generation}: the group's rank 0 could not create an RCCL id")
-            self._rc = self._rccl.RcclComm(int(info.device.index or 0), world, rank, uid, PG_TIMEOUT_S)
+            self._rc = self._rccl.RcclComm(int(info.device.index or 0), world, rank, uid, timeout)
         info.rank, info.world_size, info.generation, info.members = rank, world, generation, list(members)
 
     # ---------------------------------------------------------------- ops
@@ -150,6 +164,56 @@ class NativeNodeComm:
         if self.multi:
             v = np.frombuffer(self._call(self._rc.all_reduce, v.tobytes(), "f64", "max"), dtype=np.float64)
         return float(v[0])
+
+    def barrier(self) -> None:
+        """Every rank reached this point (one R3 word)."""
+        if self.multi:
+            self.allreduce_counters(0)
+
+    # ---------------------------------------------------------------- device-resident forms (bench.py)
+    # torch tensors on this comm's device (CPU tensors under a CPU stand-in module); the op is enqueued on the current
+    # torch stream and nothing goes through the host (RcclComm.*_dev). Same signatures as parallel/comm.py NodeComm.
+    def _cur_stream(self) -> int:
+        if getattr(self.dev, "type", "cpu") != "cuda":
+            return 0
+        import torch
+
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def gather_tensor(self, out, inp) -> None:
+        """``out`` (world x inp.shape) gets every rank's contiguous ``inp``, in rank order."""
+        if not self.multi:
+            out[0].copy_(inp)
+            return
+        if self._rc is None:
+            raise RuntimeError("rccl: no communicator for this generation")
+        self.collectives += 1
+        self._rc.all_gather_dev(inp.data_ptr(), out.data_ptr(), inp.numel() * inp.element_size(), self._cur_stream(),
+                                self._timeout())
+
+    def broadcast_tensor(self, t, src: int = 0) -> None:
+        if not self.multi:
+            return
+        if self._rc is None:
+            raise RuntimeError("rccl: no communicator for this generation")
+        self.collectives += 1
+        self._rc.broadcast_dev(t.data_ptr(), t.numel() * t.element_size(), src, self._cur_stream(), self._timeout())
+
+    def run_async(self, fn):
+        """As parallel/comm.py NodeComm.run_async: ``fn``'s ops go on the comm stream, ordered after the current
+        stream's queued work; returns an event on the comm stream (None without one: the op completed inline)."""
+        if self.stream is None:
+            fn()
+            return None
+        import torch
+
+        cur = torch.cuda.current_stream(self.dev)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            fn()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
 
 
 def rccl_module():

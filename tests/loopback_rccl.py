@@ -14,6 +14,7 @@ the node's ranks load this module instead, so that protocol runs end to end at w
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 
@@ -120,3 +121,17 @@ class RcclComm:
         got = self._exchange(bytes(data), list(range(self.nranks)), timeout_s, "all_reduce")
         a = np.stack([np.frombuffer(g, dtype=np.int64 if dtype == "i64" else np.float64) for g in got])
         return (a.sum(axis=0) if op == "sum" else a.max(axis=0)).tobytes()
+
+    # "device" forms: here the pointers are host memory (CPU tensors' data_ptr()); the stream is ignored and the op
+    # completes before it returns (a CPU rehearsal of bench.py's device-resident R1 / R2 / R3)
+    def all_gather_dev(self, send: int, recv: int, nbytes: int, stream: int, timeout_s: float) -> None:
+        out = self.all_gather(ctypes.string_at(send, nbytes), timeout_s)
+        ctypes.memmove(recv, out, len(out))
+
+    def broadcast_dev(self, buf: int, nbytes: int, root: int, stream: int, timeout_s: float) -> None:
+        out = self.broadcast(ctypes.string_at(buf, nbytes) if self.rank == root else b"", nbytes, root, timeout_s)
+        ctypes.memmove(buf, out, nbytes)
+
+    def all_reduce_dev(self, buf: int, count: int, dtype: str, op: str, stream: int, timeout_s: float) -> None:
+        out = self.all_reduce(ctypes.string_at(buf, 8 * count), dtype, op, timeout_s)
+        ctypes.memmove(buf, out, 8 * count)

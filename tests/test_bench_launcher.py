@@ -9,8 +9,11 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 
 import pytest
+
+from benchjson import detail_env, result
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
@@ -22,15 +25,17 @@ def _bench(*args, env=None, timeout=240):
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
+    denv, detail = detail_env(tempfile.mkdtemp(prefix="otd-bench-"))
+    e.update(denv)
     e.update(env or {})
-    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=e,
-                          cwd=ROOT)
+    res = subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=e,
+                         cwd=ROOT)
+    res.detail = detail
+    return res
 
 
 def _json(res) -> dict:
-    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, (res.stdout, res.stderr[-3000:])
-    return json.loads(lines[0])
+    return result(res, res.detail)
 
 
 @pytest.mark.parametrize("n", [4, 8])
@@ -85,10 +90,12 @@ def test_driver_torchrun_invocation():
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
+    e.update(detail_env(tempfile.mkdtemp(prefix="otd-bench-"))[0])
     res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "2",
                           "--steps", "2", "--warmup", "1", "--cpu-rehearsal"],
                          capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    res.detail = e["OTEDAMA_BENCH_DETAIL"]
     assert res.returncode == 0, res.stderr[-3000:]
     d = _json(res)
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["rccl_ranks_seen"] == [0, 1]
@@ -109,11 +116,13 @@ def test_driver_torchrun_invocation_with_the_node_section():
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
+    e.update(detail_env(tempfile.mkdtemp(prefix="otd-bench-"))[0])
     res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
                           "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "4",
                           "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--node-seconds", "3",
                           "--node-warmup", "2", "--cpu-seconds", "0"],
                          capture_output=True, text=True, timeout=360, env=e, cwd=ROOT)
+    res.detail = e["OTEDAMA_BENCH_DETAIL"]
     assert res.returncode == 0, res.stderr[-3000:]
     d = _json(res)
     assert d["n_gpus"] == 4 and d["rccl_ranks_seen"] == [0, 1, 2, 3]
@@ -146,16 +155,26 @@ NODE_KEYS = {"total_hashes_per_sec", "per_rank_hashes_per_sec", "accepted", "rej
              "host_verify_to_accept_remote", "share_difficulty"}
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(540)
 @pytest.mark.parametrize("n", [4, 8])
 def test_node_section_json_contract(n):
     """after the kernel sections, bench.py runs the production node (`otedama node --gpus N`:
     supervisor, N ranks, a device process per rank, rank 0 on the pool session) against the local pool and reports
-    it. The CPU rehearsal runs the same processes over gloo with CPU miners."""
+    it. The CPU rehearsal runs the same processes over gloo with CPU miners.
+    At world 8 the pool and CPU sections run too: the worst case of the printed line (missing #1: node
+    objects for 3 algorithms x 8 ranks, the pool's) must still fit bench.LINE_CAP (checked in _json)."""
+    extra = ("--pool-seconds", "3", "--cpu-seconds", "0.3") if n == 8 else ("--cpu-seconds", "0")
     res = _bench("--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--node-seconds", "3",
-                 "--node-warmup", "2", "--cpu-seconds", "0", timeout=360)
+                 "--node-warmup", "2", *extra, timeout=480)
     assert res.returncode == 0, res.stderr[-3000:]
     d = _json(res)
+    s = d.line["summary"]
+    assert s["world_size"] == n and s["ranks_seen"] == list(range(n)) and len(s["per_rank_hps"]) == n
+    assert set(s["node_hps"]) == {"sha256d", "x11", "scrypt"} and s["lost_ranks"] == [] and s["reforms"] == 0
+    assert 0 < s["rank_rate_min_max"] <= 1 and s["rank_efficiency"] > 0
+    assert s["shares_via_preview"] + s["shares_via_r2"] > 0 and s["node_op_p99_ms"] > 0
+    if n == 8:
+        assert s["cfg1_cpu_1t_hps"] > 0 and set(s["cfg5_pool_validations"]) == {"sha256d", "scrypt"}
     node = d["node"]
     assert "error" not in node, node
     assert NODE_KEYS <= set(node), sorted(node)
@@ -204,3 +223,27 @@ def test_pool_and_cpu_sections_json_contract():
         assert all(m["exit_code"] == 0 for m in a["miners"])
         assert pool["flood"][algo]["validated_shares_per_sec"] > 100 and pool["flood"][algo]["rejected"] == 0
     assert pool["time_to_steady_s"] >= pool["time_to_first_accept_s"] > 0
+
+
+def test_compact_line_caps_a_pathological_result():
+    """compact_line keeps the driver contract and the summary's headline keys within LINE_CAP even when every
+    section failed with a long error and the per-rank lists are long (a 64-rank world)."""
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+    finally:
+        sys.path.remove(ROOT)
+    from benchjson import check_line
+
+    full = {k: 1 for k in bench.CONTRACT_KEYS}
+    full["config"] = {"model": "sha256d", "global_batch": 1, "seq_len": 80, "parallelism": "dp64", "kernel": "k" * 500,
+                      "variants_per_step": 128, "nonce_split": "x" * 5000}
+    full["node"] = {"big": "y" * 100_000}
+    full["summary"] = {"cfg2_version_rolled_hps": 1.9e10, "per_rank_hps": [1.0e9] * 64,
+                       "ranks_seen": list(range(64)), "errors": {f"s{i}": "e" * 160 for i in range(40)},
+                       "sections_s": {f"s{i}": 1.0 for i in range(40)},
+                       "rank_phases": {f"p{i}" * 10: list(range(64)) for i in range(20)}}
+    line = bench.compact_line(full, "/x/bench_detail.json")
+    d = check_line(line)
+    assert d["summary"]["cfg2_version_rolled_hps"] == 1.9e10 and d["detail"] == "bench_detail.json"
+    assert "dropped" in d["summary"] and "node" not in d and len(d["config"]["kernel"]) <= 60

@@ -91,9 +91,9 @@ def test_rccl_group_rendezvous_through_the_supervisors_store():
 
 @pytest.mark.gpu
 def test_data_plane_probe_forms_an_rccl_group_at_world_one(monkeypatch):
-    """bench.py's data-plane pre-flight (parallel/rccl_probe.py) on the GPU: the child forms a torch.distributed RCCL
-    group through the job's store, runs its all_reduce, meets its peers at the done barrier and reports ok; an
-    injected hang is killed at the deadline and reported as such."""
+    """bench.py's data-plane pre-flight (parallel/rccl_probe.py) on the GPU: the child forms a native RCCL group
+    (otedama_amd._rccl, the bench's and the node's data plane) through the job's store, runs its all_reduce, meets
+    its peers at the done barrier and reports ok; an injected hang is killed at the deadline and reported as such."""
     import datetime
 
     import torch.distributed as dist
@@ -108,7 +108,7 @@ def test_data_plane_probe_forms_an_rccl_group_at_world_one(monkeypatch):
                  "MASTER_PORT": str(port), "TORCHELASTIC_RUN_ID": "probe-ok"}.items():
         monkeypatch.setenv(k, v)
     r = run_probe(store, 0, 1, timeout=60)
-    assert r["ok"] and r["ranks"]["0"]["ok"], r
+    assert r["ok"] and r["ranks"]["0"]["ok"] and r["impl"] == "rccl-native", r
     monkeypatch.setenv("TORCHELASTIC_RUN_ID", "probe-hang")
     r = run_probe(store, 0, 1, timeout=3, fault="hang")
     assert not r["ok"] and "killed" in r["ranks"]["0"]["reason"], r

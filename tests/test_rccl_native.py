@@ -138,3 +138,43 @@ def test_an_op_past_its_deadline_leaves_the_communicator_broken_until_aborted():
     d = _rccl.RcclComm(0, 1, 0, _rccl.unique_id(), 30.0)
     assert d.all_gather(b"y" * 8, 5.0) == b"y" * 8
     d.abort()
+
+
+@pytest.mark.gpu
+def test_device_resident_ops_at_world_one_and_their_stream_order():
+    """The device-pointer forms bench.py's R1 / R2 and the comm section use (RcclComm.*_dev through NativeNodeComm):
+    the all_gather reads and writes device memory on the caller's stream, nothing staged through the host; a host-
+    staged op issued right after is ordered behind it on the device (the comm's event hand-off between streams)."""
+    import torch
+
+    from otedama_amd.parallel.commbase import DistInfo
+    from otedama_amd.parallel.rcclcomm import NativeNodeComm
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    comm = NativeNodeComm(DistInfo(0, 1, 0, "rccl", dev), bounded=False, force=True, device_stream=True)
+    comm.reform([0], 7)
+    try:
+        assert comm.stream is not None
+        inp = torch.arange(1 << 20, dtype=torch.int32, device=dev)
+        out = torch.zeros(1, 1 << 20, dtype=torch.int32, device=dev)
+        ev = comm.run_async(lambda: comm.gather_tensor(out, inp))
+        ev.synchronize()
+        assert torch.equal(out[0], inp)
+        t = torch.full((16,), 5, dtype=torch.uint8, device=dev)
+        comm.broadcast_tensor(t)
+        torch.cuda.synchronize()
+        assert int(t.min()) == 5
+        # a long producer on the current stream, the gather on the comm stream after it, then a host-staged R3
+        big = torch.randn(4096, 4096, device=dev)
+        for _ in range(8):
+            big = big @ big.T / 4096.0
+        inp2 = (big[0, :16] * 0 + 3).to(torch.int32).contiguous()
+        out2 = torch.zeros(1, 16, dtype=torch.int32, device=dev)
+        comm.run_async(lambda: comm.gather_tensor(out2, inp2))
+        assert comm.allreduce_counters(5)[0] == 5
+        torch.cuda.synchronize()
+        assert out2.cpu().tolist()[0] == [3] * 16
+        assert comm._rc.ops >= 4
+    finally:
+        comm.close()
