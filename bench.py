@@ -128,7 +128,7 @@ def parse_args(argv=None):
                     help="forced new blocks (SetNewPrevHash) per node run for the node-wide job switch (0 = none)")
     ap.add_argument("--pool-seconds", type=float, default=-1.0,
                     help="BASELINE config 5 (mixed SHA-256d + scrypt pool, vardiff on): recorded seconds after every "
-                         "worker settled (-1 = 25 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+                         "worker settled (-1 = 30 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="BASELINE config 1 (native CPU miner, single thread and all cores): seconds each (0 = skip)")
     ap.add_argument("--deadline", type=float, default=DEFAULT_DEADLINE_S,
@@ -385,7 +385,7 @@ class Bench:
         return self.args.node_seconds if self.args.node_seconds >= 0 else (0.0 if self.cpu else 8.0)
 
     def pool_seconds(self) -> float:
-        return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 25.0)
+        return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 30.0)
 
     def comm_phases(self) -> list[str]:
         """The comm section's phases: idle, then under each mining algorithm (GPUs only: the CPU rehearsal has no
@@ -429,7 +429,7 @@ class Bench:
             self.shutdown()
             return 0
         need0 = {"cpu": 2.5 * self.args.cpu_seconds + 5, "latency": 60.0,
-                 "node": 40.0 + self.node_seconds() + self.args.node_warmup, "pool": 60.0 + self.pool_seconds()}
+                 "node": 40.0 + self.node_seconds() + self.args.node_warmup, "pool": 90.0 + self.pool_seconds()}
         for name, fn in (("cpu", self.cpu_miner), ("latency", self.latency), ("node", self.node),
                          ("pool", self.pool)):
             if not self.wanted(name):

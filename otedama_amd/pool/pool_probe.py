@@ -10,9 +10,11 @@ pool's native hash workers), rejects by reason, the pool's validation time (subm
 each worker's difficulty in force / retarget count / time from channel open to its last retarget, and the miners'
 device-timeline hashrates.
 
-Steady state: the recorded window opens only once every worker has converged, i.e. no retarget
-larger than SETTLE_BAND (25%) for two retarget periods; convergence time is reported on its own. The vardiff target
-is a 0.1 s share interval, so every algorithm collects a few hundred validations in the window. Each worker's share
+Steady state: the recorded window opens only once every worker's vardiff has settled (its
+difficulty rests on most of a full estimator window, no refinement is left and none is pending; pool/vardiff.py) and
+its estimate points within 10% of the difficulty in force; convergence time is reported on its own, and so is each
+worker's retarget count inside the window (0 when the window really was steady). The vardiff target is a 0.05 s
+share interval, so every algorithm collects several hundred validations in the window. Each worker's share
 interval over the window is reported against that target (the reference's relation interval = D * 2^32 / H,
 internal/engine/stats.go:502-513), and validation quantiles are computed from the pool's timed log over the window
 only. A short flood (pool/load.py: SV2 clients submitting valid shares as fast as the pool acknowledges) gives the
@@ -124,9 +126,9 @@ def flood(algorithms: list[str], seconds: float = 3.0, miners: int = 8, timeout:
     return res
 
 
-def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.1, retarget_seconds: float = 5.0,
+def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.05, retarget_seconds: float = 5.0,
                  difficulty: float = 1.0, cpu: bool = False, startup_timeout: float = 180.0,
-                 settle_timeout: float = 60.0, steady_periods: float = 2.0, flood_seconds: float = 3.0) -> dict:
+                 settle_timeout: float = 120.0, flood_seconds: float = 3.0) -> dict:
     streams = layout(gpus)
     algos = sorted({a for _, a in streams}, key=["sha256d", "scrypt"].index)
     http = f"127.0.0.1:{free_port()}"
@@ -166,22 +168,18 @@ def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.
         else:
             raise RuntimeError(f"miners not accepted within {startup_timeout:.0f} s")
         t_first = time.monotonic()
-        # steady state: every worker connected and without a retarget larger than SETTLE_BAND for steady_periods
-        # retarget windows
-        need = steady_periods * retarget_seconds
-
+        # steady state: every worker connected and its vardiff settled (pool/vardiff.py: the
+        # difficulty rests on most of a full estimator window, no refinement is left and no retarget is pending), and
+        # the estimate it holds points within 10% of the difficulty in force
         def calm(w: dict) -> bool:
-            # no >25% retarget on its way: vardiff's open window, once it holds enough shares to say, points within
-            # 25% of the difficulty in force (on a slow host a 20% miss was corrected after the window had opened)
-            r, n = w.get("window_ratio"), w.get("window_shares", 0) or 0
-            return r is None or n < 30 or abs(math.log(max(r, 1e-12))) < math.log(1.25)
+            r = w.get("window_ratio")
+            return bool(w.get("settled")) and r is not None and abs(math.log(max(r, 1e-12))) < math.log(1.10)
 
         end = time.monotonic() + settle_timeout
         settled = False
         while time.monotonic() < end:
             ws = [w for s in _pool_api(http) for w in s.get("workers", [])]
-            if len(ws) >= len(miners) and all(w["steady_for_s"] >= need and w["accepted"] > 0 and calm(w)
-                                              for w in ws):
+            if len(ws) >= len(miners) and all(w["accepted"] > 0 and calm(w) for w in ws):
                 settled = True
                 break
             time.sleep(0.25)
@@ -221,6 +219,9 @@ def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.
             n = w["accepted"] - prev.get("accepted", 0)
             interval = dt / n if n else None
             workers.append({"name": w["name"], "difficulty": w["difficulty"], "retargets": w["retargets"],
+                            "retargets_in_window": w["retargets"] - prev.get("retargets", w["retargets"]),
+                            "estimate_ratio_at_open": prev.get("window_ratio"),
+                            "estimate_shares_at_open": prev.get("window_shares"),
                             "converged_after_s": w["converged_after_s"], "settled_after_s": w["settled_after_s"],
                             "window_opened_after_s": w.get("age_s", 0.0) - (t1 - t0),
                             "connections": got, "accepted_in_window": n,
@@ -240,7 +241,8 @@ def measure_pool(gpus: int = 1, seconds: float = 25.0, share_seconds: float = 0.
            "recorded_seconds": dt, "initial_difficulty": difficulty, "retarget_seconds": retarget_seconds,
            "vardiff": True, "steady_state": settled, "time_to_first_accept_s": t_first - t_open,
            "time_to_steady_s": t_settled - t_open,
-           "steady_rule": f"no retarget > 25% for {need:.0f} s on every worker",
+           "steady_rule": "every worker's vardiff settled (no refinement left, none pending) and its estimate within "
+                          "10% of the difficulty in force",
            "definition": ("otedama pool --algorithms sha256d,scrypt (one process) + one `otedama run` per "
                           "(GPU, algorithm) stream over SV2; every accepted share re-hashed by the pool; window opened "
                           "once every worker's vardiff converged; validation quantiles over the window only")}

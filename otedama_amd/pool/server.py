@@ -227,6 +227,8 @@ class PoolServer:
             a = srv.sockets[0].getsockname()
             self.addr_v1 = f"{a[0]}:{a[1]}"
         self._tasks.append(asyncio.ensure_future(self._refresh_loop()))
+        if not self.opts.fixed_difficulty and self.opts.retarget_seconds > 0:
+            self._tasks.append(asyncio.ensure_future(self._vardiff_loop()))
         self.log("info", f"pool[{self.algo.name}]: listening sv2={self.addr_sv2 or '-'} v1={self.addr_v1 or '-'}")
         if self.opts.noise:
             self.log("info", f"pool[{self.algo.name}]: sv2 Noise NX on; authority pubkey "
@@ -257,6 +259,29 @@ class PoolServer:
             else:
                 self.new_job(clean=False)
             self._update_hashrate()
+
+    async def _vardiff_loop(self) -> None:
+        """Vardiff's periodic look also runs without a share: a worker whose difficulty is far too high may send
+        nothing for a whole period, and must still be eased down (pool/vardiff.py's no-share rule)."""
+        period = min(max(self.opts.retarget_seconds / 2.0, 0.25), 15.0)
+        while True:
+            await asyncio.sleep(period)
+            for c in list(self._v1):
+                if c.worker is not None and self._tick_worker(c.worker) is not None:
+                    c._send_difficulty()
+            for c in list(self._v2):
+                for ch, (w, _prefix) in list(c.channels.items()):
+                    new = self._tick_worker(w)
+                    if new is not None:
+                        c._send(M.SetTarget(ch, self.share_target(new)))
+
+    def _tick_worker(self, w: "_Worker") -> float | None:
+        old = w.vd.difficulty
+        new = self.vardiff.maybe_retarget(w.vd)
+        if new is not None:
+            w.retargeted(old, new)
+            self.journal.save_worker(w.name, new)
+        return new
 
     def _update_hashrate(self) -> None:
         dt = time.monotonic() - self._work_t0
@@ -475,6 +500,16 @@ class PoolServer:
         xs = sorted(self._validate_ms)
         return xs[min(len(xs) - 1, int(q * len(xs)))] if xs else None
 
+    def _vardiff_view(self, w: _Worker) -> dict:
+        """Vardiff's estimator for one live worker, read without touching it (this runs on the HTTP thread): the
+        shares it rests on, the difficulty ratio it points to (far from 1 = a retarget is on its way), and whether
+        it has settled (pool/vardiff.py: no refinement left and none pending; the pool probe opens its window on it)."""
+        if self.opts.fixed_difficulty:
+            return {"window_shares": w.vd.shares, "window_ratio": None, "settled": True}
+        dstar, n = self.vardiff.estimate(w.vd, mutate=False)
+        return {"window_shares": n, "window_ratio": dstar / w.vd.difficulty if dstar else None,
+                "settled": self.vardiff.settled(w.vd, mutate=False)}
+
     def stats(self) -> dict:
         now = time.monotonic()
         live = self._live_workers()
@@ -498,12 +533,7 @@ class PoolServer:
                          # SETTLE_BAND, and how long ago that was
                          "converged_after_s": (w.last_big_retarget_at - w.opened_at) if w.last_big_retarget_at else 0.0,
                          "steady_for_s": now - (w.last_big_retarget_at or w.opened_at),
-                         # vardiff's open window: its shares and the difficulty ratio they point to (target interval
-                         # / observed); far from 1 with many shares = a retarget is on its way
-                         "window_shares": w.vd.shares,
-                         "window_ratio": (self.vardiff.cfg.target_share_seconds * w.vd.shares
-                                          / max(self.vardiff.clock() - w.vd.window_start, 1e-9)) if w.vd.shares
-                         else None}
+                         **self._vardiff_view(w)}
                         for w in live],
         }
 

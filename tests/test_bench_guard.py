@@ -74,7 +74,7 @@ def test_stuck_node_section_keeps_the_full_json():
     assert d["sections"]["node"]["status"] == "timeout" and d["sections"]["cpu"]["status"] == "ok"
     assert d["cpu_single_thread_hashes_per_sec"] > 0
     s = d["summary"]
-    assert list(d)[-1] == "summary" and s["errors"]["node"] == "timeout after 12 s" and s["sha256d_hps"] > 0
+    assert list(d)[-1] == "summary" and s["errors"]["node"] == "timeout after 12 s" and s["cfg2_version_rolled_hps"] > 0
     assert took < 100, took
 
 

@@ -280,3 +280,102 @@ def test_vardiff_counts_a_grace_share_at_its_credited_fraction():
     assert st.shares == 1.25 and st.total_shares == 2 and st.accepted_work == 5.0
     vd.on_share(st, 7.0)  # clamped: a share is never worth more than one
     assert st.shares == 2.25
+
+
+# ------------------------------------------------------------------ vardiff estimator
+def _poisson_run(vd, s, clk, rng, hashrate, seconds, on_event=None):
+    end = clk.t + seconds
+    while clk.t < end:
+        clk.t += rng.expovariate(hashrate / s.difficulty)
+        old = s.difficulty
+        new = vd.on_share(s)
+        if on_event is not None:
+            on_event(clk.t, old, new)
+
+
+@settings(max_examples=60, deadline=None)
+@given(seed=st.integers(0, 2 ** 31), start=st.floats(0.01, 4.0), hashrate=st.floats(1e3, 1e12))
+def test_vardiff_holds_the_target_after_three_retarget_periods(seed, start, hashrate):
+    """Poisson share arrivals at a fixed rate, starting anywhere from 100x too easy to 4x too hard: after 3 retarget
+    periods the difficulty is within 10% of D* = H * T / diff1, and it stays there for the next 10 periods (the
+    estimator is not reset by its own retargets, so it keeps sharpening). A 2 ms share target and a 4096-share
+    window put 10% at ~6 standard errors of the settled estimate, so the property is about the algorithm, not luck."""
+    import math
+    import random
+
+    rng = random.Random(seed)
+    clk = FakeClock()
+    cfg = VardiffConfig(target_share_seconds=0.002, retarget_seconds=5.0, min_difficulty=1e-12, max_window_shares=4096)
+    vd = Vardiff(cfg, diff1_hashes=1.0, clock=clk)
+    ideal = hashrate * cfg.target_share_seconds
+    s = vd.new_state(ideal * start)
+    _poisson_run(vd, s, clk, rng, hashrate, 3 * cfg.retarget_seconds)
+    errs = [abs(math.log(s.difficulty / ideal))]
+    for _ in range(10):
+        _poisson_run(vd, s, clk, rng, hashrate, cfg.retarget_seconds)
+        errs.append(abs(math.log(s.difficulty / ideal)))
+    assert max(errs) < math.log(1.10), (start, errs)
+
+
+def test_vardiff_default_config_corrects_2x_and_3x_within_two_periods():
+    """at the production defaults (10 s share target, 30 s retarget: ~3 shares per period) a difficulty
+    that rests on no shares yet (the initial one) moves on a 1-standard-error deviation, so a 2x-fast and a 3x-slow
+    worker are corrected within two retarget periods in most runs (round 5's z=3 test took 120 s and 240 s). The
+    Poisson noise of 6 shares bounds "most": a 2x-fast worker that happened to send 6 shares in 60 s looks on
+    target, so the bar is the direction of the move (>= 80% of runs) and no move the wrong way past D*."""
+    import math
+    import random
+
+    ok = {2.0: 0, 1 / 3: 0}
+    runs = 60
+    for factor in ok:
+        for seed in range(runs):
+            rng = random.Random(seed)
+            clk = FakeClock()
+            cfg = VardiffConfig()
+            vd = Vardiff(cfg, diff1_hashes=2.0 ** 32, clock=clk)
+            hashrate = 1e12
+            ideal = hashrate * cfg.target_share_seconds / 2.0 ** 32
+            s = vd.new_state(ideal / factor)  # factor 2: shares twice as fast as the target
+            t_end = clk.t + 2 * cfg.retarget_seconds
+            while True:
+                nxt = clk.t + rng.expovariate(hashrate / (s.difficulty * 2.0 ** 32))
+                if nxt > t_end:  # a look at the period boundary also happens without a share (the pool's tick)
+                    clk.t = t_end
+                    vd.maybe_retarget(s)
+                    break
+                clk.t = nxt
+                vd.on_share(s)
+            moved = math.log(s.difficulty / (ideal / factor)) * (1 if factor > 1 else -1)  # > 0: toward D*
+            ok[factor] += moved > 0.1
+    assert ok[2.0] >= 0.8 * runs and ok[1 / 3] >= 0.8 * runs, ok
+
+
+def test_vardiff_settled_means_no_more_retargets():
+    """``settled()`` (the pool probe opens its window on it): across 150 Poisson runs from 1000x too easy to 100x
+    too hard at the pool bench's 0.05 s / 5 s, no retarget happens after the first moment a worker reads settled,
+    and the difficulty it settles on is within 10% of D*."""
+    import math
+    import random
+
+    for seed in range(150):
+        rng = random.Random(seed)
+        clk = FakeClock()
+        cfg = VardiffConfig(target_share_seconds=0.05, retarget_seconds=5.0)
+        vd = Vardiff(cfg, diff1_hashes=1.0, clock=clk)
+        hashrate = 1000.0
+        ideal = hashrate * cfg.target_share_seconds
+        s = vd.new_state(ideal * rng.choice([0.001, 0.3, 1.0, 3.0, 100.0]))
+        t0 = clk.t
+        state = {"settled_at": None, "late": []}
+
+        def ev(t, old, new):
+            if new is not None and state["settled_at"] is not None:
+                state["late"].append((t, old, new))
+            if state["settled_at"] is None and vd.settled(s):
+                state["settled_at"] = t
+
+        _poisson_run(vd, s, clk, rng, hashrate, 130.0, ev)
+        assert state["settled_at"] is not None and state["settled_at"] - t0 < 110.0, seed
+        assert not state["late"], (seed, state)
+        assert abs(math.log(s.difficulty / ideal)) < math.log(1.10), (seed, s.difficulty / ideal)
