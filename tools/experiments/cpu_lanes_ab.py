@@ -7,7 +7,7 @@ import statistics
 import sys
 import time
 
-sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+sys.path.insert(0, __file__.rsplit("/tools/experiments/", 1)[0])
 from otedama_amd.models.header import GENESIS_HEADER_HEX, int_to_hash  # noqa: E402
 from otedama_amd.ops.native import require_native  # noqa: E402
 

@@ -10,7 +10,7 @@ import statistics
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CHILD = ("import json, sys; sys.path.insert(0, sys.argv[1]); from otedama_amd.cli.bench_cmd import bench_cpu, cpu_share; "
          "r = bench_cpu(seconds=3.0, threads=cpu_share(), single_seconds=2.0); "
          "print(json.dumps({k: r[k] for k in ('sha256d_single_thread_hps', 'sha256d_all_threads_hps', 'threads')}))")

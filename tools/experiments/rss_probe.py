@@ -9,7 +9,7 @@ import sys
 import time
 
 os.environ["OTEDAMA_NO_TORCH"] = "1"
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def rss() -> float:

@@ -36,7 +36,7 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--bpc", default="16,20,24,28")
     a = ap.parse_args()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     res: dict = {}
     for _ in range(a.rounds):
         for b in a.bpc.split(","):
