@@ -3,7 +3,7 @@
 of SHA-256d, scrypt and X11 each, so the kernel statistics show the per-launch clock probes and the search kernels
 side by side, with no child process (a profiled process must not start other programs).
 
-Usage: python3 tools/trace_native_miner.py [seconds_per_algorithm]   (one JSON line per algorithm)"""
+Usage: python3 tools/trace_native_miner.py [seconds_per_algorithm] [algo,algo,...]   (one JSON line per algorithm)"""
 from __future__ import annotations
 
 import json
@@ -44,7 +44,8 @@ def run(N, algo: str, seconds: float) -> dict:
 def main() -> int:
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 4.0
     N = require_native()
-    for algo in ("sha256d", "scrypt", "x11"):
+    algos = sys.argv[2].split(",") if len(sys.argv) > 2 else ("sha256d", "scrypt", "x11")
+    for algo in algos:
         print(json.dumps(run(N, algo, secs)), flush=True)
     return 0
 
