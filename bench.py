@@ -1134,6 +1134,8 @@ class Bench:
             "scrypt": R.get("scrypt") or {},
             "x11_hashes_per_sec": R.get("x11_hps"),
             "x11": R.get("x11") or {},
+            # the run's data plane measured across every rank (comm section)
+            "comm": R.get("comm"),
             "p50_share_latency_ms": latency.get("p50_ms"),
             "device_hit_to_accept_p50_ms": latency.get("device_hit_to_accept_p50_ms"),
             "device_hit_to_accept_p95_ms": latency.get("device_hit_to_accept_p95_ms"),
