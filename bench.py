@@ -537,14 +537,15 @@ class Bench:
         except Exception as exc:  # noqa: BLE001 - decided together below
             comm, err = None, f"{type(exc).__name__}: {exc}"[:300]
         if self.world > 1:
-            store.set(f"otd-bench/native/{self.rank}", "1" if comm is not None else "0")
+            store.set(f"otd-bench/native/{self.rank}", "1" if comm is not None else "0" + err)
             try:
                 flags = [_wait_get(store, f"otd-bench/native/{r}", timeout + 10.0) for r in range(self.world)]
             except TimeoutError as exc:
                 flags, err = [], err or str(exc)
             if len(flags) != self.world or any(f != b"1" for f in flags):
-                bad = [r for r, f in enumerate(flags) if f != b"1"]
-                err = err or f"native communicator failed on rank(s) {bad}"
+                # every failed rank's reason (a rank that failed at once makes the others' inits time out)
+                bad = {r: f[1:].decode(errors="replace")[:100] for r, f in enumerate(flags) if f != b"1"}
+                err = f"native communicator failed on rank(s) {sorted(bad)}: {bad}" if bad else err
                 if comm is not None:
                     comm.close()
                 comm = None
@@ -589,7 +590,10 @@ class Bench:
             self.guard.set_phase("rendezvous")
         comm, native_err = None, ""
         if native_on:
-            comm, native_err = self.open_native(store, timeout=min(120.0, max(10.0, left() - 30.0)))
+            # the probe's children formed the same group in probe["seconds"]: the in-process init gets a few times
+            # that (a rank whose init fails outright leaves its peers waiting in theirs until this bound)
+            bound = 60.0 if probe is None else max(15.0, 4.0 * float(probe.get("seconds") or 0.0))
+            comm, native_err = self.open_native(store, timeout=min(bound, max(10.0, left() - 30.0)))
             if comm is None and self.world > 1:
                 backend = "gloo"
         if backend == "gloo" and self.world > 1:
