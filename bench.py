@@ -583,6 +583,8 @@ class Bench:
 
             self.guard.set_phase("data-plane probe")
             store = connect_store_from_env()
+            if fault_for(self.rank, "arrive") == "slow":  # tests: a rank that reaches the probe late
+                time.sleep(float(os.environ.get("OTEDAMA_FAULT_SLOW_S", "25")))
             probe = run_probe(store, self.rank, self.world, fault=fault_for(self.rank, "probe"),
                               budget=left() - self.PREFLIGHT_RESERVE_S)
             if not probe["ok"]:

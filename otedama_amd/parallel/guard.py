@@ -26,7 +26,8 @@ V1 read loop's 5 min deadline, internal/poolproto/stratumv1/stratumv1.go:166).
 Fault hooks for the CPU rehearsal tests: ``OTEDAMA_BENCH_FAULT=stuck:<rank>:<section>[,...]`` makes that rank hang
 at the start of that section (an uninterruptible-looking sleep), ``exit:<rank>:<section>`` makes it exit with code 7;
 ``fail:<rank>:probe`` / ``hang:<rank>:probe`` make that rank's data-plane probe child fail or hang
-(parallel/rccl_probe.py).
+(parallel/rccl_probe.py); ``slow:<rank>:arrive`` delays that rank's arrival at the probe by OTEDAMA_FAULT_SLOW_S
+(a cold-start skew); ``fail:<rank>:native`` fails its in-process native init after the probe.
 """
 from __future__ import annotations
 
@@ -85,7 +86,7 @@ def fault_for(rank: int, section: str, env=None) -> str | None:
     spec = (os.environ if env is None else env).get("OTEDAMA_BENCH_FAULT", "")
     for item in filter(None, (s.strip() for s in spec.split(","))):
         parts = item.split(":")
-        if len(parts) == 3 and parts[0] in ("stuck", "exit", "fail", "hang") and parts[2] == section:
+        if len(parts) == 3 and parts[0] in ("stuck", "exit", "fail", "hang", "slow") and parts[2] == section:
             try:
                 if int(parts[1]) == rank:
                     return parts[0]

@@ -222,3 +222,23 @@ def test_data_plane_probe_falls_back_together_and_still_measures(fault):
         assert all(v["ok"] is False for v in dp["probe"]["ranks"].values()), dp
     elif fault:
         assert "3" in dp["native_error"] or "injected" in dp["native_error"], dp
+
+
+@pytest.mark.timeout(300)
+def test_probe_with_default_deadlines_fits_the_preflight_under_skew_and_a_hang():
+    """the probe's deadlines come from the pre-flight budget (no OTEDAMA_PROBE_TIMEOUT override here). One
+    rank reaches the probe 25 s late (a cold-start skew past the derived arrival wait) and another rank's child hangs:
+    the probe still decides inside the pre-flight, every rank falls back to gloo together, and the headline is
+    measured. --preflight-timeout 90 keeps the test short; the derivation is the same as at the default 180 s."""
+    env = {"OTEDAMA_RCCL_MODULE": "loopback_rccl", "PYTHONPATH": os.path.join(ROOT, "tests"),
+           "OTEDAMA_BENCH_FAULT": "slow:2:arrive,hang:1:probe", "OTEDAMA_FAULT_SLOW_S": "25"}
+    res, took = _bench("--gpus", "4", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
+                       "--comm-ops", "10", "--preflight-timeout", "90", env=env, timeout=280)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    dp = d["preflight"]["data_plane"]
+    assert d["value"] > 0 and dp["impl"] == "gloo" and not dp["probe"]["ok"], dp
+    a, t, v = dp["probe"]["deadlines_s"]
+    assert a + t + v <= 90.0 - 40.0 + 1.0, dp["probe"]  # inside the budget minus the fallback's reserve
+    assert d["sections"]["preflight"]["status"] == "ok" and d["sections"]["preflight"]["s"] < 90.0
+    assert "killed" in dp["probe"]["ranks"]["1"]["reason"]
