@@ -102,6 +102,34 @@ def test_driver_torchrun_invocation():
     assert d["hits_duplicate"] == 0 and d["hits_verified"] == d["hits_found"]
 
 
+@pytest.mark.timeout(300)
+def test_driver_torchrun_invocation_on_the_native_data_plane():
+    """The driver's N>1 command line (torchrun, its agent's store) with the native data plane the GPU run uses: the
+    probe children form a native group through the agent's store, every rank's R1 / R2 / R3 and the comm section run
+    on the native module's API (its CPU stand-in, tests/loopback_rccl.py), and the line says rccl-native."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(detail_env(tempfile.mkdtemp(prefix="otd-bench-"))[0])
+    e.update(OTEDAMA_RCCL_MODULE="loopback_rccl", PYTHONPATH=os.path.join(ROOT, "tests"))
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "4",
+                          "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0", "--comm-ops", "20"],
+                         capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+    res.detail = e["OTEDAMA_BENCH_DETAIL"]
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d.line["summary"]["data_plane"] == "rccl-native" and d["dist_backend"] == "rccl"
+    assert d["rccl_ranks_seen"] == [0, 1, 2, 3] and d["hits_r2_gathered"] == d["hits_found"] > 0
+    assert d["comm"]["idle"]["R2_dev"]["samples"] == 20 and d["comm"]["busbw"]["blocks_ok"]
+
+
 @pytest.mark.timeout(400)
 def test_driver_torchrun_invocation_with_the_node_section():
     """The driver's N>1 command line end to end, node section included: torchrun's ranks run the kernel sections,
