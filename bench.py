@@ -478,6 +478,8 @@ class Bench:
         return 0 if "sha" in self.R else 1
 
     SHUTDOWN_S = 20.0  # bound on tearing the process group down once the JSON is out
+    HW_QUEUES_SET = False  # run_rank raised GPU_MAX_HW_QUEUES for this process (restored once HIP is up)
+    HW_QUEUES_PREV: str | None = None
 
     def shutdown(self) -> None:
         """Tear the process group down, bounded: at world > 1 the peers may already be gone (the other ranks leave
@@ -608,6 +610,11 @@ class Bench:
             impl = {"nccl": "torch-nccl"}.get(self.info.backend, self.info.backend)
         self.comm = comm
         self.dev = self.info.device
+        if self.HW_QUEUES_SET:  # HIP and the communicator are up: children started later get the value they had
+            if self.HW_QUEUES_PREV is None:
+                os.environ.pop("GPU_MAX_HW_QUEUES", None)
+            else:
+                os.environ["GPU_MAX_HW_QUEUES"] = self.HW_QUEUES_PREV
         t_pg = time.monotonic()
         self.guard.set_phase("first-collective")
         total = self.comm.allreduce_counters(1)[0]  # the first collective on the data plane (RCCL on GPUs)
@@ -1248,6 +1255,15 @@ class Bench:
         }
 
 
+# HIP hardware queues for the bench process itself (read at HIP init, and by RCCL at communicator init). The native
+# data plane's communicator brings streams of its own (RCCL's, the comm stream); at the runtime's default of 4
+# queues per process the second search stream then shares a queue and its launches no longer overlap the first's:
+# -0.25% on the headline, which 8 queues recover (profiles/r6/f_dataplane_ab/). Only this process: the value is
+# dropped from the environment once HIP and the communicator are up, so the device processes, node and pool started
+# later keep their own defaults.
+BENCH_HW_QUEUES = "8"
+
+
 def run_rank(args) -> int:
     from otedama_amd.parallel.guard import RankGuard, run_dir_for
 
@@ -1257,6 +1273,11 @@ def run_rank(args) -> int:
     if world > 1:  # RCCL warnings into the run directory, where an error JSON reads them back
         os.environ.setdefault("NCCL_DEBUG", "WARN")
         os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(run_dir, "rccl.%h.%p.log"))
+    prev = os.environ.get("GPU_MAX_HW_QUEUES")
+    if not args.cpu_rehearsal and (prev is None or (prev.isdigit() and int(prev) < int(BENCH_HW_QUEUES))):
+        os.environ["GPU_MAX_HW_QUEUES"] = BENCH_HW_QUEUES  # the box may export the runtime's default (4) explicitly
+        Bench.HW_QUEUES_PREV = prev
+        Bench.HW_QUEUES_SET = True
     bench = Bench(args, rank, world)
     bench.guard = RankGuard(rank, world, args.deadline, emit=bench.emit if rank == 0 else None, run_dir=run_dir)
     bench.guard.start(tee_stderr=world > 1)

@@ -182,7 +182,7 @@ class NativeNodeComm:
 
     def gather_tensor(self, out, inp) -> None:
         """``out`` (world x inp.shape) gets every rank's contiguous ``inp``, in rank order."""
-        if not self.multi:
+        if not self.multi or (self.info.world_size == 1 and os.environ.get("OTEDAMA_RCCL_LOCAL_R2") == "1"):
             out[0].copy_(inp)
             return
         if self._rc is None:
