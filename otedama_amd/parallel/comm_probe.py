@@ -20,6 +20,7 @@ kernels keep running while R2/R3 move.
 """
 from __future__ import annotations
 
+import contextlib
 import statistics
 import sys
 import time
@@ -276,7 +277,7 @@ def _lockstep_ops(comm, ops: int, cadence_hz: float, dev) -> dict:
             comm.allreduce_counters(1, 2, 3, 4)
         else:
             stream = comm.stream if cuda else None
-            with torch.cuda.stream(stream) if stream is not None else _null():
+            with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
                 comm.gather_tensor(gathered, slot)
             if stream is not None:
                 stream.synchronize()
@@ -284,14 +285,6 @@ def _lockstep_ops(comm, ops: int, cadence_hz: float, dev) -> dict:
                 torch.cuda.synchronize(dev)
         lat[op].append((time.perf_counter() - t) * 1e3)
     return {k: _q(v) for k, v in lat.items()}
-
-
-class _null:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
 
 
 def _busbw(comm, dev, total_bytes: int, iters: int = 5) -> dict:
