@@ -77,9 +77,15 @@ CHANGE_P = 1e-4  # significance of the rate-change test (run at every look: fals
 
 
 def _binom_two_sided(k: int, m: int, p: float) -> float:
-    """P(K <= k) or P(K >= k) for K ~ Binomial(m, p), whichever tail k is in, doubled (capped at 1)."""
+    """P(K <= k) or P(K >= k) for K ~ Binomial(m, p), whichever tail k is in, doubled (capped at 1). Exact for
+    m <= 200; above that the normal approximation with continuity correction (a look per worker per period must
+    stay cheap on a pool with many workers: the exact tail is up to m lgamma terms)."""
     if m <= 0 or not 0.0 < p < 1.0:
         return 1.0
+    if m > 200:
+        mu, sd = m * p, math.sqrt(m * p * (1.0 - p))
+        z = max(0.0, abs(k - mu) - 0.5) / max(sd, 1e-12)
+        return min(1.0, math.erfc(z / math.sqrt(2.0)))
     lp, lq = math.log(p), math.log1p(-p)
 
     def pmf(i: int) -> float:
