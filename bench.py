@@ -133,7 +133,7 @@ def parse_args(argv=None):
                     help="BASELINE config 1 (native CPU miner, single thread and all cores): seconds each (0 = skip)")
     ap.add_argument("--deadline", type=float, default=DEFAULT_DEADLINE_S,
                     help="seconds from start by which rank 0 prints its JSON, whatever is still running")
-    ap.add_argument("--preflight-timeout", type=float, default=180.0,
+    ap.add_argument("--preflight-timeout", type=float, default=240.0,
                     help="seconds from start for the rendezvous and the first collective (cold `import torch` "
                          "included)")
     ap.add_argument("--section-timeouts", default="",

@@ -229,7 +229,7 @@ def test_probe_with_default_deadlines_fits_the_preflight_under_skew_and_a_hang()
     """the probe's deadlines come from the pre-flight budget (no OTEDAMA_PROBE_TIMEOUT override here). One
     rank reaches the probe 25 s late (a cold-start skew past the derived arrival wait) and another rank's child hangs:
     the probe still decides inside the pre-flight, every rank falls back to gloo together, and the headline is
-    measured. --preflight-timeout 90 keeps the test short; the derivation is the same as at the default 180 s."""
+    measured. --preflight-timeout 90 keeps the test short; the derivation is the same as at the default 240 s."""
     env = {"OTEDAMA_RCCL_MODULE": "loopback_rccl", "PYTHONPATH": os.path.join(ROOT, "tests"),
            "OTEDAMA_BENCH_FAULT": "slow:2:arrive,hang:1:probe", "OTEDAMA_FAULT_SLOW_S": "25"}
     res, took = _bench("--gpus", "4", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
