@@ -126,6 +126,25 @@ def flood(algorithms: list[str], seconds: float = 3.0, miners: int = 8, timeout:
     return res
 
 
+def _wait_hashing(miners: list, timeout: float) -> None:
+    """Until every started miner's report shows device hashes (or ``timeout``): its GPU work is running."""
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        reps = [_read(m["report"]) for m in miners]
+        if all(any(int((c or [0])[0]) > 0 for c in (r.get("counters") or {}).values()) for r in reps):
+            return
+        if any(m["proc"].poll() is not None for m in miners):
+            raise RuntimeError(f"miner(s) exited: {[m['name'] for m in miners if m['proc'].poll() is not None]}")
+        time.sleep(0.2)
+
+
+def _hashes_per_diff1(algo: str) -> float:
+    """Expected hashes per difficulty-1 share: 2^256 / the algorithm's difficulty-1 target."""
+    from otedama_amd.models.algorithms import ALGORITHMS
+
+    return float(2 ** 256) / ALGORITHMS[algo].diff1
+
+
 def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.05, retarget_seconds: float = 5.0,
                  difficulty: float = 1.0, cpu: bool = False, startup_timeout: float = 180.0,
                  settle_timeout: float = 120.0, flood_seconds: float = 3.0) -> dict:
@@ -141,8 +160,16 @@ def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.
     miners = []
     final: dict = {}
     t_open = time.monotonic()
+    shared = len({g for g, _ in streams}) < len(streams)  # a GPU hosts two streams (one GPU: both algorithms)
     try:
-        for gpu, algo in streams:
+        # On a shared GPU the scrypt stream starts first and the SHA-256d one once scrypt is hashing: started
+        # together, SHA-256d has the GPU to itself for its first seconds (19.3 GH/s against ~13.9 shared), and those
+        # shares sat in its vardiff estimate at settling, ~4% high (profiles/r6/i_pool_flow/). scrypt's own drop when
+        # SHA-256d joins is 3.5x, which vardiff's rate-change test catches at its next look.
+        order = sorted(streams, key=lambda s: s[1] != "scrypt") if shared else streams
+        for i, (gpu, algo) in enumerate(order):
+            if shared and i > 0 and algo != order[i - 1][1]:
+                _wait_hashing(miners, 60.0)
             name = f"{'cpu' if cpu else 'gpu'}{gpu}-{algo}"
             cfg = os.path.join(tmp, f"{name}.yaml")
             with open(cfg, "w") as f:
@@ -185,8 +212,10 @@ def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.
             time.sleep(0.25)
         t_settled = time.monotonic()
         a0, t0 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
+        reps0 = {m["name"]: _read(m["report"]) for m in miners}
         time.sleep(seconds)
         a1, t1 = {s["algorithm"]: s for s in _pool_api(http)}, time.monotonic()
+        reps1 = {m["name"]: _read(m["report"]) for m in miners}
         time.sleep(0.6)
         reps = {m["name"]: _read(m["report"]) for m in miners}
     finally:
@@ -212,13 +241,26 @@ def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.
         for m in ms:
             r = window_rates(reps[m["name"]].get("samples", []), t0, t1 + 0.75)
             rates[m["name"]] = sum(r.values())
+        # the miners' own share accounting over the window (found on the device, skipped by the engine, submitted,
+        # accepted): where a gap between the hash rate's expected shares and the pool's accepted ones would come from
+        flow = {}
+        for m in ms:
+            r0, r1 = reps0.get(m["name"], {}), reps1.get(m["name"], {})
+            flow[m["name"]] = {k: (r1.get(k) or 0) - (r0.get(k) or 0)
+                               for k in ("shares_found", "submitted", "accepted", "rejected", "stale_skipped",
+                                         "below_target_skipped")}
         workers = []
         for w in s1.get("workers", []):
             got = sum(1 for v in s1.get("workers", []) if v["name"] == w["name"])
             prev = next((v for v in s0.get("workers", []) if v["name"] == w["name"]), {})
             n = w["accepted"] - prev.get("accepted", 0)
             interval = dt / n if n else None
+            miner = next((k for k in flow if w["name"].endswith("." + k)), None)
+            rate = rates.get(miner) if miner else None
             workers.append({"name": w["name"], "difficulty": w["difficulty"], "retargets": w["retargets"],
+                            "miner_flow_in_window": flow.get(miner),
+                            "shares_expected_from_rate": (rate * dt / (w["difficulty"] * _hashes_per_diff1(algo))
+                                                          if rate and w["difficulty"] else None),
                             "retargets_in_window": w["retargets"] - prev.get("retargets", w["retargets"]),
                             "estimate_ratio_at_open": prev.get("window_ratio"),
                             "estimate_shares_at_open": prev.get("window_shares"),
