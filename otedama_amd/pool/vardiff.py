@@ -242,8 +242,8 @@ class Vardiff:
     def _detect_change(self, st: VardiffState, now: float) -> None:
         """The worker's rate itself changed (a miner stopped, or a second miner took half the GPU): the segment since
         the last retarget disagrees with the older history by more than 20% and at CHANGE_P (the test runs at every
-        look, so its false alarms must be rare), so the history is dropped and the estimate restarts from that
-        segment."""
+        look, so its false alarms must be rare), so the history is dropped and the estimate restarts from the second
+        half of that stretch."""
         self._advance(st, now)
         self._trim(st, now)
         k = st.shares
@@ -256,10 +256,13 @@ class Vardiff:
         # its share of the exposure: an exact test that carries both stretches' noise (and is right for k = 0)
         m, p = int(round(old_n + k)), e_recent / (e_recent + old_e)
         if abs(k - expect) > 0.2 * expect and _binom_two_sided(int(round(k)), m, p) < CHANGE_P:
-            while st.hist and st.hist[0][1] <= st.ws_exp:
+            # the change happened somewhere in the recent stretch: keep its second half only (the first may still
+            # carry the old rate: a second miner joining the GPU a second or two after this worker's last retarget)
+            cut = max(st.ws_exp, st.hist_start_exp) + 0.5 * e_recent
+            while st.hist and st.hist[0][1] <= cut:
                 _t, _e, w = st.hist.popleft()
                 st.hist_shares -= w
-            st.hist_start_exp = max(st.ws_exp, st.hist_start_exp)
+            st.hist_start_exp = cut
             st.n_at_set = 0.0
 
     def _set(self, st: VardiffState, target: float, now: float, n: float) -> float | None:

@@ -379,3 +379,39 @@ def test_vardiff_settled_means_no_more_retargets():
         assert state["settled_at"] is not None and state["settled_at"] - t0 < 110.0, seed
         assert not state["late"], (seed, state)
         assert abs(math.log(s.difficulty / ideal)) < math.log(1.10), (seed, s.difficulty / ideal)
+
+
+def test_vardiff_follows_a_rate_step_when_a_second_miner_joins_the_gpu():
+    """A worker's rate drops 3.5x a few seconds after it connected (the pool probe's scrypt miner when the SHA-256d
+    one joins its GPU): the exact-binomial change test drops the old history, keeping the second half of the stretch
+    the change fell in, and the difficulty settles within 10% of the new D* in every one of 40 runs."""
+    import math
+    import random
+
+    for seed in range(40):
+        rng = random.Random(seed)
+        clk = FakeClock()
+        cfg = VardiffConfig(target_share_seconds=0.05, retarget_seconds=5.0)
+        vd = Vardiff(cfg, diff1_hashes=1.0, clock=clk)
+        t0 = clk.t
+        s = vd.new_state(1.0)
+        ideal = 3700.0 * cfg.target_share_seconds
+
+        def rate(t):
+            return 13000.0 if t - t0 < 7.0 else 3700.0
+
+        tick = t0 + 2.5
+        settled_at = None
+        while clk.t - t0 < 120.0:
+            gap = rng.expovariate(rate(clk.t) / s.difficulty)
+            if clk.t + gap > tick:  # the pool's periodic look
+                clk.t = tick
+                tick += 2.5
+                vd.maybe_retarget(s)
+            else:
+                clk.t += gap
+                vd.on_share(s)
+            if settled_at is None and clk.t - t0 > 8.0 and vd.settled(s):
+                settled_at = clk.t - t0
+        assert settled_at is not None and settled_at < 90.0, seed
+        assert abs(math.log(s.difficulty / ideal)) < math.log(1.10), (seed, s.difficulty / ideal)
