@@ -128,7 +128,7 @@ def parse_args(argv=None):
                     help="forced new blocks (SetNewPrevHash) per node run for the node-wide job switch (0 = none)")
     ap.add_argument("--pool-seconds", type=float, default=-1.0,
                     help="BASELINE config 5 (mixed SHA-256d + scrypt pool, vardiff on): recorded seconds after every "
-                         "worker settled (-1 = 30 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
+                         "worker settled (-1 = 45 on GPUs, 0 in the CPU rehearsal; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0,
                     help="BASELINE config 1 (native CPU miner, single thread and all cores): seconds each (0 = skip)")
     ap.add_argument("--deadline", type=float, default=DEFAULT_DEADLINE_S,
@@ -385,7 +385,7 @@ class Bench:
         return self.args.node_seconds if self.args.node_seconds >= 0 else (0.0 if self.cpu else 8.0)
 
     def pool_seconds(self) -> float:
-        return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 30.0)
+        return self.args.pool_seconds if self.args.pool_seconds >= 0 else (0.0 if self.cpu else 45.0)
 
     def comm_phases(self) -> list[str]:
         """The comm section's phases: idle, then under each mining algorithm (GPUs only: the CPU rehearsal has no
