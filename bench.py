@@ -359,6 +359,8 @@ class Bench:
         self.guard = None
         self.info = self.comm = self.N = self.dev = None
         self.budgets = self._budgets()
+        # run_rank raised GPU_MAX_HW_QUEUES for this process; preflight restores the previous value once HIP is up
+        self.hw_queues_raised, self.hw_queues_prev = False, None
 
     # ------------------------------------------------------------------ budgets
     def _budgets(self) -> dict[str, float]:
@@ -478,8 +480,6 @@ class Bench:
         return 0 if "sha" in self.R else 1
 
     SHUTDOWN_S = 20.0  # bound on tearing the process group down once the JSON is out
-    HW_QUEUES_SET = False  # run_rank raised GPU_MAX_HW_QUEUES for this process (restored once HIP is up)
-    HW_QUEUES_PREV: str | None = None
 
     def shutdown(self) -> None:
         """Tear the process group down, bounded: at world > 1 the peers may already be gone (the other ranks leave
@@ -610,11 +610,11 @@ class Bench:
             impl = {"nccl": "torch-nccl"}.get(self.info.backend, self.info.backend)
         self.comm = comm
         self.dev = self.info.device
-        if self.HW_QUEUES_SET:  # HIP and the communicator are up: children started later get the value they had
-            if self.HW_QUEUES_PREV is None:
+        if self.hw_queues_raised:  # HIP and the communicator are up: children started later get the value they had
+            if self.hw_queues_prev is None:
                 os.environ.pop("GPU_MAX_HW_QUEUES", None)
             else:
-                os.environ["GPU_MAX_HW_QUEUES"] = self.HW_QUEUES_PREV
+                os.environ["GPU_MAX_HW_QUEUES"] = self.hw_queues_prev
         t_pg = time.monotonic()
         self.guard.set_phase("first-collective")
         total = self.comm.allreduce_counters(1)[0]  # the first collective on the data plane (RCCL on GPUs)
@@ -1273,12 +1273,11 @@ def run_rank(args) -> int:
     if world > 1:  # RCCL warnings into the run directory, where an error JSON reads them back
         os.environ.setdefault("NCCL_DEBUG", "WARN")
         os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(run_dir, "rccl.%h.%p.log"))
+    bench = Bench(args, rank, world)
     prev = os.environ.get("GPU_MAX_HW_QUEUES")
     if not args.cpu_rehearsal and (prev is None or (prev.isdigit() and int(prev) < int(BENCH_HW_QUEUES))):
         os.environ["GPU_MAX_HW_QUEUES"] = BENCH_HW_QUEUES  # the box may export the runtime's default (4) explicitly
-        Bench.HW_QUEUES_PREV = prev
-        Bench.HW_QUEUES_SET = True
-    bench = Bench(args, rank, world)
+        bench.hw_queues_raised, bench.hw_queues_prev = True, prev
     bench.guard = RankGuard(rank, world, args.deadline, emit=bench.emit if rank == 0 else None, run_dir=run_dir)
     bench.guard.start(tee_stderr=world > 1)
     return bench.run()
