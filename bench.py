@@ -255,6 +255,18 @@ def _short_errors(errors: dict | None, n: int = 160) -> dict | None:
     return {str(k)[:40]: str(v)[:n] for k, v in errors.items()} if errors else None
 
 
+def _data_plane_note(dp: dict) -> str | None:
+    probe = dp.get("probe") or {}
+    if probe and not probe.get("ok"):
+        bad = [(r, v) for r, v in sorted((probe.get("ranks") or {}).items()) if not v.get("ok")]
+        if bad:
+            return f"probe: rank {bad[0][0]}: {bad[0][1].get('reason', '?')}"[:160]
+        return f"probe: {probe.get('reason', 'failed')}"[:160]
+    if dp.get("native_error"):
+        return str(dp["native_error"])[:160]
+    return None
+
+
 def error_output(args, world: int, error: str, errors: dict, diagnosis: dict | None) -> dict:
     """The result of a run that has no headline (the pre-flight failed, or rank 0 never reported). The diagnosis
     (every rank's stderr and RCCL log tail) stays in the detail file; the line carries the phases only."""
@@ -1244,6 +1256,8 @@ class Bench:
             "lost_ranks": sorted({r for v in nalg.values() for r in v.get("lost_ranks") or []}) if nalg else None,
             "node_backend": node.get("dist_backend"),
             "data_plane": dp.get("impl") or out["dist_backend"],
+            # why it is not rccl-native at N > 1 (the probe's first failing rank, or the in-process init's error)
+            "data_plane_note": _data_plane_note(dp),
             "comm_r1_p99_ms": p99("R1"),
             "comm_r2_p99_ms": p99("R2"),
             "comm_r3_p99_ms": p99("R3"),

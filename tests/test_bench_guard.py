@@ -211,6 +211,7 @@ def test_data_plane_probe_falls_back_together_and_still_measures(fault):
     assert d["value"] and d["value"] > 0 and d["hits_r2_gathered"] == d["hits_found"] > 0
     native = fault == ""
     assert dp["impl"] == ("rccl-native" if native else "gloo") == d.line["summary"]["data_plane"], dp
+    assert (d.line["summary"]["data_plane_note"] is None) is native
     assert dp["backend"] == ("rccl" if native else "gloo")
     assert dp["probe"]["ok"] is (not fault.endswith(":probe")), dp
     assert d["comm"]["idle"]["R2"]["samples"] == 20 and d["comm"]["busbw"]["blocks_ok"]
