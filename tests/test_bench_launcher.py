@@ -5,7 +5,6 @@ launcher, rank bootstrap, R1/R2/R3 collectives, hit de-duplication and JSON cont
 world sizes the 8-GPU node uses. On a host with fewer GPUs than ``--gpus`` the GPU run must refuse instead of
 silently reporting a smaller node.
 """
-import json
 import os
 import subprocess
 import sys
