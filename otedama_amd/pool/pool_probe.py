@@ -202,7 +202,9 @@ def measure_pool(gpus: int = 1, seconds: float = 30.0, share_seconds: float = 0.
             r = w.get("window_ratio")
             return bool(w.get("settled")) and r is not None and abs(math.log(max(r, 1e-12))) < math.log(1.10)
 
-        end = time.monotonic() + settle_timeout
+        # CPU miners (the rehearsal) are too slow to fill vardiff's window: their settle wait is short, the window is
+        # recorded with steady_state false
+        end = time.monotonic() + (min(settle_timeout, 30.0) if cpu else settle_timeout)
         settled = False
         while time.monotonic() < end:
             ws = [w for s in _pool_api(http) for w in s.get("workers", [])]
