@@ -423,6 +423,7 @@ class Bench:
                 self.sha256d()
         except Exception as exc:  # noqa: BLE001
             return self.fail("sha256d", f"{type(exc).__name__}: {exc}")
+        g.headline_done = True  # every rank holds the headline now (its last collective included rank 0)
         # sections every rank takes part in (collectives): rank 0 decides whether there is time and tells the rest
         need = {"single": 15.0, "scrypt": 30.0, "x11": 20.0, "miner": 2 * (self.miner_seconds() + 20.0),
                 "comm": 30.0 + 2 * len(self.comm_phases()) * 12.0}
@@ -1015,16 +1016,27 @@ class Bench:
         if not self.cpu:
             torch.cuda.empty_cache()
 
+    COMM_OP_DEADLINE_S = 30.0  # the comm section's bound on one collective (ops take ~0.1-20 ms)
+
     def comm_section(self) -> None:
         """The run's own data plane measured across every rank (parallel/comm_probe.py measure_node_comm): the node's
         R1 / R2 / R3 and the device-resident R2 as p50 / p99 over --comm-ops each, idle and with every rank's GPU
         mining, the miner-rate change the ops cause, and one large all_gather's bus bandwidth (xGMI or not)."""
         from otedama_amd.parallel.comm_probe import measure_node_comm
 
-        self.R["comm"] = measure_node_comm(self.comm, self.dev, phases=self.comm_phases(), ops=self.args.comm_ops,
-                                           cadence_hz=self.args.comm_hz,
-                                           busbw_bytes=(4 << 20) if self.cpu else self.args.comm_busbw_mib << 20,
-                                           say=self.guard.progress)
+        # Every op of this section is bounded: a collective that one rank never joins raises (CollectiveTimeout)
+        # instead of holding the run until the section's watchdog, which would end it before the node and pool
+        # sections. It is the last section every rank takes part in, so a communicator broken here harms nothing.
+        comm = self.comm
+        saved = comm.bounded, comm.deadline
+        comm.bounded, comm.deadline = True, min(self.COMM_OP_DEADLINE_S, max(5.0, self.budgets["comm"] / 4.0))
+        try:
+            self.R["comm"] = measure_node_comm(comm, self.dev, phases=self.comm_phases(), ops=self.args.comm_ops,
+                                               cadence_hz=self.args.comm_hz,
+                                               busbw_bytes=(4 << 20) if self.cpu else self.args.comm_busbw_mib << 20,
+                                               say=self.guard.progress)
+        finally:
+            comm.bounded, comm.deadline = saved
         self.R["comm"]["impl"] = (self.R.get("preflight") or {}).get("data_plane", {}).get("impl")
 
     def cpu_miner(self) -> None:

@@ -362,21 +362,36 @@ class NodeComm:
         return float(self._max_h.item())
 
     def barrier(self) -> None:
-        barrier(self.info)
+        if self.bounded and self.info.world_size > 1 and self.info.backend != "nccl":
+            self._bounded(dist.barrier(async_op=True))
+        else:
+            barrier(self.info)
+
+    def _bounded(self, work) -> None:
+        """Wait for an async collective against the deadline (CollectiveTimeout), re-raising its failure."""
+        self._poll(work.is_completed)
+        work.wait()
 
     # ---------------------------------------------------------------- device-resident forms (bench.py)
     def gather_tensor(self, out, inp) -> None:
-        """``out`` (world x inp.shape) gets every rank's contiguous ``inp`` (parallel/rcclcomm.py has the same)."""
+        """``out`` (world x inp.shape) gets every rank's contiguous ``inp`` (parallel/rcclcomm.py has the same).
+        ``bounded``: the collective is polled against the deadline instead of blocking."""
         if self.info.world_size > 1:
             self.collectives += 1
-            dist.all_gather_into_tensor(out.view(-1), inp.view(-1))
+            if self.bounded:
+                self._bounded(dist.all_gather_into_tensor(out.view(-1), inp.view(-1), async_op=True))
+            else:
+                dist.all_gather_into_tensor(out.view(-1), inp.view(-1))
         else:
             out[0].copy_(inp)
 
     def broadcast_tensor(self, t, src: int = 0) -> None:
         if self.info.world_size > 1:
             self.collectives += 1
-            dist.broadcast(t, src=src)
+            if self.bounded:
+                self._bounded(dist.broadcast(t, src=src, async_op=True))
+            else:
+                dist.broadcast(t, src=src)
 
     def _run(self, fn) -> None:
         """Blocking form: the collective runs on the comm stream and the current stream waits for it (used where

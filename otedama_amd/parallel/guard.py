@@ -125,6 +125,7 @@ class RankGuard:
         self.phase = "start"
         self.progress_on = progress and rank == 0
         self._last_progress = time.monotonic()
+        self.headline_done = False  # set by the run once its critical (headline) sections completed
 
     def progress(self, msg: str) -> None:
         """One line on stderr from rank 0: section starts / ends and a periodic heartbeat, so a watcher that kills
@@ -294,7 +295,10 @@ class RankGuard:
                 self.sections[sec] = {"s": round(time.monotonic() - self.t0, 2), "status": "timeout" if timeout
                                       else "terminated"}
         self._write_status(fired=reason)
-        code = 3
+        # a follower whose watchdog fires after the headline was measured leaves cleanly: rank 0 holds the headline
+        # and reports this section's failure in its line; a non-zero exit would make torchrun (or the launcher) call
+        # the whole job failed
+        code = 0 if self.headline_done else 3
         if self.rank == 0:
             if self.emit is not None:
                 try:

@@ -243,3 +243,20 @@ def test_probe_with_default_deadlines_fits_the_preflight_under_skew_and_a_hang()
     assert a + t + v <= 90.0 - 40.0 + 1.0, dp["probe"]  # inside the budget minus the fallback's reserve
     assert d["sections"]["preflight"]["status"] == "ok" and d["sections"]["preflight"]["s"] < 90.0
     assert "killed" in dp["probe"]["ranks"]["1"]["reason"]
+
+
+@pytest.mark.timeout(300)
+def test_a_rank_stuck_in_the_comm_section_costs_only_that_section():
+    """The comm section is the last one every rank takes part in, and its collectives are bounded: when one rank
+    never joins, the others' ops raise (CollectiveTimeout) well inside the section's budget. The section is recorded
+    as an error, and rank 0 goes on with its own sections (here the CPU miner) and prints the full line. Rehearsed on
+    the native data plane's CPU stand-in."""
+    env = {"OTEDAMA_RCCL_MODULE": "loopback_rccl", "PYTHONPATH": os.path.join(ROOT, "tests"),
+           "OTEDAMA_BENCH_FAULT": "stuck:2:comm"}
+    res, took = _bench("--gpus", "4", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0.3",
+                       "--comm-ops", "10", "--section-timeouts", "comm=24", env=env, timeout=280)
+    assert res.returncode == 0, res.stderr[-3000:]
+    d = _json(res)
+    assert d["value"] > 0 and d.line["summary"]["data_plane"] == "rccl-native"
+    assert d["sections"]["comm"]["status"] == "error" and "comm" in d["errors"], d["sections"]
+    assert d["sections"]["cpu"]["status"] == "ok" and d["cpu_single_thread_hashes_per_sec"] > 0
