@@ -427,18 +427,35 @@ class Bench:
         # sections every rank takes part in (collectives): rank 0 decides whether there is time and tells the rest
         need = {"single": 15.0, "scrypt": 30.0, "x11": 20.0, "miner": 2 * (self.miner_seconds() + 20.0),
                 "comm": 30.0 + 2 * len(self.comm_phases()) * 12.0}
+        # After the headline every collective is bounded (half the section's budget, at most 120 s): a rank stuck in
+        # one of these sections costs that section (CollectiveTimeout on the others), not the rank-0 sections after
+        # them; once the data plane failed, the remaining collective sections are skipped with the reason.
+        broken = ""
         for name, fn in (("single", self.single), ("scrypt", self.scrypt), ("x11", self.x11),
                          ("miner", self.miner), ("comm", self.comm_section)):
             if not self.wanted(name):
                 continue
+            if broken:
+                g.skip(name, f"data plane unusable after {broken}")
+                continue
             go = g.remaining() >= need[name] if self.rank == 0 else True
             if self.world > 1:
-                go = bool(self.comm.broadcast_control([int(go)])[0])
+                try:
+                    with self.bounded_comm(60.0):
+                        go = bool(self.comm.broadcast_control([int(go)])[0])
+                except Exception as exc:  # noqa: BLE001 - a peer is gone or stuck
+                    broken = f"{name} go/no-go: {type(exc).__name__}"
+                    g.skip(name, f"data plane unusable: {type(exc).__name__}: {exc}"[:200])
+                    continue
             if not go:
                 g.skip(name, f"bench deadline: {g.remaining():.0f} s left")
                 continue
             with g.section(name, self.budgets[name]):
-                fn()
+                with self.bounded_comm(min(120.0, self.budgets[name] / 2.0)):
+                    fn()
+            err = g.errors.get(name, "")
+            if self.world > 1 and ("CollectiveTimeout" in err or "rccl" in err.lower()):
+                broken = name
         if self.rank != 0:
             g.finish()
             self.shutdown()
@@ -1016,6 +1033,18 @@ class Bench:
         if not self.cpu:
             torch.cuda.empty_cache()
 
+    @contextlib.contextmanager
+    def bounded_comm(self, deadline: float):
+        """Every collective inside raises CollectiveTimeout after ``deadline`` s instead of waiting for a peer that
+        never comes (parallel/comm.py and parallel/rcclcomm.py ``bounded`` mode)."""
+        comm = self.comm
+        saved = comm.bounded, comm.deadline
+        comm.bounded, comm.deadline = True, deadline
+        try:
+            yield
+        finally:
+            comm.bounded, comm.deadline = saved
+
     COMM_OP_DEADLINE_S = 30.0  # the comm section's bound on one collective (ops take ~0.1-20 ms)
 
     def comm_section(self) -> None:
@@ -1027,16 +1056,11 @@ class Bench:
         # Every op of this section is bounded: a collective that one rank never joins raises (CollectiveTimeout)
         # instead of holding the run until the section's watchdog, which would end it before the node and pool
         # sections. It is the last section every rank takes part in, so a communicator broken here harms nothing.
-        comm = self.comm
-        saved = comm.bounded, comm.deadline
-        comm.bounded, comm.deadline = True, min(self.COMM_OP_DEADLINE_S, max(5.0, self.budgets["comm"] / 4.0))
-        try:
-            self.R["comm"] = measure_node_comm(comm, self.dev, phases=self.comm_phases(), ops=self.args.comm_ops,
+        with self.bounded_comm(min(self.COMM_OP_DEADLINE_S, max(5.0, self.budgets["comm"] / 4.0))):
+            self.R["comm"] = measure_node_comm(self.comm, self.dev, phases=self.comm_phases(), ops=self.args.comm_ops,
                                                cadence_hz=self.args.comm_hz,
                                                busbw_bytes=(4 << 20) if self.cpu else self.args.comm_busbw_mib << 20,
                                                say=self.guard.progress)
-        finally:
-            comm.bounded, comm.deadline = saved
         self.R["comm"]["impl"] = (self.R.get("preflight") or {}).get("data_plane", {}).get("impl")
 
     def cpu_miner(self) -> None:
