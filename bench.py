@@ -255,6 +255,13 @@ def _short_errors(errors: dict | None, n: int = 160) -> dict | None:
     return {str(k)[:40]: str(v)[:n] for k, v in errors.items()} if errors else None
 
 
+def _link_counts(links) -> dict | None:
+    out: dict = {}
+    for ln in links or []:
+        out[str(ln.get("type"))] = out.get(str(ln.get("type")), 0) + 1
+    return out or None
+
+
 def _data_plane_note(dp: dict) -> str | None:
     probe = dp.get("probe") or {}
     if probe and not probe.get("ok"):
@@ -1062,6 +1069,13 @@ class Bench:
                                                busbw_bytes=(4 << 20) if self.cpu else self.args.comm_busbw_mib << 20,
                                                say=self.guard.progress)
         self.R["comm"]["impl"] = (self.R.get("preflight") or {}).get("data_plane", {}).get("impl")
+        if not self.cpu:  # the links the collectives ran on (KFD topology; ranks' GPUs are ordinals 0..N-1)
+            from otedama_amd import hal
+
+            topo = hal.kfd_topology()
+            mine = set(range(self.world))
+            links = [ln for ln in topo["links"] if ln["from"] in mine and ln["to"] in mine]
+            self.R["comm"]["topology"] = {"gpus": topo["gpus"][: self.world], "links": links}
 
     def cpu_miner(self) -> None:
         """BASELINE config 1: the native CPU miner, single thread and all cores of this box's CPU share."""
@@ -1299,6 +1313,8 @@ class Bench:
             "comm_r3_p99_ms": p99("R3"),
             "comm_r2_dev_p99_ms": p99("R2_dev"),
             "comm_busbw_gbps": _r((comm.get("busbw") or {}).get("busbw_gbps")),
+            # directed GPU pairs of this run by link type (KFD topology): what the bus bandwidth ran over
+            "comm_links": _link_counts((comm.get("topology") or {}).get("links")),
             "comm_miner_rate_change_pct": comm.get("miner_rate_change_pct"),
             "sections_s": self._section_times(),
             "errors": _short_errors(errors),

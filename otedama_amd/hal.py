@@ -229,6 +229,49 @@ class KFDDriver:
         return out
 
 
+IOLINK_TYPES = {2: "pcie", 11: "xgmi"}  # hsakmttypes.h HSA_IOLINK_TYPE_PCIEXPRESS / HSA_IOLINK_TYPE_XGMI
+
+
+def kfd_topology(base_path: str | None = None) -> dict:
+    """The GPU-to-GPU links of the visible GPUs from the KFD topology (no HIP runtime): per GPU its HIP ordinal,
+    KFD node, XGMI hive id and XGMI-optimised SDMA engines; per directed GPU pair the io_link's type (``xgmi`` /
+    ``pcie`` / the raw number), weight and max bandwidth (MB/s, as KFD reports it). bench.py's comm section puts it
+    beside the measured bus bandwidth, so an 8-GPU figure reads against the links it ran on. Empty off a ROCm host."""
+    base = base_path or KFD_TOPOLOGY_PATH
+    drv = KFDDriver(base)
+    try:
+        nodes = sorted(int(d) for d in os.listdir(base) if d.isdigit())
+    except OSError:
+        return {"gpus": [], "links": []}
+    gpu_nodes = []
+    props_of = {}
+    for n in nodes:
+        p = _kfd_props(os.path.join(base, str(n), "properties"))
+        if p.get("simd_count", 0) > 0 and p.get("gfx_target_version") and drv._openable(p):
+            gpu_nodes.append(n)
+            props_of[n] = p
+    order = [gpu_nodes[k] for k in _visible(len(gpu_nodes))]
+    index_of = {n: i for i, n in enumerate(order)}
+    gpus = [{"index": i, "node": n, "hive_id": props_of[n].get("hive_id"),
+             "sdma_xgmi_engines": props_of[n].get("num_sdma_xgmi_engines")} for i, n in enumerate(order)]
+    links = []
+    for n in order:
+        ldir = os.path.join(base, str(n), "io_links")
+        try:
+            entries = sorted(os.listdir(ldir), key=lambda x: int(x) if x.isdigit() else 0)
+        except OSError:
+            continue
+        for e in entries:
+            lp = _kfd_props(os.path.join(ldir, e, "properties"))
+            to = lp.get("node_to")
+            if to not in index_of or to == n:
+                continue
+            t = lp.get("type", 0)
+            links.append({"from": index_of[n], "to": index_of[to], "type": IOLINK_TYPES.get(t, t),
+                          "weight": lp.get("weight"), "max_bandwidth": lp.get("max_bandwidth")})
+    return {"gpus": gpus, "links": links}
+
+
 DRM_BASE_PATH = "/sys/class/drm"
 
 

@@ -467,3 +467,33 @@ def test_detector_is_thread_safe_under_concurrent_calls():
     for t in ts:
         t.join(5)
     assert out == [1] * 8
+
+
+def test_kfd_topology_reads_gpu_to_gpu_links(tmp_path, monkeypatch):
+    """hal.kfd_topology: GPU nodes in HIP ordinal order (CPU nodes skipped), their hive ids, and the directed
+    GPU-to-GPU io_links with their type named (11 = xgmi, 2 = pcie); links to CPU nodes are left out."""
+    from otedama_amd import hal
+
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+
+    def node(n, props, links=()):
+        d = tmp_path / str(n)
+        d.mkdir()
+        (d / "properties").write_text("\n".join(f"{k} {v}" for k, v in props.items()) + "\n")
+        for i, lp in enumerate(links):
+            ld = d / "io_links" / str(i)
+            ld.mkdir(parents=True)
+            (ld / "properties").write_text("\n".join(f"{k} {v}" for k, v in lp.items()) + "\n")
+
+    gpu = {"simd_count": 1024, "simd_per_cu": 4, "gfx_target_version": 90500, "hive_id": 77,
+           "num_sdma_xgmi_engines": 14}
+    node(0, {"simd_count": 0, "cpu_cores_count": 64})
+    node(1, gpu, [{"type": 2, "node_from": 1, "node_to": 0, "weight": 20},
+                  {"type": 11, "node_from": 1, "node_to": 2, "weight": 15, "max_bandwidth": 50000}])
+    node(2, gpu, [{"type": 11, "node_from": 2, "node_to": 1, "weight": 15, "max_bandwidth": 50000}])
+    t = hal.kfd_topology(str(tmp_path))
+    assert [g["node"] for g in t["gpus"]] == [1, 2] and t["gpus"][0]["hive_id"] == 77
+    assert t["links"] == [{"from": 0, "to": 1, "type": "xgmi", "weight": 15, "max_bandwidth": 50000},
+                          {"from": 1, "to": 0, "type": "xgmi", "weight": 15, "max_bandwidth": 50000}]
+    assert hal.kfd_topology(str(tmp_path / "missing")) == {"gpus": [], "links": []}
