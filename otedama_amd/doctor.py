@@ -652,18 +652,42 @@ def check_gpu_runtime() -> Check:
 
 
 def check_collectives() -> Check:
+    """The multi-GPU data plane: the native RCCL module the node and bench.py use (``otedama_amd._rccl``), the
+    torch.distributed fallback backends, dmabuf IPC, and the xGMI links between the visible GPUs (KFD topology)."""
     def run():
+        status, fix, parts = Status.PASS, "", []
+        try:
+            from otedama_amd.parallel.rcclcomm import rccl_module
+
+            parts.append(f"native RCCL module {rccl_module().version()}")
+        except Exception as exc:  # noqa: BLE001
+            status, fix = Status.WARN, "python -m otedama_amd._build (builds otedama_amd._rccl against librccl)"
+            parts.append(f"native RCCL module unavailable ({type(exc).__name__})")
         try:
             import torch.distributed as dist
+
+            nccl = dist.is_nccl_available()
+            parts.append(f"fallback backends: nccl(RCCL)={'yes' if nccl else 'no'}, "
+                         f"gloo={'yes' if dist.is_gloo_available() else 'no'}")
         except Exception as exc:  # noqa: BLE001
-            return Result(status=Status.WARN, detail=f"torch.distributed unavailable: {exc}",
-                          fix="multi-GPU mining needs PyTorch with RCCL")
-        nccl = dist.is_nccl_available()
+            nccl = False
+            parts.append(f"torch.distributed unavailable ({type(exc).__name__})")
         if os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "") != "0" and nccl:
-            return Result(status=Status.WARN, detail="RCCL available but HSA_ENABLE_IPC_MODE_LEGACY is not 0",
-                          fix="export HSA_ENABLE_IPC_MODE_LEGACY=0 (dmabuf IPC) for multi-process RCCL")
-        return Result(detail=f"torch.distributed backends: nccl(RCCL)={'yes' if nccl else 'no'}, "
-                             f"gloo={'yes' if dist.is_gloo_available() else 'no'}")
+            status, fix = Status.WARN, "export HSA_ENABLE_IPC_MODE_LEGACY=0 (dmabuf IPC) for multi-process RCCL"
+            parts.append("HSA_ENABLE_IPC_MODE_LEGACY is not 0")
+        from otedama_amd import hal
+
+        topo = hal.kfd_topology()
+        n = len(topo["gpus"])
+        if n > 1:
+            pairs = n * (n - 1)
+            x = sum(1 for ln in topo["links"] if ln.get("type") == "xgmi")
+            hives = {g.get("hive_id") for g in topo["gpus"]}
+            parts.append(f"{n} GPUs: {x}/{pairs} directed pairs on xGMI, {len(hives)} hive(s)")
+            if x < pairs and status == Status.PASS:
+                status = Status.WARN
+                fix = "GPU pairs without xGMI move R1/R2/R3 over PCIe; check the node's topology (rocm-smi --showtopo)"
+        return Result(status=status, detail="; ".join(parts), fix=fix)
     return Check("Collectives", run)
 
 

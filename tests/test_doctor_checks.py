@@ -437,3 +437,20 @@ def test_default_checks_cover_the_reference_and_mi355x_set():
               "Network", "System clock accuracy", "Hardware", "Native extension", "GPU runtime", "Collectives",
               "PoW self-test"):
         assert n in names
+
+
+def test_collectives_check_reports_the_native_module_and_xgmi_pairs(monkeypatch):
+    """The Collectives check names the node's data plane (the native RCCL module), and on a multi-GPU host counts
+    the xGMI-linked GPU pairs from the KFD topology: all pairs linked passes, a pair without xGMI warns."""
+    from otedama_amd import doctor, hal
+
+    monkeypatch.setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    gpus = [{"index": i, "node": i + 2, "hive_id": 7, "sdma_xgmi_engines": 14} for i in range(3)]
+    full = [{"from": a, "to": b, "type": "xgmi", "weight": 15, "max_bandwidth": 76000}
+            for a in range(3) for b in range(3) if a != b]
+    monkeypatch.setattr(hal, "kfd_topology", lambda base_path=None: {"gpus": gpus, "links": full})
+    r = doctor.check_collectives().run()
+    assert "native RCCL module" in r.detail and "3 GPUs: 6/6 directed pairs on xGMI, 1 hive(s)" in r.detail
+    monkeypatch.setattr(hal, "kfd_topology", lambda base_path=None: {"gpus": gpus, "links": full[:4]})
+    r = doctor.check_collectives().run()
+    assert r.status == doctor.Status.WARN and "4/6" in r.detail and "PCIe" in r.fix
