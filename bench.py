@@ -1336,9 +1336,10 @@ def run_rank(args) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     run_dir = run_dir_for()
-    if world > 1:  # RCCL warnings into the run directory, where an error JSON reads them back
-        os.environ.setdefault("NCCL_DEBUG", "WARN")
-        os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(run_dir, "rccl.%h.%p.log"))
+    # RCCL's messages into the run directory, where an error JSON reads them back, and never on stdout, whose last
+    # line is the driver's (at N=1 an unset NCCL_DEBUG let RCCL print its version banner there)
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
+    os.environ.setdefault("NCCL_DEBUG_FILE", os.path.join(run_dir, "rccl.%h.%p.log"))
     bench = Bench(args, rank, world)
     prev = os.environ.get("GPU_MAX_HW_QUEUES")
     if not args.cpu_rehearsal and (prev is None or (prev.isdigit() and int(prev) < int(BENCH_HW_QUEUES))):
