@@ -255,6 +255,23 @@ def _short_errors(errors: dict | None, n: int = 160) -> dict | None:
     return {str(k)[:40]: str(v)[:n] for k, v in errors.items()} if errors else None
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """fd 1 points at fd 2 inside: C-level prints (RCCL's init banner) stay off the stdout whose last line is the
+    driver's."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        try:
+            sys.stdout.flush()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+
+
 def _link_counts(links) -> dict | None:
     out: dict = {}
     for ln in links or []:
@@ -572,7 +589,8 @@ class Bench:
             if fault_for(self.rank, "native") == "fail":  # tests: this rank's in-process init fails after the probe
                 raise RuntimeError("injected native init failure")
             comm = NativeNodeComm(info, bounded=False, force=True, device_stream=True)
-            comm.reform(list(range(self.world)), 1, timeout=timeout)
+            with _stdout_to_stderr():  # RCCL prints a version banner on stdout at init, whatever NCCL_DEBUG says
+                comm.reform(list(range(self.world)), 1, timeout=timeout)
         except Exception as exc:  # noqa: BLE001 - decided together below
             comm, err = None, f"{type(exc).__name__}: {exc}"[:300]
         if self.world > 1:
