@@ -27,7 +27,8 @@ Fault hooks for the CPU rehearsal tests: ``OTEDAMA_BENCH_FAULT=stuck:<rank>:<sec
 at the start of that section (an uninterruptible-looking sleep), ``exit:<rank>:<section>`` makes it exit with code 7;
 ``fail:<rank>:probe`` / ``hang:<rank>:probe`` make that rank's data-plane probe child fail or hang
 (parallel/rccl_probe.py); ``slow:<rank>:arrive`` delays that rank's arrival at the probe by OTEDAMA_FAULT_SLOW_S
-(a cold-start skew); ``fail:<rank>:native`` fails its in-process native init after the probe.
+(a cold-start skew); ``fail:<rank>:native`` fails its in-process native init after the probe;
+``fail:<rank>:<section>`` makes that section raise at its start.
 """
 from __future__ import annotations
 
@@ -212,6 +213,8 @@ class RankGuard:
         if fault == "exit":
             os._exit(7)
         try:
+            if fault == "fail":  # tests: the section raises at once (a start that failed, not a hang)
+                raise RuntimeError(f"injected failure in section {name}")
             yield
         except Exception as exc:  # noqa: BLE001 - a failed section is recorded; the run goes on
             with self._lock:

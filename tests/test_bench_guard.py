@@ -260,3 +260,16 @@ def test_a_rank_stuck_in_the_comm_section_costs_only_that_section():
     assert d["value"] > 0 and d.line["summary"]["data_plane"] == "rccl-native"
     assert d["sections"]["comm"]["status"] == "error" and "comm" in d["errors"], d["sections"]
     assert d["sections"]["cpu"]["status"] == "ok" and d["cpu_single_thread_hashes_per_sec"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_a_failed_headline_section_prints_a_capped_error_line():
+    """bench.fail(): the headline section raises on rank 0 (not a hang) at world 8. Rank 0 prints the error line
+    under the driver's cap, with the section's error in ``summary``, stops its peers and exits non-zero."""
+    res, took = _bench("--gpus", "8", "--steps", "2", "--warmup", "1", "--cpu-rehearsal", "--cpu-seconds", "0",
+                       "--comm-ops", "0", env={"OTEDAMA_BENCH_FAULT": "fail:0:sha256d"}, timeout=240)
+    assert res.returncode != 0
+    d = _json(res)
+    assert d["value"] is None and "injected failure in section sha256d" in d["error"]
+    assert "sha256d" in d.line["summary"]["errors"]
+    assert took < 150, took
